@@ -1,0 +1,238 @@
+// oracle/ref_shim.cpp — TEST INFRASTRUCTURE ONLY (never linked into the product).
+//
+// A thin C-ABI shim over the *reference* libbitcoinconsensus + libsecp256k1, compiled from the
+// unmodified sources under /root/reference by oracle/Makefile into oracle/_ref/libref_consensus.so.
+// It exposes the reference's own per-signature semantics so that tests/, smoke() and bench.py's
+// cpu_baseline leg can use the reference as the checker / CPU baseline:
+//
+//   * ref_pubkey_verify   -> CPubKey(pub).Verify(hash, sig)          depend/bitcoin/src/pubkey.cpp:191-207
+//                            (lax DER + normalize-S + secp256k1_ecdsa_verify)
+//   * ref_capture_script  -> VerifyScript with a checker that records every
+//                            (pubkey, sig, sighash, verdict) the interpreter asks for
+//                            (GenericTransactionSignatureChecker::VerifyECDSASignature,
+//                             depend/bitcoin/src/script/interpreter.cpp:1644-1676)
+//   * ref_schnorr_verify  -> secp256k1_schnorrsig_verify            secp256k1/src/modules/schnorrsig/main_impl.h:190-237
+//   * ref_sign / ref_pubkey_create / ref_schnorr_sign: fixture generation only
+//   * ref_bench_*         -> std::thread pool timing of the reference entry points (cpu_baseline)
+//
+// The shim contains no consensus logic of its own: every verdict comes from the reference.
+#include <script/bitcoinconsensus.h>
+#include <script/interpreter.h>
+#include <primitives/transaction.h>
+#include <pubkey.h>
+#include <version.h>
+#include <secp256k1.h>
+#include <secp256k1_schnorrsig.h>
+#include <secp256k1_extrakeys.h>
+
+#include <atomic>
+#include <chrono>
+#include <cstdint>
+#include <cstring>
+#include <thread>
+#include <vector>
+
+namespace {
+
+secp256k1_context* sign_ctx() {
+    static secp256k1_context* ctx =
+        secp256k1_context_create(SECP256K1_CONTEXT_SIGN | SECP256K1_CONTEXT_VERIFY);
+    return ctx;
+}
+
+// Minimal byte-reader with the Unserialize stream interface (avoids CDataStream, whose
+// allocator pulls support/cleanse.cpp, which build.rs does not compile).
+class ByteReader {
+public:
+    ByteReader(const unsigned char* p, size_t n) : m_p(p), m_n(n) {}
+    void read(char* dst, size_t k) {
+        if (k > m_n) throw std::ios_base::failure("end of data");
+        memcpy(dst, m_p, k);
+        m_p += k;
+        m_n -= k;
+    }
+    template <typename T> ByteReader& operator>>(T&& obj) {
+        ::Unserialize(*this, obj);
+        return *this;
+    }
+    int GetVersion() const { return PROTOCOL_VERSION; }
+    int GetType() const { return SER_NETWORK; }
+
+private:
+    const unsigned char* m_p;
+    size_t m_n;
+};
+
+struct Capture {
+    std::vector<unsigned char> pub, sig;  // sig without the hashtype byte
+    uint256 sighash;
+    bool verdict;
+};
+
+class CapturingChecker : public TransactionSignatureChecker {
+public:
+    mutable std::vector<Capture> log;
+    CapturingChecker(const CTransaction* tx, unsigned int nIn, const CAmount& amount,
+                     const PrecomputedTransactionData& txdata)
+        : TransactionSignatureChecker(tx, nIn, amount, txdata) {}
+
+protected:
+    bool VerifyECDSASignature(const std::vector<unsigned char>& vchSig, const CPubKey& pubkey,
+                              const uint256& sighash) const override {
+        bool ok = TransactionSignatureChecker::VerifyECDSASignature(vchSig, pubkey, sighash);
+        log.push_back(Capture{std::vector<unsigned char>(pubkey.begin(), pubkey.end()), vchSig,
+                              sighash, ok});
+        return ok;
+    }
+};
+
+}  // namespace
+
+extern "C" {
+
+int ref_version() { return (int)bitcoinconsensus_version(); }
+
+int ref_verify_script_with_amount(const unsigned char* spk, unsigned int spklen, int64_t amount,
+                                  const unsigned char* tx, unsigned int txlen, unsigned int nIn,
+                                  unsigned int flags, int* err) {
+    bitcoinconsensus_error e = bitcoinconsensus_ERR_OK;
+    int r = bitcoinconsensus_verify_script_with_amount(spk, spklen, amount, tx, txlen, nIn, flags, &e);
+    if (err) *err = (int)e;
+    return r;
+}
+
+int ref_verify_script(const unsigned char* spk, unsigned int spklen, const unsigned char* tx,
+                      unsigned int txlen, unsigned int nIn, unsigned int flags, int* err) {
+    bitcoinconsensus_error e = bitcoinconsensus_ERR_OK;
+    int r = bitcoinconsensus_verify_script(spk, spklen, tx, txlen, nIn, flags, &e);
+    if (err) *err = (int)e;
+    return r;
+}
+
+// CPubKey::Verify semantics: pub = 33/65 serialized bytes, hash32 = raw sighash bytes
+// (uint256::begin()), sig = DER signature WITHOUT the hashtype byte.
+int ref_pubkey_verify(const unsigned char* pub, size_t publen, const unsigned char* hash32,
+                      const unsigned char* sig, size_t siglen) {
+    CPubKey key(pub, pub + publen);
+    uint256 h(std::vector<unsigned char>(hash32, hash32 + 32));
+    std::vector<unsigned char> vs(sig, sig + siglen);
+    return key.Verify(h, vs) ? 1 : 0;
+}
+
+// Runs the reference VerifyScript on (spk, tx, nIn, amount, flags) with a capturing checker.
+// Writes up to `cap` records into the out arrays: pub (65 B slot + len), sig (80 B slot + len),
+// sighash (32 B raw), verdict. Returns the script result (1/0), or -1 on deserialize error.
+int ref_capture_script(const unsigned char* spk, unsigned int spklen, int64_t amount,
+                       const unsigned char* txb, unsigned int txlen, unsigned int nIn,
+                       unsigned int flags, int cap, unsigned char* pub65, int* publen,
+                       unsigned char* sig80, int* siglen, unsigned char* hash32, int* verdict,
+                       int* ncaptured, int* script_error) {
+    try {
+        ByteReader ss(txb, txlen);
+        CTransaction tx(deserialize, ss);
+        if (nIn >= tx.vin.size()) return -2;
+        PrecomputedTransactionData txdata(tx);
+        CapturingChecker chk(&tx, nIn, amount, txdata);
+        ScriptError serr = SCRIPT_ERR_OK;
+        bool ok = VerifyScript(tx.vin[nIn].scriptSig, CScript(spk, spk + spklen),
+                               &tx.vin[nIn].scriptWitness, flags, chk, &serr);
+        int n = 0;
+        for (const auto& c : chk.log) {
+            if (n >= cap) break;
+            memset(pub65 + 65 * n, 0, 65);
+            memset(sig80 + 80 * n, 0, 80);
+            memcpy(pub65 + 65 * n, c.pub.data(), c.pub.size() > 65 ? 65 : c.pub.size());
+            publen[n] = (int)c.pub.size();
+            size_t sl = c.sig.size() > 80 ? 80 : c.sig.size();
+            memcpy(sig80 + 80 * n, c.sig.data(), sl);
+            siglen[n] = (int)c.sig.size();
+            memcpy(hash32 + 32 * n, c.sighash.begin(), 32);
+            verdict[n] = c.verdict ? 1 : 0;
+            ++n;
+        }
+        *ncaptured = (int)chk.log.size();
+        if (script_error) *script_error = (int)serr;
+        return ok ? 1 : 0;
+    } catch (const std::exception&) {
+        return -1;
+    }
+}
+
+int ref_schnorr_verify(const unsigned char* sig64, const unsigned char* msg32,
+                       const unsigned char* xonly32) {
+    secp256k1_xonly_pubkey pk;
+    if (!secp256k1_xonly_pubkey_parse(sign_ctx(), &pk, xonly32)) return 0;
+    return secp256k1_schnorrsig_verify(sign_ctx(), sig64, msg32, &pk);
+}
+
+// ---- fixture generation helpers (NOT used by any parity check as a verdict source) ----
+int ref_pubkey_create(const unsigned char* seckey32, int compressed, unsigned char* out,
+                      size_t* outlen) {
+    secp256k1_pubkey pk;
+    if (!secp256k1_ec_pubkey_create(sign_ctx(), &pk, seckey32)) return 0;
+    return secp256k1_ec_pubkey_serialize(sign_ctx(), out, outlen, &pk,
+                                         compressed ? SECP256K1_EC_COMPRESSED
+                                                    : SECP256K1_EC_UNCOMPRESSED);
+}
+
+int ref_sign(const unsigned char* seckey32, const unsigned char* msg32, unsigned char* der72,
+             size_t* derlen) {
+    secp256k1_ecdsa_signature sig;
+    if (!secp256k1_ecdsa_sign(sign_ctx(), &sig, msg32, seckey32, nullptr, nullptr)) return 0;
+    return secp256k1_ecdsa_signature_serialize_der(sign_ctx(), der72, derlen, &sig);
+}
+
+int ref_schnorr_sign(const unsigned char* seckey32, const unsigned char* msg32,
+                     const unsigned char* aux32, unsigned char* sig64, unsigned char* xonly32) {
+    secp256k1_keypair kp;
+    if (!secp256k1_keypair_create(sign_ctx(), &kp, seckey32)) return 0;
+    secp256k1_xonly_pubkey xpk;
+    if (!secp256k1_keypair_xonly_pub(sign_ctx(), &xpk, nullptr, &kp)) return 0;
+    if (!secp256k1_xonly_pubkey_serialize(sign_ctx(), xonly32, &xpk)) return 0;
+    return secp256k1_schnorrsig_sign(sign_ctx(), sig64, msg32, &kp, nullptr, (void*)aux32);
+}
+
+// ---- CPU baseline timing: std::thread pool, static contiguous chunks (rayon-like) ----
+// items are given as concatenated blobs with offset arrays. Returns wall seconds; writes the
+// per-item return codes into ret (so the caller can also cross-check verdicts).
+double ref_bench_verify_script(int nthreads, long n, const unsigned char* spk_blob,
+                               const long* spk_off, const unsigned char* tx_blob,
+                               const long* tx_off, const int64_t* amounts,
+                               const unsigned int* nin, unsigned int flags, int* ret) {
+    auto t0 = std::chrono::steady_clock::now();
+    std::vector<std::thread> pool;
+    for (int t = 0; t < nthreads; ++t) {
+        pool.emplace_back([=]() {
+            long lo = n * t / nthreads, hi = n * (t + 1) / nthreads;
+            for (long i = lo; i < hi; ++i) {
+                bitcoinconsensus_error e;
+                ret[i] = bitcoinconsensus_verify_script_with_amount(
+                    spk_blob + spk_off[i], (unsigned)(spk_off[i + 1] - spk_off[i]), amounts[i],
+                    tx_blob + tx_off[i], (unsigned)(tx_off[i + 1] - tx_off[i]), nin[i], flags, &e);
+            }
+        });
+    }
+    for (auto& th : pool) th.join();
+    return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+}
+
+// Tuple-level baseline: CPubKey::Verify over (pub, hash, sig) tuples. pub in 65-B slots with
+// lengths, sig in 80-B slots with lengths.
+double ref_bench_pubkey_verify(int nthreads, long n, const unsigned char* pub65, const int* publen,
+                               const unsigned char* hash32, const unsigned char* sig80,
+                               const int* siglen, int* ret) {
+    auto t0 = std::chrono::steady_clock::now();
+    std::vector<std::thread> pool;
+    for (int t = 0; t < nthreads; ++t) {
+        pool.emplace_back([=]() {
+            long lo = n * t / nthreads, hi = n * (t + 1) / nthreads;
+            for (long i = lo; i < hi; ++i)
+                ret[i] = ref_pubkey_verify(pub65 + 65 * i, (size_t)publen[i], hash32 + 32 * i,
+                                           sig80 + 80 * i, (size_t)siglen[i]);
+        });
+    }
+    for (auto& th : pool) th.join();
+    return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+}
+
+}  // extern "C"

@@ -1,0 +1,328 @@
+// Per-lane ECDSA verification: one lane = one (pubkey, msg32, r, s) tuple.
+//
+// Restates secp256k1_ecdsa_verify semantics (secp256k1.c:423-438 + ecdsa_impl.h:207-275 +
+// eckey_impl.h:17-35) with a SIMT-friendly algorithm:
+//   R = u1*G + u2*Q,  u2 = k1 + lambda*k2 (GLV),  u1 = lo + 2^128*hi
+//   four 128-bit scalars, each recoded into SIGNED ODD fixed windows (every digit nonzero, so
+//   every lane of a wave adds at the same bit positions: no wNAF divergence);
+//   Q table {1,3,..,15}Q on an isomorphic curve (shared Z, no inversion), G tables in LDS;
+//   inversion-free final test r*Z^2 == X (or (r+n)*Z^2 == X when r < p-n).
+// Verdicts are a pure function of the group arithmetic, so they equal the reference's on every
+// input, including the exceptional additions (P == +-Q) that adversarial inputs can reach.
+#pragma once
+#include "secp256k1_device.h"
+
+namespace bcc {
+
+// window widths
+constexpr int WQ = 4;                         // Q / lambda*Q digits: table of 8 odd multiples
+constexpr int WG = 8;                         // G / 2^128*G digits: tables of 128 odd multiples
+constexpr int QTAB = 1 << (WQ - 1);           // 8
+constexpr int GTAB = 1 << (WG - 1);           // 128
+constexpr int TOPQ = 124;                     // WQ * 31: top digit position for 128-bit scalars
+constexpr int TOPG = 120;                     // WG * 15
+
+// (k >> pos) & (2^w - 1) for a 128-bit k (4 limbs), 0 <= pos < 128, w <= 8
+BCC_HD u32 bits_at(u32 l0, u32 l1, u32 l2, u32 l3, int pos, int w) {
+    int li = pos >> 5, sh = pos & 31;
+    u32 a = li == 0 ? l0 : li == 1 ? l1 : li == 2 ? l2 : l3;
+    u32 b = li == 0 ? l1 : li == 1 ? l2 : li == 2 ? l3 : 0u;
+    u32 v = sh ? ((a >> sh) | (b << (32 - sh))) : a;
+    return v & ((1u << w) - 1u);
+}
+
+// Signed odd fixed-window recoding of an ODD scalar k < 2^128, closed form:
+//   k = sum_i d_i 2^(w i),  d_i = 2*((k >> (w i + 1)) mod 2^w) + 1 - 2^w   (i < top)
+//   d_top = 2*(k >> (w top + 1)) + 1            (positive, < 2^w for k < 2^128)
+// Returns the table index (|d| - 1) / 2 and sets neg = (d < 0).
+BCC_HD u32 digit_index(u32 l0, u32 l1, u32 l2, u32 l3, int pos, int w, int top, bool& neg) {
+    u32 v = bits_at(l0, l1, l2, l3, pos + 1, w);
+    if (pos == top) {
+        neg = false;
+        return v;
+    }
+    u32 half = 1u << (w - 1), mask = half - 1u;
+    bool positive = (v & half) != 0;
+    neg = !positive;
+    return positive ? (v & mask) : (~v & mask);
+}
+
+// Per-lane Q table: entry i holds x, beta*x, y of (2i+1)Q on the shared-Z curve E'.
+// Host version: a plain array (device version lives in ecdsa_verify.hip).
+struct QTableArray {
+    fe e[QTAB][3];
+    BCC_HD void put(int i, int f, const fe& a) { e[i][f] = a; }
+    BCC_HD void get(int i, int f, fe& a) const { a = e[i][f]; }
+};
+
+// Host version of the G tables: affine (2i+1) * 2^(128 tab) * G.
+struct GTableArray {
+    const fe* xy;  // [2][GTAB][2]
+    BCC_HD void get(int tab, int i, fe& x, fe& y) const {
+        x = xy[(tab * GTAB + i) * 2 + 0];
+        y = xy[(tab * GTAB + i) * 2 + 1];
+    }
+};
+
+// acc += point; the point is (px, py) affine on E (use_zinv, scale sigma) or on E' (plain).
+// Handles acc == infinity (rare) by materialising the point on E'.
+BCC_HD void acc_add(gej& acc, bool& inf, const fe& px, const fe& py, const fe& sigma,
+                    bool use_zinv) {
+    if (inf) {  // rare: only after an adversarial cancellation
+        if (use_zinv) {
+            fe s2, s3;
+            fe_sqr(s2, sigma);
+            fe_mul(s3, s2, sigma);
+            fe_mul(acc.x, px, s2);
+            fe_mul(acc.y, py, s3);
+        } else {
+            acc.x = px;
+            acc.y = py;
+        }
+        acc.z = fe_one();
+        inf = false;
+        return;
+    }
+    gej r;
+    bool rinf;
+    gej_add_zinv(r, rinf, acc, px, py, sigma, use_zinv);
+    acc = r;
+    inf = rinf;
+}
+
+// Verify one tuple. tag = pubkey header byte (0 for "length invalid"), px/py as parsed from the
+// big-endian bytes (py ignored for compressed keys), r/s/m as raw integers from big-endian bytes.
+template <class QT, class GT>
+BCC_HD int ecdsa_verify_lane(u32 tag, const fe& px_in, const fe& py_in, const sc& r_in,
+                             const sc& s_in, const sc& m_in, QT& qt, const GT& gt) {
+    const u32 N[8] = BCC_N_LIMBS;
+    // ---- pubkey parse (eckey_impl.h:17-35) ----
+    bool compressed = (tag == 2u || tag == 3u);
+    bool full = (tag == 4u || tag == 6u || tag == 7u);
+    if (!compressed && !full) return 0;
+    fe qx = px_in, qy = py_in;
+    if (!fe_lt_p(qx)) return 0;
+    {
+        fe x3, t;
+        fe_sqr(x3, qx);
+        fe_mul(x3, x3, qx);
+        fe seven = fe_const(7, 0, 0, 0, 0, 0, 0, 0);
+        fe_add(x3, x3, seven);                   // x^3 + 7
+        if (compressed) {
+            if (!fe_sqrt(qy, x3)) return 0;      // ge_set_xo_var: no square root
+            fe_normalize(qy);
+            if ((qy.v[0] & 1u) != (tag == 3u ? 1u : 0u)) fe_neg(qy, qy);
+        } else {
+            if (!fe_lt_p(qy)) return 0;
+            if (tag != 4u && (qy.v[0] & 1u) != (tag == 7u ? 1u : 0u)) return 0;  // hybrid parity
+            fe_sqr(t, qy);
+            if (!fe_equal(t, x3)) return 0;      // ge_is_valid_var
+        }
+    }
+    // ---- scalars (ecdsa_impl.h:216-222) ----
+    if (u256_is_zero(r_in.v) || u256_is_zero(s_in.v)) return 0;
+    if (!u256_lt(r_in.v, N) || !u256_lt(s_in.v, N)) return 0;
+    sc m = m_in;
+    if (!u256_lt(m.v, N)) {                      // scalar_set_b32 reduction
+        u32 tmp[8];
+        u256_sub(tmp, m.v, N);
+        for (int i = 0; i < 8; i++) m.v[i] = tmp[i];
+    }
+    sc sinv, u1, u2, k1, k2;
+    sc_inv(sinv, s_in);
+    sc_mul(u1, m, sinv);
+    sc_mul(u2, r_in, sinv);
+    sc_split_lambda(k1, k2, u2);
+    // |k| < 2^128: a split half whose upper 128 bits are nonzero is negative (n - |k|)
+    bool neg0 = (k1.v[4] | k1.v[5] | k1.v[6] | k1.v[7]) != 0;
+    bool neg1 = (k2.v[4] | k2.v[5] | k2.v[6] | k2.v[7]) != 0;
+    if (neg0) sc_neg(k1, k1);
+    if (neg1) sc_neg(k2, k2);
+    // the four 128-bit scalars: 0 = k1 (Q), 1 = k2 (lambda Q), 2 = u1 lo (G), 3 = u1 hi (2^128 G)
+    u32 a0 = k1.v[0], a1 = k1.v[1], a2 = k1.v[2], a3 = k1.v[3];
+    u32 b0 = k2.v[0], b1 = k2.v[1], b2 = k2.v[2], b3 = k2.v[3];
+    u32 c0 = u1.v[0], c1 = u1.v[1], c2 = u1.v[2], c3 = u1.v[3];
+    u32 d0 = u1.v[4], d1 = u1.v[5], d2 = u1.v[6], d3 = u1.v[7];
+    // make each scalar odd: k even -> use k+1, subtract the base point once at the end
+    bool corr0 = (a0 & 1u) == 0, corr1 = (b0 & 1u) == 0, corr2 = (c0 & 1u) == 0,
+         corr3 = (d0 & 1u) == 0;
+    a0 |= 1u; b0 |= 1u; c0 |= 1u; d0 |= 1u;
+
+    // ---- Q table: odd multiples on E' (shared Z; ecmult_odd_multiples_table restated) ----
+    fe sigma;  // E' = E scaled by sigma: a point (x, y) of E is (x sigma^2, y sigma^3) on E'
+    {
+        gej q1, d;
+        q1.x = qx; q1.y = qy; q1.z = fe_one();
+        gej_double(d, q1);                       // D = 2Q (Jacobian on E)
+        fe zd2, zd3, one = fe_one();
+        fe_sqr(zd2, d.z);
+        fe_mul(zd3, zd2, d.z);
+        gej cur;                                 // on E_{Zd}, D is affine (d.x, d.y)
+        fe_mul(cur.x, qx, zd2);
+        fe_mul(cur.y, qy, zd3);
+        cur.z = one;
+        qt.put(0, 0, cur.x);
+        qt.put(0, 2, cur.y);
+        for (int i = 1; i < QTAB; i++) {         // T_i = T_{i-1} + D, Z_i = Z_{i-1} * H_i
+            bool inf_unused;
+            gej nxt;
+            fe h;
+            gej_add_zinv(nxt, inf_unused, cur, d.x, d.y, one, false, &h);
+            cur = nxt;
+            qt.put(i, 0, cur.x);
+            qt.put(i, 2, cur.y);
+            qt.put(i, 1, h);                     // slot 1 holds H_i until the rescale pass
+        }
+        // rescale to the common Z_last: f_i = prod_{j>i} H_j
+        fe f = one, f2, f3, beta;
+        {
+            const u32 bl[8] = BCC_BETA_LIMBS;
+            fe_set(beta, bl);
+        }
+        for (int i = QTAB - 1; i >= 0; i--) {
+            fe ex, ey, h;
+            qt.get(i, 0, ex);
+            qt.get(i, 2, ey);
+            if (i > 0) qt.get(i, 1, h);
+            fe_sqr(f2, f);
+            fe_mul(f3, f2, f);
+            fe_mul(ex, ex, f2);
+            fe_mul(ey, ey, f3);
+            fe bx;
+            fe_mul(bx, ex, beta);
+            qt.put(i, 0, ex);
+            qt.put(i, 1, bx);
+            qt.put(i, 2, ey);
+            if (i > 0) fe_mul(f, f, h);
+        }
+        fe_mul(sigma, d.z, cur.z);               // total scale Zd * Z_last
+    }
+
+    // ---- Strauss loop over bit positions TOPQ..0 (shared doublings) ----
+    gej acc;
+    bool inf = false;
+    {
+        bool ng;
+        u32 idx = digit_index(a0, a1, a2, a3, TOPQ, WQ, TOPQ, ng);
+        qt.get((int)idx, 0, acc.x);
+        qt.get((int)idx, 2, acc.y);
+        if (neg0) fe_neg(acc.y, acc.y);
+        acc.z = fe_one();
+    }
+    for (int pos = TOPQ; pos >= 0; pos--) {
+        if (pos != TOPQ && !inf) {
+            gej t;
+            gej_double(t, acc);
+            acc = t;
+        }
+        for (int slot = 0; slot < 4; slot++) {
+            bool isg = slot >= 2;
+            bool active = isg ? ((pos % WG) == 0 && pos <= TOPG) : ((pos % WQ) == 0);
+            if (slot == 0 && pos == TOPQ) active = false;  // initial value
+            if (!active) continue;
+            u32 l0 = slot == 0 ? a0 : slot == 1 ? b0 : slot == 2 ? c0 : d0;
+            u32 l1 = slot == 0 ? a1 : slot == 1 ? b1 : slot == 2 ? c1 : d1;
+            u32 l2 = slot == 0 ? a2 : slot == 1 ? b2 : slot == 2 ? c2 : d2;
+            u32 l3 = slot == 0 ? a3 : slot == 1 ? b3 : slot == 2 ? c3 : d3;
+            bool dneg;
+            u32 idx = digit_index(l0, l1, l2, l3, pos, isg ? WG : WQ, isg ? TOPG : TOPQ, dneg);
+            fe px, py;
+            if (isg) {
+                gt.get(slot - 2, (int)idx, px, py);
+            } else {
+                qt.get((int)idx, slot == 0 ? 0 : 1, px);
+                qt.get((int)idx, 2, py);
+            }
+            bool sneg = dneg ^ (slot == 0 ? neg0 : slot == 1 ? neg1 : false);
+            if (sneg) fe_neg(py, py);
+            acc_add(acc, inf, px, py, sigma, isg);
+        }
+    }
+    // ---- corrections for the scalars that were made odd: acc -= base point ----
+    for (int slot = 0; slot < 4; slot++) {
+        bool active = slot == 0 ? corr0 : slot == 1 ? corr1 : slot == 2 ? corr2 : corr3;
+        if (!active) continue;
+        bool isg = slot >= 2;
+        fe px, py;
+        if (isg) {
+            gt.get(slot - 2, 0, px, py);
+        } else {
+            qt.get(0, slot == 0 ? 0 : 1, px);
+            qt.get(0, 2, py);
+        }
+        bool sneg = !(slot == 0 ? neg0 : slot == 1 ? neg1 : false);
+        if (sneg) fe_neg(py, py);
+        acc_add(acc, inf, px, py, sigma, isg);
+    }
+    if (inf) return 0;                           // R = infinity (ecdsa_impl.h:225-227)
+    // ---- x-coordinate test (ecdsa_impl.h:241-273): back on E, Z_E = Z * sigma ----
+    fe ze, z2, lhs, xr;
+    fe_mul(ze, acc.z, sigma);
+    fe_sqr(z2, ze);
+    for (int i = 0; i < 8; i++) xr.v[i] = r_in.v[i];  // r < n < p
+    fe_mul(lhs, xr, z2);
+    if (fe_equal(lhs, acc.x)) return 1;
+    {
+        const u32 PMN[8] = BCC_PMN_LIMBS;
+        if (!u256_lt(r_in.v, PMN)) return 0;     // xr + n >= p
+        u32 xn[8];
+        u256_add(xn, r_in.v, N);
+        for (int i = 0; i < 8; i++) xr.v[i] = xn[i];
+        fe_mul(lhs, xr, z2);
+        if (fe_equal(lhs, acc.x)) return 1;
+    }
+    return 0;
+}
+
+// Affine G tables: xy[(tab*GTAB + i)*2 + {0,1}] = (2i+1) * 2^(128 tab) * G.  Host-side build
+// (once per process; exact group arithmetic, then one inversion per point).
+inline void build_g_tables(fe* xy) {
+    fe gx, gy;
+    {
+        const u32 X[8] = BCC_GX_LIMBS, Y[8] = BCC_GY_LIMBS;
+        fe_set(gx, X);
+        fe_set(gy, Y);
+    }
+    gej base;
+    base.x = gx; base.y = gy; base.z = fe_one();
+    for (int tab = 0; tab < 2; tab++) {
+        if (tab == 1) {  // base = 2^128 G
+            for (int i = 0; i < 128; i++) {
+                gej t;
+                gej_double(t, base);
+                base = t;
+            }
+        }
+        gej b2;
+        gej_double(b2, base);
+        // b2 to affine for mixed adds
+        fe zi, zi2, zi3, b2x, b2y;
+        fe_inv(zi, b2.z);
+        fe_sqr(zi2, zi);
+        fe_mul(zi3, zi2, zi);
+        fe_mul(b2x, b2.x, zi2);
+        fe_mul(b2y, b2.y, zi3);
+        gej cur = base;
+        for (int i = 0; i < GTAB; i++) {
+            if (i > 0) {
+                gej nxt;
+                bool inf_unused;
+                fe one = fe_one();
+                gej_add_zinv(nxt, inf_unused, cur, b2x, b2y, one, false);
+                cur = nxt;
+            }
+            fe x, y;
+            fe_inv(zi, cur.z);
+            fe_sqr(zi2, zi);
+            fe_mul(zi3, zi2, zi);
+            fe_mul(x, cur.x, zi2);
+            fe_mul(y, cur.y, zi3);
+            fe_normalize(x);
+            fe_normalize(y);
+            xy[(tab * GTAB + i) * 2 + 0] = x;
+            xy[(tab * GTAB + i) * 2 + 1] = y;
+        }
+    }
+}
+
+}  // namespace bcc

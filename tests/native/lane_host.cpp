@@ -1,0 +1,97 @@
+// tests/native/lane_host.cpp — TEST ONLY. Runs the product's per-lane ECDSA code
+// (rust-bitcoinconsensus_amd/csrc/ecdsa_lane.h) on the CPU, so the exact arithmetic the HIP kernel
+// executes can be checked against the oracle without a GPU. Never linked into the product.
+#include "../../rust-bitcoinconsensus_amd/csrc/ecdsa_lane.h"
+
+#include <cstring>
+#include <vector>
+
+using namespace bcc;
+
+static std::vector<fe>& gtab() {
+    static std::vector<fe> t;
+    if (t.empty()) {
+        t.resize(2 * GTAB * 2);
+        build_g_tables(t.data());
+    }
+    return t;
+}
+
+extern "C" int lane_verify(unsigned tag, const unsigned char* x32, const unsigned char* y32,
+                           const unsigned char* r32, const unsigned char* s32,
+                           const unsigned char* m32) {
+    fe px, py;
+    sc r, s, m;
+    fe_from_be_bytes(px, x32);
+    fe_from_be_bytes(py, y32);
+    fe t;
+    fe_from_be_bytes(t, r32);
+    memcpy(r.v, t.v, 32);
+    fe_from_be_bytes(t, s32);
+    memcpy(s.v, t.v, 32);
+    fe_from_be_bytes(t, m32);
+    memcpy(m.v, t.v, 32);
+    QTableArray qt;
+    GTableArray gt{gtab().data()};
+    return ecdsa_verify_lane(tag, px, py, r, s, m, qt, gt);
+}
+
+// field/scalar primitives for unit tests
+extern "C" void lane_fe_mul(const unsigned char* a32, const unsigned char* b32, unsigned char* o32) {
+    fe a, b, r;
+    fe_from_be_bytes(a, a32);
+    fe_from_be_bytes(b, b32);
+    fe_mul(r, a, b);
+    fe_normalize(r);
+    fe_to_be_bytes(o32, r);
+}
+extern "C" void lane_fe_sqr(const unsigned char* a32, unsigned char* o32) {
+    fe a, r;
+    fe_from_be_bytes(a, a32);
+    fe_sqr(r, a);
+    fe_normalize(r);
+    fe_to_be_bytes(o32, r);
+}
+extern "C" void lane_fe_addsub(const unsigned char* a32, const unsigned char* b32, unsigned char* sum,
+                               unsigned char* diff) {
+    fe a, b, r;
+    fe_from_be_bytes(a, a32);
+    fe_from_be_bytes(b, b32);
+    fe_add(r, a, b);
+    fe_normalize(r);
+    fe_to_be_bytes(sum, r);
+    fe_sub(r, a, b);
+    fe_normalize(r);
+    fe_to_be_bytes(diff, r);
+}
+extern "C" void lane_sc_mul(const unsigned char* a32, const unsigned char* b32, unsigned char* o32) {
+    fe t;
+    sc a, b, r;
+    fe_from_be_bytes(t, a32);
+    memcpy(a.v, t.v, 32);
+    fe_from_be_bytes(t, b32);
+    memcpy(b.v, t.v, 32);
+    sc_mul(r, a, b);
+    memcpy(t.v, r.v, 32);
+    fe_to_be_bytes(o32, t);
+}
+extern "C" void lane_sc_inv(const unsigned char* a32, unsigned char* o32) {
+    fe t;
+    sc a, r;
+    fe_from_be_bytes(t, a32);
+    memcpy(a.v, t.v, 32);
+    sc_inv(r, a);
+    memcpy(t.v, r.v, 32);
+    fe_to_be_bytes(o32, t);
+}
+extern "C" void lane_split(const unsigned char* k32, unsigned char* k1, unsigned char* k2) {
+    fe t;
+    sc k, a, b;
+    fe_from_be_bytes(t, k32);
+    memcpy(k.v, t.v, 32);
+    sc_split_lambda(a, b, k);
+    memcpy(t.v, a.v, 32);
+    fe_to_be_bytes(k1, t);
+    memcpy(t.v, b.v, 32);
+    fe_to_be_bytes(k2, t);
+}

@@ -1,0 +1,172 @@
+"""ctypes access to the CHECKERS (test infrastructure only).
+
+* ``Oracle``    — the plain-C restatement, oracle/_build/libbcc_oracle.so (oracle/bcc_oracle.c)
+* ``Reference`` — the reference itself, oracle/_ref/libref_consensus.so, compiled from
+                  /root/reference by oracle/Makefile (present here and shipped to the GPU box).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import this module.
+"""
+import ctypes
+import os
+import subprocess
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_SO = os.path.join(ROOT, "oracle", "_build", "libbcc_oracle.so")
+REF_SO = os.path.join(ROOT, "oracle", "_ref", "libref_consensus.so")
+
+c_u8p = ctypes.c_char_p
+c_sz = ctypes.c_size_t
+
+
+def _build_oracle():
+    if not os.path.exists(ORACLE_SO):
+        subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle")])
+
+
+class Oracle:
+    """CPU restatement of the hot path (oracle/bcc_oracle.h)."""
+
+    def __init__(self):
+        _build_oracle()
+        L = ctypes.CDLL(ORACLE_SO)
+        self.L = L
+        L.bcco_sha256.argtypes = [c_u8p, c_sz, c_u8p]
+        L.bcco_sha256d.argtypes = [c_u8p, c_sz, c_u8p]
+        L.bcco_der_parse_lax.argtypes = [c_u8p, c_sz, c_u8p, c_u8p]
+        L.bcco_pubkey_parse.argtypes = [c_u8p, c_sz, c_u8p, c_u8p]
+        L.bcco_ecdsa_verify_raw.argtypes = [c_u8p] * 5
+        L.bcco_pubkey_verify.argtypes = [c_u8p, c_sz, c_u8p, c_u8p, c_sz]
+        L.bcco_schnorr_verify.argtypes = [c_u8p, c_u8p, c_u8p]
+        L.bcco_ecmult_gen.argtypes = [c_u8p, c_u8p, c_u8p]
+        L.bcco_sighash.argtypes = [c_u8p, c_sz, ctypes.c_uint, c_u8p, c_sz, ctypes.c_int,
+                                   ctypes.c_int64, ctypes.c_int, c_u8p]
+
+    def sha256(self, b):
+        o = ctypes.create_string_buffer(32)
+        self.L.bcco_sha256(b, len(b), o)
+        return o.raw
+
+    def sha256d(self, b):
+        o = ctypes.create_string_buffer(32)
+        self.L.bcco_sha256d(b, len(b), o)
+        return o.raw
+
+    def der_parse_lax(self, sig):
+        r = ctypes.create_string_buffer(32)
+        s = ctypes.create_string_buffer(32)
+        ok = self.L.bcco_der_parse_lax(sig, len(sig), r, s)
+        return ok, r.raw, s.raw
+
+    def pubkey_parse(self, pub):
+        x = ctypes.create_string_buffer(32)
+        y = ctypes.create_string_buffer(32)
+        ok = self.L.bcco_pubkey_parse(pub, len(pub), x, y)
+        return (x.raw, y.raw) if ok else None
+
+    def ecdsa_verify_raw(self, qx, qy, r, s, msg):
+        return self.L.bcco_ecdsa_verify_raw(qx, qy, r, s, msg)
+
+    def pubkey_verify(self, pub, hash32, sig):
+        return self.L.bcco_pubkey_verify(pub, len(pub), hash32, sig, len(sig))
+
+    def schnorr_verify(self, sig64, msg32, xonly32):
+        return self.L.bcco_schnorr_verify(sig64, msg32, xonly32)
+
+    def ecmult_gen(self, k32):
+        x = ctypes.create_string_buffer(32)
+        y = ctypes.create_string_buffer(32)
+        ok = self.L.bcco_ecmult_gen(k32, x, y)
+        return (x.raw, y.raw) if ok else None
+
+    def sighash(self, tx, nin, script, hashtype, amount, sigversion):
+        o = ctypes.create_string_buffer(32)
+        ok = self.L.bcco_sighash(tx, len(tx), nin, script, len(script), hashtype, amount,
+                                 sigversion, o)
+        return o.raw if ok else None
+
+
+class Reference:
+    """The reference (Bitcoin Core v0.21 libbitcoinconsensus + libsecp256k1), see ref_shim.cpp."""
+
+    def __init__(self):
+        if not os.path.exists(REF_SO):
+            raise FileNotFoundError(REF_SO)
+        L = ctypes.CDLL(REF_SO)
+        self.L = L
+        L.ref_verify_script_with_amount.argtypes = [c_u8p, ctypes.c_uint, ctypes.c_int64, c_u8p,
+                                                    ctypes.c_uint, ctypes.c_uint, ctypes.c_uint,
+                                                    ctypes.POINTER(ctypes.c_int)]
+        L.ref_verify_script.argtypes = [c_u8p, ctypes.c_uint, c_u8p, ctypes.c_uint, ctypes.c_uint,
+                                        ctypes.c_uint, ctypes.POINTER(ctypes.c_int)]
+        L.ref_pubkey_verify.argtypes = [c_u8p, c_sz, c_u8p, c_u8p, c_sz]
+        L.ref_schnorr_verify.argtypes = [c_u8p, c_u8p, c_u8p]
+        L.ref_pubkey_create.argtypes = [c_u8p, ctypes.c_int, c_u8p, ctypes.POINTER(c_sz)]
+        L.ref_sign.argtypes = [c_u8p, c_u8p, c_u8p, ctypes.POINTER(c_sz)]
+        L.ref_schnorr_sign.argtypes = [c_u8p, c_u8p, c_u8p, c_u8p, c_u8p]
+        i32p = ctypes.POINTER(ctypes.c_int)
+        L.ref_capture_script.argtypes = [c_u8p, ctypes.c_uint, ctypes.c_int64, c_u8p, ctypes.c_uint,
+                                         ctypes.c_uint, ctypes.c_uint, ctypes.c_int, c_u8p, i32p,
+                                         c_u8p, i32p, c_u8p, i32p, i32p, i32p]
+        L.ref_bench_verify_script.restype = ctypes.c_double
+        L.ref_bench_pubkey_verify.restype = ctypes.c_double
+
+    def verify_script_with_amount(self, spk, amount, tx, nin, flags):
+        e = ctypes.c_int(0)
+        r = self.L.ref_verify_script_with_amount(spk, len(spk), amount, tx, len(tx), nin, flags,
+                                                 ctypes.byref(e))
+        return r, e.value
+
+    def verify_script(self, spk, tx, nin, flags):
+        e = ctypes.c_int(0)
+        r = self.L.ref_verify_script(spk, len(spk), tx, len(tx), nin, flags, ctypes.byref(e))
+        return r, e.value
+
+    def pubkey_verify(self, pub, hash32, sig):
+        return self.L.ref_pubkey_verify(pub, len(pub), hash32, sig, len(sig))
+
+    def schnorr_verify(self, sig64, msg32, xonly32):
+        return self.L.ref_schnorr_verify(sig64, msg32, xonly32)
+
+    def pubkey_create(self, sk, compressed=True):
+        out = ctypes.create_string_buffer(65)
+        n = c_sz(65)
+        if not self.L.ref_pubkey_create(sk, 1 if compressed else 0, out, ctypes.byref(n)):
+            return None
+        return out.raw[: n.value]
+
+    def sign(self, sk, msg32):
+        out = ctypes.create_string_buffer(72)
+        n = c_sz(72)
+        if not self.L.ref_sign(sk, msg32, out, ctypes.byref(n)):
+            return None
+        return out.raw[: n.value]
+
+    def schnorr_sign(self, sk, msg32, aux32):
+        sig = ctypes.create_string_buffer(64)
+        xo = ctypes.create_string_buffer(32)
+        if not self.L.ref_schnorr_sign(sk, msg32, aux32, sig, xo):
+            return None
+        return sig.raw, xo.raw
+
+    def capture_script(self, spk, amount, tx, nin, flags, cap=64):
+        pub = ctypes.create_string_buffer(65 * cap)
+        sig = ctypes.create_string_buffer(80 * cap)
+        h = ctypes.create_string_buffer(32 * cap)
+        publen = (ctypes.c_int * cap)()
+        siglen = (ctypes.c_int * cap)()
+        verdict = (ctypes.c_int * cap)()
+        ncap = ctypes.c_int(0)
+        serr = ctypes.c_int(0)
+        r = self.L.ref_capture_script(spk, len(spk), amount, tx, len(tx), nin, flags, cap, pub,
+                                      publen, sig, siglen, h, verdict, ctypes.byref(ncap),
+                                      ctypes.byref(serr))
+        recs = []
+        for i in range(min(cap, ncap.value)):
+            recs.append(dict(pub=pub.raw[65 * i: 65 * i + publen[i]],
+                             sig=sig.raw[80 * i: 80 * i + min(80, siglen[i])],
+                             sighash=h.raw[32 * i: 32 * i + 32], verdict=verdict[i]))
+        return r, serr.value, recs
+
+
+def reference_available():
+    return os.path.exists(REF_SO)

@@ -1,0 +1,50 @@
+"""CPU: pin the oracle (plain-C restatement) against the reference's fixtures and the reference."""
+import random
+
+import pytest
+
+from fixtures import ecdsa_tuples, load_json
+from oracle_ctypes import Oracle, Reference, reference_available
+
+O = Oracle()
+N = 0xFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFEBAAEDCE6AF48A03BBFD25E8CD0364141
+
+
+def test_oracle_tuples_match_reference_verdicts():
+    bad = [(t["cls"], i) for i, t in enumerate(ecdsa_tuples())
+           if O.pubkey_verify(t["pub"], t["hash"], t["sig"]) != t["verdict"]]
+    assert not bad, bad[:10]
+
+
+def test_oracle_legacy_sighash_goldens():
+    rows = load_json("sighash_legacy.json")
+    assert len(rows) == 500
+    for r in rows:
+        h = O.sighash(bytes.fromhex(r["tx"]), r["nin"], bytes.fromhex(r["script"]), r["hashtype"], 0, 0)
+        assert h is not None and h.hex() == r["sighash_raw"], r
+
+
+def test_oracle_bip340_vectors():
+    for v in load_json("bip340_vectors.json"):
+        got = O.schnorr_verify(bytes.fromhex(v["sig"]), bytes.fromhex(v["msg"]), bytes.fromhex(v["pubkey"]))
+        assert got == int(v["expected"]) == v["ref_verdict"], v
+
+
+def test_oracle_sha256_known_answers():
+    assert O.sha256(b"abc").hex() == "ba7816bf8f01cfea414140de5dae2223b00361a396177a9cb410ff61f20015ad"
+    assert O.sha256(b"").hex() == "e3b0c44298fc1c149afbf4c8996fb92427ae41e4649b934ca495991b7852b855"
+    assert O.sha256(b"a" * 1000).hex() == "41edece42d63e8d9bf515a9ba6932e1c20cbc9f5a5d134645adb5db1b9737ea3"
+
+
+@pytest.mark.skipif(not reference_available(), reason="oracle/_ref not built")
+def test_oracle_vs_reference_random():
+    R = Reference()
+    rng = random.Random(7)
+    for i in range(200):
+        sk = rng.randrange(1, N).to_bytes(32, "big")
+        msg = rng.randbytes(32)
+        pub = R.pubkey_create(sk, i % 2 == 0)
+        sig = R.sign(sk, msg)
+        if i % 3 == 1:
+            msg = bytes([msg[0] ^ 0x80]) + msg[1:]
+        assert O.pubkey_verify(pub, msg, sig) == R.pubkey_verify(pub, msg, sig)
