@@ -1,0 +1,81 @@
+/* bcc_amd.h — engine-level C ABI of librbc_amd.so below the drop-in interface.
+ *
+ * These are the entry points the reference's FFI would bind for the signature hot path once the
+ * interpreter defers its checks ("New ABI to add"), plus the device-pointer and
+ * workload entry points bench.py drives.  No torch / HIP types appear in any signature: device
+ * buffers and streams are passed as plain pointers.
+ */
+#ifndef BCC_AMD_H
+#define BCC_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- tuple level: the deferred CHECKSIG queue flushed to the GPU ---------------------------
+ * Replaces the per-signature call CPubKey::Verify -> secp256k1_ecdsa_verify
+ * (depend/bitcoin/src/pubkey.cpp:191-207, secp256k1/src/secp256k1.c:423-438).
+ * pub65[i] = header byte || x || y (y ignored for 02/03; header 0 marks a key the caller's
+ * CPubKey length filter already rejected); msg32 = raw sighash bytes; r32/s32 = big-endian
+ * scalars after lax-DER parsing (both zero on overflow).  verdict[i] = 1 iff valid. */
+int mi_ecdsa_verify_tuples(const uint8_t* pub65, const uint8_t* msg32, const uint8_t* r32,
+                           const uint8_t* s32, uint8_t* verdict, size_t n, int device);
+
+/* Same with all buffers device-resident (separate tag / x / y / r / s / m rows), launched on
+ * `stream` (a hipStream_t or NULL).  Asynchronous. */
+int mi_ecdsa_verify_device(const uint8_t* d_tag, const uint8_t* d_x, const uint8_t* d_y,
+                           const uint8_t* d_r, const uint8_t* d_s, const uint8_t* d_m,
+                           uint8_t* d_verdict, size_t n, void* stream);
+
+/* ---- engine configuration / statistics ---------------------------------------------------- */
+/* Device used by the bitcoinconsensus_* entry points of the calling process (default 0, or the
+ * BCC_DEVICE environment variable). */
+int bcc_set_device(int device);
+
+typedef struct bcc_batch_stats {
+    size_t items, tuples, rounds, preimages, aux_messages, host_rejected;
+    double host_seconds, gpu_seconds;
+} bcc_batch_stats;
+/* Statistics of the calling thread's last bitcoinconsensus_verify_batch / verify call. */
+void bcc_last_batch_stats(bcc_batch_stats* out);
+
+/* ---- synthetic workloads (bench.py / tests): built and staged on the device ---------------- */
+typedef struct bcc_workload bcc_workload;
+
+/* C2: n synthetic P2WPKH spends (1-in/1-out v2 txs, BIP143 SIGHASH_ALL, low-S DER), keys,
+ * nonces and amounts derived from `seed`.  Keys and signatures are produced by
+ * the engine's own GPU kernels; txs / sighash jobs are staged in HBM. */
+bcc_workload* bcc_workload_p2wpkh(size_t n, uint64_t seed, int device);
+void bcc_workload_free(bcc_workload* w);
+size_t bcc_workload_size(const bcc_workload* w);
+/* launch the full hot path (sighash kernels + ECDSA kernel) on the staged inputs */
+int bcc_workload_run(bcc_workload* w, void* stream);
+int bcc_workload_run_sighash(bcc_workload* w, void* stream);
+int bcc_workload_run_ecdsa(bcc_workload* w, void* stream);
+/* copy back verdicts (n bytes) */
+int bcc_workload_verdicts(bcc_workload* w, uint8_t* out);
+/* algorithmic work of one run: bytes hashed + written by the sighash stage, tuples verified */
+void bcc_workload_shape(const bcc_workload* w, size_t* tuples, size_t* sighash_blocks,
+                        size_t* aux_blocks, size_t* preimages, size_t* aux_messages);
+/* export item i as (spk, amount, tx) for CPU-baseline / parity checks: returns tx length and
+ * copies up to cap bytes; *spk_len <= 64 */
+size_t bcc_workload_item(const bcc_workload* w, size_t i, uint8_t* spk, size_t* spk_len,
+                         int64_t* amount, uint8_t* tx, size_t cap);
+
+/* ---- generator kernels (synthetic inputs; not on the verification path) -------------------- */
+int mi_gen_pubkeys(const uint8_t* d32, size_t n, uint8_t* x32, uint8_t* y32, uint8_t* ok,
+                   int device);
+int mi_gen_sign(const uint8_t* d32, const uint8_t* m32, const uint8_t* k32, size_t n,
+                uint8_t* r32, uint8_t* s32, uint8_t* ok, int device);
+
+/* ---- integer-ALU microbenchmark (the roofline peak) ---------------------------------------- */
+int mi_microbench(int op, int iters, double* rate);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

@@ -1,0 +1,94 @@
+/* bitcoinconsensus.h — drop-in C ABI of the MI355X engine (librbc_amd.so).
+ *
+ * Same symbols, signatures, return convention and error ordering as libbitcoinconsensus v0.21,
+ * which rust-bitcoinconsensus binds in src/lib.rs:145-161:
+ *
+ *   bitcoinconsensus_verify_script_with_amount  replaces depend/bitcoin/src/script/bitcoinconsensus.h:200-202
+ *                                               (bitcoinconsensus.cpp:104-110), bound at src/lib.rs:151-160
+ *   bitcoinconsensus_verify_script              replaces bitcoinconsensus.h:196-198 (bitcoinconsensus.cpp:113-123)
+ *   bitcoinconsensus_version                    replaces bitcoinconsensus.h:204 (bitcoinconsensus.cpp:125-129),
+ *                                               bound at src/lib.rs:148
+ *
+ * plus the north-star extension
+ *
+ *   bitcoinconsensus_verify_batch               N independent (script, amount, tx, nIn) checks; per-item
+ *                                               results equal N calls of ..._with_amount
+ *
+ * Return convention: 1 = valid, 0 = invalid or error; *err is written only when err != NULL.
+ * Check order: flags -> deserialize -> nIn -> size -> (ERR_OK) -> script.
+ * Every signature check runs on the GPU (HIP, gfx950); there is no CPU verification fallback.
+ * Thread safety: reentrant; concurrent callers share the device under an internal lock.
+ */
+#ifndef BCC_AMD_BITCOINCONSENSUS_H
+#define BCC_AMD_BITCOINCONSENSUS_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BITCOINCONSENSUS_API_VER 1
+
+typedef enum bitcoinconsensus_error_t {
+    bitcoinconsensus_ERR_OK = 0,
+    bitcoinconsensus_ERR_TX_INDEX,
+    bitcoinconsensus_ERR_TX_SIZE_MISMATCH,
+    bitcoinconsensus_ERR_TX_DESERIALIZE,
+    bitcoinconsensus_ERR_AMOUNT_REQUIRED,
+    bitcoinconsensus_ERR_INVALID_FLAGS,
+} bitcoinconsensus_error;
+
+/* Script verification flags accepted by this interface (the libconsensus subset). */
+enum {
+    bitcoinconsensus_SCRIPT_FLAGS_VERIFY_NONE = 0,
+    bitcoinconsensus_SCRIPT_FLAGS_VERIFY_P2SH = (1U << 0),
+    bitcoinconsensus_SCRIPT_FLAGS_VERIFY_DERSIG = (1U << 2),
+    bitcoinconsensus_SCRIPT_FLAGS_VERIFY_NULLDUMMY = (1U << 4),
+    bitcoinconsensus_SCRIPT_FLAGS_VERIFY_CHECKLOCKTIMEVERIFY = (1U << 9),
+    bitcoinconsensus_SCRIPT_FLAGS_VERIFY_CHECKSEQUENCEVERIFY = (1U << 10),
+    bitcoinconsensus_SCRIPT_FLAGS_VERIFY_WITNESS = (1U << 11),
+    bitcoinconsensus_SCRIPT_FLAGS_VERIFY_ALL =
+        bitcoinconsensus_SCRIPT_FLAGS_VERIFY_P2SH | bitcoinconsensus_SCRIPT_FLAGS_VERIFY_DERSIG |
+        bitcoinconsensus_SCRIPT_FLAGS_VERIFY_NULLDUMMY |
+        bitcoinconsensus_SCRIPT_FLAGS_VERIFY_CHECKLOCKTIMEVERIFY |
+        bitcoinconsensus_SCRIPT_FLAGS_VERIFY_CHECKSEQUENCEVERIFY |
+        bitcoinconsensus_SCRIPT_FLAGS_VERIFY_WITNESS,
+};
+
+int bitcoinconsensus_verify_script(const unsigned char* scriptPubKey, unsigned int scriptPubKeyLen,
+                                   const unsigned char* txTo, unsigned int txToLen,
+                                   unsigned int nIn, unsigned int flags, bitcoinconsensus_error* err);
+
+int bitcoinconsensus_verify_script_with_amount(const unsigned char* scriptPubKey,
+                                               unsigned int scriptPubKeyLen, int64_t amount,
+                                               const unsigned char* txTo, unsigned int txToLen,
+                                               unsigned int nIn, unsigned int flags,
+                                               bitcoinconsensus_error* err);
+
+unsigned int bitcoinconsensus_version(void);
+
+/* One spend to verify.  Buffers are borrowed for the duration of the call only; items may share
+ * the same txTo buffer (it is then deserialized once). */
+typedef struct bcc_batch_item {
+    const unsigned char* script_pubkey;
+    unsigned int script_pubkey_len;
+    int64_t amount;
+    const unsigned char* tx_to;
+    unsigned int tx_to_len;
+    unsigned int n_in;
+} bcc_batch_item;
+
+/* Verifies n items with `flags`.  ret_out[i] / err_out[i] (err_out may be NULL) receive exactly
+ * what bitcoinconsensus_verify_script_with_amount would return / write for item i.
+ * Returns the number of valid items, or -1 if the device pipeline failed (then ret_out is 0 and
+ * err_out is bitcoinconsensus_ERR_TX_DESERIALIZE for the unfinished items). */
+long bitcoinconsensus_verify_batch(const bcc_batch_item* items, size_t n, unsigned int flags,
+                                   int* ret_out, bitcoinconsensus_error* err_out);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

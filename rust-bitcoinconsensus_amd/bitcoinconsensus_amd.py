@@ -62,8 +62,175 @@ def lib():
         L.mi_ecdsa_verify_tuples.argtypes = [u8p, u8p, u8p, u8p, u8p, sz, ctypes.c_int]
         L.mi_ecdsa_verify_device.argtypes = [vp] * 7 + [sz, vp]
         L.mi_microbench.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_double)]
+        _bind_consensus(L)
         _lib = L
     return _lib
+
+
+class BatchItem(ctypes.Structure):
+    """struct bcc_batch_item (include/bitcoinconsensus.h)."""
+    _fields_ = [("script_pubkey", ctypes.c_void_p), ("script_pubkey_len", ctypes.c_uint),
+                ("amount", ctypes.c_int64), ("tx_to", ctypes.c_void_p),
+                ("tx_to_len", ctypes.c_uint), ("n_in", ctypes.c_uint)]
+
+
+class BatchStats(ctypes.Structure):
+    _fields_ = [("items", ctypes.c_size_t), ("tuples", ctypes.c_size_t),
+                ("rounds", ctypes.c_size_t), ("preimages", ctypes.c_size_t),
+                ("aux_messages", ctypes.c_size_t), ("host_rejected", ctypes.c_size_t),
+                ("host_seconds", ctypes.c_double), ("gpu_seconds", ctypes.c_double)]
+
+
+def _bind_consensus(L):
+    u8p, ui = ctypes.c_char_p, ctypes.c_uint
+    ip = ctypes.POINTER(ctypes.c_int)
+    L.bitcoinconsensus_verify_script_with_amount.argtypes = [u8p, ui, ctypes.c_int64, u8p, ui, ui,
+                                                             ui, ip]
+    L.bitcoinconsensus_verify_script.argtypes = [u8p, ui, u8p, ui, ui, ui, ip]
+    L.bitcoinconsensus_version.restype = ui
+    L.bitcoinconsensus_verify_batch.argtypes = [ctypes.POINTER(BatchItem), ctypes.c_size_t, ui,
+                                                ip, ip]
+    L.bitcoinconsensus_verify_batch.restype = ctypes.c_long
+    L.bcc_set_device.argtypes = [ctypes.c_int]
+    L.bcc_last_batch_stats.argtypes = [ctypes.POINTER(BatchStats)]
+    vp, sz = ctypes.c_void_p, ctypes.c_size_t
+    L.bcc_workload_p2wpkh.argtypes = [sz, ctypes.c_uint64, ctypes.c_int]
+    L.bcc_workload_p2wpkh.restype = vp
+    L.bcc_workload_free.argtypes = [vp]
+    L.bcc_workload_size.argtypes = [vp]
+    L.bcc_workload_size.restype = sz
+    for f in (L.bcc_workload_run, L.bcc_workload_run_sighash, L.bcc_workload_run_ecdsa):
+        f.argtypes = [vp, vp]
+    L.bcc_workload_verdicts.argtypes = [vp, u8p]
+    szp = ctypes.POINTER(sz)
+    L.bcc_workload_shape.argtypes = [vp, szp, szp, szp, szp, szp]
+    L.bcc_workload_item.argtypes = [vp, sz, u8p, szp, ctypes.POINTER(ctypes.c_int64), u8p, sz]
+    L.bcc_workload_item.restype = sz
+    L.mi_gen_pubkeys.argtypes = [u8p, sz, u8p, u8p, u8p, ctypes.c_int]
+    L.mi_gen_sign.argtypes = [u8p, u8p, u8p, sz, u8p, u8p, u8p, ctypes.c_int]
+
+
+class Workload:
+    """A synthetic workload staged in HBM (include/bcc_amd.h, bcc_workload_*)."""
+
+    def __init__(self, n, seed=0x5EED0001, device=0, kind="p2wpkh"):
+        assert kind == "p2wpkh"
+        self.h = lib().bcc_workload_p2wpkh(n, seed, device)
+        if not self.h:
+            raise RuntimeError("bcc_workload_p2wpkh failed")
+        self.n = n
+
+    def run(self, stream=None):
+        rc = lib().bcc_workload_run(self.h, stream)
+        if rc:
+            raise RuntimeError(f"bcc_workload_run: {rc}")
+
+    def run_sighash(self, stream=None):
+        rc = lib().bcc_workload_run_sighash(self.h, stream)
+        if rc:
+            raise RuntimeError(f"bcc_workload_run_sighash: {rc}")
+
+    def run_ecdsa(self, stream=None):
+        rc = lib().bcc_workload_run_ecdsa(self.h, stream)
+        if rc:
+            raise RuntimeError(f"bcc_workload_run_ecdsa: {rc}")
+
+    def verdicts(self):
+        out = ctypes.create_string_buffer(max(1, self.n))
+        rc = lib().bcc_workload_verdicts(self.h, out)
+        if rc:
+            raise RuntimeError(f"bcc_workload_verdicts: {rc}")
+        return out.raw[: self.shape()["tuples"]]
+
+    def shape(self):
+        v = [ctypes.c_size_t() for _ in range(5)]
+        lib().bcc_workload_shape(self.h, *[ctypes.byref(x) for x in v])
+        return dict(zip(("tuples", "sighash_blocks", "aux_blocks", "preimages", "aux_messages"),
+                        (x.value for x in v)))
+
+    def item(self, i):
+        spk = ctypes.create_string_buffer(64)
+        sl = ctypes.c_size_t(0)
+        amt = ctypes.c_int64(0)
+        tx = ctypes.create_string_buffer(512)
+        n = lib().bcc_workload_item(self.h, i, spk, ctypes.byref(sl), ctypes.byref(amt), tx, 512)
+        return spk.raw[: sl.value], amt.value, tx.raw[:n]
+
+    def free(self):
+        if self.h:
+            lib().bcc_workload_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+def version():
+    """Returns libbitcoinconsensus API version (src/lib.rs:68)."""
+    return lib().bitcoinconsensus_version()
+
+
+def verify_script_with_amount(spk, amount, tx, n_in, flags):
+    """Raw C-ABI call: returns (ret, err) exactly as bitcoinconsensus_verify_script_with_amount."""
+    e = ctypes.c_int(0)
+    r = lib().bitcoinconsensus_verify_script_with_amount(
+        spk, len(spk) & 0xffffffff, amount, tx, len(tx) & 0xffffffff, n_in & 0xffffffff,
+        flags & 0xffffffff, ctypes.byref(e))
+    return r, e.value
+
+
+def verify_with_flags(spent_output_script, amount, spending_transaction, input_index, flags):
+    """src/lib.rs:113-139: raises ConsensusError(err) unless the spend is valid.  Lengths and the
+    index are truncated to c_uint exactly as the Rust `as c_uint` casts do."""
+    amount = amount - (1 << 64) if amount >= (1 << 63) else amount  # u64 -> int64 ABI slot
+    ret, err = verify_script_with_amount(spent_output_script, amount, spending_transaction,
+                                         input_index, flags)
+    if ret != 1:
+        raise ConsensusError(Error(err))
+
+
+def verify(spent_output, amount, spending_transaction, input_index):
+    """src/lib.rs:103-110: verify_with_flags(..., VERIFY_ALL)."""
+    verify_with_flags(spent_output, amount, spending_transaction, input_index, VERIFY_ALL)
+
+
+def verify_batch(items, flags=VERIFY_ALL):
+    """items: iterable of (spent_output_script, amount, spending_transaction, input_index).
+    Returns a list of (ret, Error) equal to calling the C ABI once per item; all signature work
+    of the batch runs on the GPU in as few device rounds as the scripts allow."""
+    items = list(items)
+    n = len(items)
+    arr = (BatchItem * max(n, 1))()
+    keep, txbufs = [], {}
+    for i, (spk, amount, tx, nin) in enumerate(items):
+        amount = amount - (1 << 64) if amount >= (1 << 63) else amount
+        bs = ctypes.create_string_buffer(bytes(spk), max(1, len(spk)))
+        tx = bytes(tx)
+        bt = txbufs.get(tx)
+        if bt is None:  # one buffer per distinct tx: the engine then deserializes it once
+            bt = txbufs[tx] = ctypes.create_string_buffer(tx, max(1, len(tx)))
+        keep.append(bs)
+        arr[i] = BatchItem(ctypes.addressof(bs), len(spk), amount, ctypes.addressof(bt), len(tx),
+                           nin & 0xffffffff)
+    ret = (ctypes.c_int * max(n, 1))()
+    err = (ctypes.c_int * max(n, 1))()
+    rc = lib().bitcoinconsensus_verify_batch(arr, n, flags & 0xffffffff, ret, err)
+    if rc < 0:
+        raise RuntimeError("bitcoinconsensus_verify_batch: device pipeline failed")
+    return [(ret[i], Error(err[i])) for i in range(n)]
+
+
+def last_batch_stats():
+    s = BatchStats()
+    lib().bcc_last_batch_stats(ctypes.byref(s))
+    return {k: getattr(s, k) for k, _ in BatchStats._fields_}
+
+
+def set_device(device):
+    lib().bcc_set_device(device)
 
 
 def height_to_flags(height):

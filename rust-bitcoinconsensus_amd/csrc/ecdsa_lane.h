@@ -274,6 +274,94 @@ BCC_HD int ecdsa_verify_lane(u32 tag, const fe& px_in, const fe& py_in, const sc
     return 0;
 }
 
+// k*G -> affine (x, y), normalized.  Used by the synthetic-workload generator (keygen, signing),
+// not by verification.  Same signed-odd-window ladder as the verify loop, G slots only.
+// Returns false for k == 0 (mod n) or a zero result.
+template <class GT>
+BCC_HD bool ecmult_gen_lane(const sc& k_in, fe& xo, fe& yo, const GT& gt) {
+    if (sc_is_zero(k_in)) return false;
+    u32 c0 = k_in.v[0], c1 = k_in.v[1], c2 = k_in.v[2], c3 = k_in.v[3];
+    u32 d0 = k_in.v[4], d1 = k_in.v[5], d2 = k_in.v[6], d3 = k_in.v[7];
+    bool corr2 = (c0 & 1u) == 0, corr3 = (d0 & 1u) == 0;
+    c0 |= 1u;
+    d0 |= 1u;
+    fe one = fe_one();
+    gej acc;
+    bool inf = false;
+    {
+        bool ng;
+        u32 idx = digit_index(c0, c1, c2, c3, TOPG, WG, TOPG, ng);
+        gt.get(0, (int)idx, acc.x, acc.y);
+        acc.z = one;
+    }
+    for (int pos = TOPG; pos >= 0; pos--) {
+        if (pos != TOPG && !inf) {
+            gej t;
+            gej_double(t, acc);
+            acc = t;
+        }
+        if (pos % WG) continue;
+        for (int slot = 2; slot < 4; slot++) {
+            if (slot == 2 && pos == TOPG) continue;
+            bool dneg;
+            u32 idx = slot == 2 ? digit_index(c0, c1, c2, c3, pos, WG, TOPG, dneg)
+                                : digit_index(d0, d1, d2, d3, pos, WG, TOPG, dneg);
+            fe px, py;
+            gt.get(slot - 2, (int)idx, px, py);
+            if (dneg) fe_neg(py, py);
+            acc_add(acc, inf, px, py, one, false);
+        }
+    }
+    for (int slot = 2; slot < 4; slot++) {
+        if (!(slot == 2 ? corr2 : corr3)) continue;
+        fe px, py;
+        gt.get(slot - 2, 0, px, py);
+        fe_neg(py, py);
+        acc_add(acc, inf, px, py, one, false);
+    }
+    if (inf) return false;
+    fe zi, zi2, zi3;
+    fe_inv(zi, acc.z);
+    fe_sqr(zi2, zi);
+    fe_mul(zi3, zi2, zi);
+    fe_mul(xo, acc.x, zi2);
+    fe_mul(yo, acc.y, zi3);
+    fe_normalize(xo);
+    fe_normalize(yo);
+    return true;
+}
+
+// ECDSA signing for the generator: r = x(kG) mod n, s = k^-1 (m + r d) mod n, low-S.
+template <class GT>
+BCC_HD bool ecdsa_sign_lane(const sc& d, const sc& m_in, const sc& k, sc& r, sc& s, const GT& gt) {
+    const u32 N[8] = BCC_N_LIMBS;
+    fe rx, ry;
+    if (!ecmult_gen_lane(k, rx, ry, gt)) return false;
+    for (int i = 0; i < 8; i++) r.v[i] = rx.v[i];
+    if (!u256_lt(r.v, N)) {
+        u32 t[8];
+        u256_sub(t, r.v, N);
+        for (int i = 0; i < 8; i++) r.v[i] = t[i];
+    }
+    if (sc_is_zero(r)) return false;
+    sc m = m_in, kinv, t;
+    if (!u256_lt(m.v, N)) {
+        u32 tt[8];
+        u256_sub(tt, m.v, N);
+        for (int i = 0; i < 8; i++) m.v[i] = tt[i];
+    }
+    sc_inv(kinv, k);
+    sc_mul(t, r, d);
+    sc_add(t, t, m);
+    sc_mul(s, kinv, t);
+    if (sc_is_zero(s)) return false;
+    // low-S: s > n/2 -> n - s  (n/2 = 7FFFFFFF FFFFFFFF FFFFFFFF FFFFFFFF 5D576E73 57A4501D DFE92F46 681B20A0)
+    const u32 H[8] = {0x681B20A0u, 0xDFE92F46u, 0x57A4501Du, 0x5D576E73u,
+                      0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0x7FFFFFFFu};
+    if (u256_lt(H, s.v)) sc_neg(s, s);
+    return true;
+}
+
 // Affine G tables: xy[(tab*GTAB + i)*2 + {0,1}] = (2i+1) * 2^(128 tab) * G.  Host-side build
 // (once per process; exact group arithmetic, then one inversion per point).
 inline void build_g_tables(fe* xy) {

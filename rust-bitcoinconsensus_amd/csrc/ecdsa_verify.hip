@@ -185,7 +185,7 @@ int mi_ecdsa_verify_tuples(const uint8_t* pub65, const uint8_t* msg32, const uin
         (rc = (int)hipMemcpy(verdict, d_v, n, hipMemcpyDeviceToHost))) {
         fprintf(stderr, "[bcc] mi_ecdsa_verify_tuples failed: %d\n", rc);
     }
-    hipFree(d);
+    (void)hipFree(d);
     return rc;
 }
 

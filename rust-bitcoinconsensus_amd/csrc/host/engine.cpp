@@ -1,0 +1,428 @@
+// The drop-in C ABI (include/bitcoinconsensus.h) and the batch engine behind it.
+//
+// verify_script semantics (script/bitcoinconsensus.cpp:79-102): flags -> deserialize -> nIn ->
+// size -> ERR_OK -> VerifyScript.  VerifyScript runs on the host (script.cpp) with a DEFERRING
+// checker: every CHECKSIG / CHECKMULTISIG pair is recorded as a GPU tuple and answered
+// speculatively with `true`.  After the GPU round (sighash kernels + ECDSA kernel) an item whose
+// deferred checks all came back true is final (its speculative run WAS the reference run);
+// otherwise it is re-run with the verdicts learned so far, deferring only the checks it has not
+// seen (e.g. the next multisig key), until a run needs no unknown verdict.  This reproduces the
+// reference's verdict-dependent control flow (CHECKMULTISIG key advance, CHECKSIG NOT) exactly.
+#include <chrono>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../pipeline.h"
+#include "bcc_amd.h"
+#include "bitcoinconsensus.h"
+#include "engine.h"
+#include "script.h"
+#include "sighash.h"
+
+namespace bcc {
+namespace host {
+
+namespace {
+
+int g_device = -1;
+std::mutex g_device_mu;
+
+int current_device() {
+    std::lock_guard<std::mutex> lk(g_device_mu);
+    if (g_device < 0) {
+        const char* e = getenv("BCC_DEVICE");
+        g_device = e ? atoi(e) : 0;
+    }
+    return g_device;
+}
+
+thread_local bcc_batch_stats t_stats;
+
+struct TxEntry {
+    Tx tx;
+    bool ok = false;
+    int32_t aux[3] = {-1, -1, -1};  // aux message index per AuxKind in the current round
+};
+
+struct Item {
+    const bcc_batch_item* in;
+    TxEntry* tx = nullptr;
+    int ret = 0;
+    bitcoinconsensus_error err = bitcoinconsensus_ERR_OK;
+    bool active = false;  // needs (another) interpreter run
+    bool result = false;
+    std::unordered_map<std::string, int8_t> cache;  // tuple key -> 0/1, -1 = deferred
+    std::vector<uint32_t> pending;                  // tuple rows deferred in the last run
+};
+
+struct Pending {
+    uint32_t item;
+    std::string key;
+};
+
+std::string tuple_key(const Bytes& pub, const Bytes& sig, const Bytes& code, SigVersion sv) {
+    std::string k;
+    k.reserve(pub.size() + sig.size() + code.size() + 16);
+    auto put = [&](const Bytes& b) {
+        uint32_t n = (uint32_t)b.size();
+        k.append((const char*)&n, 4);
+        k.append((const char*)b.data(), b.size());
+    };
+    k.push_back((char)sv);
+    put(pub);
+    put(sig);
+    put(code);
+    return k;
+}
+
+class Round;
+
+// The deferral seam (BaseSignatureChecker::CheckECDSASignature, interpreter.h:227)
+class DeferringChecker : public SigChecker {
+public:
+    DeferringChecker(Round& rd, uint32_t idx, Item& it) : rd_(rd), idx_(idx), it_(it) {}
+    bool check_ecdsa(const Bytes& sig, const Bytes& pub, const Bytes& code, SigVersion sv) override;
+    bool check_locktime(int64_t n) override { return tx_check_locktime(it_.tx->tx, it_.in->n_in, n); }
+    bool check_sequence(int64_t n) override { return tx_check_sequence(it_.tx->tx, it_.in->n_in, n); }
+
+private:
+    Round& rd_;
+    uint32_t idx_;
+    Item& it_;
+};
+
+// One GPU round: the tuples deferred by this round's interpreter runs.
+class Round {
+public:
+    SighashJobs jobs;
+    TupleRows rows;
+    std::vector<Pending> pending;
+    std::vector<uint8_t> scratch;
+    std::vector<TxEntry*> touched;
+    size_t host_rejected = 0;
+
+    // GenericTransactionSignatureChecker::CheckECDSASignature (interpreter.cpp:1656-1676) up to
+    // the point where the sighash + secp256k1 verify would run; those become a GPU tuple.
+    bool defer(uint32_t item_idx, Item& it, const Bytes& sig, const Bytes& pub, const Bytes& code,
+               SigVersion sv) {
+        std::string key = tuple_key(pub, sig, code, sv);
+        auto f = it.cache.find(key);
+        if (f != it.cache.end()) return f->second != 0;  // known (or already deferred: true)
+        // CPubKey filter, empty signature, lax-DER: decided on the host (no secp work)
+        uint8_t r[32], s[32];
+        bool reject = !pubkey_size_valid(pub.data(), pub.size()) || sig.empty() ||
+                      !der_parse_lax(sig.data(), sig.size() - 1, r, s);
+        if (!reject) {
+            bool rz = true, sz = true;
+            for (int i = 0; i < 32; i++) {
+                rz &= r[i] == 0;
+                sz &= s[i] == 0;
+            }
+            reject = rz || sz;  // secp256k1_ecdsa_sig_verify rejects r == 0 || s == 0
+        }
+        if (reject) {
+            it.cache.emplace(std::move(key), 0);
+            host_rejected++;
+            return false;
+        }
+        const Tx& tx = it.tx->tx;
+        const unsigned nin = it.in->n_in;
+        const int hashtype = sig.back();
+        uint8_t one[32] = {0};
+        one[0] = 1;  // uint256::ONE as raw bytes: the SIGHASH_SINGLE-bug message
+        uint8_t ybuf[32] = {0};
+        const uint8_t* y = pub.size() == 65 ? pub.data() + 33 : ybuf;  // y unused for 02/03
+        uint32_t row = rows.add(pub[0], pub.data() + 1, y, r, s, one);
+        if (sv == SIGVERSION_BASE) {
+            if (build_legacy_preimage(tx, nin, code, hashtype, scratch))
+                jobs.add_pre(scratch.data(), scratch.size(), row);
+            // else: SIGHASH_SINGLE bug, msg stays ONE
+        } else {
+            Bip143Job job;
+            build_bip143_preimage(tx, nin, code, hashtype, it.in->amount, job);
+            uint32_t pre = jobs.add_pre(job.preimage.data(), job.preimage.size(), row);
+            size_t base = (size_t)jobs.pre_off[pre] * 64;
+            for (int k = 0; k < 3; k++) {
+                if (!job.need[k]) continue;
+                int32_t aux;
+                if (k == AUX_OUTPUTS && job.single_output) {
+                    const Span& o = tx.vout[nin].ser;
+                    aux = (int32_t)jobs.add_aux(o.p, o.n);
+                } else {
+                    if (it.tx->aux[k] < 0) {
+                        build_aux_message(tx, (AuxKind)k, scratch);
+                        it.tx->aux[k] = (int32_t)jobs.add_aux(scratch.data(), scratch.size());
+                        touched.push_back(it.tx);
+                    }
+                    aux = it.tx->aux[k];
+                }
+                jobs.patches.push_back(PatchRec{(uint32_t)(base + job.off[k]), (uint32_t)aux});
+            }
+        }
+        it.cache.emplace(key, (int8_t)-1);
+        it.pending.push_back((uint32_t)pending.size());
+        pending.push_back(Pending{item_idx, std::move(key)});
+        return true;  // speculative
+    }
+
+    void reset() {
+        jobs.clear();
+        rows.clear();
+        pending.clear();
+        for (auto* t : touched) t->aux[0] = t->aux[1] = t->aux[2] = -1;
+        touched.clear();
+    }
+};
+
+bool DeferringChecker::check_ecdsa(const Bytes& sig, const Bytes& pub, const Bytes& code,
+                                   SigVersion sv) {
+    return rd_.defer(idx_, it_, sig, pub, code, sv);
+}
+
+int set_err(bitcoinconsensus_error* e, bitcoinconsensus_error v) {
+    if (e) *e = v;
+    return 0;
+}
+
+struct BatchState {
+    std::vector<Item> st;
+    std::unordered_map<std::string, TxEntry> txs;  // parse each distinct tx buffer once
+    unsigned flags = 0;
+};
+
+// verify_script's pre-checks (bitcoinconsensus.cpp:83-95) in reference order.
+void prepare(BatchState& b, const bcc_batch_item* items, size_t n, unsigned flags) {
+    b.st.assign(n, Item());
+    b.flags = flags;
+    auto& st = b.st;
+    auto& txs = b.txs;
+    const bool flags_ok = (flags & ~(unsigned)FLAGS_VERIFY_ALL) == 0;
+    for (size_t i = 0; i < n; i++) {
+        Item& it = st[i];
+        it.in = &items[i];
+        if (!flags_ok) {
+            it.err = bitcoinconsensus_ERR_INVALID_FLAGS;
+            continue;
+        }
+        std::string tk((const char*)&items[i].tx_to, sizeof(void*));
+        tk.append((const char*)&items[i].tx_to_len, sizeof(unsigned));
+        auto f = txs.find(tk);
+        if (f == txs.end()) {
+            f = txs.emplace(tk, TxEntry()).first;
+            f->second.ok = items[i].tx_to != nullptr &&
+                           parse_tx(items[i].tx_to, items[i].tx_to_len, f->second.tx);
+        }
+        it.tx = &f->second;
+        if (!it.tx->ok) {
+            it.err = bitcoinconsensus_ERR_TX_DESERIALIZE;
+            continue;
+        }
+        if (items[i].n_in >= it.tx->tx.vin.size()) {
+            it.err = bitcoinconsensus_ERR_TX_INDEX;
+            continue;
+        }
+        if (it.tx->tx.ser_size != items[i].tx_to_len) {
+            it.err = bitcoinconsensus_ERR_TX_SIZE_MISMATCH;
+            continue;
+        }
+        it.err = bitcoinconsensus_ERR_OK;
+        it.active = true;
+    }
+}
+
+// One interpreter pass over the active items; deferred checks land in rd.  Returns whether any
+// item ran.
+bool interpret_round(BatchState& b, Round& rd) {
+    bool any = false;
+    for (size_t i = 0; i < b.st.size(); i++) {
+        Item& it = b.st[i];
+        if (!it.active) continue;
+        any = true;
+        it.pending.clear();
+        DeferringChecker chk(rd, (uint32_t)i, it);
+        const TxIn& in = it.tx->tx.vin[it.in->n_in];
+        Span spk{it.in->script_pubkey, it.in->script_pubkey_len};
+        ScriptErr se;
+        try {
+            it.result = verify_script(in.script_sig, spk, in.witness, b.flags, chk, &se);
+        } catch (...) {  // bitcoinconsensus.cpp:99: any std::exception -> TX_DESERIALIZE
+            it.result = false;
+            it.err = bitcoinconsensus_ERR_TX_DESERIALIZE;
+            it.pending.clear();
+        }
+        it.active = false;
+    }
+    return any;
+}
+
+// Runs the batch; fills ret/err per item.  Returns -1 if the device pipeline failed.
+long run_batch(const bcc_batch_item* items, size_t n, unsigned flags, int* ret_out,
+               bitcoinconsensus_error* err_out) {
+    using clk = std::chrono::steady_clock;
+    t_stats = bcc_batch_stats{};
+    t_stats.items = n;
+    double host_s = 0, gpu_s = 0;
+    auto t0 = clk::now();
+    BatchState b;
+    prepare(b, items, n, flags);
+    auto& st = b.st;
+    const int dev = current_device();
+    Round rd;
+    std::vector<uint8_t> verdict;
+    long status = 0;
+    for (size_t round = 0;; round++) {
+        rd.reset();
+        bool any = interpret_round(b, rd);
+        if (!any || rd.pending.empty()) break;
+        t_stats.rounds++;
+        t_stats.tuples += rd.rows.size();
+        t_stats.preimages += rd.jobs.pre_off.size();
+        t_stats.aux_messages += rd.jobs.aux_off.size();
+        auto g0 = clk::now();
+        verdict.assign(rd.rows.size(), 0);
+        int e = gpu_verify_batch(dev, rd.jobs, rd.rows, verdict.data());
+        gpu_s += std::chrono::duration<double>(clk::now() - g0).count();
+        if (e != 0) {
+            status = -1;
+            for (auto& it : st)
+                if (!it.pending.empty()) {
+                    it.result = false;
+                    it.err = bitcoinconsensus_ERR_TX_DESERIALIZE;
+                    it.pending.clear();
+                }
+            break;
+        }
+        for (size_t k = 0; k < rd.pending.size(); k++) {
+            Item& it = st[rd.pending[k].item];
+            it.cache[rd.pending[k].key] = (int8_t)verdict[k];
+        }
+        for (auto& it : st) {
+            if (it.pending.empty()) continue;
+            bool all_true = true;
+            for (uint32_t k : it.pending) all_true &= verdict[k] != 0;
+            if (!all_true) it.active = true;  // speculation was wrong somewhere: re-run
+        }
+    }
+    t_stats.host_rejected = rd.host_rejected;
+    long valid = 0;
+    for (size_t i = 0; i < n; i++) {
+        Item& it = st[i];
+        int ret = (it.err == bitcoinconsensus_ERR_OK && it.result) ? 1 : 0;
+        ret_out[i] = ret;
+        if (err_out) err_out[i] = it.err;
+        valid += ret;
+    }
+    host_s = std::chrono::duration<double>(clk::now() - t0).count() - gpu_s;
+    t_stats.host_seconds = host_s;
+    t_stats.gpu_seconds = gpu_s;
+    return status < 0 ? -1 : valid;
+}
+
+}  // namespace
+
+size_t build_first_round(const bcc_batch_item* items, size_t n, unsigned flags, SighashJobs& jobs,
+                         TupleRows& rows, std::vector<uint32_t>* tuple_item) {
+    BatchState b;
+    prepare(b, items, n, flags);
+    Round rd;
+    interpret_round(b, rd);
+    if (tuple_item) {
+        tuple_item->clear();
+        for (const auto& p : rd.pending) tuple_item->push_back(p.item);
+    }
+    jobs = std::move(rd.jobs);
+    rows = std::move(rd.rows);
+    return rows.size();
+}
+
+void append_round(SighashJobs& dst, TupleRows& drows, const SighashJobs& src,
+                  const TupleRows& srows) {
+    const uint32_t row0 = (uint32_t)drows.size();
+    const uint32_t aux_blk0 = (uint32_t)(dst.aux.size() / 64), pre_blk0 = (uint32_t)(dst.pre.size() / 64);
+    const uint32_t aux_idx0 = (uint32_t)dst.aux_off.size();
+    auto cat = [](std::vector<uint8_t>& a, const std::vector<uint8_t>& b) { a.insert(a.end(), b.begin(), b.end()); };
+    cat(drows.tag, srows.tag);
+    cat(drows.x, srows.x);
+    cat(drows.y, srows.y);
+    cat(drows.r, srows.r);
+    cat(drows.s, srows.s);
+    cat(drows.msg, srows.msg);
+    cat(dst.aux, src.aux);
+    cat(dst.pre, src.pre);
+    for (size_t i = 0; i < src.aux_off.size(); i++) {
+        dst.aux_off.push_back(src.aux_off[i] + aux_blk0);
+        dst.aux_nblk.push_back(src.aux_nblk[i]);
+    }
+    for (size_t i = 0; i < src.pre_off.size(); i++) {
+        dst.pre_off.push_back(src.pre_off[i] + pre_blk0);
+        dst.pre_nblk.push_back(src.pre_nblk[i]);
+        dst.pre_row.push_back(src.pre_row[i] + row0);
+    }
+    for (const auto& p : src.patches)
+        dst.patches.push_back(PatchRec{p.pre_byte + pre_blk0 * 64, p.aux + aux_idx0});
+}
+
+}  // namespace host
+}  // namespace bcc
+
+using namespace bcc::host;
+
+extern "C" {
+
+int bitcoinconsensus_verify_script_with_amount(const unsigned char* scriptPubKey,
+                                               unsigned int scriptPubKeyLen, int64_t amount,
+                                               const unsigned char* txTo, unsigned int txToLen,
+                                               unsigned int nIn, unsigned int flags,
+                                               bitcoinconsensus_error* err) {
+    bcc_batch_item item{scriptPubKey, scriptPubKeyLen, amount, txTo, txToLen, nIn};
+    int ret = 0;
+    bitcoinconsensus_error e = bitcoinconsensus_ERR_OK;
+    try {
+        run_batch(&item, 1, flags, &ret, &e);
+    } catch (...) {
+        return set_err(err, bitcoinconsensus_ERR_TX_DESERIALIZE);
+    }
+    // set_error semantics (bitcoinconsensus.cpp:58-63): errors return 0 and write *err;
+    // a completed script run writes ERR_OK
+    if (err) *err = e;
+    return ret;
+}
+
+int bitcoinconsensus_verify_script(const unsigned char* scriptPubKey, unsigned int scriptPubKeyLen,
+                                   const unsigned char* txTo, unsigned int txToLen,
+                                   unsigned int nIn, unsigned int flags, bitcoinconsensus_error* err) {
+    if (flags & bitcoinconsensus_SCRIPT_FLAGS_VERIFY_WITNESS)
+        return set_err(err, bitcoinconsensus_ERR_AMOUNT_REQUIRED);
+    return bitcoinconsensus_verify_script_with_amount(scriptPubKey, scriptPubKeyLen, 0, txTo,
+                                                      txToLen, nIn, flags, err);
+}
+
+unsigned int bitcoinconsensus_version(void) { return BITCOINCONSENSUS_API_VER; }
+
+long bitcoinconsensus_verify_batch(const bcc_batch_item* items, size_t n, unsigned int flags,
+                                   int* ret_out, bitcoinconsensus_error* err_out) {
+    try {
+        return run_batch(items, n, flags, ret_out, err_out);
+    } catch (...) {
+        for (size_t i = 0; i < n; i++) {
+            ret_out[i] = 0;
+            if (err_out) err_out[i] = bitcoinconsensus_ERR_TX_DESERIALIZE;
+        }
+        return -1;
+    }
+}
+
+int bcc_set_device(int device) {
+    std::lock_guard<std::mutex> lk(g_device_mu);
+    g_device = device;
+    return 0;
+}
+
+void bcc_last_batch_stats(bcc_batch_stats* out) {
+    if (out) *out = t_stats;
+}
+
+}  // extern "C"

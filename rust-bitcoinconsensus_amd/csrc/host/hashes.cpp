@@ -1,0 +1,222 @@
+// Host hash functions (see hashes.h).  Straightforward implementations of the published
+// algorithms (FIPS 180-4 SHA-256 / SHA-1, Dobbertin-Bosselaers-Preneel RIPEMD-160).
+#include "hashes.h"
+
+#include <cstring>
+
+namespace bcc {
+namespace host {
+
+namespace {
+
+inline uint32_t rotr(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }
+inline uint32_t rotl(uint32_t x, int n) { return (x << n) | (x >> (32 - n)); }
+inline uint32_t be32(const uint8_t* p) {
+    return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
+}
+inline uint32_t le32(const uint8_t* p) {
+    return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+
+const uint32_t K256[64] = {
+    0x428a2f98, 0x71374491, 0xb5c0fbcf, 0xe9b5dba5, 0x3956c25b, 0x59f111f1, 0x923f82a4, 0xab1c5ed5,
+    0xd807aa98, 0x12835b01, 0x243185be, 0x550c7dc3, 0x72be5d74, 0x80deb1fe, 0x9bdc06a7, 0xc19bf174,
+    0xe49b69c1, 0xefbe4786, 0x0fc19dc6, 0x240ca1cc, 0x2de92c6f, 0x4a7484aa, 0x5cb0a9dc, 0x76f988da,
+    0x983e5152, 0xa831c66d, 0xb00327c8, 0xbf597fc7, 0xc6e00bf3, 0xd5a79147, 0x06ca6351, 0x14292967,
+    0x27b70a85, 0x2e1b2138, 0x4d2c6dfc, 0x53380d13, 0x650a7354, 0x766a0abb, 0x81c2c92e, 0x92722c85,
+    0xa2bfe8a1, 0xa81a664b, 0xc24b8b70, 0xc76c51a3, 0xd192e819, 0xd6990624, 0xf40e3585, 0x106aa070,
+    0x19a4c116, 0x1e376c08, 0x2748774c, 0x34b0bcb5, 0x391c0cb3, 0x4ed8aa4a, 0x5b9cca4f, 0x682e6ff3,
+    0x748f82ee, 0x78a5636f, 0x84c87814, 0x8cc70208, 0x90befffa, 0xa4506ceb, 0xbef9a3f7, 0xc67178f2};
+
+void sha256_block(uint32_t s[8], const uint8_t* blk) {
+    uint32_t w[64];
+    for (int i = 0; i < 16; i++) w[i] = be32(blk + 4 * i);
+    for (int i = 16; i < 64; i++) {
+        uint32_t s0 = rotr(w[i - 15], 7) ^ rotr(w[i - 15], 18) ^ (w[i - 15] >> 3);
+        uint32_t s1 = rotr(w[i - 2], 17) ^ rotr(w[i - 2], 19) ^ (w[i - 2] >> 10);
+        w[i] = w[i - 16] + s0 + w[i - 7] + s1;
+    }
+    uint32_t a = s[0], b = s[1], c = s[2], d = s[3], e = s[4], f = s[5], g = s[6], h = s[7];
+    for (int i = 0; i < 64; i++) {
+        uint32_t t1 = h + (rotr(e, 6) ^ rotr(e, 11) ^ rotr(e, 25)) + ((e & f) ^ (~e & g)) + K256[i] + w[i];
+        uint32_t t2 = (rotr(a, 2) ^ rotr(a, 13) ^ rotr(a, 22)) + ((a & b) ^ (a & c) ^ (b & c));
+        h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
+    }
+    s[0] += a; s[1] += b; s[2] += c; s[3] += d; s[4] += e; s[5] += f; s[6] += g; s[7] += h;
+}
+
+}  // namespace
+
+Sha256::Sha256() : bytes(0) {
+    static const uint32_t iv[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a,
+                                   0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
+    memcpy(s, iv, sizeof s);
+}
+
+Sha256& Sha256::write(const uint8_t* p, size_t n) {
+    size_t fill = (size_t)(bytes & 63);
+    bytes += n;
+    if (fill) {
+        size_t take = 64 - fill < n ? 64 - fill : n;
+        memcpy(buf + fill, p, take);
+        p += take;
+        n -= take;
+        if (fill + take < 64) return *this;
+        sha256_block(s, buf);
+    }
+    while (n >= 64) {
+        sha256_block(s, p);
+        p += 64;
+        n -= 64;
+    }
+    if (n) memcpy(buf, p, n);
+    return *this;
+}
+
+void Sha256::finalize(uint8_t out[32]) {
+    uint64_t bits = bytes * 8;
+    uint8_t pad[72];
+    size_t padlen = 1 + ((119 - (bytes % 64)) % 64);
+    memset(pad, 0, sizeof pad);
+    pad[0] = 0x80;
+    for (int i = 0; i < 8; i++) pad[padlen + i] = (uint8_t)(bits >> (56 - 8 * i));
+    write(pad, padlen + 8);
+    for (int i = 0; i < 8; i++) {
+        out[4 * i] = (uint8_t)(s[i] >> 24);
+        out[4 * i + 1] = (uint8_t)(s[i] >> 16);
+        out[4 * i + 2] = (uint8_t)(s[i] >> 8);
+        out[4 * i + 3] = (uint8_t)s[i];
+    }
+}
+
+void sha256(const uint8_t* p, size_t n, uint8_t out[32]) { Sha256().write(p, n).finalize(out); }
+
+void sha256d(const uint8_t* p, size_t n, uint8_t out[32]) {
+    uint8_t t[32];
+    sha256(p, n, t);
+    sha256(t, 32, out);
+}
+
+// ---------------------------------------------------------------- SHA-1 (crypto/sha1.cpp)
+void sha1(const uint8_t* p, size_t n, uint8_t out[20]) {
+    uint32_t h[5] = {0x67452301, 0xEFCDAB89, 0x98BADCFE, 0x10325476, 0xC3D2E1F0};
+    uint64_t bits = (uint64_t)n * 8;
+    size_t total = ((n + 8) / 64 + 1) * 64;
+    for (size_t off = 0; off < total; off += 64) {
+        uint8_t blk[64];
+        for (int i = 0; i < 64; i++) {
+            size_t k = off + i;
+            uint8_t v;
+            if (k < n) v = p[k];
+            else if (k == n) v = 0x80;
+            else if (k >= total - 8) v = (uint8_t)(bits >> (8 * (total - 1 - k)));
+            else v = 0;
+            blk[i] = v;
+        }
+        uint32_t w[80];
+        for (int i = 0; i < 16; i++) w[i] = be32(blk + 4 * i);
+        for (int i = 16; i < 80; i++) w[i] = rotl(w[i - 3] ^ w[i - 8] ^ w[i - 14] ^ w[i - 16], 1);
+        uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4];
+        for (int i = 0; i < 80; i++) {
+            uint32_t f, k;
+            if (i < 20) { f = (b & c) | (~b & d); k = 0x5A827999; }
+            else if (i < 40) { f = b ^ c ^ d; k = 0x6ED9EBA1; }
+            else if (i < 60) { f = (b & c) | (b & d) | (c & d); k = 0x8F1BBCDC; }
+            else { f = b ^ c ^ d; k = 0xCA62C1D6; }
+            uint32_t t = rotl(a, 5) + f + e + k + w[i];
+            e = d; d = c; c = rotl(b, 30); b = a; a = t;
+        }
+        h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e;
+    }
+    for (int i = 0; i < 5; i++) {
+        out[4 * i] = (uint8_t)(h[i] >> 24);
+        out[4 * i + 1] = (uint8_t)(h[i] >> 16);
+        out[4 * i + 2] = (uint8_t)(h[i] >> 8);
+        out[4 * i + 3] = (uint8_t)h[i];
+    }
+}
+
+// ---------------------------------------------------------------- RIPEMD-160 (crypto/ripemd160.cpp)
+namespace {
+const uint8_t RL[80] = {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15,
+                        7, 4, 13, 1, 10, 6, 15, 3, 12, 0, 9, 5, 2, 14, 11, 8,
+                        3, 10, 14, 4, 9, 15, 8, 1, 2, 7, 0, 6, 13, 11, 5, 12,
+                        1, 9, 11, 10, 0, 8, 12, 4, 13, 3, 7, 15, 14, 5, 6, 2,
+                        4, 0, 5, 9, 7, 12, 2, 10, 14, 1, 3, 8, 11, 6, 15, 13};
+const uint8_t RR[80] = {5, 14, 7, 0, 9, 2, 11, 4, 13, 6, 15, 8, 1, 10, 3, 12,
+                        6, 11, 3, 7, 0, 13, 5, 10, 14, 15, 8, 12, 4, 9, 1, 2,
+                        15, 5, 1, 3, 7, 14, 6, 9, 11, 8, 12, 2, 10, 0, 4, 13,
+                        8, 6, 4, 1, 3, 11, 15, 0, 5, 12, 2, 13, 9, 7, 10, 14,
+                        12, 15, 10, 4, 1, 5, 8, 7, 6, 2, 13, 14, 0, 3, 9, 11};
+const uint8_t SL[80] = {11, 14, 15, 12, 5, 8, 7, 9, 11, 13, 14, 15, 6, 7, 9, 8,
+                        7, 6, 8, 13, 11, 9, 7, 15, 7, 12, 15, 9, 11, 7, 13, 12,
+                        11, 13, 6, 7, 14, 9, 13, 15, 14, 8, 13, 6, 5, 12, 7, 5,
+                        11, 12, 14, 15, 14, 15, 9, 8, 9, 14, 5, 6, 8, 6, 5, 12,
+                        9, 15, 5, 11, 6, 8, 13, 12, 5, 12, 13, 14, 11, 8, 5, 6};
+const uint8_t SR[80] = {8, 9, 9, 11, 13, 15, 15, 5, 7, 7, 8, 11, 14, 14, 12, 6,
+                        9, 13, 15, 7, 12, 8, 9, 11, 7, 7, 12, 7, 6, 15, 13, 11,
+                        9, 7, 15, 11, 8, 6, 6, 14, 12, 13, 5, 14, 13, 13, 7, 5,
+                        15, 5, 8, 11, 14, 14, 6, 14, 6, 9, 12, 9, 12, 5, 15, 8,
+                        8, 5, 12, 9, 12, 5, 14, 6, 8, 13, 6, 5, 15, 13, 11, 11};
+const uint32_t KL[5] = {0x00000000, 0x5A827999, 0x6ED9EBA1, 0x8F1BBCDC, 0xA953FD4E};
+const uint32_t KR[5] = {0x50A28BE6, 0x5C4DD124, 0x6D703EF3, 0x7A6D76E9, 0x00000000};
+
+inline uint32_t rf(int j, uint32_t x, uint32_t y, uint32_t z) {
+    switch (j / 16) {
+        case 0: return x ^ y ^ z;
+        case 1: return (x & y) | (~x & z);
+        case 2: return (x | ~y) ^ z;
+        case 3: return (x & z) | (y & ~z);
+        default: return x ^ (y | ~z);
+    }
+}
+}  // namespace
+
+void ripemd160(const uint8_t* p, size_t n, uint8_t out[20]) {
+    uint32_t h[5] = {0x67452301, 0xEFCDAB89, 0x98BADCFE, 0x10325476, 0xC3D2E1F0};
+    uint64_t bits = (uint64_t)n * 8;
+    size_t total = ((n + 8) / 64 + 1) * 64;
+    for (size_t off = 0; off < total; off += 64) {
+        uint8_t blk[64];
+        for (int i = 0; i < 64; i++) {
+            size_t k = off + i;
+            uint8_t v;
+            if (k < n) v = p[k];
+            else if (k == n) v = 0x80;
+            else if (k >= total - 8) v = (uint8_t)(bits >> (8 * (k - (total - 8))));  // little-endian
+            else v = 0;
+            blk[i] = v;
+        }
+        uint32_t X[16];
+        for (int i = 0; i < 16; i++) X[i] = le32(blk + 4 * i);
+        uint32_t al = h[0], bl = h[1], cl = h[2], dl = h[3], el = h[4];
+        uint32_t ar = h[0], br = h[1], cr = h[2], dr = h[3], er = h[4];
+        for (int j = 0; j < 80; j++) {
+            uint32_t t = rotl(al + rf(j, bl, cl, dl) + X[RL[j]] + KL[j / 16], SL[j]) + el;
+            al = el; el = dl; dl = rotl(cl, 10); cl = bl; bl = t;
+            t = rotl(ar + rf(79 - j, br, cr, dr) + X[RR[j]] + KR[j / 16], SR[j]) + er;
+            ar = er; er = dr; dr = rotl(cr, 10); cr = br; br = t;
+        }
+        uint32_t t = h[1] + cl + dr;
+        h[1] = h[2] + dl + er;
+        h[2] = h[3] + el + ar;
+        h[3] = h[4] + al + br;
+        h[4] = h[0] + bl + cr;
+        h[0] = t;
+    }
+    for (int i = 0; i < 5; i++) {
+        out[4 * i] = (uint8_t)h[i];
+        out[4 * i + 1] = (uint8_t)(h[i] >> 8);
+        out[4 * i + 2] = (uint8_t)(h[i] >> 16);
+        out[4 * i + 3] = (uint8_t)(h[i] >> 24);
+    }
+}
+
+void hash160(const uint8_t* p, size_t n, uint8_t out[20]) {
+    uint8_t t[32];
+    sha256(p, n, t);
+    ripemd160(t, 32, out);
+}
+
+}  // namespace host
+}  // namespace bcc

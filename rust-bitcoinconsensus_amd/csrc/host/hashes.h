@@ -1,0 +1,28 @@
+// Host-side hash functions used by the script interpreter (OP_SHA256 / OP_HASH160 / ...), by the
+// sighash preimage builders and by the synthetic-workload generator.
+// Restates crypto/sha256.cpp, crypto/sha1.cpp, crypto/ripemd160.cpp (standard FIPS 180-4 /
+// RIPEMD-160 algorithms) and hash.h's CHash256 / CHash160 compositions.
+#pragma once
+#include <cstddef>
+#include <cstdint>
+
+namespace bcc {
+namespace host {
+
+struct Sha256 {
+    uint32_t s[8];
+    uint8_t buf[64];
+    uint64_t bytes;
+    Sha256();
+    Sha256& write(const uint8_t* p, size_t n);
+    void finalize(uint8_t out[32]);
+};
+
+void sha256(const uint8_t* p, size_t n, uint8_t out[32]);
+void sha256d(const uint8_t* p, size_t n, uint8_t out[32]);              // CHash256
+void sha1(const uint8_t* p, size_t n, uint8_t out[20]);
+void ripemd160(const uint8_t* p, size_t n, uint8_t out[20]);
+void hash160(const uint8_t* p, size_t n, uint8_t out[20]);              // RIPEMD160(SHA256(x))
+
+}  // namespace host
+}  // namespace bcc

@@ -1,0 +1,143 @@
+// Transaction deserializer (see tx.h).
+#include "tx.h"
+
+namespace bcc {
+namespace host {
+
+namespace {
+
+constexpr uint64_t MAX_SIZE = 0x02000000;  // serialize.h:31
+
+struct Reader {
+    const uint8_t* p;
+    size_t n, pos = 0;
+    bool bad = false;
+    const uint8_t* take(size_t k) {
+        if (bad || k > n - pos) {
+            bad = true;
+            return nullptr;
+        }
+        const uint8_t* q = p + pos;
+        pos += k;
+        return q;
+    }
+    uint64_t le(int k) {
+        const uint8_t* q = take((size_t)k);
+        if (!q) return 0;
+        uint64_t v = 0;
+        for (int i = k - 1; i >= 0; i--) v = (v << 8) | q[i];
+        return v;
+    }
+    // ReadCompactSize with range_check (serialize.h:318-347)
+    uint64_t compact() {
+        uint64_t c = le(1), v;
+        if (bad) return 0;
+        if (c < 253) {
+            v = c;
+        } else if (c == 253) {
+            v = le(2);
+            if (v < 253) bad = true;
+        } else if (c == 254) {
+            v = le(4);
+            if (v < 0x10000u) bad = true;
+        } else {
+            v = le(8);
+            if (v < 0x100000000ULL) bad = true;
+        }
+        if (v > MAX_SIZE) bad = true;
+        return bad ? 0 : v;
+    }
+    Span bytes() {
+        uint64_t k = compact();
+        Span s;
+        if (bad) return s;
+        s.p = take((size_t)k);
+        s.n = bad ? 0 : (size_t)k;
+        return s;
+    }
+};
+
+bool read_vin(Reader& r, std::vector<TxIn>& vin) {
+    uint64_t k = r.compact();
+    if (r.bad || k > r.n - r.pos) return false;  // every element needs >= 1 byte: EOF anyway
+    vin.resize((size_t)k);
+    for (auto& in : vin) {
+        in.prevout = r.take(36);
+        in.script_sig = r.bytes();
+        in.sequence = (uint32_t)r.le(4);
+        if (r.bad) return false;
+    }
+    return true;
+}
+
+bool read_vout(Reader& r, std::vector<TxOut>& vout) {
+    uint64_t k = r.compact();
+    if (r.bad || k > r.n - r.pos) return false;
+    vout.resize((size_t)k);
+    for (auto& o : vout) {
+        size_t start = r.pos;
+        o.value = (int64_t)r.le(8);
+        o.script = r.bytes();
+        if (r.bad) return false;
+        o.ser.p = r.p + start;
+        o.ser.n = r.pos - start;
+    }
+    return true;
+}
+
+}  // namespace
+
+bool parse_tx(const uint8_t* data, size_t len, Tx& tx) {
+    Reader r{data, len};
+    tx = Tx();
+    tx.version = (int32_t)(uint32_t)r.le(4);
+    if (r.bad) return false;
+    uint8_t flags = 0;
+    if (!read_vin(r, tx.vin)) return false;
+    if (tx.vin.empty()) {           // dummy (segwit marker) or an empty vin
+        flags = (uint8_t)r.le(1);
+        if (r.bad) return false;
+        if (flags != 0) {
+            if (!read_vin(r, tx.vin)) return false;
+            if (!read_vout(r, tx.vout)) return false;
+        }
+    } else {
+        if (!read_vout(r, tx.vout)) return false;
+    }
+    if (flags & 1) {
+        flags ^= 1;
+        for (auto& in : tx.vin) {
+            uint64_t k = r.compact();
+            if (r.bad || k > r.n - r.pos) return false;
+            in.witness.resize((size_t)k);
+            for (auto& w : in.witness) {
+                w = r.bytes();
+                if (r.bad) return false;
+            }
+        }
+        if (!tx.has_witness()) return false;  // "Superfluous witness record"
+    }
+    if (flags) return false;                  // "Unknown transaction optional data"
+    tx.locktime = (uint32_t)r.le(4);
+    if (r.bad) return false;
+    tx.ser_size = r.pos;
+    return true;
+}
+
+void put_compact_size(std::vector<uint8_t>& out, uint64_t v) {
+    if (v < 253) {
+        out.push_back((uint8_t)v);
+    } else if (v <= 0xFFFF) {
+        out.push_back(253);
+        for (int i = 0; i < 2; i++) out.push_back((uint8_t)(v >> (8 * i)));
+    } else if (v <= 0xFFFFFFFFULL) {
+        out.push_back(254);
+        for (int i = 0; i < 4; i++) out.push_back((uint8_t)(v >> (8 * i)));
+    } else {
+        out.push_back(255);
+        for (int i = 0; i < 8; i++) out.push_back((uint8_t)(v >> (8 * i)));
+    }
+}
+
+}  // namespace host
+}  // namespace bcc

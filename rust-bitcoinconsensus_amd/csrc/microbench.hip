@@ -87,9 +87,9 @@ int mi_microbench(int op, int iters, double* rate) {
     float ms = 0;
     BCC_HIP_TRY(hipEventElapsedTime(&ms, e0, e1));
     *rate = (double)grid * block * iters * 8 / (ms * 1e-3);
-    hipEventDestroy(e0);
-    hipEventDestroy(e1);
-    hipFree(out);
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    (void)hipFree(out);
     return 0;
 }
 

@@ -1,0 +1,109 @@
+// Internal (C++) interface of the device pipeline: host-built signature jobs -> HBM ->
+//   K1 sha256d(aux messages)        BIP143 hashPrevouts / hashSequence / hashOutputs per tx
+//   K2 patch(aux digests -> preimages)
+//   K3 sha256d(preimages)           legacy + BIP143 sighashes, written as the tuple msg rows
+//   K4 ecdsa_verify(tuples)         csrc/ecdsa_verify.hip
+// All four launch back-to-back on one stream with inputs resident in HBM.
+#pragma once
+#include <cstddef>
+#include <cstdint>
+#include <cstring>
+#include <vector>
+
+namespace bcc {
+
+struct PatchRec {
+    uint32_t pre_byte;  // absolute byte offset in the padded preimage buffer
+    uint32_t aux;       // index of the aux message whose digest goes there
+};
+
+// SHA-256 padding appended on the host so that the kernels only run whole 64-byte blocks.
+inline size_t sha_padded_len(size_t n) { return ((n + 8) / 64 + 1) * 64; }
+inline void sha_append_padded(std::vector<uint8_t>& buf, const uint8_t* m, size_t n) {
+    size_t L = sha_padded_len(n), base = buf.size();
+    buf.resize(base + L, 0);
+    if (n) memcpy(&buf[base], m, n);
+    buf[base + n] = 0x80;
+    uint64_t bits = (uint64_t)n * 8;
+    for (int i = 0; i < 8; i++) buf[base + L - 1 - i] = (uint8_t)(bits >> (8 * i));
+}
+
+struct SighashJobs {
+    std::vector<uint8_t> aux, pre;                  // padded messages, back to back
+    std::vector<uint32_t> aux_off, aux_nblk;        // offsets / lengths in 64-byte blocks
+    std::vector<uint32_t> pre_off, pre_nblk, pre_row;
+    std::vector<PatchRec> patches;
+    uint32_t add_aux(const uint8_t* m, size_t n) {
+        aux_off.push_back((uint32_t)(aux.size() / 64));
+        sha_append_padded(aux, m, n);
+        aux_nblk.push_back((uint32_t)(sha_padded_len(n) / 64));
+        return (uint32_t)aux_off.size() - 1;
+    }
+    uint32_t add_pre(const uint8_t* m, size_t n, uint32_t row) {
+        pre_off.push_back((uint32_t)(pre.size() / 64));
+        sha_append_padded(pre, m, n);
+        pre_nblk.push_back((uint32_t)(sha_padded_len(n) / 64));
+        pre_row.push_back(row);
+        return (uint32_t)pre_off.size() - 1;
+    }
+    void clear() {
+        aux.clear(); pre.clear(); aux_off.clear(); aux_nblk.clear();
+        pre_off.clear(); pre_nblk.clear(); pre_row.clear(); patches.clear();
+    }
+};
+
+// ECDSA tuple rows (big-endian 32-byte values).  msg rows whose sighash comes from a preimage
+// are overwritten on the device by K3; constant ones (SIGHASH_SINGLE bug) are set by the host.
+struct TupleRows {
+    std::vector<uint8_t> tag, x, y, r, s, msg;
+    size_t size() const { return tag.size(); }
+    uint32_t add(uint8_t t, const uint8_t* x32, const uint8_t* y32, const uint8_t* r32,
+                 const uint8_t* s32, const uint8_t* m32) {
+        tag.push_back(t);
+        x.insert(x.end(), x32, x32 + 32);
+        y.insert(y.end(), y32, y32 + 32);
+        r.insert(r.end(), r32, r32 + 32);
+        s.insert(s.end(), s32, s32 + 32);
+        msg.insert(msg.end(), m32, m32 + 32);
+        return (uint32_t)tag.size() - 1;
+    }
+    void clear() { tag.clear(); x.clear(); y.clear(); r.clear(); s.clear(); msg.clear(); }
+};
+
+// Device-resident batch (one per device / per caller thread).  stage() uploads, run() only
+// launches kernels (graph-capturable: no allocation, no synchronisation).
+class DeviceBatch {
+public:
+    explicit DeviceBatch(int device);
+    ~DeviceBatch();
+    int stage(const SighashJobs& jobs, const TupleRows& rows);
+    int run(void* stream);                       // K1..K4
+    int run_sighash(void* stream);               // K1..K3 only
+    int run_ecdsa(void* stream);                 // K4 only
+    int fetch_verdicts(uint8_t* out);            // synchronous D2H
+    int fetch_msgs(uint8_t* out);                // synchronous D2H (tests)
+    size_t n_tuples() const { return n_rows_; }
+    size_t n_pre() const { return n_pre_; }
+    size_t n_aux() const { return n_aux_; }
+    size_t pre_blocks() const { return pre_blocks_; }
+    size_t aux_blocks() const { return aux_blocks_; }
+    int device() const { return dev_; }
+    // raw device pointers (bench / profiling)
+    uint8_t *d_tag = nullptr, *d_x = nullptr, *d_y = nullptr, *d_r = nullptr, *d_s = nullptr,
+            *d_m = nullptr, *d_v = nullptr;
+
+private:
+    int dev_;
+    void* arena_ = nullptr;
+    size_t cap_ = 0;
+    size_t n_rows_ = 0, n_pre_ = 0, n_aux_ = 0, n_patch_ = 0, pre_blocks_ = 0, aux_blocks_ = 0;
+    uint8_t *d_aux_ = nullptr, *d_pre_ = nullptr, *d_auxd_ = nullptr;
+    uint32_t *d_aux_off_ = nullptr, *d_aux_nblk_ = nullptr, *d_pre_off_ = nullptr,
+             *d_pre_nblk_ = nullptr, *d_pre_row_ = nullptr;
+    PatchRec* d_patch_ = nullptr;
+};
+
+// One-shot helper: stage + run + fetch on `device` (synchronous).
+int gpu_verify_batch(int device, const SighashJobs& jobs, const TupleRows& rows, uint8_t* verdict);
+
+}  // namespace bcc

@@ -1,0 +1,176 @@
+// Hot-path stage (a) on gfx950: SHA-256d over host-padded messages, one lane per message.
+//   K1 sha256d_msgs   aux messages (BIP143 hashPrevouts / hashSequence / hashOutputs) -> 32 B
+//   K2 patch_digests  scatter aux digests into the BIP143 preimage slots
+//   K3 sha256d_msgs   preimages -> sighash, written straight into the ECDSA tuple msg rows
+// Integer-ALU bound (~2k VALU ops per 64-byte block); HBM traffic per launch is reported by
+// bench.py as the algorithmic bytes (message bytes in + 32 B out per message).
+#include "gpu_common.h"
+#include "pipeline.h"
+#include "sha256_device.h"
+
+extern "C" int mi_ecdsa_verify_device(const uint8_t* d_tag, const uint8_t* d_x, const uint8_t* d_y,
+                                      const uint8_t* d_r, const uint8_t* d_s, const uint8_t* d_m,
+                                      uint8_t* d_verdict, size_t n, void* stream);
+
+namespace bcc {
+
+__device__ __forceinline__ uint32_t bswap_u32(uint32_t x) { return __builtin_bswap32(x); }
+
+// Each lane streams its own message 64 bytes at a time (four 16-byte loads; messages are
+// 64-byte aligned so every load is a full aligned 16-byte access).
+__global__ __launch_bounds__(256) void sha256d_msgs_kernel(const uint8_t* __restrict__ buf,
+                                                           const uint32_t* __restrict__ off_blk,
+                                                           const uint32_t* __restrict__ nblk,
+                                                           uint32_t nmsg, uint8_t* __restrict__ out,
+                                                           const uint32_t* __restrict__ out_row) {
+    uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
+    if (m >= nmsg) return;
+    const uint4* p = reinterpret_cast<const uint4*>(buf + (size_t)off_blk[m] * 64);
+    uint32_t st[8];
+    sha256_init_state(st);
+    const uint32_t nb = nblk[m];
+    for (uint32_t b = 0; b < nb; b++) {
+        uint32_t w[16];
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            uint4 v = p[b * 4 + q];
+            w[4 * q + 0] = bswap_u32(v.x);
+            w[4 * q + 1] = bswap_u32(v.y);
+            w[4 * q + 2] = bswap_u32(v.z);
+            w[4 * q + 3] = bswap_u32(v.w);
+        }
+        sha256_compress(st, w);
+    }
+    uint32_t d[8];
+    sha256_of_digest(d, st);
+    uint32_t row = out_row ? out_row[m] : m;
+    uint4* o = reinterpret_cast<uint4*>(out + (size_t)row * 32);
+    o[0] = make_uint4(bswap_u32(d[0]), bswap_u32(d[1]), bswap_u32(d[2]), bswap_u32(d[3]));
+    o[1] = make_uint4(bswap_u32(d[4]), bswap_u32(d[5]), bswap_u32(d[6]), bswap_u32(d[7]));
+}
+
+__global__ __launch_bounds__(256) void patch_digests_kernel(uint8_t* __restrict__ pre,
+                                                            const PatchRec* __restrict__ patches,
+                                                            const uint8_t* __restrict__ auxd,
+                                                            uint32_t npatch) {
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= npatch * 32) return;
+    PatchRec p = patches[i >> 5];
+    uint32_t k = i & 31;
+    pre[(size_t)p.pre_byte + k] = auxd[(size_t)p.aux * 32 + k];
+}
+
+// ------------------------------------------------------------------------------------------
+DeviceBatch::DeviceBatch(int device) : dev_(device) {}
+
+DeviceBatch::~DeviceBatch() {
+    if (arena_) {
+        (void)hipSetDevice(dev_);
+        (void)hipFree(arena_);
+    }
+}
+
+static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+int DeviceBatch::stage(const SighashJobs& j, const TupleRows& rows) {
+    BCC_HIP_TRY(hipSetDevice(dev_));
+    n_rows_ = rows.size();
+    n_pre_ = j.pre_off.size();
+    n_aux_ = j.aux_off.size();
+    n_patch_ = j.patches.size();
+    pre_blocks_ = j.pre.size() / 64;
+    aux_blocks_ = j.aux.size() / 64;
+    const size_t R = n_rows_;
+    size_t sizes[] = {R,         32 * R,           32 * R,         32 * R,        32 * R,
+                      32 * R,    R,                j.aux.size(),   j.pre.size(),  32 * n_aux_,
+                      4 * n_aux_, 4 * n_aux_,      4 * n_pre_,     4 * n_pre_,    4 * n_pre_,
+                      sizeof(PatchRec) * n_patch_};
+    const int NB = sizeof(sizes) / sizeof(sizes[0]);
+    size_t total = 0;
+    for (int i = 0; i < NB; i++) total += align256(sizes[i]);
+    if (total > cap_) {
+        if (arena_) BCC_HIP_TRY(hipFree(arena_));
+        arena_ = nullptr;
+        cap_ = 0;
+        BCC_HIP_TRY(hipMalloc(&arena_, total));
+        cap_ = total;
+    }
+    uint8_t* p = (uint8_t*)arena_;
+    uint8_t* ptr[NB];
+    for (int i = 0; i < NB; i++) {
+        ptr[i] = p;
+        p += align256(sizes[i]);
+    }
+    d_tag = ptr[0]; d_x = ptr[1]; d_y = ptr[2]; d_r = ptr[3]; d_s = ptr[4]; d_m = ptr[5];
+    d_v = ptr[6]; d_aux_ = ptr[7]; d_pre_ = ptr[8]; d_auxd_ = ptr[9];
+    d_aux_off_ = (uint32_t*)ptr[10]; d_aux_nblk_ = (uint32_t*)ptr[11];
+    d_pre_off_ = (uint32_t*)ptr[12]; d_pre_nblk_ = (uint32_t*)ptr[13];
+    d_pre_row_ = (uint32_t*)ptr[14]; d_patch_ = (PatchRec*)ptr[15];
+    const void* src[] = {rows.tag.data(), rows.x.data(), rows.y.data(), rows.r.data(),
+                         rows.s.data(), rows.msg.data(), nullptr, j.aux.data(), j.pre.data(),
+                         nullptr, j.aux_off.data(), j.aux_nblk.data(), j.pre_off.data(),
+                         j.pre_nblk.data(), j.pre_row.data(), j.patches.data()};
+    for (int i = 0; i < NB; i++)
+        if (src[i] && sizes[i]) BCC_HIP_TRY(hipMemcpy(ptr[i], src[i], sizes[i], hipMemcpyHostToDevice));
+    return 0;
+}
+
+int DeviceBatch::run_sighash(void* stream) {
+    hipStream_t st = (hipStream_t)stream;
+    if (n_aux_) {
+        hipLaunchKernelGGL(sha256d_msgs_kernel, dim3((unsigned)((n_aux_ + 255) / 256)), dim3(256), 0, st,
+                           d_aux_, d_aux_off_, d_aux_nblk_, (uint32_t)n_aux_, d_auxd_, nullptr);
+        BCC_HIP_TRY(hipGetLastError());
+    }
+    if (n_patch_) {
+        size_t th = n_patch_ * 32;
+        hipLaunchKernelGGL(patch_digests_kernel, dim3((unsigned)((th + 255) / 256)), dim3(256), 0, st,
+                           d_pre_, d_patch_, d_auxd_, (uint32_t)n_patch_);
+        BCC_HIP_TRY(hipGetLastError());
+    }
+    if (n_pre_) {
+        hipLaunchKernelGGL(sha256d_msgs_kernel, dim3((unsigned)((n_pre_ + 255) / 256)), dim3(256), 0, st,
+                           d_pre_, d_pre_off_, d_pre_nblk_, (uint32_t)n_pre_, d_m, d_pre_row_);
+        BCC_HIP_TRY(hipGetLastError());
+    }
+    return 0;
+}
+
+int DeviceBatch::run_ecdsa(void* stream) {
+    BCC_HIP_TRY(hipSetDevice(dev_));
+    return mi_ecdsa_verify_device(d_tag, d_x, d_y, d_r, d_s, d_m, d_v, n_rows_, stream);
+}
+
+int DeviceBatch::run(void* stream) {
+    BCC_HIP_TRY(hipSetDevice(dev_));
+    if (int e = run_sighash(stream)) return e;
+    return run_ecdsa(stream);
+}
+
+int DeviceBatch::fetch_verdicts(uint8_t* out) {
+    BCC_HIP_TRY(hipSetDevice(dev_));
+    BCC_HIP_TRY(hipDeviceSynchronize());
+    if (n_rows_) BCC_HIP_TRY(hipMemcpy(out, d_v, n_rows_, hipMemcpyDeviceToHost));
+    return 0;
+}
+
+int DeviceBatch::fetch_msgs(uint8_t* out) {
+    BCC_HIP_TRY(hipSetDevice(dev_));
+    BCC_HIP_TRY(hipDeviceSynchronize());
+    if (n_rows_) BCC_HIP_TRY(hipMemcpy(out, d_m, 32 * n_rows_, hipMemcpyDeviceToHost));
+    return 0;
+}
+
+int gpu_verify_batch(int device, const SighashJobs& jobs, const TupleRows& rows, uint8_t* verdict) {
+    if (rows.size() == 0) return 0;
+    // one cached batch per (thread, device): repeated calls reuse the device arena
+    thread_local std::vector<DeviceBatch*> cache;
+    if ((int)cache.size() <= device) cache.resize(device + 1, nullptr);
+    if (!cache[device]) cache[device] = new DeviceBatch(device);
+    DeviceBatch& b = *cache[device];
+    if (int e = b.stage(jobs, rows)) return e;
+    if (int e = b.run(nullptr)) return e;
+    return b.fetch_verdicts(verdict);
+}
+
+}  // namespace bcc

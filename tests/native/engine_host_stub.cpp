@@ -1,0 +1,54 @@
+// tests/native/engine_host_stub.cpp — TEST ONLY.
+//
+// Lets the product's HOST logic (tx parser, interpreter, deferring checker, sighash job builder,
+// round/re-run stitching in csrc/host/*.cpp) run in a CPU-only test build: this file replaces
+// the device pipeline (csrc/sighash.hip + ecdsa_verify.hip) with the ORACLE (oracle/bcc_oracle.c)
+// evaluating the very jobs the host built (unpad -> SHA-256d -> patch -> SHA-256d -> ECDSA).
+// It is linked only into tests/native/_build/engine_host.so, never into librbc_amd.so.
+#include <cstring>
+#include <vector>
+
+#include "../../oracle/bcc_oracle.h"
+#include "../../rust-bitcoinconsensus_amd/csrc/pipeline.h"
+
+namespace bcc {
+
+static size_t unpadded_len(const uint8_t* m, size_t padded) {
+    uint64_t bits = 0;
+    for (int i = 0; i < 8; i++) bits = (bits << 8) | m[padded - 8 + i];
+    return (size_t)(bits / 8);
+}
+
+int gpu_verify_batch(int, const SighashJobs& j, const TupleRows& rows, uint8_t* verdict) {
+    std::vector<uint8_t> auxd(32 * j.aux_off.size());
+    for (size_t a = 0; a < j.aux_off.size(); a++) {
+        const uint8_t* m = &j.aux[(size_t)j.aux_off[a] * 64];
+        size_t L = (size_t)j.aux_nblk[a] * 64;
+        bcco_sha256d(m, unpadded_len(m, L), &auxd[32 * a]);
+    }
+    std::vector<uint8_t> pre = j.pre;
+    for (const auto& p : j.patches) memcpy(&pre[p.pre_byte], &auxd[32 * p.aux], 32);
+    std::vector<uint8_t> msg = rows.msg;
+    for (size_t k = 0; k < j.pre_off.size(); k++) {
+        const uint8_t* m = &pre[(size_t)j.pre_off[k] * 64];
+        size_t L = (size_t)j.pre_nblk[k] * 64;
+        bcco_sha256d(m, unpadded_len(m, L), &msg[32 * j.pre_row[k]]);
+    }
+    for (size_t i = 0; i < rows.size(); i++) {
+        uint8_t pub[65];
+        pub[0] = rows.tag[i];
+        memcpy(pub + 1, &rows.x[32 * i], 32);
+        memcpy(pub + 33, &rows.y[32 * i], 32);
+        size_t plen = (pub[0] == 2 || pub[0] == 3) ? 33 : 65;
+        uint8_t qx[32], qy[32];
+        if (!bcco_pubkey_parse(pub, plen, qx, qy)) {
+            verdict[i] = 0;
+            continue;
+        }
+        verdict[i] = (uint8_t)bcco_ecdsa_verify_raw(qx, qy, &rows.r[32 * i], &rows.s[32 * i],
+                                                    &msg[32 * i]);
+    }
+    return 0;
+}
+
+}  // namespace bcc

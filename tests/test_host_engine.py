@@ -1,0 +1,107 @@
+"""CPU: the engine's HOST logic (tx parser, interpreter, deferring checker, sighash job builder,
+re-run stitching; csrc/host/*.cpp) against the reference on the reference's own script / tx test
+data (tests/golden/script_cases.json.gz) and the crate vectors.
+
+The device pipeline is replaced by tests/native/engine_host_stub.cpp, which evaluates the host-built
+jobs with the oracle -- test-only; the product library is exercised by the -m gpu twins of these
+tests (test_consensus_gpu.py)."""
+import ctypes
+import gzip
+import json
+import os
+import subprocess
+
+import pytest
+
+from fixtures import load_json
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+SO = os.path.join(HERE, "native", "_build", "engine_host.so")
+
+
+class Item(ctypes.Structure):
+    _fields_ = [("script_pubkey", ctypes.c_void_p), ("script_pubkey_len", ctypes.c_uint),
+                ("amount", ctypes.c_int64), ("tx_to", ctypes.c_void_p),
+                ("tx_to_len", ctypes.c_uint), ("n_in", ctypes.c_uint)]
+
+
+@pytest.fixture(scope="module")
+def eng():
+    srcs = [os.path.join(HERE, "native", "engine_host_stub.cpp")]
+    hostdir = os.path.join(ROOT, "rust-bitcoinconsensus_amd", "csrc", "host")
+    srcs += [os.path.join(hostdir, f) for f in sorted(os.listdir(hostdir))
+             if f.endswith(".cpp") and f != "workload.cpp"]  # workload needs the GPU generator
+    deps = srcs + [os.path.join(hostdir, f) for f in os.listdir(hostdir) if f.endswith(".h")]
+    deps += [os.path.join(ROOT, "oracle", "bcc_oracle.c"),
+             os.path.join(ROOT, "rust-bitcoinconsensus_amd", "csrc", "pipeline.h")]
+    if not os.path.exists(SO) or any(os.path.getmtime(d) > os.path.getmtime(SO) for d in deps):
+        os.makedirs(os.path.dirname(SO), exist_ok=True)
+        subprocess.check_call(["g++", "-O2", "-std=c++17", "-shared", "-fPIC",
+                               "-I" + os.path.join(ROOT, "include"),
+                               "-I" + os.path.join(ROOT, "rust-bitcoinconsensus_amd", "csrc"),
+                               "-o", SO] + srcs + ["-x", "c", os.path.join(ROOT, "oracle", "bcc_oracle.c")])
+    L = ctypes.CDLL(SO)
+    L.bitcoinconsensus_verify_batch.restype = ctypes.c_long
+    return L
+
+
+def call(L, spk, amount, tx, nin, flags):
+    e = ctypes.c_int(-1)
+    r = L.bitcoinconsensus_verify_script_with_amount(spk, len(spk), ctypes.c_int64(amount), tx,
+                                                     len(tx), nin, flags, ctypes.byref(e))
+    return r, e.value
+
+
+def test_crate_vectors(eng):
+    for v in load_json("crate_vectors.json"):
+        got = call(eng, bytes.fromhex(v["spk"]), v["amount"], bytes.fromhex(v["tx"]), v["nin"], v["flags"])
+        assert got == (v["ret"], v["err"]), v["name"]
+
+
+def test_verify_script_no_amount(eng):
+    v = load_json("crate_vectors.json")[0]
+    spk, tx = bytes.fromhex(v["spk"]), bytes.fromhex(v["tx"])
+    e = ctypes.c_int(-1)
+    assert eng.bitcoinconsensus_verify_script(spk, len(spk), tx, len(tx), 0, 0xE15, ctypes.byref(e)) == 0
+    assert e.value == 4  # ERR_AMOUNT_REQUIRED
+    assert eng.bitcoinconsensus_verify_script(spk, len(spk), tx, len(tx), 0, 0x205, ctypes.byref(e)) == 1
+    assert e.value == 0
+    assert eng.bitcoinconsensus_version() == 1
+
+
+def cases():
+    return json.load(gzip.open(os.path.join(HERE, "golden", "script_cases.json.gz"), "rt"))
+
+
+def test_script_cases_single_calls(eng):
+    bad = []
+    for c in cases():
+        got = call(eng, bytes.fromhex(c["spk"]), c["amount"], bytes.fromhex(c["tx"]), c["nin"], c["flags"])
+        if got != (c["ret"], c["err"]):
+            bad.append((c["src"], c["flags"], got, (c["ret"], c["err"])))
+    assert not bad, bad[:10]
+
+
+def test_script_cases_as_batches(eng):
+    """verify_batch per flag set == single calls (shared tx buffers parsed once)."""
+    allc = cases()
+    by_flags = {}
+    for c in allc:
+        by_flags.setdefault(c["flags"], []).append(c)
+    for flags, cs in by_flags.items():
+        keep, txbufs = [], {}
+        arr = (Item * len(cs))()
+        for i, c in enumerate(cs):
+            spk, tx = bytes.fromhex(c["spk"]), bytes.fromhex(c["tx"])
+            bs = ctypes.create_string_buffer(spk, max(1, len(spk)))
+            bt = txbufs.setdefault(tx, ctypes.create_string_buffer(tx, max(1, len(tx))))
+            keep.append(bs)
+            arr[i] = Item(ctypes.addressof(bs), len(spk), c["amount"], ctypes.addressof(bt), len(tx), c["nin"])
+        ret = (ctypes.c_int * len(cs))()
+        err = (ctypes.c_int * len(cs))()
+        nvalid = eng.bitcoinconsensus_verify_batch(arr, len(cs), flags, ret, err)
+        exp = [(c["ret"], c["err"]) for c in cs]
+        got = list(zip(ret, err))
+        assert got == exp
+        assert nvalid == sum(r for r, _ in exp)
