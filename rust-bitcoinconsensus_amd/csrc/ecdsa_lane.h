@@ -90,18 +90,35 @@ BCC_HD void acc_add(gej& acc, bool& inf, const fe& px, const fe& py, const fe& s
     inf = rinf;
 }
 
-// Verify one tuple. tag = pubkey header byte (0 for "length invalid"), px/py as parsed from the
-// big-endian bytes (py ignored for compressed keys), r/s/m as raw integers from big-endian bytes.
-template <class QT, class GT>
-BCC_HD int ecdsa_verify_lane(u32 tag, const fe& px_in, const fe& py_in, const sc& r_in,
-                             const sc& s_in, const sc& m_in, QT& qt, const GT& gt) {
+// Everything the ladder needs after the prep phase (the Q table lives in the QT store).
+struct LadderState {
+    u32 k[4][4];   // the four odd 128-bit scalars: k1 (Q), k2 (lambda Q), u1 lo (G), u1 hi (2^128 G)
+    u32 flags;     // bit0 valid, bit1 neg(k1), bit2 neg(k2), bits 3..6 odd-corrections of k[0..3]
+    fe sigma;      // E' = E scaled by sigma: a point (x, y) of E is (x sigma^2, y sigma^3) on E'
+    sc r;          // signature r (for the x-coordinate test)
+};
+
+enum : u32 {
+    LS_VALID = 1u, LS_NEG0 = 2u, LS_NEG1 = 4u, LS_CORR0 = 8u,  // LS_CORR0 << slot
+};
+
+// Prep phase: pubkey parse/decompression (stage b), scalar checks, u1/u2, GLV split, odd fix-ups
+// and the Q table.  Returns false (and st.flags = 0) when the tuple is rejected outright.
+// tag = pubkey header byte (0 for "length invalid"), px/py as parsed from the big-endian bytes
+// (py ignored for compressed keys), r/s/m as raw integers from big-endian bytes.
+// sinv_pre: s^-1 mod n from the batched-inversion kernel (nullptr: invert here).
+template <class QT>
+BCC_HD bool ecdsa_prep_lane(u32 tag, const fe& px_in, const fe& py_in, const sc& r_in,
+                            const sc& s_in, const sc& m_in, const sc* sinv_pre, QT& qt,
+                            LadderState& st) {
     const u32 N[8] = BCC_N_LIMBS;
+    st.flags = 0;
     // ---- pubkey parse (eckey_impl.h:17-35) ----
     bool compressed = (tag == 2u || tag == 3u);
     bool full = (tag == 4u || tag == 6u || tag == 7u);
-    if (!compressed && !full) return 0;
+    if (!compressed && !full) return false;
     fe qx = px_in, qy = py_in;
-    if (!fe_lt_p(qx)) return 0;
+    if (!fe_lt_p(qx)) return false;
     {
         fe x3, t;
         fe_sqr(x3, qx);
@@ -109,19 +126,19 @@ BCC_HD int ecdsa_verify_lane(u32 tag, const fe& px_in, const fe& py_in, const sc
         fe seven = fe_const(7, 0, 0, 0, 0, 0, 0, 0);
         fe_add(x3, x3, seven);                   // x^3 + 7
         if (compressed) {
-            if (!fe_sqrt(qy, x3)) return 0;      // ge_set_xo_var: no square root
+            if (!fe_sqrt(qy, x3)) return false;  // ge_set_xo_var: no square root
             fe_normalize(qy);
             if ((qy.v[0] & 1u) != (tag == 3u ? 1u : 0u)) fe_neg(qy, qy);
         } else {
-            if (!fe_lt_p(qy)) return 0;
-            if (tag != 4u && (qy.v[0] & 1u) != (tag == 7u ? 1u : 0u)) return 0;  // hybrid parity
+            if (!fe_lt_p(qy)) return false;
+            if (tag != 4u && (qy.v[0] & 1u) != (tag == 7u ? 1u : 0u)) return false;  // hybrid parity
             fe_sqr(t, qy);
-            if (!fe_equal(t, x3)) return 0;      // ge_is_valid_var
+            if (!fe_equal(t, x3)) return false;  // ge_is_valid_var
         }
     }
     // ---- scalars (ecdsa_impl.h:216-222) ----
-    if (u256_is_zero(r_in.v) || u256_is_zero(s_in.v)) return 0;
-    if (!u256_lt(r_in.v, N) || !u256_lt(s_in.v, N)) return 0;
+    if (u256_is_zero(r_in.v) || u256_is_zero(s_in.v)) return false;
+    if (!u256_lt(r_in.v, N) || !u256_lt(s_in.v, N)) return false;
     sc m = m_in;
     if (!u256_lt(m.v, N)) {                      // scalar_set_b32 reduction
         u32 tmp[8];
@@ -129,81 +146,96 @@ BCC_HD int ecdsa_verify_lane(u32 tag, const fe& px_in, const fe& py_in, const sc
         for (int i = 0; i < 8; i++) m.v[i] = tmp[i];
     }
     sc sinv, u1, u2, k1, k2;
-    sc_inv(sinv, s_in);
+    if (sinv_pre) sinv = *sinv_pre;
+    else sc_inv(sinv, s_in);
     sc_mul(u1, m, sinv);
     sc_mul(u2, r_in, sinv);
     sc_split_lambda(k1, k2, u2);
     // |k| < 2^128: a split half whose upper 128 bits are nonzero is negative (n - |k|)
-    bool neg0 = (k1.v[4] | k1.v[5] | k1.v[6] | k1.v[7]) != 0;
-    bool neg1 = (k2.v[4] | k2.v[5] | k2.v[6] | k2.v[7]) != 0;
-    if (neg0) sc_neg(k1, k1);
-    if (neg1) sc_neg(k2, k2);
-    // the four 128-bit scalars: 0 = k1 (Q), 1 = k2 (lambda Q), 2 = u1 lo (G), 3 = u1 hi (2^128 G)
-    u32 a0 = k1.v[0], a1 = k1.v[1], a2 = k1.v[2], a3 = k1.v[3];
-    u32 b0 = k2.v[0], b1 = k2.v[1], b2 = k2.v[2], b3 = k2.v[3];
-    u32 c0 = u1.v[0], c1 = u1.v[1], c2 = u1.v[2], c3 = u1.v[3];
-    u32 d0 = u1.v[4], d1 = u1.v[5], d2 = u1.v[6], d3 = u1.v[7];
-    // make each scalar odd: k even -> use k+1, subtract the base point once at the end
-    bool corr0 = (a0 & 1u) == 0, corr1 = (b0 & 1u) == 0, corr2 = (c0 & 1u) == 0,
-         corr3 = (d0 & 1u) == 0;
-    a0 |= 1u; b0 |= 1u; c0 |= 1u; d0 |= 1u;
+    u32 flags = LS_VALID;
+    if ((k1.v[4] | k1.v[5] | k1.v[6] | k1.v[7]) != 0) {
+        sc_neg(k1, k1);
+        flags |= LS_NEG0;
+    }
+    if ((k2.v[4] | k2.v[5] | k2.v[6] | k2.v[7]) != 0) {
+        sc_neg(k2, k2);
+        flags |= LS_NEG1;
+    }
+    for (int i = 0; i < 4; i++) {
+        st.k[0][i] = k1.v[i];
+        st.k[1][i] = k2.v[i];
+        st.k[2][i] = u1.v[i];
+        st.k[3][i] = u1.v[4 + i];
+    }
+    // make each scalar odd: k even -> use k+1 (never carries), subtract the base point at the end
+    for (int s = 0; s < 4; s++) {
+        if ((st.k[s][0] & 1u) == 0) flags |= LS_CORR0 << s;
+        st.k[s][0] |= 1u;
+    }
+    st.flags = flags;
+    st.r = r_in;
 
     // ---- Q table: odd multiples on E' (shared Z; ecmult_odd_multiples_table restated) ----
-    fe sigma;  // E' = E scaled by sigma: a point (x, y) of E is (x sigma^2, y sigma^3) on E'
-    {
-        gej q1, d;
-        q1.x = qx; q1.y = qy; q1.z = fe_one();
-        gej_double(d, q1);                       // D = 2Q (Jacobian on E)
-        fe zd2, zd3, one = fe_one();
-        fe_sqr(zd2, d.z);
-        fe_mul(zd3, zd2, d.z);
-        gej cur;                                 // on E_{Zd}, D is affine (d.x, d.y)
-        fe_mul(cur.x, qx, zd2);
-        fe_mul(cur.y, qy, zd3);
-        cur.z = one;
-        qt.put(0, 0, cur.x);
-        qt.put(0, 2, cur.y);
-        for (int i = 1; i < QTAB; i++) {         // T_i = T_{i-1} + D, Z_i = Z_{i-1} * H_i
-            bool inf_unused;
-            gej nxt;
-            fe h;
-            gej_add_zinv(nxt, inf_unused, cur, d.x, d.y, one, false, &h);
-            cur = nxt;
-            qt.put(i, 0, cur.x);
-            qt.put(i, 2, cur.y);
-            qt.put(i, 1, h);                     // slot 1 holds H_i until the rescale pass
-        }
-        // rescale to the common Z_last: f_i = prod_{j>i} H_j
-        fe f = one, f2, f3, beta;
-        {
-            const u32 bl[8] = BCC_BETA_LIMBS;
-            fe_set(beta, bl);
-        }
-        for (int i = QTAB - 1; i >= 0; i--) {
-            fe ex, ey, h;
-            qt.get(i, 0, ex);
-            qt.get(i, 2, ey);
-            if (i > 0) qt.get(i, 1, h);
-            fe_sqr(f2, f);
-            fe_mul(f3, f2, f);
-            fe_mul(ex, ex, f2);
-            fe_mul(ey, ey, f3);
-            fe bx;
-            fe_mul(bx, ex, beta);
-            qt.put(i, 0, ex);
-            qt.put(i, 1, bx);
-            qt.put(i, 2, ey);
-            if (i > 0) fe_mul(f, f, h);
-        }
-        fe_mul(sigma, d.z, cur.z);               // total scale Zd * Z_last
+    gej q1, d;
+    q1.x = qx; q1.y = qy; q1.z = fe_one();
+    gej_double(d, q1);                           // D = 2Q (Jacobian on E)
+    fe zd2, zd3, one = fe_one();
+    fe_sqr(zd2, d.z);
+    fe_mul(zd3, zd2, d.z);
+    gej cur;                                     // on E_{Zd}, D is affine (d.x, d.y)
+    fe_mul(cur.x, qx, zd2);
+    fe_mul(cur.y, qy, zd3);
+    cur.z = one;
+    qt.put(0, 0, cur.x);
+    qt.put(0, 2, cur.y);
+    for (int i = 1; i < QTAB; i++) {             // T_i = T_{i-1} + D, Z_i = Z_{i-1} * H_i
+        bool inf_unused;
+        gej nxt;
+        fe h;
+        gej_add_zinv(nxt, inf_unused, cur, d.x, d.y, one, false, &h);
+        cur = nxt;
+        qt.put(i, 0, cur.x);
+        qt.put(i, 2, cur.y);
+        qt.put(i, 1, h);                         // slot 1 holds H_i until the rescale pass
     }
+    // rescale to the common Z_last: f_i = prod_{j>i} H_j
+    fe f = one, f2, f3, beta;
+    {
+        const u32 bl[8] = BCC_BETA_LIMBS;
+        fe_set(beta, bl);
+    }
+    for (int i = QTAB - 1; i >= 0; i--) {
+        fe ex, ey, h;
+        qt.get(i, 0, ex);
+        qt.get(i, 2, ey);
+        if (i > 0) qt.get(i, 1, h);
+        fe_sqr(f2, f);
+        fe_mul(f3, f2, f);
+        fe_mul(ex, ex, f2);
+        fe_mul(ey, ey, f3);
+        fe bx;
+        fe_mul(bx, ex, beta);
+        qt.put(i, 0, ex);
+        qt.put(i, 1, bx);
+        qt.put(i, 2, ey);
+        if (i > 0) fe_mul(f, f, h);
+    }
+    fe_mul(st.sigma, d.z, cur.z);                // total scale Zd * Z_last
+    return true;
+}
 
-    // ---- Strauss loop over bit positions TOPQ..0 (shared doublings) ----
+// Ladder phase: Strauss over bit positions TOPQ..0 with shared doublings, odd-fix corrections,
+// and the inversion-free x-coordinate test.  Returns the verdict.
+template <class QT, class GT>
+BCC_HD int ecdsa_ladder_lane(const LadderState& st, const QT& qt, const GT& gt) {
+    const u32 N[8] = BCC_N_LIMBS;
+    if (!(st.flags & LS_VALID)) return 0;
+    const bool neg0 = (st.flags & LS_NEG0) != 0, neg1 = (st.flags & LS_NEG1) != 0;
     gej acc;
     bool inf = false;
     {
         bool ng;
-        u32 idx = digit_index(a0, a1, a2, a3, TOPQ, WQ, TOPQ, ng);
+        u32 idx = digit_index(st.k[0][0], st.k[0][1], st.k[0][2], st.k[0][3], TOPQ, WQ, TOPQ, ng);
         qt.get((int)idx, 0, acc.x);
         qt.get((int)idx, 2, acc.y);
         if (neg0) fe_neg(acc.y, acc.y);
@@ -220,10 +252,10 @@ BCC_HD int ecdsa_verify_lane(u32 tag, const fe& px_in, const fe& py_in, const sc
             bool active = isg ? ((pos % WG) == 0 && pos <= TOPG) : ((pos % WQ) == 0);
             if (slot == 0 && pos == TOPQ) active = false;  // initial value
             if (!active) continue;
-            u32 l0 = slot == 0 ? a0 : slot == 1 ? b0 : slot == 2 ? c0 : d0;
-            u32 l1 = slot == 0 ? a1 : slot == 1 ? b1 : slot == 2 ? c1 : d1;
-            u32 l2 = slot == 0 ? a2 : slot == 1 ? b2 : slot == 2 ? c2 : d2;
-            u32 l3 = slot == 0 ? a3 : slot == 1 ? b3 : slot == 2 ? c3 : d3;
+            u32 l0 = slot == 0 ? st.k[0][0] : slot == 1 ? st.k[1][0] : slot == 2 ? st.k[2][0] : st.k[3][0];
+            u32 l1 = slot == 0 ? st.k[0][1] : slot == 1 ? st.k[1][1] : slot == 2 ? st.k[2][1] : st.k[3][1];
+            u32 l2 = slot == 0 ? st.k[0][2] : slot == 1 ? st.k[1][2] : slot == 2 ? st.k[2][2] : st.k[3][2];
+            u32 l3 = slot == 0 ? st.k[0][3] : slot == 1 ? st.k[1][3] : slot == 2 ? st.k[2][3] : st.k[3][3];
             bool dneg;
             u32 idx = digit_index(l0, l1, l2, l3, pos, isg ? WG : WQ, isg ? TOPG : TOPQ, dneg);
             fe px, py;
@@ -235,13 +267,12 @@ BCC_HD int ecdsa_verify_lane(u32 tag, const fe& px_in, const fe& py_in, const sc
             }
             bool sneg = dneg ^ (slot == 0 ? neg0 : slot == 1 ? neg1 : false);
             if (sneg) fe_neg(py, py);
-            acc_add(acc, inf, px, py, sigma, isg);
+            acc_add(acc, inf, px, py, st.sigma, isg);
         }
     }
     // ---- corrections for the scalars that were made odd: acc -= base point ----
     for (int slot = 0; slot < 4; slot++) {
-        bool active = slot == 0 ? corr0 : slot == 1 ? corr1 : slot == 2 ? corr2 : corr3;
-        if (!active) continue;
+        if (!(st.flags & (LS_CORR0 << slot))) continue;
         bool isg = slot >= 2;
         fe px, py;
         if (isg) {
@@ -252,26 +283,36 @@ BCC_HD int ecdsa_verify_lane(u32 tag, const fe& px_in, const fe& py_in, const sc
         }
         bool sneg = !(slot == 0 ? neg0 : slot == 1 ? neg1 : false);
         if (sneg) fe_neg(py, py);
-        acc_add(acc, inf, px, py, sigma, isg);
+        acc_add(acc, inf, px, py, st.sigma, isg);
     }
     if (inf) return 0;                           // R = infinity (ecdsa_impl.h:225-227)
     // ---- x-coordinate test (ecdsa_impl.h:241-273): back on E, Z_E = Z * sigma ----
     fe ze, z2, lhs, xr;
-    fe_mul(ze, acc.z, sigma);
+    fe_mul(ze, acc.z, st.sigma);
     fe_sqr(z2, ze);
-    for (int i = 0; i < 8; i++) xr.v[i] = r_in.v[i];  // r < n < p
+    for (int i = 0; i < 8; i++) xr.v[i] = st.r.v[i];  // r < n < p
     fe_mul(lhs, xr, z2);
     if (fe_equal(lhs, acc.x)) return 1;
     {
         const u32 PMN[8] = BCC_PMN_LIMBS;
-        if (!u256_lt(r_in.v, PMN)) return 0;     // xr + n >= p
+        if (!u256_lt(st.r.v, PMN)) return 0;     // xr + n >= p
         u32 xn[8];
-        u256_add(xn, r_in.v, N);
+        u256_add(xn, st.r.v, N);
         for (int i = 0; i < 8; i++) xr.v[i] = xn[i];
         fe_mul(lhs, xr, z2);
         if (fe_equal(lhs, acc.x)) return 1;
     }
     return 0;
+}
+
+// Both phases back to back (host tests, small batches).
+template <class QT, class GT>
+BCC_HD int ecdsa_verify_lane(u32 tag, const fe& px_in, const fe& py_in, const sc& r_in,
+                             const sc& s_in, const sc& m_in, QT& qt, const GT& gt,
+                             const sc* sinv_pre = nullptr) {
+    LadderState st;
+    if (!ecdsa_prep_lane(tag, px_in, py_in, r_in, s_in, m_in, sinv_pre, qt, st)) return 0;
+    return ecdsa_ladder_lane(st, qt, gt);
 }
 
 // k*G -> affine (x, y), normalized.  Used by the synthetic-workload generator (keygen, signing),

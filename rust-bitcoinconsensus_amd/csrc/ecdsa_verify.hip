@@ -1,6 +1,13 @@
-// ECDSA verify kernel for gfx950 (stage (c) of the hot path, plus stage (b) pubkey
-// decompression fused in front).  One lane = one tuple; the per-lane algorithm is
-// ecdsa_lane.h.  Inputs are the reference's b32 convention: big-endian 32-byte values.
+// ECDSA verify on gfx950: stage (c) of the hot path, with stage (b) (pubkey decompression)
+// in its prep phase.  One lane = one tuple; the per-lane algorithm is ecdsa_lane.h.
+//
+//   K_inv     batch_sinv_kernel     s^-1 mod n by Montgomery's trick over strided chunks of <= 16
+//                                   tuples (3 mults/tuple + one Fermat inversion per chunk)
+//   K_prep    ecdsa_prep_kernel     pubkey parse/decompress, u1/u2, GLV split, Q table
+//   K_ladder  ecdsa_ladder_kernel   Strauss ladder (shared doublings) + inversion-free x-check
+// K_prep and K_ladder are separate launches so that each gets its own register allocation: the
+// ladder, which is ~85% of the work, then runs at 3+ waves per SIMD instead of 1.  Tuples are
+// processed in chunks so the per-tuple scratch (Q table + ladder state, ~900 B) stays bounded.
 //
 // HBM layout (all device-resident):
 //   tag[n]            u8   pubkey header byte (0 = rejected by the host length filter)
@@ -8,16 +15,18 @@
 //   r[n][32], s[n][32]     signature scalars after lax-DER (zero on overflow)
 //   m[n][32]               sighash (raw SHA-256d bytes == big-endian integer)
 //   verdict[n]        u8   1 = valid
-// Each lane reads its 32-byte rows with two 16-byte loads; across a wave the union is one
-// contiguous 2 KiB span per row array, so the loads are fully coalesced.
+//   scratch                s^-1 [n][8] u32; per chunk: Q table [24 fe words][C], state [33][C]
+// Row loads are two 16-byte loads per lane (a wave covers one contiguous 2 KiB span); scratch is
+// word-interleaved by tuple ([word][C]) so every scratch access of a wave is one 256-byte line.
+#include <cstdlib>
+
 #include "ecdsa_lane.h"
 #include "gpu_common.h"
 
 namespace bcc {
 
-// Per-lane Q table in global memory, lane-interleaved: word (entry i, field f, limb j) of lane L
-// is at base[((i*3 + f)*8 + j) * stride + L] -> every table access of a wave is one coalesced
-// 256-byte transaction per limb.
+// Per-tuple Q table, word-interleaved: word (entry i, field f, limb j) of tuple t at
+// base[((i*3 + f)*8 + j) * stride + t].
 struct QTableGlobal {
     u32* base;
     size_t stride;
@@ -32,6 +41,8 @@ struct QTableGlobal {
         for (int j = 0; j < 8; j++) a.v[j] = p[(size_t)j * stride];
     }
 };
+constexpr int QTABLE_WORDS = QTAB * 3 * 8;  // 192
+constexpr int STATE_WORDS = 16 + 1 + 8 + 8;  // LadderState
 
 // G tables staged in LDS (16 KiB per workgroup).
 struct GTableLDS {
@@ -48,43 +59,142 @@ __device__ __forceinline__ void load_be32(fe& r, const uint8_t* p) {
     u32 w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
     fe_from_be_words(r, w);
 }
+__device__ __forceinline__ void load_be32(sc& r, const uint8_t* p) {
+    fe t;
+    load_be32(t, p);
+#pragma unroll
+    for (int k = 0; k < 8; k++) r.v[k] = t.v[k];
+}
+__device__ __forceinline__ void load_limbs(sc& r, const u32* p) {
+    const uint4* q = reinterpret_cast<const uint4*>(p);
+    uint4 a = q[0], b = q[1];
+    r.v[0] = a.x; r.v[1] = a.y; r.v[2] = a.z; r.v[3] = a.w;
+    r.v[4] = b.x; r.v[5] = b.y; r.v[6] = b.z; r.v[7] = b.w;
+}
+__device__ __forceinline__ void store_limbs(u32* p, const sc& a) {
+    uint4* q = reinterpret_cast<uint4*>(p);
+    q[0] = make_uint4(a.v[0], a.v[1], a.v[2], a.v[3]);
+    q[1] = make_uint4(a.v[4], a.v[5], a.v[6], a.v[7]);
+}
 
-__global__ __launch_bounds__(256) void ecdsa_verify_kernel(
-    const uint8_t* __restrict__ tag, const uint8_t* __restrict__ px, const uint8_t* __restrict__ py,
-    const uint8_t* __restrict__ pr, const uint8_t* __restrict__ ps, const uint8_t* __restrict__ pm,
-    uint8_t* __restrict__ verdict, u32* __restrict__ qscratch, const fe* __restrict__ gtab,
-    size_t n) {
-    __shared__ fe g_lds[2 * GTAB * 2];
-    for (int i = threadIdx.x; i < 2 * GTAB * 2; i += blockDim.x) g_lds[i] = gtab[i];
-    __syncthreads();
-    const size_t lanes = (size_t)gridDim.x * blockDim.x;
-    const size_t gid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    QTableGlobal qt{qscratch + gid, lanes};
-    GTableLDS gt{g_lds};
-    for (size_t i = gid; i < n; i += lanes) {
-        fe x, y, t;
-        sc r, s, m;
-        load_be32(x, px + 32 * i);
-        load_be32(y, py + 32 * i);
-        load_be32(t, pr + 32 * i);
-        for (int k = 0; k < 8; k++) r.v[k] = t.v[k];
-        load_be32(t, ps + 32 * i);
-        for (int k = 0; k < 8; k++) s.v[k] = t.v[k];
-        load_be32(t, pm + 32 * i);
-        for (int k = 0; k < 8; k++) m.v[k] = t.v[k];
-        verdict[i] = (uint8_t)ecdsa_verify_lane(tag[i], x, y, r, s, m, qt, gt);
+__device__ __forceinline__ void sanitize_s(sc& s) {
+    const u32 N[8] = BCC_N_LIMBS;
+    if (u256_is_zero(s.v) || !u256_lt(s.v, N)) {
+        s.v[0] = 1;
+#pragma unroll
+        for (int k = 1; k < 8; k++) s.v[k] = 0;
     }
 }
 
-// ------------------------------------------------------------------------------------------
-// per-device state: G tables + Q scratch
-// ------------------------------------------------------------------------------------------
-static constexpr int VERIFY_BLOCK = 256;
+// Montgomery's simultaneous inversion over the strided chunk {t, t+T, t+2T, ...} (coalesced:
+// at every step the wave touches 64 consecutive tuples).  s == 0 or s >= n is replaced by 1;
+// the prep kernel rejects those tuples on the original s anyway.
+__global__ __launch_bounds__(256) void batch_sinv_kernel(const uint8_t* __restrict__ ps,
+                                                         u32* __restrict__ sinv, size_t n,
+                                                         size_t T) {
+    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n || t >= T) return;
+    sc acc, s;
+    size_t last = t;
+    load_be32(acc, ps + 32 * t);
+    sanitize_s(acc);
+    store_limbs(sinv + 8 * t, acc);
+    for (size_t i = t + T; i < n; i += T) {
+        load_be32(s, ps + 32 * i);
+        sanitize_s(s);
+        sc_mul(acc, acc, s);
+        store_limbs(sinv + 8 * i, acc);  // prefix product s_t * ... * s_i
+        last = i;
+    }
+    sc inv;
+    sc_inv(inv, acc);
+    for (size_t i = last; i >= t + T; i -= T) {
+        load_be32(s, ps + 32 * i);
+        sanitize_s(s);
+        sc prev, out;
+        load_limbs(prev, sinv + 8 * (i - T));
+        sc_mul(out, inv, prev);  // (s_t..s_i)^-1 * (s_t..s_{i-1}) = s_i^-1
+        sc_mul(inv, inv, s);     // (s_t..s_{i-1})^-1
+        store_limbs(sinv + 8 * i, out);
+    }
+    store_limbs(sinv + 8 * t, inv);
+}
 
+__device__ __forceinline__ void store_state(u32* st, size_t C, const LadderState& s) {
+    int w = 0;
+#pragma unroll
+    for (int a = 0; a < 4; a++)
+#pragma unroll
+        for (int b = 0; b < 4; b++) st[(size_t)(w++) * C] = s.k[a][b];
+    st[(size_t)(w++) * C] = s.flags;
+#pragma unroll
+    for (int j = 0; j < 8; j++) st[(size_t)(w++) * C] = s.sigma.v[j];
+#pragma unroll
+    for (int j = 0; j < 8; j++) st[(size_t)(w++) * C] = s.r.v[j];
+}
+
+__device__ __forceinline__ void load_state(LadderState& s, const u32* st, size_t C) {
+    int w = 0;
+#pragma unroll
+    for (int a = 0; a < 4; a++)
+#pragma unroll
+        for (int b = 0; b < 4; b++) s.k[a][b] = st[(size_t)(w++) * C];
+    s.flags = st[(size_t)(w++) * C];
+#pragma unroll
+    for (int j = 0; j < 8; j++) s.sigma.v[j] = st[(size_t)(w++) * C];
+#pragma unroll
+    for (int j = 0; j < 8; j++) s.r.v[j] = st[(size_t)(w++) * C];
+}
+
+__global__ __launch_bounds__(256) void ecdsa_prep_kernel(
+    const uint8_t* __restrict__ tag, const uint8_t* __restrict__ px, const uint8_t* __restrict__ py,
+    const uint8_t* __restrict__ pr, const uint8_t* __restrict__ ps, const uint8_t* __restrict__ pm,
+    const u32* __restrict__ psinv, size_t base, size_t cnt, size_t C, u32* __restrict__ qtab,
+    u32* __restrict__ state) {
+    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= cnt) return;
+    const size_t i = base + t;
+    fe x, y;
+    sc r, s, m, si;
+    load_be32(x, px + 32 * i);
+    load_be32(y, py + 32 * i);
+    load_be32(r, pr + 32 * i);
+    load_be32(s, ps + 32 * i);
+    load_be32(m, pm + 32 * i);
+    load_limbs(si, psinv + 8 * i);
+    QTableGlobal qt{qtab + t, C};
+    LadderState st;
+    ecdsa_prep_lane(tag[i], x, y, r, s, m, &si, qt, st);
+    store_state(state + t, C, st);
+}
+
+__global__ __launch_bounds__(256) void ecdsa_ladder_kernel(const u32* __restrict__ state,
+                                                           const u32* __restrict__ qtab,
+                                                           const fe* __restrict__ gtab,
+                                                           uint8_t* __restrict__ verdict,
+                                                           size_t base, size_t cnt, size_t C) {
+    __shared__ fe g_lds[2 * GTAB * 2];
+    for (int i = threadIdx.x; i < 2 * GTAB * 2; i += blockDim.x) g_lds[i] = gtab[i];
+    __syncthreads();
+    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= cnt) return;
+    LadderState st;
+    load_state(st, state + t, C);
+    QTableGlobal qt{const_cast<u32*>(qtab) + t, C};
+    GTableLDS gt{g_lds};
+    verdict[base + t] = (uint8_t)ecdsa_ladder_lane(st, qt, gt);
+}
+
+// ------------------------------------------------------------------------------------------
+// per-device state: G tables, scratch
+// ------------------------------------------------------------------------------------------
 struct EcdsaDeviceState {
     fe* d_gtab = nullptr;
-    u32* d_qscratch = nullptr;
-    int grid = 0;
+    u32* d_sinv = nullptr;
+    size_t sinv_cap = 0;
+    u32* d_chunk = nullptr;  // Q tables + ladder states for one chunk
+    size_t chunk = 0;
+    int cus = 0;
 };
 
 static std::mutex g_state_mu;
@@ -100,19 +210,25 @@ static const std::vector<fe>& host_gtab() {
     return t;
 }
 
-static int ensure_state(int dev, EcdsaDeviceState** out) {
+static int ensure_state(int dev, size_t n, EcdsaDeviceState** out) {
     std::lock_guard<std::mutex> lk(g_state_mu);
     EcdsaDeviceState& st = g_state[dev];
     if (!st.d_gtab) {
-        BCC_HIP_TRY(hipSetDevice(dev));
         const auto& h = host_gtab();
         BCC_HIP_TRY(hipMalloc(&st.d_gtab, h.size() * sizeof(fe)));
         BCC_HIP_TRY(hipMemcpy(st.d_gtab, h.data(), h.size() * sizeof(fe), hipMemcpyHostToDevice));
-        int cus = 0;
-        BCC_HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-        st.grid = cus * 4;  // 4 resident 256-thread blocks per CU (VGPR-limited), grid-stride
-        size_t lanes = (size_t)st.grid * VERIFY_BLOCK;
-        BCC_HIP_TRY(hipMalloc(&st.d_qscratch, lanes * QTAB * 3 * 8 * sizeof(u32)));
+        BCC_HIP_TRY(hipDeviceGetAttribute(&st.cus, hipDeviceAttributeMultiprocessorCount, dev));
+        const char* e = getenv("BCC_CHUNK");
+        st.chunk = e ? (size_t)atol(e) : (size_t)262144;
+        st.chunk = (st.chunk + 255) & ~(size_t)255;
+        BCC_HIP_TRY(hipMalloc(&st.d_chunk, st.chunk * (QTABLE_WORDS + STATE_WORDS) * sizeof(u32)));
+    }
+    if (n > st.sinv_cap) {
+        if (st.d_sinv) BCC_HIP_TRY(hipFree(st.d_sinv));
+        st.d_sinv = nullptr;
+        size_t cap = std::max<size_t>(n, 1 << 16);
+        BCC_HIP_TRY(hipMalloc(&st.d_sinv, cap * 8 * sizeof(u32)));
+        st.sinv_cap = cap;
     }
     *out = &st;
     return 0;
@@ -126,6 +242,7 @@ extern "C" {
 
 // Device-pointer entry: all buffers already resident on the current device; launches on
 // `stream` (hipStream_t, may be null). Returns 0 on success, else a hipError_t value.
+// Concurrent callers on one device must use one stream (the scratch is per device).
 int mi_ecdsa_verify_device(const uint8_t* d_tag, const uint8_t* d_x, const uint8_t* d_y,
                            const uint8_t* d_r, const uint8_t* d_s, const uint8_t* d_m,
                            uint8_t* d_verdict, size_t n, void* stream) {
@@ -133,20 +250,28 @@ int mi_ecdsa_verify_device(const uint8_t* d_tag, const uint8_t* d_x, const uint8
     int dev = 0;
     BCC_HIP_TRY(hipGetDevice(&dev));
     EcdsaDeviceState* st = nullptr;
-    if (int e = ensure_state(dev, &st)) return e;
-    int blocks = (int)std::min<size_t>((n + VERIFY_BLOCK - 1) / VERIFY_BLOCK, (size_t)st->grid);
-    // The Q scratch is sized for st->grid blocks; the kernel strides by its own grid, so a
-    // smaller grid simply uses a prefix of it.
-    hipLaunchKernelGGL(ecdsa_verify_kernel, dim3(blocks), dim3(VERIFY_BLOCK), 0,
-                       (hipStream_t)stream, d_tag, d_x, d_y, d_r, d_s, d_m, d_verdict,
-                       st->d_qscratch, st->d_gtab, n);
+    if (int e = ensure_state(dev, n, &st)) return e;
+    hipStream_t sm = (hipStream_t)stream;
+    // K_inv: chunks of <= 16 tuples, but at least one wave per SIMD
+    size_t T = std::max<size_t>((n + 15) / 16, std::min<size_t>(n, (size_t)st->cus * 256));
+    hipLaunchKernelGGL(batch_sinv_kernel, dim3((unsigned)((T + 255) / 256)), dim3(256), 0, sm, d_s,
+                       st->d_sinv, n, T);
     BCC_HIP_TRY(hipGetLastError());
+    const size_t C = st->chunk;
+    u32* qtab = st->d_chunk;
+    u32* state = st->d_chunk + C * QTABLE_WORDS;
+    for (size_t base = 0; base < n; base += C) {
+        size_t cnt = std::min(C, n - base);
+        unsigned blocks = (unsigned)((cnt + 255) / 256);
+        hipLaunchKernelGGL(ecdsa_prep_kernel, dim3(blocks), dim3(256), 0, sm, d_tag, d_x, d_y, d_r,
+                           d_s, d_m, st->d_sinv, base, cnt, C, qtab, state);
+        BCC_HIP_TRY(hipGetLastError());
+        hipLaunchKernelGGL(ecdsa_ladder_kernel, dim3(blocks), dim3(256), 0, sm, state, qtab,
+                           st->d_gtab, d_verdict, base, cnt, C);
+        BCC_HIP_TRY(hipGetLastError());
+    }
     return 0;
 }
-
-}  // extern "C"
-
-extern "C" {
 
 // Host-buffer entry (the inner C ABI of SURVEY §8b): pub65[n] = header byte || x || y (y ignored
 // for 02/03; header 0 = rejected by the caller's CPubKey length filter), msg32/r32/s32 big-endian.
@@ -155,23 +280,19 @@ int mi_ecdsa_verify_tuples(const uint8_t* pub65, const uint8_t* msg32, const uin
                            const uint8_t* s32, uint8_t* verdict, size_t n, int device) {
     if (n == 0) return 0;
     BCC_HIP_TRY(hipSetDevice(device));
-    std::vector<uint8_t> tag(n), xy(n * 64);
-    for (size_t i = 0; i < n; i++) {
-        tag[i] = pub65[65 * i];
-        memcpy(&xy[64 * i], pub65 + 65 * i + 1, 64);
-    }
     uint8_t* d = nullptr;
-    // layout: tag | x | y | r | s | m | verdict  (32-byte rows 16-byte aligned)
+    // layout: tag | x | y | r | s | m | verdict  (32-byte rows 256-byte aligned)
     size_t tag_bytes = (n + 255) & ~(size_t)255;
     size_t row = 32 * n;
     size_t total = tag_bytes + 5 * row + tag_bytes;
     BCC_HIP_TRY(hipMalloc(&d, total));
     uint8_t *d_tag = d, *d_x = d + tag_bytes, *d_y = d_x + row, *d_r = d_y + row, *d_s = d_r + row,
             *d_m = d_s + row, *d_v = d_m + row;
-    std::vector<uint8_t> xs(row), ys(row);
+    std::vector<uint8_t> tag(n), xs(row), ys(row);
     for (size_t i = 0; i < n; i++) {
-        memcpy(&xs[32 * i], &xy[64 * i], 32);
-        memcpy(&ys[32 * i], &xy[64 * i + 32], 32);
+        tag[i] = pub65[65 * i];
+        memcpy(&xs[32 * i], pub65 + 65 * i + 1, 32);
+        memcpy(&ys[32 * i], pub65 + 65 * i + 33, 32);
     }
     int rc = 0;
     if ((rc = (int)hipMemcpy(d_tag, tag.data(), n, hipMemcpyHostToDevice)) ||

@@ -20,6 +20,7 @@
 
 #if defined(__HIPCC__)
 #include <hip/hip_runtime.h>
+#include "fe_asm.h"
 #define BCC_HD __host__ __device__ __attribute__((always_inline)) inline
 #define BCC_HD_NOINLINE __host__ __device__ __attribute__((noinline))
 #else
@@ -176,16 +177,28 @@ BCC_HD void fe_reduce512(fe& r, const u32 (&t)[16]) {
     }
 }
 
+// Device builds use the inline-asm carry-chain product / reduction (fe_asm.h); host builds
+// (tests/native) use the portable formulation above.  Both compute the same weak residue class.
 BCC_HD void fe_mul(fe& r, const fe& a, const fe& b) {
     u32 t[16];
+#if defined(__HIP_DEVICE_COMPILE__)
+    mul_256x256_asm(t, a.v, b.v);
+    fe_reduce512_asm(r.v, t);
+#else
     mul_256x256(t, a.v, b.v);
     fe_reduce512(r, t);
+#endif
 }
 
 BCC_HD void fe_sqr(fe& r, const fe& a) {
     u32 t[16];
+#if defined(__HIP_DEVICE_COMPILE__)
+    sqr_256_asm(t, a.v);
+    fe_reduce512_asm(r.v, t);
+#else
     sqr_256(t, a.v);
     fe_reduce512(r, t);
+#endif
 }
 
 // r = a + b mod p (weak)
@@ -570,13 +583,21 @@ BCC_HD void sc_reduce512(sc& r, const u32 (&t)[16]) {
 
 BCC_HD void sc_mul(sc& r, const sc& a, const sc& b) {
     u32 t[16];
+#if defined(__HIP_DEVICE_COMPILE__)
+    mul_256x256_asm(t, a.v, b.v);
+#else
     mul_256x256(t, a.v, b.v);
+#endif
     sc_reduce512(r, t);
 }
 
 BCC_HD void sc_sqr(sc& r, const sc& a) {
     u32 t[16];
+#if defined(__HIP_DEVICE_COMPILE__)
+    sqr_256_asm(t, a.v);
+#else
     sqr_256(t, a.v);
+#endif
     sc_reduce512(r, t);
 }
 
