@@ -75,6 +75,20 @@ def cpu_baseline(wl, sample, threads):
                 single_core_value=n1 / secs1, cpu_seconds=secs * threads)
 
 
+def aggregate(elapsed, n_valid, world, device="cuda"):
+    """Max of the per-rank timed wall clocks and the sum of valid verdicts over all ranks.
+    The only collectives of a bench run; they sit outside the timed region."""
+    if world <= 1:
+        return elapsed, n_valid
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    c = torch.tensor([n_valid], device=device, dtype=torch.int64)
+    dist.all_reduce(c)
+    return t.item(), int(c.item())
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -129,15 +143,7 @@ def main():
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - ts
-    if world > 1:
-        t = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = t.item()
-        cnt = torch.tensor([n_valid], device="cuda", dtype=torch.int64)
-        dist.all_reduce(cnt)
-        n_valid_all = int(cnt.item())
-    else:
-        n_valid_all = n_valid
+    elapsed, n_valid_all = aggregate(elapsed, n_valid, world)
 
     # per-kernel timing with HIP events on the launch stream (outside the timed region)
     reps = max(3, args.steps)

@@ -1,0 +1,59 @@
+"""CPU: the C-ABI library loads (no GPU needed) and exports every function include/*.h declares;
+the Python mirror exposes the Rust crate's API surface (src/lib.rs)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "rust-bitcoinconsensus_amd", "librbc_amd.so")
+
+
+def declared_functions():
+    names = set()
+    for h in ("bitcoinconsensus.h", "bcc_amd.h"):
+        src = open(os.path.join(ROOT, "include", h)).read()
+        src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+        for m in re.finditer(r"\b([a-z_][a-z0-9_]*)\s*\([^;{]*\)\s*;", src):
+            names.add(m.group(1))
+    return names - {"sizeof"}
+
+
+@pytest.fixture(scope="module")
+def lib():
+    if not os.path.exists(LIB):
+        subprocess.check_call(["make", "-s", "-C", os.path.dirname(LIB), "-j8"])
+    return ctypes.CDLL(LIB)
+
+
+def test_exports_every_declared_symbol(lib):
+    names = declared_functions()
+    assert {"bitcoinconsensus_verify_script", "bitcoinconsensus_verify_script_with_amount",
+            "bitcoinconsensus_version", "bitcoinconsensus_verify_batch",
+            "mi_ecdsa_verify_tuples"} <= names
+    missing = [n for n in sorted(names) if not hasattr(lib, n)]
+    assert not missing, missing
+
+
+def test_version_and_flag_check_need_no_gpu(lib):
+    assert lib.bitcoinconsensus_version() == 1
+    e = ctypes.c_int(-1)
+    # invalid flags are rejected before any device work (bitcoinconsensus.cpp:83-85)
+    assert lib.bitcoinconsensus_verify_script_with_amount(b"", 0, ctypes.c_int64(0), b"", 0, 0,
+                                                          0xE16, ctypes.byref(e)) == 0
+    assert e.value == 5
+    assert lib.bitcoinconsensus_verify_script(b"", 0, b"", 0, 0, 0x800, ctypes.byref(e)) == 0
+    assert e.value == 4  # ERR_AMOUNT_REQUIRED
+
+
+def test_python_mirror_api_surface():
+    import bitcoinconsensus_amd as B
+    assert B.VERIFY_ALL == 0xE15
+    assert [e.value for e in B.Error] == [0, 1, 2, 3, 4, 5]
+    assert B.height_to_flags(0) == 0
+    assert B.height_to_flags(173805) == B.VERIFY_P2SH
+    assert B.height_to_flags(481824) == B.VERIFY_ALL
+    for name in ("verify", "verify_with_flags", "verify_batch", "version", "height_to_flags"):
+        assert callable(getattr(B, name))

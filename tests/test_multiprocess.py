@@ -1,0 +1,48 @@
+"""CPU, world_size 2 over gloo: the multi-GPU bench path's aggregation (max wall time over ranks,
+sum of valid verdicts) and per-rank shard seeding, exercised without a GPU."""
+import os
+import socket
+import sys
+
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    import torch.distributed as dist
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import bench
+    elapsed, valid = bench.aggregate(1.0 + rank, 100 + rank, world, device="cpu")
+    q.put((rank, elapsed, valid))
+    dist.destroy_process_group()
+
+
+def test_aggregate_world2_gloo():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    for p in ps:
+        p.join(120)
+        assert p.exitcode == 0
+    res = sorted(q.get() for _ in range(2))
+    assert res == [(0, 2.0, 201), (1, 2.0, 201)]
+
+
+def test_single_rank_passthrough():
+    sys.path.insert(0, ROOT)
+    import bench
+    assert bench.aggregate(3.5, 7, 1) == (3.5, 7)
