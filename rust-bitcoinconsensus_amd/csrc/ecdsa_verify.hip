@@ -168,7 +168,7 @@ __global__ __launch_bounds__(256) void ecdsa_prep_kernel(
     store_state(state + t, C, st);
 }
 
-__global__ __launch_bounds__(256) void ecdsa_ladder_kernel(const u32* __restrict__ state,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void ecdsa_ladder_kernel(const u32* __restrict__ state,
                                                            const u32* __restrict__ qtab,
                                                            const fe* __restrict__ gtab,
                                                            uint8_t* __restrict__ verdict,

@@ -21,6 +21,7 @@
 #if defined(__HIPCC__)
 #include <hip/hip_runtime.h>
 #include "fe_asm.h"
+#include "fe_asm_gen.h"
 #define BCC_HD __host__ __device__ __attribute__((always_inline)) inline
 #define BCC_HD_NOINLINE __host__ __device__ __attribute__((noinline))
 #else
@@ -182,7 +183,7 @@ BCC_HD void fe_reduce512(fe& r, const u32 (&t)[16]) {
 BCC_HD void fe_mul(fe& r, const fe& a, const fe& b) {
     u32 t[16];
 #if defined(__HIP_DEVICE_COMPILE__)
-    mul_256x256_asm(t, a.v, b.v);
+    mul_256x256_col(t, a.v, b.v);
     fe_reduce512_asm(r.v, t);
 #else
     mul_256x256(t, a.v, b.v);
@@ -193,7 +194,7 @@ BCC_HD void fe_mul(fe& r, const fe& a, const fe& b) {
 BCC_HD void fe_sqr(fe& r, const fe& a) {
     u32 t[16];
 #if defined(__HIP_DEVICE_COMPILE__)
-    sqr_256_asm(t, a.v);
+    sqr_256_col(t, a.v);
     fe_reduce512_asm(r.v, t);
 #else
     sqr_256(t, a.v);
@@ -584,7 +585,7 @@ BCC_HD void sc_reduce512(sc& r, const u32 (&t)[16]) {
 BCC_HD void sc_mul(sc& r, const sc& a, const sc& b) {
     u32 t[16];
 #if defined(__HIP_DEVICE_COMPILE__)
-    mul_256x256_asm(t, a.v, b.v);
+    mul_256x256_col(t, a.v, b.v);
 #else
     mul_256x256(t, a.v, b.v);
 #endif
@@ -594,7 +595,7 @@ BCC_HD void sc_mul(sc& r, const sc& a, const sc& b) {
 BCC_HD void sc_sqr(sc& r, const sc& a) {
     u32 t[16];
 #if defined(__HIP_DEVICE_COMPILE__)
-    sqr_256_asm(t, a.v);
+    sqr_256_col(t, a.v);
 #else
     sqr_256(t, a.v);
 #endif

@@ -2,6 +2,7 @@
 // hipcc --offload-arch=gfx950 -O3 -shared -fPIC -I rust-bitcoinconsensus_amd/csrc tools/fe_bench.hip -o tools/_build/fe_bench.so
 #include "ecdsa_lane.h"
 #include "fe_asm.h"
+#include "fe_asm_gen.h"
 #include "gpu_common.h"
 
 using namespace bcc;
@@ -10,6 +11,7 @@ __device__ __forceinline__ void mul_v(int v, fe& r, const fe& a, const fe& b) {
     u32 t[16];
 #if defined(__HIP_DEVICE_COMPILE__)
     if (v == 1) { mul_256x256_asm(t, a.v, b.v); fe_reduce512_asm(r.v, t); return; }
+    if (v == 2) { mul_256x256_col(t, a.v, b.v); fe_reduce512_asm(r.v, t); return; }
 #endif
     mul_256x256(t, a.v, b.v);
     fe_reduce512(r, t);
@@ -18,6 +20,7 @@ __device__ __forceinline__ void sqr_v(int v, fe& r, const fe& a) {
     u32 t[16];
 #if defined(__HIP_DEVICE_COMPILE__)
     if (v == 1) { sqr_256_asm(t, a.v); fe_reduce512_asm(r.v, t); return; }
+    if (v == 2) { sqr_256_col(t, a.v); fe_reduce512_asm(r.v, t); return; }
 #endif
     sqr_256(t, a.v);
     fe_reduce512(r, t);
@@ -49,7 +52,9 @@ extern "C" int fe_bench(int variant, int sq, int iters, const void* in, void* ou
     BCC_HIP_TRY(hipMalloc(&d, bytes));
     BCC_HIP_TRY(hipMemcpy(d, in, bytes, hipMemcpyHostToDevice));
     auto launch = [&]() {
-        if (variant == 1 && sq) hipLaunchKernelGGL((k_fe<1, 1>), dim3(nblocks), dim3(256), 0, 0, d, iters);
+        if (variant == 2 && sq) hipLaunchKernelGGL((k_fe<2, 1>), dim3(nblocks), dim3(256), 0, 0, d, iters);
+        else if (variant == 2) hipLaunchKernelGGL((k_fe<2, 0>), dim3(nblocks), dim3(256), 0, 0, d, iters);
+        else if (variant == 1 && sq) hipLaunchKernelGGL((k_fe<1, 1>), dim3(nblocks), dim3(256), 0, 0, d, iters);
         else if (variant == 1) hipLaunchKernelGGL((k_fe<1, 0>), dim3(nblocks), dim3(256), 0, 0, d, iters);
         else if (sq) hipLaunchKernelGGL((k_fe<0, 1>), dim3(nblocks), dim3(256), 0, 0, d, iters);
         else hipLaunchKernelGGL((k_fe<0, 0>), dim3(nblocks), dim3(256), 0, 0, d, iters);
