@@ -74,6 +74,11 @@ int mi_gen_sign(const uint8_t* d32, const uint8_t* m32, const uint8_t* k32, size
 /* ---- integer-ALU microbenchmark (the roofline peak) ---------------------------------------- */
 int mi_microbench(int op, int iters, double* rate);
 
+/* ---- field self-test (tests only): one device Fp operation over n operand pairs ------------
+ * a, b, out: n x 8 little-endian u32 limbs.  op: 0 add, 1 sub, 2 mul, 3 sqr, 4/5/6 shift by
+ * 1/2/3, 7 neg, 8 is_zero (out[0]), 9 normalize.  Results are weak (< 2^256) except 8, 9. */
+int mi_fe_selftest(int op, const uint32_t* a, const uint32_t* b, uint32_t* out, size_t n);
+
 #ifdef __cplusplus
 }
 #endif

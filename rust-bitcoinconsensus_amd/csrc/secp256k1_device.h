@@ -204,6 +204,10 @@ BCC_HD void fe_sqr(fe& r, const fe& a) {
 
 // r = a + b mod p (weak)
 BCC_HD void fe_add(fe& r, const fe& a, const fe& b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    fe_add_asm(r.v, a.v, b.v);
+    return;
+#endif
     u64 c = 0;
 #pragma unroll
     for (int i = 0; i < 8; i++) {
@@ -235,6 +239,10 @@ BCC_HD void fe_add(fe& r, const fe& a, const fe& b) {
 
 // r = a - b mod p (weak)
 BCC_HD void fe_sub(fe& r, const fe& a, const fe& b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    fe_sub_asm(r.v, a.v, b.v);
+    return;
+#endif
     u64 c = 0;  // borrow propagation via two's complement
     u32 borrow = 0;
 #pragma unroll
@@ -304,10 +312,14 @@ BCC_HD bool fe_is_zero_norm(const fe& a) {  // a must be normalized
     return x == 0;
 }
 
+// a weak value (< 2^256) is 0 mod p iff it is 0 or p: no carry chain needed
 BCC_HD bool fe_is_zero(const fe& a) {
-    fe t = a;
-    fe_normalize(t);
-    return fe_is_zero_norm(t);
+    u32 z = 0, q = (a.v[0] ^ 0xFFFFFC2Fu) | (a.v[1] ^ 0xFFFFFFFEu);
+#pragma unroll
+    for (int i = 0; i < 8; i++) z |= a.v[i];
+#pragma unroll
+    for (int i = 2; i < 8; i++) q |= ~a.v[i];
+    return z == 0 || q == 0;
 }
 
 BCC_HD bool fe_equal(const fe& a, const fe& b) {
@@ -353,6 +365,16 @@ BCC_HD void fe_mul_int(fe& r, const fe& a, u32 k) {  // small k (< 2^20)
             r.v[i] = lo32(c);
         }
     }
+}
+
+// r = 2^S a (S = 1..3)
+template <int S>
+BCC_HD void fe_shl(fe& r, const fe& a) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    fe_shl_asm<S>(r.v, a.v);
+#else
+    fe_mul_int(r, a, 1u << S);
+#endif
 }
 
 BCC_HD void fe_sqr_n(fe& r, const fe& a, int n) {
@@ -692,16 +714,17 @@ BCC_HD void gej_double(gej& r, const gej& a) {
     fe_sqr(t, t);            // (X+B)^2
     fe_sub(t, t, A);
     fe_sub(t, t, C);
-    fe_add(D, t, t);         // D = 2((X+B)^2 - A - C)
-    fe_mul_int(E, A, 3);     // E = 3A
+    fe_shl<1>(D, t);         // D = 2((X+B)^2 - A - C)
+    fe_shl<1>(E, A);
+    fe_add(E, E, A);         // E = 3A
     fe_sqr(F, E);            // F = E^2
     fe_mul(r.z, a.y, a.z);
-    fe_add(r.z, r.z, r.z);   // Z3 = 2YZ
-    fe_add(t, D, D);
+    fe_shl<1>(r.z, r.z);     // Z3 = 2YZ
+    fe_shl<1>(t, D);
     fe_sub(r.x, F, t);       // X3 = F - 2D
     fe_sub(t, D, r.x);
     fe_mul(t, E, t);
-    fe_mul_int(C, C, 8);
+    fe_shl<3>(C, C);
     fe_sub(r.y, t, C);       // Y3 = E(D - X3) - 8C
 }
 

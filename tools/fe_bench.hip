@@ -3,6 +3,7 @@
 #include "ecdsa_lane.h"
 #include "fe_asm.h"
 #include "fe_asm_gen.h"
+#include "fe29.h"
 #include "gpu_common.h"
 
 using namespace bcc;
@@ -29,6 +30,27 @@ __device__ __forceinline__ void sqr_v(int v, fe& r, const fe& a) {
 template <int V, int SQ>
 __global__ __launch_bounds__(256) void k_fe(fe* io, int iters) {
     size_t g = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    if (V == 3) {  // radix 2^29
+        fe9 a9, b9, c9;
+        fe9_from_fe(a9, io[2 * g]);
+        fe9_from_fe(b9, io[2 * g + 1]);
+        c9 = b9;
+        for (int i = 0; i < iters; i++) {
+            if (SQ) {
+                fe9_sqr(a9, a9);
+                fe9_sqr(c9, c9);
+            } else {
+                fe9_mul(a9, a9, b9);
+                fe9_mul(c9, c9, b9);
+            }
+        }
+        fe a, c;
+        fe9_to_fe(a, a9);
+        fe9_to_fe(c, c9);
+        io[2 * g] = a;
+        io[2 * g + 1] = c;
+        return;
+    }
     fe a = io[2 * g], b = io[2 * g + 1], c = b;
     for (int i = 0; i < iters; i++) {
         if (SQ) {
@@ -52,7 +74,9 @@ extern "C" int fe_bench(int variant, int sq, int iters, const void* in, void* ou
     BCC_HIP_TRY(hipMalloc(&d, bytes));
     BCC_HIP_TRY(hipMemcpy(d, in, bytes, hipMemcpyHostToDevice));
     auto launch = [&]() {
-        if (variant == 2 && sq) hipLaunchKernelGGL((k_fe<2, 1>), dim3(nblocks), dim3(256), 0, 0, d, iters);
+        if (variant == 3 && sq) hipLaunchKernelGGL((k_fe<3, 1>), dim3(nblocks), dim3(256), 0, 0, d, iters);
+        else if (variant == 3) hipLaunchKernelGGL((k_fe<3, 0>), dim3(nblocks), dim3(256), 0, 0, d, iters);
+        else if (variant == 2 && sq) hipLaunchKernelGGL((k_fe<2, 1>), dim3(nblocks), dim3(256), 0, 0, d, iters);
         else if (variant == 2) hipLaunchKernelGGL((k_fe<2, 0>), dim3(nblocks), dim3(256), 0, 0, d, iters);
         else if (variant == 1 && sq) hipLaunchKernelGGL((k_fe<1, 1>), dim3(nblocks), dim3(256), 0, 0, d, iters);
         else if (variant == 1) hipLaunchKernelGGL((k_fe<1, 0>), dim3(nblocks), dim3(256), 0, 0, d, iters);
