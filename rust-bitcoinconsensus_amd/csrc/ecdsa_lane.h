@@ -96,6 +96,9 @@ struct LadderState {
     u32 flags;     // bit0 valid, bit1 neg(k1), bit2 neg(k2), bits 3..6 odd-corrections of k[0..3]
     fe sigma;      // E' = E scaled by sigma: a point (x, y) of E is (x sigma^2, y sigma^3) on E'
     sc r;          // signature r (for the x-coordinate test)
+    // the ladder reads the state through these (the device view loads k and r at use)
+    BCC_HD u32 kword(int s, int w) const { return k[s][w]; }
+    BCC_HD void get_r(sc& o) const { o = r; }
 };
 
 enum : u32 {
@@ -226,8 +229,8 @@ BCC_HD bool ecdsa_prep_lane(u32 tag, const fe& px_in, const fe& py_in, const sc&
 
 // Ladder phase: Strauss over bit positions TOPQ..0 with shared doublings, odd-fix corrections,
 // and the inversion-free x-coordinate test.  Returns the verdict.
-template <class QT, class GT>
-BCC_HD int ecdsa_ladder_lane(const LadderState& st, const QT& qt, const GT& gt) {
+template <class ST, class QT, class GT>
+BCC_HD int ecdsa_ladder_lane(const ST& st, const QT& qt, const GT& gt) {
     const u32 N[8] = BCC_N_LIMBS;
     if (!(st.flags & LS_VALID)) return 0;
     const bool neg0 = (st.flags & LS_NEG0) != 0, neg1 = (st.flags & LS_NEG1) != 0;
@@ -235,29 +238,42 @@ BCC_HD int ecdsa_ladder_lane(const LadderState& st, const QT& qt, const GT& gt) 
     bool inf = false;
     {
         bool ng;
-        u32 idx = digit_index(st.k[0][0], st.k[0][1], st.k[0][2], st.k[0][3], TOPQ, WQ, TOPQ, ng);
+        u32 idx = digit_index(st.kword(0, 0), st.kword(0, 1), st.kword(0, 2), st.kword(0, 3), TOPQ, WQ,
+                              TOPQ, ng);
         qt.get((int)idx, 0, acc.x);
         qt.get((int)idx, 2, acc.y);
         if (neg0) fe_neg(acc.y, acc.y);
         acc.z = fe_one();
     }
-    for (int pos = TOPQ; pos >= 0; pos--) {
-        if (pos != TOPQ && !inf) {
+    // One loop, one call site of the doubling and of the addition: the body is compiled once
+    // (a few thousand instructions) and stays resident in the instruction cache.  pos == -1 is
+    // the odd-fix step: for every scalar that was made odd, add the negated base point.
+#pragma unroll 1
+    for (int pos = TOPQ; pos >= -1; pos--) {
+        if (pos >= 0 && pos != TOPQ && !inf) {
             gej t;
             gej_double(t, acc);
             acc = t;
         }
+#pragma unroll 1
         for (int slot = 0; slot < 4; slot++) {
-            bool isg = slot >= 2;
-            bool active = isg ? ((pos % WG) == 0 && pos <= TOPG) : ((pos % WQ) == 0);
-            if (slot == 0 && pos == TOPQ) active = false;  // initial value
-            if (!active) continue;
-            u32 l0 = slot == 0 ? st.k[0][0] : slot == 1 ? st.k[1][0] : slot == 2 ? st.k[2][0] : st.k[3][0];
-            u32 l1 = slot == 0 ? st.k[0][1] : slot == 1 ? st.k[1][1] : slot == 2 ? st.k[2][1] : st.k[3][1];
-            u32 l2 = slot == 0 ? st.k[0][2] : slot == 1 ? st.k[1][2] : slot == 2 ? st.k[2][2] : st.k[3][2];
-            u32 l3 = slot == 0 ? st.k[0][3] : slot == 1 ? st.k[1][3] : slot == 2 ? st.k[2][3] : st.k[3][3];
-            bool dneg;
-            u32 idx = digit_index(l0, l1, l2, l3, pos, isg ? WG : WQ, isg ? TOPG : TOPQ, dneg);
+            const bool isg = slot >= 2;
+            const bool kneg = slot == 0 ? neg0 : slot == 1 ? neg1 : false;
+            u32 idx;
+            bool sneg;
+            if (pos >= 0) {
+                bool active = isg ? ((pos % WG) == 0 && pos <= TOPG) : ((pos % WQ) == 0);
+                if (slot == 0 && pos == TOPQ) active = false;  // initial value
+                if (!active) continue;
+                bool dneg;
+                idx = digit_index(st.kword(slot, 0), st.kword(slot, 1), st.kword(slot, 2),
+                                  st.kword(slot, 3), pos, isg ? WG : WQ, isg ? TOPG : TOPQ, dneg);
+                sneg = dneg ^ kneg;
+            } else {
+                if (!(st.flags & (LS_CORR0 << slot))) continue;  // per lane
+                idx = 0;
+                sneg = !kneg;
+            }
             fe px, py;
             if (isg) {
                 gt.get(slot - 2, (int)idx, px, py);
@@ -265,39 +281,25 @@ BCC_HD int ecdsa_ladder_lane(const LadderState& st, const QT& qt, const GT& gt) 
                 qt.get((int)idx, slot == 0 ? 0 : 1, px);
                 qt.get((int)idx, 2, py);
             }
-            bool sneg = dneg ^ (slot == 0 ? neg0 : slot == 1 ? neg1 : false);
             if (sneg) fe_neg(py, py);
             acc_add(acc, inf, px, py, st.sigma, isg);
         }
     }
-    // ---- corrections for the scalars that were made odd: acc -= base point ----
-    for (int slot = 0; slot < 4; slot++) {
-        if (!(st.flags & (LS_CORR0 << slot))) continue;
-        bool isg = slot >= 2;
-        fe px, py;
-        if (isg) {
-            gt.get(slot - 2, 0, px, py);
-        } else {
-            qt.get(0, slot == 0 ? 0 : 1, px);
-            qt.get(0, 2, py);
-        }
-        bool sneg = !(slot == 0 ? neg0 : slot == 1 ? neg1 : false);
-        if (sneg) fe_neg(py, py);
-        acc_add(acc, inf, px, py, st.sigma, isg);
-    }
     if (inf) return 0;                           // R = infinity (ecdsa_impl.h:225-227)
     // ---- x-coordinate test (ecdsa_impl.h:241-273): back on E, Z_E = Z * sigma ----
     fe ze, z2, lhs, xr;
+    sc sr;
+    st.get_r(sr);
     fe_mul(ze, acc.z, st.sigma);
     fe_sqr(z2, ze);
-    for (int i = 0; i < 8; i++) xr.v[i] = st.r.v[i];  // r < n < p
+    for (int i = 0; i < 8; i++) xr.v[i] = sr.v[i];  // r < n < p
     fe_mul(lhs, xr, z2);
     if (fe_equal(lhs, acc.x)) return 1;
     {
         const u32 PMN[8] = BCC_PMN_LIMBS;
-        if (!u256_lt(st.r.v, PMN)) return 0;     // xr + n >= p
+        if (!u256_lt(sr.v, PMN)) return 0;       // xr + n >= p
         u32 xn[8];
-        u256_add(xn, st.r.v, N);
+        u256_add(xn, sr.v, N);
         for (int i = 0; i < 8; i++) xr.v[i] = xn[i];
         fe_mul(lhs, xr, z2);
         if (fe_equal(lhs, acc.x)) return 1;

@@ -146,7 +146,26 @@ __device__ __forceinline__ void load_state(LadderState& s, const u32* st, size_t
     for (int j = 0; j < 8; j++) s.r.v[j] = st[(size_t)(w++) * C];
 }
 
-__global__ __launch_bounds__(256) void ecdsa_prep_kernel(
+// The ladder's view of its state: flags and sigma live in registers; the scalar words and r
+// are loaded where they are used (store_state layout), which keeps 24 VGPRs free across the
+// loop.  The empty asm hides the address from LICM so the loads stay at their use.
+struct LadderStateView {
+    const u32* p;
+    size_t C;
+    u32 flags;
+    fe sigma;
+    __device__ __forceinline__ u32 kword(int s, int w) const {
+        const u32* q = p;
+        asm volatile("" : "+v"(q));
+        return q[(size_t)(s * 4 + w) * C];
+    }
+    __device__ __forceinline__ void get_r(sc& o) const {
+#pragma unroll
+        for (int j = 0; j < 8; j++) o.v[j] = p[(25 + j) * C];
+    }
+};
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void ecdsa_prep_kernel(
     const uint8_t* __restrict__ tag, const uint8_t* __restrict__ px, const uint8_t* __restrict__ py,
     const uint8_t* __restrict__ pr, const uint8_t* __restrict__ ps, const uint8_t* __restrict__ pm,
     const u32* __restrict__ psinv, size_t base, size_t cnt, size_t C, u32* __restrict__ qtab,
@@ -168,7 +187,7 @@ __global__ __launch_bounds__(256) void ecdsa_prep_kernel(
     store_state(state + t, C, st);
 }
 
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void ecdsa_ladder_kernel(const u32* __restrict__ state,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) void ecdsa_ladder_kernel(const u32* __restrict__ state,
                                                            const u32* __restrict__ qtab,
                                                            const fe* __restrict__ gtab,
                                                            uint8_t* __restrict__ verdict,
@@ -178,8 +197,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
     __syncthreads();
     const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= cnt) return;
-    LadderState st;
-    load_state(st, state + t, C);
+    LadderStateView st;
+    st.p = state + t;
+    st.C = C;
+    st.flags = st.p[16 * C];
+#pragma unroll
+    for (int j = 0; j < 8; j++) st.sigma.v[j] = st.p[(17 + j) * C];
     QTableGlobal qt{const_cast<u32*>(qtab) + t, C};
     GTableLDS gt{g_lds};
     verdict[base + t] = (uint8_t)ecdsa_ladder_lane(st, qt, gt);

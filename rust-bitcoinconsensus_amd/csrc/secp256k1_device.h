@@ -379,6 +379,7 @@ BCC_HD void fe_shl(fe& r, const fe& a) {
 
 BCC_HD void fe_sqr_n(fe& r, const fe& a, int n) {
     r = a;
+#pragma unroll 1
     for (int i = 0; i < n; i++) fe_sqr(r, r);
 }
 
