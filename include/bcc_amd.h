@@ -30,6 +30,19 @@ int mi_ecdsa_verify_device(const uint8_t* d_tag, const uint8_t* d_x, const uint8
                            const uint8_t* d_r, const uint8_t* d_s, const uint8_t* d_m,
                            uint8_t* d_verdict, size_t n, void* stream);
 
+/* ---- BIP340 Schnorr (config C5) -------------------------------------------------------------
+ * Replaces secp256k1_xonly_pubkey_parse + secp256k1_schnorrsig_verify per signature
+ * (secp256k1/src/modules/extrakeys/main_impl.h:21-39, modules/schnorrsig/main_impl.h:190-237),
+ * as bound by Core's XOnlyPubKey::VerifySchnorr (depend/bitcoin/src/pubkey.cpp:176-182).
+ * Row i: sig64 = r.x || s, msg32, xonly32 = the key's 32 serialized bytes (a key that does not
+ * parse verifies false).  verdict[i] = 1 iff valid. */
+int mi_schnorr_verify_tuples(const uint8_t* sig64, const uint8_t* msg32, const uint8_t* xonly32,
+                             uint8_t* verdict, size_t n, int device);
+/* Same with device-resident rows, launched on `stream`.  Asynchronous. */
+int mi_schnorr_verify_device(const uint8_t* d_sig64, const uint8_t* d_msg32,
+                             const uint8_t* d_xonly32, uint8_t* d_verdict, size_t n,
+                             void* stream);
+
 /* ---- engine configuration / statistics ---------------------------------------------------- */
 /* Device used by the bitcoinconsensus_* entry points of the calling process (default 0, or the
  * BCC_DEVICE environment variable). */
@@ -70,6 +83,9 @@ int mi_gen_pubkeys(const uint8_t* d32, size_t n, uint8_t* x32, uint8_t* y32, uin
                    int device);
 int mi_gen_sign(const uint8_t* d32, const uint8_t* m32, const uint8_t* k32, size_t n,
                 uint8_t* r32, uint8_t* s32, uint8_t* ok, int device);
+/* BIP340 sig64 (nonce k given) + the x-only key of d, for n (d, m, k) rows. */
+int mi_gen_schnorr_sign(const uint8_t* d32, const uint8_t* m32, const uint8_t* k32, size_t n,
+                        uint8_t* sig64, uint8_t* xonly32, uint8_t* ok, int device);
 
 /* ---- integer-ALU microbenchmark (the roofline peak) ---------------------------------------- */
 int mi_microbench(int op, int iters, double* rate);

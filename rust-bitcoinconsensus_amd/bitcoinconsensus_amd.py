@@ -61,6 +61,8 @@ def lib():
         vp = ctypes.c_void_p
         L.mi_ecdsa_verify_tuples.argtypes = [u8p, u8p, u8p, u8p, u8p, sz, ctypes.c_int]
         L.mi_ecdsa_verify_device.argtypes = [vp] * 7 + [sz, vp]
+        L.mi_schnorr_verify_tuples.argtypes = [u8p, u8p, u8p, u8p, sz, ctypes.c_int]
+        L.mi_schnorr_verify_device.argtypes = [vp] * 4 + [sz, vp]
         L.mi_microbench.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_double)]
         _bind_consensus(L)
         _lib = L
@@ -108,6 +110,7 @@ def _bind_consensus(L):
     L.bcc_workload_item.restype = sz
     L.mi_gen_pubkeys.argtypes = [u8p, sz, u8p, u8p, u8p, ctypes.c_int]
     L.mi_gen_sign.argtypes = [u8p, u8p, u8p, sz, u8p, u8p, u8p, ctypes.c_int]
+    L.mi_gen_schnorr_sign.argtypes = [u8p, u8p, u8p, sz, u8p, u8p, u8p, ctypes.c_int]
 
 
 class Workload:
@@ -258,6 +261,37 @@ def ecdsa_verify_tuples(pub65, msg32, r32, s32, device=0):
     if rc != 0:
         raise RuntimeError(f"mi_ecdsa_verify_tuples failed: hip error {rc}")
     return out.raw[:n]
+
+
+def schnorr_verify_tuples(sig64, msg32, xonly32, device=0):
+    """BIP340 tuple ABI (config C5): n rows as concatenated byte strings -> bytes of verdicts.
+    Row semantics of secp256k1_xonly_pubkey_parse + secp256k1_schnorrsig_verify."""
+    n = len(msg32) // 32
+    assert len(sig64) == 64 * n and len(xonly32) == 32 * n
+    out = ctypes.create_string_buffer(max(n, 1))
+    rc = lib().mi_schnorr_verify_tuples(sig64, msg32, xonly32, out, n, device)
+    if rc != 0:
+        raise RuntimeError(f"mi_schnorr_verify_tuples failed: hip error {rc}")
+    return out.raw[:n]
+
+
+def schnorr_verify_device(d_sig64, d_msg32, d_xonly32, d_verdict, n, stream=None):
+    """Device-pointer BIP340 entry (pointers as ints, e.g. torch tensor data_ptr())."""
+    rc = lib().mi_schnorr_verify_device(d_sig64, d_msg32, d_xonly32, d_verdict, n, stream)
+    if rc != 0:
+        raise RuntimeError(f"mi_schnorr_verify_device failed: hip error {rc}")
+
+
+def gen_schnorr_sign(d32, m32, k32, device=0):
+    """Synthetic-input generator: BIP340 (sig64, xonly32, ok) for n (d, m, nonce) rows."""
+    n = len(d32) // 32
+    sig = ctypes.create_string_buffer(64 * max(n, 1))
+    xo = ctypes.create_string_buffer(32 * max(n, 1))
+    ok = ctypes.create_string_buffer(max(n, 1))
+    rc = lib().mi_gen_schnorr_sign(d32, m32, k32, n, sig, xo, ok, device)
+    if rc != 0:
+        raise RuntimeError(f"mi_gen_schnorr_sign failed: hip error {rc}")
+    return sig.raw[: 64 * n], xo.raw[: 32 * n], ok.raw[:n]
 
 
 def microbench(op, iters=4096):

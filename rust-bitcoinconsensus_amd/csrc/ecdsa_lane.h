@@ -1,16 +1,19 @@
-// Per-lane ECDSA verification: one lane = one (pubkey, msg32, r, s) tuple.
+// Per-lane signature verification: one lane = one (pubkey, msg32, r, s) tuple.
 //
-// Restates secp256k1_ecdsa_verify semantics (secp256k1.c:423-438 + ecdsa_impl.h:207-275 +
-// eckey_impl.h:17-35) with a SIMT-friendly algorithm:
+// ECDSA restates secp256k1_ecdsa_verify semantics (secp256k1.c:423-438 + ecdsa_impl.h:207-275 +
+// eckey_impl.h:17-35); BIP340 restates secp256k1_schnorrsig_verify (modules/schnorrsig/
+// main_impl.h:190-237) with the x-only lift of modules/extrakeys/main_impl.h:21-39.  Both share
+// one SIMT-friendly multi-scalar ladder:
 //   R = u1*G + u2*Q,  u2 = k1 + lambda*k2 (GLV),  u1 = lo + 2^128*hi
 //   four 128-bit scalars, each recoded into SIGNED ODD fixed windows (every digit nonzero, so
 //   every lane of a wave adds at the same bit positions: no wNAF divergence);
 //   Q table {1,3,..,15}Q on an isomorphic curve (shared Z, no inversion), G tables in LDS;
-//   inversion-free final test r*Z^2 == X (or (r+n)*Z^2 == X when r < p-n).
+//   inversion-free final test r*Z^2 == X (ECDSA also (r+n)*Z^2 == X when r < p-n).
 // Verdicts are a pure function of the group arithmetic, so they equal the reference's on every
 // input, including the exceptional additions (P == +-Q) that adversarial inputs can reach.
 #pragma once
 #include "secp256k1_device.h"
+#include "sha256_device.h"
 
 namespace bcc {
 
@@ -95,7 +98,7 @@ struct LadderState {
     u32 k[4][4];   // the four odd 128-bit scalars: k1 (Q), k2 (lambda Q), u1 lo (G), u1 hi (2^128 G)
     u32 flags;     // bit0 valid, bit1 neg(k1), bit2 neg(k2), bits 3..6 odd-corrections of k[0..3]
     fe sigma;      // E' = E scaled by sigma: a point (x, y) of E is (x sigma^2, y sigma^3) on E'
-    sc r;          // signature r (for the x-coordinate test)
+    sc r;          // x-coordinate to test against: ECDSA r, or BIP340 r.x (< p)
     // the ladder reads the state through these (the device view loads k and r at use)
     BCC_HD u32 kword(int s, int w) const { return k[s][w]; }
     BCC_HD void get_r(sc& o) const { o = r; }
@@ -105,54 +108,10 @@ enum : u32 {
     LS_VALID = 1u, LS_NEG0 = 2u, LS_NEG1 = 4u, LS_CORR0 = 8u,  // LS_CORR0 << slot
 };
 
-// Prep phase: pubkey parse/decompression (stage b), scalar checks, u1/u2, GLV split, odd fix-ups
-// and the Q table.  Returns false (and st.flags = 0) when the tuple is rejected outright.
-// tag = pubkey header byte (0 for "length invalid"), px/py as parsed from the big-endian bytes
-// (py ignored for compressed keys), r/s/m as raw integers from big-endian bytes.
-// sinv_pre: s^-1 mod n from the batched-inversion kernel (nullptr: invert here).
-template <class QT>
-BCC_HD bool ecdsa_prep_lane(u32 tag, const fe& px_in, const fe& py_in, const sc& r_in,
-                            const sc& s_in, const sc& m_in, const sc* sinv_pre, QT& qt,
-                            LadderState& st) {
-    const u32 N[8] = BCC_N_LIMBS;
-    st.flags = 0;
-    // ---- pubkey parse (eckey_impl.h:17-35) ----
-    bool compressed = (tag == 2u || tag == 3u);
-    bool full = (tag == 4u || tag == 6u || tag == 7u);
-    if (!compressed && !full) return false;
-    fe qx = px_in, qy = py_in;
-    if (!fe_lt_p(qx)) return false;
-    {
-        fe x3, t;
-        fe_sqr(x3, qx);
-        fe_mul(x3, x3, qx);
-        fe seven = fe_const(7, 0, 0, 0, 0, 0, 0, 0);
-        fe_add(x3, x3, seven);                   // x^3 + 7
-        if (compressed) {
-            if (!fe_sqrt(qy, x3)) return false;  // ge_set_xo_var: no square root
-            fe_normalize(qy);
-            if ((qy.v[0] & 1u) != (tag == 3u ? 1u : 0u)) fe_neg(qy, qy);
-        } else {
-            if (!fe_lt_p(qy)) return false;
-            if (tag != 4u && (qy.v[0] & 1u) != (tag == 7u ? 1u : 0u)) return false;  // hybrid parity
-            fe_sqr(t, qy);
-            if (!fe_equal(t, x3)) return false;  // ge_is_valid_var
-        }
-    }
-    // ---- scalars (ecdsa_impl.h:216-222) ----
-    if (u256_is_zero(r_in.v) || u256_is_zero(s_in.v)) return false;
-    if (!u256_lt(r_in.v, N) || !u256_lt(s_in.v, N)) return false;
-    sc m = m_in;
-    if (!u256_lt(m.v, N)) {                      // scalar_set_b32 reduction
-        u32 tmp[8];
-        u256_sub(tmp, m.v, N);
-        for (int i = 0; i < 8; i++) m.v[i] = tmp[i];
-    }
-    sc sinv, u1, u2, k1, k2;
-    if (sinv_pre) sinv = *sinv_pre;
-    else sc_inv(sinv, s_in);
-    sc_mul(u1, m, sinv);
-    sc_mul(u2, r_in, sinv);
+// The ladder's scalars: u2 (for Q) split by GLV into k1 + lambda k2, u1 (for G) split at bit
+// 128 (ecmult_impl.h:446-559 splits the same way); every half made odd.  Sets st.k, st.flags.
+BCC_HD void set_ladder_scalars(LadderState& st, const sc& u1, const sc& u2) {
+    sc k1, k2;
     sc_split_lambda(k1, k2, u2);
     // |k| < 2^128: a split half whose upper 128 bits are nonzero is negative (n - |k|)
     u32 flags = LS_VALID;
@@ -176,9 +135,13 @@ BCC_HD bool ecdsa_prep_lane(u32 tag, const fe& px_in, const fe& py_in, const sc&
         st.k[s][0] |= 1u;
     }
     st.flags = flags;
-    st.r = r_in;
+}
 
-    // ---- Q table: odd multiples on E' (shared Z; ecmult_odd_multiples_table restated) ----
+// Q table: odd multiples {1,3,..,15}Q on E' with one shared Z (ecmult_odd_multiples_table +
+// ge_globalz_set_table_gej restated, ecmult_impl.h:85-143), plus the lambda images beta*x.
+// Returns sigma, the scale of E' (total Z of the table).
+template <class QT>
+BCC_HD void build_q_table(const fe& qx, const fe& qy, QT& qt, fe& sigma) {
     gej q1, d;
     q1.x = qx; q1.y = qy; q1.z = fe_one();
     gej_double(d, q1);                           // D = 2Q (Jacobian on E)
@@ -223,18 +186,73 @@ BCC_HD bool ecdsa_prep_lane(u32 tag, const fe& px_in, const fe& py_in, const sc&
         qt.put(i, 2, ey);
         if (i > 0) fe_mul(f, f, h);
     }
-    fe_mul(st.sigma, d.z, cur.z);                // total scale Zd * Z_last
+    fe_mul(sigma, d.z, cur.z);                   // total scale Zd * Z_last
+}
+
+// x^3 + 7
+BCC_HD void curve_rhs(fe& r, const fe& x) {
+    fe seven = fe_const(7, 0, 0, 0, 0, 0, 0, 0);
+    fe_sqr(r, x);
+    fe_mul(r, r, x);
+    fe_add(r, r, seven);
+}
+
+// Prep phase: pubkey parse/decompression (stage b), scalar checks, u1/u2, GLV split, odd fix-ups
+// and the Q table.  Returns false (and st.flags = 0) when the tuple is rejected outright.
+// tag = pubkey header byte (0 for "length invalid"), px/py as parsed from the big-endian bytes
+// (py ignored for compressed keys), r/s/m as raw integers from big-endian bytes.
+// sinv_pre: s^-1 mod n from the batched-inversion kernel (nullptr: invert here).
+template <class QT>
+BCC_HD bool ecdsa_prep_lane(u32 tag, const fe& px_in, const fe& py_in, const sc& r_in,
+                            const sc& s_in, const sc& m_in, const sc* sinv_pre, QT& qt,
+                            LadderState& st) {
+    const u32 N[8] = BCC_N_LIMBS;
+    st.flags = 0;
+    // ---- pubkey parse (eckey_impl.h:17-35) ----
+    bool compressed = (tag == 2u || tag == 3u);
+    bool full = (tag == 4u || tag == 6u || tag == 7u);
+    if (!compressed && !full) return false;
+    fe qx = px_in, qy = py_in;
+    if (!fe_lt_p(qx)) return false;
+    {
+        fe x3, t;
+        curve_rhs(x3, qx);                       // x^3 + 7
+        if (compressed) {
+            if (!fe_sqrt(qy, x3)) return false;  // ge_set_xo_var: no square root
+            fe_normalize(qy);
+            if ((qy.v[0] & 1u) != (tag == 3u ? 1u : 0u)) fe_neg(qy, qy);
+        } else {
+            if (!fe_lt_p(qy)) return false;
+            if (tag != 4u && (qy.v[0] & 1u) != (tag == 7u ? 1u : 0u)) return false;  // hybrid parity
+            fe_sqr(t, qy);
+            if (!fe_equal(t, x3)) return false;  // ge_is_valid_var
+        }
+    }
+    // ---- scalars (ecdsa_impl.h:216-222) ----
+    if (u256_is_zero(r_in.v) || u256_is_zero(s_in.v)) return false;
+    if (!u256_lt(r_in.v, N) || !u256_lt(s_in.v, N)) return false;
+    sc m = m_in;
+    if (!u256_lt(m.v, N)) {                      // scalar_set_b32 reduction
+        u32 tmp[8];
+        u256_sub(tmp, m.v, N);
+        for (int i = 0; i < 8; i++) m.v[i] = tmp[i];
+    }
+    sc sinv, u1, u2;
+    if (sinv_pre) sinv = *sinv_pre;
+    else sc_inv(sinv, s_in);
+    sc_mul(u1, m, sinv);
+    sc_mul(u2, r_in, sinv);
+    set_ladder_scalars(st, u1, u2);
+    st.r = r_in;
+    build_q_table(qx, qy, qt, st.sigma);
     return true;
 }
 
-// Ladder phase: Strauss over bit positions TOPQ..0 with shared doublings, odd-fix corrections,
-// and the inversion-free x-coordinate test.  Returns the verdict.
+// Strauss over bit positions TOPQ..0 with shared doublings and the odd-fix corrections.
+// acc receives R on E' (Jacobian); returns true when R is the point at infinity.
 template <class ST, class QT, class GT>
-BCC_HD int ecdsa_ladder_lane(const ST& st, const QT& qt, const GT& gt) {
-    const u32 N[8] = BCC_N_LIMBS;
-    if (!(st.flags & LS_VALID)) return 0;
+BCC_HD bool ladder_accumulate(const ST& st, const QT& qt, const GT& gt, gej& acc) {
     const bool neg0 = (st.flags & LS_NEG0) != 0, neg1 = (st.flags & LS_NEG1) != 0;
-    gej acc;
     bool inf = false;
     {
         bool ng;
@@ -285,7 +303,17 @@ BCC_HD int ecdsa_ladder_lane(const ST& st, const QT& qt, const GT& gt) {
             acc_add(acc, inf, px, py, st.sigma, isg);
         }
     }
-    if (inf) return 0;                           // R = infinity (ecdsa_impl.h:225-227)
+    return inf;
+}
+
+// ECDSA ladder phase: R = u1 G + u2 Q, then the inversion-free x-coordinate test.  Returns the
+// verdict.
+template <class ST, class QT, class GT>
+BCC_HD int ecdsa_ladder_lane(const ST& st, const QT& qt, const GT& gt) {
+    const u32 N[8] = BCC_N_LIMBS;
+    if (!(st.flags & LS_VALID)) return 0;
+    gej acc;
+    if (ladder_accumulate(st, qt, gt, acc)) return 0;  // R = infinity (ecdsa_impl.h:225-227)
     // ---- x-coordinate test (ecdsa_impl.h:241-273): back on E, Z_E = Z * sigma ----
     fe ze, z2, lhs, xr;
     sc sr;
@@ -315,6 +343,113 @@ BCC_HD int ecdsa_verify_lane(u32 tag, const fe& px_in, const fe& py_in, const sc
     LadderState st;
     if (!ecdsa_prep_lane(tag, px_in, py_in, r_in, s_in, m_in, sinv_pre, qt, st)) return 0;
     return ecdsa_ladder_lane(st, qt, gt);
+}
+
+// ------------------------------------------------------------------------------------------
+// BIP340 (config C5): secp256k1_schnorrsig_verify, modules/schnorrsig/main_impl.h:190-237
+// ------------------------------------------------------------------------------------------
+
+// e = SHA256(SHA256(tag) || SHA256(tag) || rx || px || m) mod n, tag = "BIP0340/challenge":
+// the 64-byte tag prefix is the fixed midstate of secp256k1_schnorrsig_sha256_tagged
+// (main_impl.h:98-109), so the challenge is two compressions (96 message bytes + padding,
+// total length 160 bytes).  rx, px, m are the raw 32-byte strings read as big-endian integers
+// (rx, px < p, so their fe_get_b32 serialisations are those same bytes).
+BCC_HD void schnorr_challenge(sc& e, const fe& rx, const fe& px, const sc& m) {
+    const u32 N[8] = BCC_N_LIMBS;
+    u32 s[8] = {0x9cecba11u, 0x23925381u, 0x11679112u, 0xd1627e0fu,
+                0x97c87550u, 0x003cc765u, 0x90f61164u, 0x33e9b66au};
+    u32 w[16];
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+        w[j] = rx.v[7 - j];                      // big-endian word j of the 32-byte string
+        w[8 + j] = px.v[7 - j];
+    }
+    sha256_compress(s, w);
+#pragma unroll
+    for (int j = 0; j < 8; j++) w[j] = m.v[7 - j];
+    w[8] = 0x80000000u;
+#pragma unroll
+    for (int j = 9; j < 15; j++) w[j] = 0;
+    w[15] = 160 * 8;
+    sha256_compress(s, w);
+#pragma unroll
+    for (int i = 0; i < 8; i++) e.v[i] = s[7 - i];
+    if (!u256_lt(e.v, N)) {                      // scalar_set_b32 reduction (main_impl.h:124)
+        u32 tmp[8];
+        u256_sub(tmp, e.v, N);
+        for (int i = 0; i < 8; i++) e.v[i] = tmp[i];
+    }
+}
+
+// Prep phase of a BIP340 verify: rx < p (main_impl.h:207), s < n (:211-214), x-only lift of
+// the key with even y (extrakeys/main_impl.h:21-39: x < p and x^3 + 7 a square), challenge e,
+// then the ladder scalars for R = s G + (-e) P (main_impl.h:224-227).
+template <class QT>
+BCC_HD bool schnorr_prep_lane(const fe& px, const fe& rx, const sc& s_in, const sc& m, QT& qt,
+                              LadderState& st) {
+    const u32 N[8] = BCC_N_LIMBS;
+    st.flags = 0;
+    if (!fe_lt_p(rx)) return false;
+    if (!u256_lt(s_in.v, N)) return false;
+    if (!fe_lt_p(px)) return false;
+    fe py, x3;
+    curve_rhs(x3, px);
+    if (!fe_sqrt(py, x3)) return false;
+    fe_normalize(py);
+    if (py.v[0] & 1u) fe_neg(py, py);            // the even-y lift
+    sc e, ne;
+    schnorr_challenge(e, rx, px, m);
+    sc_neg(ne, e);
+    set_ladder_scalars(st, s_in, ne);
+#pragma unroll
+    for (int i = 0; i < 8; i++) st.r.v[i] = rx.v[i];
+    build_q_table(px, py, qt, st.sigma);
+    return true;
+}
+
+// Ladder phase of a BIP340 verify.  Returns 1 when R != infinity and x(R) == rx (tested
+// inversion-free as rx * Z_E^2 == X); ye / ze then hold Y and Z_E with y(R) = ye / ze^3, whose
+// parity (main_impl.h:234-236) needs one field inversion: batched across lanes on the device
+// (schnorr_parity_kernel), per lane in schnorr_verify_lane.
+template <class ST, class QT, class GT>
+BCC_HD int schnorr_ladder_lane(const ST& st, const QT& qt, const GT& gt, fe& ye, fe& ze) {
+    if (!(st.flags & LS_VALID)) return 0;
+    gej acc;
+    if (ladder_accumulate(st, qt, gt, acc)) return 0;  // ge_set_gej_var(inf) -> reject (:229-232)
+    fe z2, lhs, xr;
+    sc sr;
+    st.get_r(sr);
+    fe_mul(ze, acc.z, st.sigma);
+    if (fe_is_zero(ze)) return 0;                // unreachable for a finite R; keeps the batch
+                                                 // inversion well-defined regardless
+    fe_sqr(z2, ze);
+    for (int i = 0; i < 8; i++) xr.v[i] = sr.v[i];
+    fe_mul(lhs, xr, z2);
+    if (!fe_equal(lhs, acc.x)) return 0;
+    ye = acc.y;
+    return 1;
+}
+
+// y = ye * zinv^3 normalised; true when even (!secp256k1_fe_is_odd).
+BCC_HD bool schnorr_y_even(const fe& ye, const fe& zinv) {
+    fe z2, z3, y;
+    fe_sqr(z2, zinv);
+    fe_mul(z3, z2, zinv);
+    fe_mul(y, ye, z3);
+    fe_normalize(y);
+    return (y.v[0] & 1u) == 0;
+}
+
+// Whole BIP340 verify on one lane (host tests, small batches).
+template <class QT, class GT>
+BCC_HD int schnorr_verify_lane(const fe& px, const fe& rx, const sc& s, const sc& m, QT& qt,
+                               const GT& gt) {
+    LadderState st;
+    if (!schnorr_prep_lane(px, rx, s, m, qt, st)) return 0;
+    fe ye, ze, zi;
+    if (!schnorr_ladder_lane(st, qt, gt, ye, ze)) return 0;
+    fe_inv(zi, ze);
+    return schnorr_y_even(ye, zi) ? 1 : 0;
 }
 
 // k*G -> affine (x, y), normalized.  Used by the synthetic-workload generator (keygen, signing),
@@ -402,6 +537,26 @@ BCC_HD bool ecdsa_sign_lane(const sc& d, const sc& m_in, const sc& k, sc& r, sc&
     const u32 H[8] = {0x681B20A0u, 0xDFE92F46u, 0x57A4501Du, 0x5D576E73u,
                       0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0x7FFFFFFFu};
     if (u256_lt(H, s.v)) sc_neg(s, s);
+    return true;
+}
+
+// BIP340 signing for the generator (secp256k1_schnorrsig_sign, main_impl.h:127-188, with the
+// caller's nonce k instead of the BIP340 nonce function): the key is negated when its point
+// has odd y, R = kG with k negated when R has odd y, sig = x(R) || k + e d.  Returns false for
+// d or k == 0.  xonly receives P.x.
+template <class GT>
+BCC_HD bool schnorr_sign_lane(const sc& d_in, const sc& m, const sc& k_in, fe& rx, sc& s,
+                              fe& xonly, const GT& gt) {
+    fe px, py, ry;
+    if (!ecmult_gen_lane(d_in, px, py, gt)) return false;
+    if (!ecmult_gen_lane(k_in, rx, ry, gt)) return false;
+    sc d = d_in, k = k_in, e, t;
+    if (py.v[0] & 1u) sc_neg(d, d);
+    if (ry.v[0] & 1u) sc_neg(k, k);
+    xonly = px;
+    schnorr_challenge(e, rx, px, m);
+    sc_mul(t, e, d);
+    sc_add(s, t, k);
     return true;
 }
 

@@ -209,6 +209,99 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
 }
 
 // ------------------------------------------------------------------------------------------
+// BIP340 (config C5).  Rows: sig[n][64] = r.x || s, msg[n][32], xonly[n][32] (the argument
+// order of secp256k1_schnorrsig_verify).  Same prep / ladder split and scratch layout as ECDSA;
+// the even-y test needs y(R) = Y / Z_E^3, so the ladder parks (Y, Z_E) in its lane's own Q-table
+// words 0..15 and schnorr_parity_kernel inverts all Z_E of a chunk by Montgomery's trick.
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void schnorr_prep_kernel(
+    const uint8_t* __restrict__ psig, const uint8_t* __restrict__ pm,
+    const uint8_t* __restrict__ ppk, size_t base, size_t cnt, size_t C, u32* __restrict__ qtab,
+    u32* __restrict__ state) {
+    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= cnt) return;
+    const size_t i = base + t;
+    fe px, rx;
+    sc s, m;
+    load_be32(rx, psig + 64 * i);
+    load_be32(s, psig + 64 * i + 32);
+    load_be32(m, pm + 32 * i);
+    load_be32(px, ppk + 32 * i);
+    QTableGlobal qt{qtab + t, C};
+    LadderState st;
+    schnorr_prep_lane(px, rx, s, m, qt, st);
+    store_state(state + t, C, st);
+}
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) void schnorr_ladder_kernel(
+    const u32* __restrict__ state, u32* __restrict__ qtab, const fe* __restrict__ gtab,
+    uint8_t* __restrict__ verdict, size_t base, size_t cnt, size_t C) {
+    __shared__ fe g_lds[2 * GTAB * 2];
+    for (int i = threadIdx.x; i < 2 * GTAB * 2; i += blockDim.x) g_lds[i] = gtab[i];
+    __syncthreads();
+    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= cnt) return;
+    LadderStateView st;
+    st.p = state + t;
+    st.C = C;
+    st.flags = st.p[16 * C];
+#pragma unroll
+    for (int j = 0; j < 8; j++) st.sigma.v[j] = st.p[(17 + j) * C];
+    QTableGlobal qt{qtab + t, C};
+    GTableLDS gt{g_lds};
+    fe ye, ze;
+    int ok = schnorr_ladder_lane(st, qt, gt, ye, ze);
+    if (!ok) {  // neutral element for the batch inversion
+        ye = fe_zero();
+        ze = fe_one();
+    }
+    qt.put(0, 0, ye);  // the lane's own table column; the ladder no longer reads it
+    qt.put(0, 1, ze);
+    verdict[base + t] = (uint8_t)ok;
+}
+
+// y-parity of R for every lane of a chunk: Z_E^-1 by Montgomery's trick over the strided
+// sub-chunk {t, t+T, ...} (3 mults per lane + one Fermat inversion per thread), prefix products
+// in Q-table words 16..23.  verdict &= (y even).
+__global__ __launch_bounds__(256) void schnorr_parity_kernel(u32* __restrict__ qtab,
+                                                             uint8_t* __restrict__ verdict,
+                                                             size_t base, size_t cnt, size_t C,
+                                                             size_t T) {
+    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= cnt || t >= T) return;
+    fe acc, z, ye;
+    QTableGlobal q0{qtab + t, C};
+    q0.get(0, 1, acc);
+    q0.put(0, 2, acc);
+    size_t last = t;
+    for (size_t i = t + T; i < cnt; i += T) {
+        QTableGlobal qi{qtab + i, C};
+        qi.get(0, 1, z);
+        fe_mul(acc, acc, z);
+        qi.put(0, 2, acc);  // Z_t * ... * Z_i
+        last = i;
+    }
+    fe inv;
+    fe_inv(inv, acc);
+    for (size_t i = last; i >= t + T; i -= T) {
+        QTableGlobal qi{qtab + i, C}, qp{qtab + i - T, C};
+        fe prev, zi;
+        qp.get(0, 2, prev);
+        fe_mul(zi, inv, prev);  // Z_i^-1
+        qi.get(0, 1, z);
+        fe_mul(inv, inv, z);    // (Z_t ... Z_{i-1})^-1
+        if (verdict[base + i]) {
+            qi.get(0, 0, ye);
+            verdict[base + i] = (uint8_t)schnorr_y_even(ye, zi);
+        }
+    }
+    if (verdict[base + t]) {
+        q0.get(0, 0, ye);
+        verdict[base + t] = (uint8_t)schnorr_y_even(ye, inv);
+    }
+}
+
+// ------------------------------------------------------------------------------------------
 // per-device state: G tables, scratch
 // ------------------------------------------------------------------------------------------
 struct EcdsaDeviceState {
@@ -294,6 +387,61 @@ int mi_ecdsa_verify_device(const uint8_t* d_tag, const uint8_t* d_x, const uint8
         BCC_HIP_TRY(hipGetLastError());
     }
     return 0;
+}
+
+// BIP340 device-pointer entry: sig64 / msg32 / xonly32 rows resident on the current device
+// (secp256k1_schnorrsig_verify per row, with the x-only key given as its 32 serialized bytes and
+// parsed as secp256k1_xonly_pubkey_parse would; an unparsable key verifies false).
+int mi_schnorr_verify_device(const uint8_t* d_sig64, const uint8_t* d_msg32,
+                             const uint8_t* d_xonly32, uint8_t* d_verdict, size_t n,
+                             void* stream) {
+    if (n == 0) return 0;
+    int dev = 0;
+    BCC_HIP_TRY(hipGetDevice(&dev));
+    EcdsaDeviceState* st = nullptr;
+    if (int e = ensure_state(dev, 0, &st)) return e;
+    hipStream_t sm = (hipStream_t)stream;
+    const size_t C = st->chunk;
+    u32* qtab = st->d_chunk;
+    u32* state = st->d_chunk + C * QTABLE_WORDS;
+    for (size_t base = 0; base < n; base += C) {
+        size_t cnt = std::min(C, n - base);
+        unsigned blocks = (unsigned)((cnt + 255) / 256);
+        hipLaunchKernelGGL(schnorr_prep_kernel, dim3(blocks), dim3(256), 0, sm, d_sig64, d_msg32,
+                           d_xonly32, base, cnt, C, qtab, state);
+        BCC_HIP_TRY(hipGetLastError());
+        hipLaunchKernelGGL(schnorr_ladder_kernel, dim3(blocks), dim3(256), 0, sm, state, qtab,
+                           st->d_gtab, d_verdict, base, cnt, C);
+        BCC_HIP_TRY(hipGetLastError());
+        // parity: sub-chunks of <= 16 lanes, at least one wave per SIMD
+        size_t T = std::max<size_t>((cnt + 15) / 16, std::min<size_t>(cnt, (size_t)st->cus * 256));
+        hipLaunchKernelGGL(schnorr_parity_kernel, dim3((unsigned)((T + 255) / 256)), dim3(256), 0,
+                           sm, qtab, d_verdict, base, cnt, C, T);
+        BCC_HIP_TRY(hipGetLastError());
+    }
+    return 0;
+}
+
+// BIP340 host-buffer entry: n rows of sig64 / msg32 / xonly32; synchronous on `device`.
+int mi_schnorr_verify_tuples(const uint8_t* sig64, const uint8_t* msg32, const uint8_t* xonly32,
+                             uint8_t* verdict, size_t n, int device) {
+    if (n == 0) return 0;
+    BCC_HIP_TRY(hipSetDevice(device));
+    uint8_t* d = nullptr;
+    size_t vbytes = (n + 255) & ~(size_t)255;
+    BCC_HIP_TRY(hipMalloc(&d, 128 * n + vbytes));
+    uint8_t *d_sig = d, *d_m = d + 64 * n, *d_pk = d_m + 32 * n, *d_v = d_pk + 32 * n;
+    int rc = 0;
+    if ((rc = (int)hipMemcpy(d_sig, sig64, 64 * n, hipMemcpyHostToDevice)) ||
+        (rc = (int)hipMemcpy(d_m, msg32, 32 * n, hipMemcpyHostToDevice)) ||
+        (rc = (int)hipMemcpy(d_pk, xonly32, 32 * n, hipMemcpyHostToDevice)) ||
+        (rc = mi_schnorr_verify_device(d_sig, d_m, d_pk, d_v, n, nullptr)) ||
+        (rc = (int)hipDeviceSynchronize()) ||
+        (rc = (int)hipMemcpy(verdict, d_v, n, hipMemcpyDeviceToHost))) {
+        fprintf(stderr, "[bcc] mi_schnorr_verify_tuples failed: %d\n", rc);
+    }
+    (void)hipFree(d);
+    return rc;
 }
 
 // Host-buffer entry (the inner C ABI of SURVEY §8b): pub65[n] = header byte || x || y (y ignored

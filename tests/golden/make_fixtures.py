@@ -13,8 +13,12 @@ Outputs (all small):
   crate_vectors.json the six src/lib.rs:223-263 vectors + invalid_flags_test, with (ret, err)
   bip340_vectors.json the 15 BIP340 test vectors (test/functional/test_framework/bip340_test_vectors.csv)
                      with the reference's secp256k1_schnorrsig_verify verdict
+  schnorr_tuples.npz BIP340 (sig64, msg32, xonly32) tuples over every reject path of
+                     secp256k1_schnorrsig_verify, with the reference's verdict
+                     (`python3 tests/golden/make_fixtures.py schnorr` regenerates only this file)
 """
 import csv
+import hashlib
 import json
 import os
 import random
@@ -300,8 +304,137 @@ def make_tuples(R, rng):
     return cases
 
 
+def tagged_hash(tag, msg):
+    t = hashlib.sha256(tag).digest()
+    return hashlib.sha256(t + t + msg).digest()
+
+
+def schnorr_sign_py(d, msg, k, odd_r=False):
+    """BIP340 signing with an explicit nonce, for crafting inputs (verdicts come from the
+    reference).  odd_r=True keeps an odd-y R instead of negating k (an invalid signature)."""
+    P = ec_mul(d, G)
+    if P[1] & 1:
+        d = N - d
+    Rp = ec_mul(k, G)
+    if (Rp[1] & 1) and not odd_r:
+        k = N - k
+        Rp = ec_neg(Rp)
+    rb, pb = Rp[0].to_bytes(32, "big"), P[0].to_bytes(32, "big")
+    e = int.from_bytes(tagged_hash(b"BIP0340/challenge", rb + pb + msg), "big") % N
+    return rb + ((k + e * d) % N).to_bytes(32, "big"), pb
+
+
+def make_schnorr_tuples(R, rng):
+    """BIP340 (sig64, msg32, xonly32) tuples over every reject path of secp256k1_schnorrsig_verify
+    (modules/schnorrsig/main_impl.h:190-237) and xonly_pubkey_parse (extrakeys/main_impl.h:21-39)."""
+    cases = []
+
+    def rb(k):
+        return bytes(rng.getrandbits(8) for _ in range(k))
+
+    def flip(b, lo=0, hi=None):
+        b = bytearray(b)
+        j = rng.randrange(lo, hi if hi is not None else len(b))
+        b[j] ^= 1 << rng.randrange(8)
+        return bytes(b)
+
+    valid = []
+    for i in range(400):
+        sk = (rng.randrange(1, N)).to_bytes(32, "big")
+        msg = rb(32)
+        out = R.schnorr_sign(sk, msg, rb(32))
+        sig, pk = out
+        valid.append((sig, msg, pk))
+        cases.append(("valid", sig, msg, pk))
+    for i in range(60):  # small / structured keys and nonces
+        d = rng.choice([1, 2, 3, 7, N - 1, N - 2, rng.randrange(1, 1 << 16)])
+        k = rng.choice([1, 2, 3, N - 1, rng.randrange(1, 1 << 16), rng.randrange(1, N)])
+        msg = rng.choice([bytes(32), b"\xff" * 32, rb(32)])
+        sig, pk = schnorr_sign_py(d, msg, k)
+        cases.append(("small_scalars", sig, msg, pk))
+    for i in range(60):
+        d, k, msg = rng.randrange(1, N), rng.randrange(1, N), rb(32)
+        if not (ec_mul(k, G)[1] & 1):
+            k = N - k
+        sig, pk = schnorr_sign_py(d, msg, k, odd_r=True)
+        cases.append(("odd_y_R", sig, msg, pk))
+    for i in range(150):
+        sig, msg, pk = rng.choice(valid)
+        cases.append(("msg_flip", sig, flip(msg), pk))
+    for i in range(100):
+        sig, msg, pk = rng.choice(valid)
+        cases.append(("r_flip", flip(sig, 0, 32), msg, pk))
+    for i in range(100):
+        sig, msg, pk = rng.choice(valid)
+        cases.append(("s_flip", flip(sig, 32, 64), msg, pk))
+    for i in range(100):
+        sig, msg, pk = rng.choice(valid)
+        cases.append(("pub_flip", sig, msg, flip(pk)))
+    for i in range(60):
+        sig, msg, pk = rng.choice(valid)
+        other = rng.choice(valid)[2]
+        cases.append(("wrong_key", sig, msg, other))
+    for i in range(40):
+        sig, msg, pk = rng.choice(valid)
+        r = rng.choice([P, P + 1, 2**256 - 1, P + rng.randrange(1, 2**32 - 977)])
+        cases.append(("r_ge_p", r.to_bytes(32, "big") + sig[32:], msg, pk))
+    for i in range(20):
+        sig, msg, pk = rng.choice(valid)
+        cases.append(("r_zero", bytes(32) + sig[32:], msg, pk))
+    for i in range(40):
+        sig, msg, pk = rng.choice(valid)
+        s = int.from_bytes(sig[32:], "big")
+        s2 = rng.choice([N, N + 1, 2**256 - 1, s + N if s + N < 2**256 else N + 5])
+        cases.append(("s_ge_n", sig[:32] + s2.to_bytes(32, "big"), msg, pk))
+    for i in range(30):
+        sig, msg, pk = rng.choice(valid)
+        s = int.from_bytes(sig[32:], "big")
+        s2 = rng.choice([0, N - s, N - 1])
+        cases.append(("s_edge", sig[:32] + s2.to_bytes(32, "big"), msg, pk))
+    for i in range(30):
+        sig, msg, pk = rng.choice(valid)
+        x = rng.choice([P, P + 1, 2**256 - 1, P + rng.randrange(1, 2**32 - 977)])
+        cases.append(("pub_ge_p", sig, msg, x.to_bytes(32, "big")))
+    n_off = 0
+    while n_off < 40:
+        x = rng.randrange(0, P)
+        if pow((x**3 + 7) % P, (P - 1) // 2, P) == P - 1:  # no square root: not on the curve
+            sig, msg, pk = rng.choice(valid)
+            cases.append(("pub_off_curve", sig, msg, x.to_bytes(32, "big")))
+            n_off += 1
+    cases.append(("zero_everything", bytes(64), bytes(32), bytes(32)))
+    rng.shuffle(cases)
+    return cases
+
+
+def write_schnorr(R):
+    rng = random.Random(0x5EED0005)
+    cases = make_schnorr_tuples(R, rng)
+    n = len(cases)
+    sig = np.zeros((n, 64), np.uint8)
+    msg = np.zeros((n, 32), np.uint8)
+    pub = np.zeros((n, 32), np.uint8)
+    verdict = np.zeros(n, np.uint8)
+    classes = sorted({c for c, *_ in cases})
+    cls = np.zeros(n, np.int32)
+    for i, (c, sb, mb, pb) in enumerate(cases):
+        sig[i] = np.frombuffer(sb, np.uint8)
+        msg[i] = np.frombuffer(mb, np.uint8)
+        pub[i] = np.frombuffer(pb, np.uint8)
+        verdict[i] = R.schnorr_verify(sb, mb, pb)
+        cls[i] = classes.index(c)
+    np.savez_compressed(os.path.join(HERE, "schnorr_tuples.npz"), sig=sig, msg=msg, pub=pub,
+                        verdict=verdict, cls=cls, classes=np.array(classes))
+    summary = {c: [int(verdict[cls == k].sum()), int((cls == k).sum())] for k, c in enumerate(classes)}
+    print("schnorr_tuples:", n, "tuples;", "valid/total per class:", json.dumps(summary))
+
+
 def main():
     R = Reference()
+    if sys.argv[1:] == ["schnorr"]:
+        write_schnorr(R)
+        return
+    write_schnorr(R)
     rng = random.Random(0x5EED00C4)
     cases = make_tuples(R, rng)
     n = len(cases)

@@ -36,6 +36,43 @@ extern "C" int lane_verify(unsigned tag, const unsigned char* x32, const unsigne
     return ecdsa_verify_lane(tag, px, py, r, s, m, qt, gt);
 }
 
+// BIP340: sig64 = r.x || s, msg32, x-only key (secp256k1_schnorrsig_verify argument order)
+extern "C" int lane_schnorr_verify(const unsigned char* sig64, const unsigned char* msg32,
+                                   const unsigned char* xonly32) {
+    fe px, rx, t;
+    sc s, m;
+    fe_from_be_bytes(rx, sig64);
+    fe_from_be_bytes(t, sig64 + 32);
+    memcpy(s.v, t.v, 32);
+    fe_from_be_bytes(t, msg32);
+    memcpy(m.v, t.v, 32);
+    fe_from_be_bytes(px, xonly32);
+    QTableArray qt;
+    GTableArray gt{gtab().data()};
+    return schnorr_verify_lane(px, rx, s, m, qt, gt);
+}
+
+// the generator's BIP340 signer (nonce supplied): returns 0 for d or k == 0
+extern "C" int lane_schnorr_sign(const unsigned char* d32, const unsigned char* msg32,
+                                 const unsigned char* k32, unsigned char* sig64,
+                                 unsigned char* xonly32) {
+    fe t, rx, px;
+    sc d, m, k, s;
+    fe_from_be_bytes(t, d32);
+    memcpy(d.v, t.v, 32);
+    fe_from_be_bytes(t, msg32);
+    memcpy(m.v, t.v, 32);
+    fe_from_be_bytes(t, k32);
+    memcpy(k.v, t.v, 32);
+    GTableArray gt{gtab().data()};
+    if (!schnorr_sign_lane(d, m, k, rx, s, px, gt)) return 0;
+    fe_to_be_bytes(sig64, rx);
+    memcpy(t.v, s.v, 32);
+    fe_to_be_bytes(sig64 + 32, t);
+    fe_to_be_bytes(xonly32, px);
+    return 1;
+}
+
 // field/scalar primitives for unit tests
 extern "C" void lane_fe_mul(const unsigned char* a32, const unsigned char* b32, unsigned char* o32) {
     fe a, b, r;

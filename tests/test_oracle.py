@@ -3,7 +3,7 @@ import random
 
 import pytest
 
-from fixtures import ecdsa_tuples, load_json
+from fixtures import ecdsa_tuples, load_json, schnorr_tuples
 from oracle_ctypes import Oracle, Reference, reference_available
 
 O = Oracle()
@@ -28,6 +28,14 @@ def test_oracle_bip340_vectors():
     for v in load_json("bip340_vectors.json"):
         got = O.schnorr_verify(bytes.fromhex(v["sig"]), bytes.fromhex(v["msg"]), bytes.fromhex(v["pubkey"]))
         assert got == int(v["expected"]) == v["ref_verdict"], v
+
+
+def test_oracle_schnorr_tuples_match_reference_verdicts():
+    ts = schnorr_tuples()
+    assert sum(t["verdict"] for t in ts) >= 400 and len({t["cls"] for t in ts}) >= 14
+    bad = [(t["cls"], i) for i, t in enumerate(ts)
+           if O.schnorr_verify(t["sig"], t["msg"], t["pub"]) != t["verdict"]]
+    assert not bad, bad[:10]
 
 
 def test_oracle_sha256_known_answers():

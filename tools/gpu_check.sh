@@ -5,7 +5,7 @@ export TMPDIR=/tmp
 TAG=${1:-check}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
-timeout -k 10 400 python -m pytest tests -m gpu -x -q > $OUT/pytest_gpu.log 2>&1 || { tail -30 $OUT/pytest_gpu.log; exit 1; }
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 || { tail -30 $OUT/pytest_gpu.log; exit 1; }
 tail -3 $OUT/pytest_gpu.log
 timeout -k 10 300 python bench.py --steps 5 --warmup 2 --no-cpu > $OUT/bench.json 2> $OUT/bench.err || { tail -20 $OUT/bench.err; exit 2; }
 cat $OUT/bench.json
