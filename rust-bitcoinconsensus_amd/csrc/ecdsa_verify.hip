@@ -19,9 +19,11 @@
 // Row loads are two 16-byte loads per lane (a wave covers one contiguous 2 KiB span); scratch is
 // word-interleaved by tuple ([word][C]) so every scratch access of a wave is one 256-byte line.
 #include <cstdlib>
+#include <memory>
 
 #include "ecdsa_lane.h"
 #include "gpu_common.h"
+#include "pipeline.h"
 
 namespace bcc {
 
@@ -302,19 +304,11 @@ __global__ __launch_bounds__(256) void schnorr_parity_kernel(u32* __restrict__ q
 }
 
 // ------------------------------------------------------------------------------------------
-// per-device state: G tables, scratch
+// G tables (one read-only copy per device) and caller-owned scratch
 // ------------------------------------------------------------------------------------------
-struct EcdsaDeviceState {
-    fe* d_gtab = nullptr;
-    u32* d_sinv = nullptr;
-    size_t sinv_cap = 0;
-    u32* d_chunk = nullptr;  // Q tables + ladder states for one chunk
-    size_t chunk = 0;
-    int cus = 0;
-};
-
-static std::mutex g_state_mu;
-static EcdsaDeviceState g_state[64];
+static std::mutex g_gtab_mu;
+static fe* g_gtab[64];
+static int g_cus[64];
 
 static const std::vector<fe>& host_gtab() {
     static std::vector<fe> t;
@@ -326,27 +320,160 @@ static const std::vector<fe>& host_gtab() {
     return t;
 }
 
-static int ensure_state(int dev, size_t n, EcdsaDeviceState** out) {
-    std::lock_guard<std::mutex> lk(g_state_mu);
-    EcdsaDeviceState& st = g_state[dev];
-    if (!st.d_gtab) {
-        const auto& h = host_gtab();
-        BCC_HIP_TRY(hipMalloc(&st.d_gtab, h.size() * sizeof(fe)));
-        BCC_HIP_TRY(hipMemcpy(st.d_gtab, h.data(), h.size() * sizeof(fe), hipMemcpyHostToDevice));
-        BCC_HIP_TRY(hipDeviceGetAttribute(&st.cus, hipDeviceAttributeMultiprocessorCount, dev));
+static size_t chunk_lanes() {
+    static const size_t c = [] {
         const char* e = getenv("BCC_CHUNK");
-        st.chunk = e ? (size_t)atol(e) : (size_t)262144;
-        st.chunk = (st.chunk + 255) & ~(size_t)255;
-        BCC_HIP_TRY(hipMalloc(&st.d_chunk, st.chunk * (QTABLE_WORDS + STATE_WORDS) * sizeof(u32)));
+        size_t v = e ? (size_t)atol(e) : (size_t)262144;
+        return std::max<size_t>(256, (v + 255) & ~(size_t)255);
+    }();
+    return c;
+}
+
+// Current device, its G tables and CU count.
+static int device_tables(int* dev, fe** gtab, int* cus) {
+    BCC_HIP_TRY(hipGetDevice(dev));
+    if (*dev < 0 || *dev >= 64) return (int)hipErrorInvalidDevice;
+    std::lock_guard<std::mutex> lk(g_gtab_mu);
+    if (!g_gtab[*dev]) {
+        const auto& h = host_gtab();
+        fe* d = nullptr;
+        BCC_HIP_TRY(hipMalloc(&d, h.size() * sizeof(fe)));
+        BCC_HIP_TRY(hipMemcpy(d, h.data(), h.size() * sizeof(fe), hipMemcpyHostToDevice));
+        BCC_HIP_TRY(hipDeviceGetAttribute(&g_cus[*dev], hipDeviceAttributeMultiprocessorCount, *dev));
+        g_gtab[*dev] = d;
     }
-    if (n > st.sinv_cap) {
-        if (st.d_sinv) BCC_HIP_TRY(hipFree(st.d_sinv));
-        st.d_sinv = nullptr;
-        size_t cap = std::max<size_t>(n, 1 << 16);
-        BCC_HIP_TRY(hipMalloc(&st.d_sinv, cap * 8 * sizeof(u32)));
-        st.sinv_cap = cap;
+    *gtab = g_gtab[*dev];
+    *cus = g_cus[*dev];
+    return 0;
+}
+
+SigScratch::~SigScratch() {
+    if (dev >= 0 && (sinv || chunk)) {
+        int cur = 0;
+        (void)hipGetDevice(&cur);
+        (void)hipSetDevice(dev);
+        if (sinv) (void)hipFree(sinv);
+        if (chunk) (void)hipFree(chunk);
+        (void)hipSetDevice(cur);
     }
-    *out = &st;
+}
+
+// Grows sc to n tuples (sinv rows when with_sinv) and min(n, chunk) lanes of chunk scratch;
+// returns the chunk stride C.
+static int ensure_scratch(SigScratch& sc, int dev, size_t n, bool with_sinv, size_t* C) {
+    if (sc.dev >= 0 && sc.dev != dev) return (int)hipErrorInvalidDevice;
+    sc.dev = dev;
+    const size_t want = std::min(chunk_lanes(), (n + 255) & ~(size_t)255);
+    if (want > sc.chunk_cap) {
+        if (sc.chunk) BCC_HIP_TRY(hipFree(sc.chunk));
+        sc.chunk = nullptr;
+        sc.chunk_cap = 0;
+        BCC_HIP_TRY(hipMalloc(&sc.chunk, want * (QTABLE_WORDS + STATE_WORDS) * sizeof(u32)));
+        sc.chunk_cap = want;
+    }
+    if (with_sinv && n > sc.sinv_cap) {
+        if (sc.sinv) BCC_HIP_TRY(hipFree(sc.sinv));
+        sc.sinv = nullptr;
+        sc.sinv_cap = 0;
+        size_t cap = std::max<size_t>(n, 1 << 12);
+        BCC_HIP_TRY(hipMalloc(&sc.sinv, cap * 8 * sizeof(u32)));
+        sc.sinv_cap = cap;
+    }
+    *C = want;
+    return 0;
+}
+
+int ecdsa_launch(SigScratch& sc, const uint8_t* d_tag, const uint8_t* d_x, const uint8_t* d_y,
+                 const uint8_t* d_r, const uint8_t* d_s, const uint8_t* d_m, uint8_t* d_verdict,
+                 size_t n, void* stream) {
+    if (n == 0) return 0;
+    int dev = 0, cus = 0;
+    fe* gtab = nullptr;
+    size_t C = 0;
+    if (int e = device_tables(&dev, &gtab, &cus)) return e;
+    if (int e = ensure_scratch(sc, dev, n, true, &C)) return e;
+    hipStream_t sm = (hipStream_t)stream;
+    u32* sinv = (u32*)sc.sinv;
+    // K_inv: chunks of <= 16 tuples, but at least one wave per SIMD
+    size_t T = std::max<size_t>((n + 15) / 16, std::min<size_t>(n, (size_t)cus * 256));
+    hipLaunchKernelGGL(batch_sinv_kernel, dim3((unsigned)((T + 255) / 256)), dim3(256), 0, sm, d_s,
+                       sinv, n, T);
+    BCC_HIP_TRY(hipGetLastError());
+    u32* qtab = (u32*)sc.chunk;
+    u32* state = qtab + C * QTABLE_WORDS;
+    for (size_t base = 0; base < n; base += C) {
+        size_t cnt = std::min(C, n - base);
+        unsigned blocks = (unsigned)((cnt + 255) / 256);
+        hipLaunchKernelGGL(ecdsa_prep_kernel, dim3(blocks), dim3(256), 0, sm, d_tag, d_x, d_y, d_r,
+                           d_s, d_m, sinv, base, cnt, C, qtab, state);
+        BCC_HIP_TRY(hipGetLastError());
+        hipLaunchKernelGGL(ecdsa_ladder_kernel, dim3(blocks), dim3(256), 0, sm, state, qtab, gtab,
+                           d_verdict, base, cnt, C);
+        BCC_HIP_TRY(hipGetLastError());
+    }
+    return 0;
+}
+
+int schnorr_launch(SigScratch& sc, const uint8_t* d_sig64, const uint8_t* d_msg32,
+                   const uint8_t* d_xonly32, uint8_t* d_verdict, size_t n, void* stream) {
+    if (n == 0) return 0;
+    int dev = 0, cus = 0;
+    fe* gtab = nullptr;
+    size_t C = 0;
+    if (int e = device_tables(&dev, &gtab, &cus)) return e;
+    if (int e = ensure_scratch(sc, dev, n, false, &C)) return e;
+    hipStream_t sm = (hipStream_t)stream;
+    u32* qtab = (u32*)sc.chunk;
+    u32* state = qtab + C * QTABLE_WORDS;
+    for (size_t base = 0; base < n; base += C) {
+        size_t cnt = std::min(C, n - base);
+        unsigned blocks = (unsigned)((cnt + 255) / 256);
+        hipLaunchKernelGGL(schnorr_prep_kernel, dim3(blocks), dim3(256), 0, sm, d_sig64, d_msg32,
+                           d_xonly32, base, cnt, C, qtab, state);
+        BCC_HIP_TRY(hipGetLastError());
+        hipLaunchKernelGGL(schnorr_ladder_kernel, dim3(blocks), dim3(256), 0, sm, state, qtab, gtab,
+                           d_verdict, base, cnt, C);
+        BCC_HIP_TRY(hipGetLastError());
+        // parity: sub-chunks of <= 16 lanes, at least one wave per SIMD
+        size_t T = std::max<size_t>((cnt + 15) / 16, std::min<size_t>(cnt, (size_t)cus * 256));
+        hipLaunchKernelGGL(schnorr_parity_kernel, dim3((unsigned)((T + 255) / 256)), dim3(256), 0,
+                           sm, qtab, d_verdict, base, cnt, C, T);
+        BCC_HIP_TRY(hipGetLastError());
+    }
+    return 0;
+}
+
+// The device-pointer ABI entries share one scratch per device (launches must be ordered on one
+// stream per device, as documented in bcc_amd.h); the host-buffer entries below use a scratch and
+// stream of their own per (thread, device).
+static std::mutex g_shared_mu;
+static SigScratch* g_shared[64];
+
+static SigScratch* shared_scratch() {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+    std::lock_guard<std::mutex> lk(g_shared_mu);
+    if (!g_shared[dev]) g_shared[dev] = new SigScratch();  // lives for the process
+    return g_shared[dev];
+}
+
+struct ThreadCtx {
+    SigScratch sc;
+    hipStream_t stream = nullptr;
+    ~ThreadCtx() {
+        if (stream) (void)hipStreamDestroy(stream);
+    }
+};
+
+static int thread_ctx(int device, ThreadCtx** out) {
+    thread_local std::unique_ptr<ThreadCtx> ctx[64];
+    if (device < 0 || device >= 64) return (int)hipErrorInvalidDevice;
+    if (!ctx[device]) {
+        auto c = std::make_unique<ThreadCtx>();
+        BCC_HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+        ctx[device] = std::move(c);
+    }
+    *out = ctx[device].get();
     return 0;
 }
 
@@ -358,35 +485,13 @@ extern "C" {
 
 // Device-pointer entry: all buffers already resident on the current device; launches on
 // `stream` (hipStream_t, may be null). Returns 0 on success, else a hipError_t value.
-// Concurrent callers on one device must use one stream (the scratch is per device).
 int mi_ecdsa_verify_device(const uint8_t* d_tag, const uint8_t* d_x, const uint8_t* d_y,
                            const uint8_t* d_r, const uint8_t* d_s, const uint8_t* d_m,
                            uint8_t* d_verdict, size_t n, void* stream) {
     if (n == 0) return 0;
-    int dev = 0;
-    BCC_HIP_TRY(hipGetDevice(&dev));
-    EcdsaDeviceState* st = nullptr;
-    if (int e = ensure_state(dev, n, &st)) return e;
-    hipStream_t sm = (hipStream_t)stream;
-    // K_inv: chunks of <= 16 tuples, but at least one wave per SIMD
-    size_t T = std::max<size_t>((n + 15) / 16, std::min<size_t>(n, (size_t)st->cus * 256));
-    hipLaunchKernelGGL(batch_sinv_kernel, dim3((unsigned)((T + 255) / 256)), dim3(256), 0, sm, d_s,
-                       st->d_sinv, n, T);
-    BCC_HIP_TRY(hipGetLastError());
-    const size_t C = st->chunk;
-    u32* qtab = st->d_chunk;
-    u32* state = st->d_chunk + C * QTABLE_WORDS;
-    for (size_t base = 0; base < n; base += C) {
-        size_t cnt = std::min(C, n - base);
-        unsigned blocks = (unsigned)((cnt + 255) / 256);
-        hipLaunchKernelGGL(ecdsa_prep_kernel, dim3(blocks), dim3(256), 0, sm, d_tag, d_x, d_y, d_r,
-                           d_s, d_m, st->d_sinv, base, cnt, C, qtab, state);
-        BCC_HIP_TRY(hipGetLastError());
-        hipLaunchKernelGGL(ecdsa_ladder_kernel, dim3(blocks), dim3(256), 0, sm, state, qtab,
-                           st->d_gtab, d_verdict, base, cnt, C);
-        BCC_HIP_TRY(hipGetLastError());
-    }
-    return 0;
+    SigScratch* sc = shared_scratch();
+    if (!sc) return (int)hipErrorInvalidDevice;
+    return ecdsa_launch(*sc, d_tag, d_x, d_y, d_r, d_s, d_m, d_verdict, n, stream);
 }
 
 // BIP340 device-pointer entry: sig64 / msg32 / xonly32 rows resident on the current device
@@ -396,30 +501,9 @@ int mi_schnorr_verify_device(const uint8_t* d_sig64, const uint8_t* d_msg32,
                              const uint8_t* d_xonly32, uint8_t* d_verdict, size_t n,
                              void* stream) {
     if (n == 0) return 0;
-    int dev = 0;
-    BCC_HIP_TRY(hipGetDevice(&dev));
-    EcdsaDeviceState* st = nullptr;
-    if (int e = ensure_state(dev, 0, &st)) return e;
-    hipStream_t sm = (hipStream_t)stream;
-    const size_t C = st->chunk;
-    u32* qtab = st->d_chunk;
-    u32* state = st->d_chunk + C * QTABLE_WORDS;
-    for (size_t base = 0; base < n; base += C) {
-        size_t cnt = std::min(C, n - base);
-        unsigned blocks = (unsigned)((cnt + 255) / 256);
-        hipLaunchKernelGGL(schnorr_prep_kernel, dim3(blocks), dim3(256), 0, sm, d_sig64, d_msg32,
-                           d_xonly32, base, cnt, C, qtab, state);
-        BCC_HIP_TRY(hipGetLastError());
-        hipLaunchKernelGGL(schnorr_ladder_kernel, dim3(blocks), dim3(256), 0, sm, state, qtab,
-                           st->d_gtab, d_verdict, base, cnt, C);
-        BCC_HIP_TRY(hipGetLastError());
-        // parity: sub-chunks of <= 16 lanes, at least one wave per SIMD
-        size_t T = std::max<size_t>((cnt + 15) / 16, std::min<size_t>(cnt, (size_t)st->cus * 256));
-        hipLaunchKernelGGL(schnorr_parity_kernel, dim3((unsigned)((T + 255) / 256)), dim3(256), 0,
-                           sm, qtab, d_verdict, base, cnt, C, T);
-        BCC_HIP_TRY(hipGetLastError());
-    }
-    return 0;
+    SigScratch* sc = shared_scratch();
+    if (!sc) return (int)hipErrorInvalidDevice;
+    return schnorr_launch(*sc, d_sig64, d_msg32, d_xonly32, d_verdict, n, stream);
 }
 
 // BIP340 host-buffer entry: n rows of sig64 / msg32 / xonly32; synchronous on `device`.
@@ -432,11 +516,13 @@ int mi_schnorr_verify_tuples(const uint8_t* sig64, const uint8_t* msg32, const u
     BCC_HIP_TRY(hipMalloc(&d, 128 * n + vbytes));
     uint8_t *d_sig = d, *d_m = d + 64 * n, *d_pk = d_m + 32 * n, *d_v = d_pk + 32 * n;
     int rc = 0;
+    ThreadCtx* ctx = nullptr;
     if ((rc = (int)hipMemcpy(d_sig, sig64, 64 * n, hipMemcpyHostToDevice)) ||
         (rc = (int)hipMemcpy(d_m, msg32, 32 * n, hipMemcpyHostToDevice)) ||
         (rc = (int)hipMemcpy(d_pk, xonly32, 32 * n, hipMemcpyHostToDevice)) ||
-        (rc = mi_schnorr_verify_device(d_sig, d_m, d_pk, d_v, n, nullptr)) ||
-        (rc = (int)hipDeviceSynchronize()) ||
+        (rc = thread_ctx(device, &ctx)) ||
+        (rc = schnorr_launch(ctx->sc, d_sig, d_m, d_pk, d_v, n, ctx->stream)) ||
+        (rc = (int)hipStreamSynchronize(ctx->stream)) ||
         (rc = (int)hipMemcpy(verdict, d_v, n, hipMemcpyDeviceToHost))) {
         fprintf(stderr, "[bcc] mi_schnorr_verify_tuples failed: %d\n", rc);
     }
@@ -446,7 +532,8 @@ int mi_schnorr_verify_tuples(const uint8_t* sig64, const uint8_t* msg32, const u
 
 // Host-buffer entry (the inner C ABI of SURVEY §8b): pub65[n] = header byte || x || y (y ignored
 // for 02/03; header 0 = rejected by the caller's CPubKey length filter), msg32/r32/s32 big-endian.
-// Copies in, verifies on `device`, copies verdicts out. Synchronous.
+// Copies in, verifies on `device`, copies verdicts out. Synchronous and reentrant: each calling
+// thread has its own stream and scratch.
 int mi_ecdsa_verify_tuples(const uint8_t* pub65, const uint8_t* msg32, const uint8_t* r32,
                            const uint8_t* s32, uint8_t* verdict, size_t n, int device) {
     if (n == 0) return 0;
@@ -466,14 +553,16 @@ int mi_ecdsa_verify_tuples(const uint8_t* pub65, const uint8_t* msg32, const uin
         memcpy(&ys[32 * i], pub65 + 65 * i + 33, 32);
     }
     int rc = 0;
+    ThreadCtx* ctx = nullptr;
     if ((rc = (int)hipMemcpy(d_tag, tag.data(), n, hipMemcpyHostToDevice)) ||
         (rc = (int)hipMemcpy(d_x, xs.data(), row, hipMemcpyHostToDevice)) ||
         (rc = (int)hipMemcpy(d_y, ys.data(), row, hipMemcpyHostToDevice)) ||
         (rc = (int)hipMemcpy(d_r, r32, row, hipMemcpyHostToDevice)) ||
         (rc = (int)hipMemcpy(d_s, s32, row, hipMemcpyHostToDevice)) ||
         (rc = (int)hipMemcpy(d_m, msg32, row, hipMemcpyHostToDevice)) ||
-        (rc = mi_ecdsa_verify_device(d_tag, d_x, d_y, d_r, d_s, d_m, d_v, n, nullptr)) ||
-        (rc = (int)hipDeviceSynchronize()) ||
+        (rc = thread_ctx(device, &ctx)) ||
+        (rc = ecdsa_launch(ctx->sc, d_tag, d_x, d_y, d_r, d_s, d_m, d_v, n, ctx->stream)) ||
+        (rc = (int)hipStreamSynchronize(ctx->stream)) ||
         (rc = (int)hipMemcpy(verdict, d_v, n, hipMemcpyDeviceToHost))) {
         fprintf(stderr, "[bcc] mi_ecdsa_verify_tuples failed: %d\n", rc);
     }

@@ -70,8 +70,33 @@ struct TupleRows {
     void clear() { tag.clear(); x.clear(); y.clear(); r.clear(); s.clear(); msg.clear(); }
 };
 
+// Device scratch of the signature kernels: s^-1 rows (ECDSA) and, for one chunk of lanes, the
+// Q tables + ladder states.  Every synchronous entry point owns one per (thread, device), so
+// concurrent callers never share scratch (the reference ABI is reentrant).  Launches
+// that share a scratch must be ordered (one stream).
+struct SigScratch {
+    int dev = -1;
+    void* sinv = nullptr;
+    size_t sinv_cap = 0;   // tuples
+    void* chunk = nullptr;
+    size_t chunk_cap = 0;  // lanes
+    SigScratch() = default;
+    SigScratch(const SigScratch&) = delete;
+    SigScratch& operator=(const SigScratch&) = delete;
+    ~SigScratch();
+};
+
+// Asynchronous launches of the ECDSA / BIP340 kernels on `stream` with caller-owned scratch
+// (grown here when needed; growing synchronises the device).  Return 0 or a hipError_t value.
+int ecdsa_launch(SigScratch& sc, const uint8_t* d_tag, const uint8_t* d_x, const uint8_t* d_y,
+                 const uint8_t* d_r, const uint8_t* d_s, const uint8_t* d_m, uint8_t* d_verdict,
+                 size_t n, void* stream);
+int schnorr_launch(SigScratch& sc, const uint8_t* d_sig64, const uint8_t* d_msg32,
+                   const uint8_t* d_xonly32, uint8_t* d_verdict, size_t n, void* stream);
+
 // Device-resident batch (one per device / per caller thread).  stage() uploads, run() only
-// launches kernels (graph-capturable: no allocation, no synchronisation).
+// launches kernels (graph-capturable: no allocation, no synchronisation, once the scratch has
+// grown to the batch).  A null stream means the batch's own non-blocking stream.
 class DeviceBatch {
 public:
     explicit DeviceBatch(int device);
@@ -80,7 +105,7 @@ public:
     int run(void* stream);                       // K1..K4
     int run_sighash(void* stream);               // K1..K3 only
     int run_ecdsa(void* stream);                 // K4 only
-    int fetch_verdicts(uint8_t* out);            // synchronous D2H
+    int fetch_verdicts(uint8_t* out);            // synchronous D2H (waits for the last run)
     int fetch_msgs(uint8_t* out);                // synchronous D2H (tests)
     size_t n_tuples() const { return n_rows_; }
     size_t n_pre() const { return n_pre_; }
@@ -93,7 +118,12 @@ public:
             *d_m = nullptr, *d_v = nullptr;
 
 private:
+    int sync();
+    void* pick(void* stream);
     int dev_;
+    void* own_stream_ = nullptr;   // hipStream_t, created on first use
+    void* last_stream_ = nullptr;  // stream of the last run
+    SigScratch scratch_;
     void* arena_ = nullptr;
     size_t cap_ = 0;
     size_t n_rows_ = 0, n_pre_ = 0, n_aux_ = 0, n_patch_ = 0, pre_blocks_ = 0, aux_blocks_ = 0;

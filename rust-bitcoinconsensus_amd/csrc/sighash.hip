@@ -4,13 +4,11 @@
 //   K3 sha256d_msgs   preimages -> sighash, written straight into the ECDSA tuple msg rows
 // Integer-ALU bound (~2k VALU ops per 64-byte block); HBM traffic per launch is reported by
 // bench.py as the algorithmic bytes (message bytes in + 32 B out per message).
+#include <memory>
+
 #include "gpu_common.h"
 #include "pipeline.h"
 #include "sha256_device.h"
-
-extern "C" int mi_ecdsa_verify_device(const uint8_t* d_tag, const uint8_t* d_x, const uint8_t* d_y,
-                                      const uint8_t* d_r, const uint8_t* d_s, const uint8_t* d_m,
-                                      uint8_t* d_verdict, size_t n, void* stream);
 
 namespace bcc {
 
@@ -64,16 +62,34 @@ __global__ __launch_bounds__(256) void patch_digests_kernel(uint8_t* __restrict_
 DeviceBatch::DeviceBatch(int device) : dev_(device) {}
 
 DeviceBatch::~DeviceBatch() {
-    if (arena_) {
-        (void)hipSetDevice(dev_);
-        (void)hipFree(arena_);
+    (void)hipSetDevice(dev_);
+    if (own_stream_) (void)hipStreamDestroy((hipStream_t)own_stream_);
+    if (arena_) (void)hipFree(arena_);
+}
+
+void* DeviceBatch::pick(void* stream) {
+    if (!stream) {
+        if (!own_stream_) {
+            hipStream_t s = nullptr;
+            if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return nullptr;
+            own_stream_ = s;
+        }
+        stream = own_stream_;
     }
+    last_stream_ = stream;
+    return stream;
+}
+
+int DeviceBatch::sync() {
+    BCC_HIP_TRY(hipSetDevice(dev_));
+    if (last_stream_) BCC_HIP_TRY(hipStreamSynchronize((hipStream_t)last_stream_));
+    return 0;
 }
 
 static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 int DeviceBatch::stage(const SighashJobs& j, const TupleRows& rows) {
-    BCC_HIP_TRY(hipSetDevice(dev_));
+    if (int e = sync()) return e;  // the previous run may still read the arena
     n_rows_ = rows.size();
     n_pre_ = j.pre_off.size();
     n_aux_ = j.aux_off.size();
@@ -116,7 +132,9 @@ int DeviceBatch::stage(const SighashJobs& j, const TupleRows& rows) {
 }
 
 int DeviceBatch::run_sighash(void* stream) {
-    hipStream_t st = (hipStream_t)stream;
+    BCC_HIP_TRY(hipSetDevice(dev_));
+    hipStream_t st = (hipStream_t)pick(stream);
+    if (!st) return (int)hipErrorOutOfMemory;
     if (n_aux_) {
         hipLaunchKernelGGL(sha256d_msgs_kernel, dim3((unsigned)((n_aux_ + 255) / 256)), dim3(256), 0, st,
                            d_aux_, d_aux_off_, d_aux_nblk_, (uint32_t)n_aux_, d_auxd_, nullptr);
@@ -138,35 +156,36 @@ int DeviceBatch::run_sighash(void* stream) {
 
 int DeviceBatch::run_ecdsa(void* stream) {
     BCC_HIP_TRY(hipSetDevice(dev_));
-    return mi_ecdsa_verify_device(d_tag, d_x, d_y, d_r, d_s, d_m, d_v, n_rows_, stream);
+    void* st = pick(stream);
+    if (!st) return (int)hipErrorOutOfMemory;
+    return ecdsa_launch(scratch_, d_tag, d_x, d_y, d_r, d_s, d_m, d_v, n_rows_, st);
 }
 
 int DeviceBatch::run(void* stream) {
-    BCC_HIP_TRY(hipSetDevice(dev_));
     if (int e = run_sighash(stream)) return e;
     return run_ecdsa(stream);
 }
 
 int DeviceBatch::fetch_verdicts(uint8_t* out) {
-    BCC_HIP_TRY(hipSetDevice(dev_));
-    BCC_HIP_TRY(hipDeviceSynchronize());
+    if (int e = sync()) return e;
     if (n_rows_) BCC_HIP_TRY(hipMemcpy(out, d_v, n_rows_, hipMemcpyDeviceToHost));
     return 0;
 }
 
 int DeviceBatch::fetch_msgs(uint8_t* out) {
-    BCC_HIP_TRY(hipSetDevice(dev_));
-    BCC_HIP_TRY(hipDeviceSynchronize());
+    if (int e = sync()) return e;
     if (n_rows_) BCC_HIP_TRY(hipMemcpy(out, d_m, 32 * n_rows_, hipMemcpyDeviceToHost));
     return 0;
 }
 
 int gpu_verify_batch(int device, const SighashJobs& jobs, const TupleRows& rows, uint8_t* verdict) {
     if (rows.size() == 0) return 0;
-    // one cached batch per (thread, device): repeated calls reuse the device arena
-    thread_local std::vector<DeviceBatch*> cache;
-    if ((int)cache.size() <= device) cache.resize(device + 1, nullptr);
-    if (!cache[device]) cache[device] = new DeviceBatch(device);
+    // one cached batch per (thread, device): repeated calls reuse the device arena, scratch and
+    // stream, and concurrent callers never share any of them
+    thread_local std::vector<std::unique_ptr<DeviceBatch>> cache;
+    if (device < 0) return (int)hipErrorInvalidDevice;
+    if ((int)cache.size() <= device) cache.resize(device + 1);
+    if (!cache[device]) cache[device] = std::make_unique<DeviceBatch>(device);
     DeviceBatch& b = *cache[device];
     if (int e = b.stage(jobs, rows)) return e;
     if (int e = b.run(nullptr)) return e;

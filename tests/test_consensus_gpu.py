@@ -54,3 +54,35 @@ def test_script_cases_batch():
         assert [(r, int(e)) for r, e in res] == [(c["ret"], c["err"]) for c in cs]
     st = B.last_batch_stats()
     assert st["items"] > 0
+
+
+def test_concurrent_callers():
+    """The reference ABI is reentrant: threads calling the drop-in concurrently (ctypes
+    drops the GIL for the call) must get exactly the single-threaded verdicts; each thread owns its
+    device arena, scratch and stream."""
+    import threading
+    import bitcoinconsensus_amd as B
+    allc = [c for c in cases() if c["flags"] == 0xE15][:600]
+    exp = [(c["ret"], c["err"]) for c in allc]
+    args = [(bytes.fromhex(c["spk"]), c["amount"], bytes.fromhex(c["tx"]), c["nin"]) for c in allc]
+    errors = []
+
+    def single(k):
+        for i in range(k, len(allc), 4):
+            got = B.verify_script_with_amount(args[i][0], args[i][1], args[i][2], args[i][3], 0xE15)
+            if got != exp[i]:
+                errors.append(("single", i, got, exp[i]))
+
+    def batch(k):
+        for _ in range(3):
+            res = B.verify_batch(args[k::2], 0xE15)
+            if [(r, int(e)) for r, e in res] != exp[k::2]:
+                errors.append(("batch", k))
+
+    th = [threading.Thread(target=single, args=(k,)) for k in range(4)]
+    th += [threading.Thread(target=batch, args=(k,)) for k in range(2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errors, errors[:5]

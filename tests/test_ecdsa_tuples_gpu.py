@@ -51,3 +51,25 @@ def test_ecdsa_kernel_random_vs_oracle():
     v = B.ecdsa_verify_tuples(*_pack(sample))
     exp = [O.pubkey_verify(t["pub"], t["hash"], t["sig"]) for t in sample]
     assert list(v) == exp
+
+
+def test_ecdsa_tuples_concurrent_threads():
+    """mi_ecdsa_verify_tuples from 6 threads at once (each with its own scratch + stream) returns
+    the reference fixture verdicts in every thread."""
+    import threading
+    import bitcoinconsensus_amd as B
+    ts = ecdsa_tuples()
+    packed = _pack(ts)
+    exp = bytes(t["verdict"] for t in ts)
+    out = []
+
+    def work():
+        for _ in range(3):
+            out.append(B.ecdsa_verify_tuples(*packed) == exp)
+
+    th = [threading.Thread(target=work) for _ in range(6)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert len(out) == 18 and all(out)
