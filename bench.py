@@ -44,12 +44,13 @@ def cpu_baseline(wl, sample, threads):
         return None
     L = ctypes.CDLL(ref)
     L.ref_bench_verify_script.restype = ctypes.c_double
-    spks, txs, amts = [], [], []
+    spks, txs, amts, nins = [], [], [], []
     for i in range(sample):
-        s, a, t = wl.item(i)
+        s, a, t, k = wl.item(i)
         spks.append(s)
         txs.append(t)
         amts.append(a)
+        nins.append(k)
 
     def blob(parts):
         off = [0]
@@ -60,7 +61,7 @@ def cpu_baseline(wl, sample, threads):
     sb, so = blob(spks)
     tb, to = blob(txs)
     am = (ctypes.c_int64 * sample)(*amts)
-    nin = (ctypes.c_uint * sample)()
+    nin = (ctypes.c_uint * sample)(*nins)
     ret = (ctypes.c_int * sample)()
     args = (ctypes.c_long(sample), sb, so, tb, to, am, nin, ctypes.c_uint(0xE15), ret)
     L.ref_bench_verify_script(ctypes.c_int(threads), ctypes.c_long(min(sample, 2000)), *args[1:])  # warm

@@ -11,6 +11,8 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include "bitcoinconsensus.h"
+
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -62,7 +64,15 @@ typedef struct bcc_workload bcc_workload;
  * nonces and amounts derived from `seed`.  Keys and signatures are produced by
  * the engine's own GPU kernels; txs / sighash jobs are staged in HBM. */
 bcc_workload* bcc_workload_p2wpkh(size_t n, uint64_t seed, int device);
+/* C3: block replay.  ntx transactions with tx_nin[j] inputs / tx_nout[j] outputs (the histogram
+ * of the reference's bench/data/block413567.raw), inputs 60 % P2PKH / 30 % P2WPKH / 10 % P2SH
+ * 2-of-3 multisig, re-signed with synthetic keys from `seed`.  One item per
+ * input, in transaction order. */
+bcc_workload* bcc_workload_block(const uint32_t* tx_nin, const uint32_t* tx_nout, size_t ntx,
+                                 uint64_t seed, int device);
 void bcc_workload_free(bcc_workload* w);
+/* the workload's items (valid while w lives), e.g. for bitcoinconsensus_verify_batch */
+const bcc_batch_item* bcc_workload_items(const bcc_workload* w, size_t* n);
 size_t bcc_workload_size(const bcc_workload* w);
 /* launch the full hot path (sighash kernels + ECDSA kernel) on the staged inputs */
 int bcc_workload_run(bcc_workload* w, void* stream);

@@ -98,6 +98,11 @@ def _bind_consensus(L):
     vp, sz = ctypes.c_void_p, ctypes.c_size_t
     L.bcc_workload_p2wpkh.argtypes = [sz, ctypes.c_uint64, ctypes.c_int]
     L.bcc_workload_p2wpkh.restype = vp
+    u32p = ctypes.POINTER(ctypes.c_uint32)
+    L.bcc_workload_block.argtypes = [u32p, u32p, sz, ctypes.c_uint64, ctypes.c_int]
+    L.bcc_workload_block.restype = vp
+    L.bcc_workload_items.argtypes = [vp, ctypes.POINTER(sz)]
+    L.bcc_workload_items.restype = ctypes.POINTER(BatchItem)
     L.bcc_workload_free.argtypes = [vp]
     L.bcc_workload_size.argtypes = [vp]
     L.bcc_workload_size.restype = sz
@@ -114,14 +119,36 @@ def _bind_consensus(L):
 
 
 class Workload:
-    """A synthetic workload staged in HBM (include/bcc_amd.h, bcc_workload_*)."""
+    """A synthetic workload staged in HBM (include/bcc_amd.h, bcc_workload_*).
 
-    def __init__(self, n, seed=0x5EED0001, device=0, kind="p2wpkh"):
-        assert kind == "p2wpkh"
-        self.h = lib().bcc_workload_p2wpkh(n, seed, device)
+    kind "p2wpkh": config C2, n one-input P2WPKH spends.
+    kind "block":  config C3, transactions shaped by `shape` = [(n_inputs, n_outputs), ...]
+                   (one item per input)."""
+
+    def __init__(self, n=0, seed=0x5EED0001, device=0, kind="p2wpkh", shape=None):
+        if kind == "p2wpkh":
+            self.h = lib().bcc_workload_p2wpkh(n, seed, device)
+        elif kind == "block":
+            nin = (ctypes.c_uint32 * len(shape))(*[a for a, _ in shape])
+            nout = (ctypes.c_uint32 * len(shape))(*[b for _, b in shape])
+            self.h = lib().bcc_workload_block(nin, nout, len(shape), seed, device)
+        else:
+            raise ValueError(kind)
         if not self.h:
-            raise RuntimeError("bcc_workload_p2wpkh failed")
-        self.n = n
+            raise RuntimeError(f"bcc_workload_{kind} failed")
+        self.n = lib().bcc_workload_size(self.h)
+        self.kind = kind
+
+    def verify_batch(self, flags=VERIFY_ALL):
+        """bitcoinconsensus_verify_batch over all items (host interpreter + GPU rounds, end to
+        end, host buffers as the drop-in receives them).  Returns (n_valid, ret bytes)."""
+        cnt = ctypes.c_size_t(0)
+        items = lib().bcc_workload_items(self.h, ctypes.byref(cnt))
+        ret = (ctypes.c_int * max(1, cnt.value))()
+        rc = lib().bitcoinconsensus_verify_batch(items, cnt.value, flags & 0xffffffff, ret, None)
+        if rc < 0:
+            raise RuntimeError("bitcoinconsensus_verify_batch: device pipeline failed")
+        return rc, bytes(ret[i] for i in range(cnt.value))
 
     def run(self, stream=None):
         rc = lib().bcc_workload_run(self.h, stream)
@@ -152,12 +179,11 @@ class Workload:
                         (x.value for x in v)))
 
     def item(self, i):
-        spk = ctypes.create_string_buffer(64)
-        sl = ctypes.c_size_t(0)
-        amt = ctypes.c_int64(0)
-        tx = ctypes.create_string_buffer(512)
-        n = lib().bcc_workload_item(self.h, i, spk, ctypes.byref(sl), ctypes.byref(amt), tx, 512)
-        return spk.raw[: sl.value], amt.value, tx.raw[:n]
+        """(spent script, amount, tx bytes, input index) of item i."""
+        cnt = ctypes.c_size_t(0)
+        it = lib().bcc_workload_items(self.h, ctypes.byref(cnt))[i]
+        return (ctypes.string_at(it.script_pubkey, it.script_pubkey_len), it.amount,
+                ctypes.string_at(it.tx_to, it.tx_to_len), it.n_in)
 
     def free(self):
         if self.h:

@@ -8,10 +8,13 @@
 // otherwise it is re-run with the verdicts learned so far, deferring only the checks it has not
 // seen (e.g. the next multisig key), until a run needs no unknown verdict.  This reproduces the
 // reference's verdict-dependent control flow (CHECKMULTISIG key advance, CHECKSIG NOT) exactly.
+#include <algorithm>
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -193,29 +196,65 @@ struct BatchState {
     unsigned flags = 0;
 };
 
-// verify_script's pre-checks (bitcoinconsensus.cpp:83-95) in reference order.
-void prepare(BatchState& b, const bcc_batch_item* items, size_t n, unsigned flags) {
+unsigned host_threads() {
+    static const unsigned t = [] {
+        const char* e = getenv("BCC_HOST_THREADS");
+        unsigned v = e ? (unsigned)atoi(e) : std::min(16u, std::thread::hardware_concurrency());
+        return std::max(1u, v);
+    }();
+    return t;
+}
+
+// Runs f(t) for t in [0, T) on T threads (inline when T == 1).
+template <class F>
+void run_threads(unsigned T, F f) {
+    if (T <= 1) {
+        f(0u);
+        return;
+    }
+    std::vector<std::thread> th;
+    th.reserve(T - 1);
+    for (unsigned t = 1; t < T; t++) th.emplace_back(f, t);
+    f(0u);
+    for (auto& x : th) x.join();
+}
+
+// verify_script's pre-checks (bitcoinconsensus.cpp:83-95) in reference order.  Distinct tx
+// buffers are deserialized once each, in parallel over T threads.
+void prepare(BatchState& b, const bcc_batch_item* items, size_t n, unsigned flags, unsigned T) {
     b.st.assign(n, Item());
     b.flags = flags;
     auto& st = b.st;
     auto& txs = b.txs;
     const bool flags_ok = (flags & ~(unsigned)FLAGS_VERIFY_ALL) == 0;
+    std::vector<std::pair<const bcc_batch_item*, TxEntry*>> fresh;
     for (size_t i = 0; i < n; i++) {
         Item& it = st[i];
         it.in = &items[i];
-        if (!flags_ok) {
-            it.err = bitcoinconsensus_ERR_INVALID_FLAGS;
-            continue;
-        }
+        if (!flags_ok) continue;
         std::string tk((const char*)&items[i].tx_to, sizeof(void*));
         tk.append((const char*)&items[i].tx_to_len, sizeof(unsigned));
         auto f = txs.find(tk);
         if (f == txs.end()) {
             f = txs.emplace(tk, TxEntry()).first;
-            f->second.ok = items[i].tx_to != nullptr &&
-                           parse_tx(items[i].tx_to, items[i].tx_to_len, f->second.tx);
+            fresh.emplace_back(&items[i], &f->second);
         }
         it.tx = &f->second;
+    }
+    if (fresh.size() < 64) T = 1;
+    run_threads(T, [&](unsigned t) {
+        for (size_t k = t; k < fresh.size(); k += T) {
+            const bcc_batch_item* in = fresh[k].first;
+            TxEntry* e = fresh[k].second;
+            e->ok = in->tx_to != nullptr && parse_tx(in->tx_to, in->tx_to_len, e->tx);
+        }
+    });
+    for (size_t i = 0; i < n; i++) {
+        Item& it = st[i];
+        if (!flags_ok) {
+            it.err = bitcoinconsensus_ERR_INVALID_FLAGS;
+            continue;
+        }
         if (!it.tx->ok) {
             it.err = bitcoinconsensus_ERR_TX_DESERIALIZE;
             continue;
@@ -233,16 +272,16 @@ void prepare(BatchState& b, const bcc_batch_item* items, size_t n, unsigned flag
     }
 }
 
-// One interpreter pass over the active items; deferred checks land in rd.  Returns whether any
-// item ran.
-bool interpret_round(BatchState& b, Round& rd) {
+// Interpreter pass over the active items of one shard; deferred checks land in rd.  Returns
+// whether any item ran.
+bool interpret_shard(BatchState& b, const std::vector<uint32_t>& idx, Round& rd) {
     bool any = false;
-    for (size_t i = 0; i < b.st.size(); i++) {
+    for (uint32_t i : idx) {
         Item& it = b.st[i];
         if (!it.active) continue;
         any = true;
         it.pending.clear();
-        DeferringChecker chk(rd, (uint32_t)i, it);
+        DeferringChecker chk(rd, i, it);
         const TxIn& in = it.tx->tx.vin[it.in->n_in];
         Span spk{it.in->script_pubkey, it.in->script_pubkey_len};
         ScriptErr se;
@@ -258,7 +297,25 @@ bool interpret_round(BatchState& b, Round& rd) {
     return any;
 }
 
+// Splits the items into T shards of whole transactions (items of one tx share its TxEntry, whose
+// BIP143 aux slots the shard's Round owns), balanced by item count.
+std::vector<std::vector<uint32_t>> make_shards(const BatchState& b, unsigned T) {
+    const size_t n = b.st.size();
+    std::vector<std::vector<uint32_t>> sh(T);
+    std::unordered_map<const TxEntry*, unsigned> owner;
+    for (size_t i = 0; i < n; i++) {
+        const TxEntry* e = b.st[i].tx;
+        unsigned t = (unsigned)(i * T / std::max<size_t>(n, 1));
+        if (e) t = owner.emplace(e, t).first->second;
+        sh[t].push_back((uint32_t)i);
+    }
+    return sh;
+}
+
 // Runs the batch; fills ret/err per item.  Returns -1 if the device pipeline failed.
+// Host work (deserialization, interpreter passes, preimage building) runs on up to
+// host_threads() threads over whole-transaction shards; each round's deferred checks of all
+// shards go to the GPU as one batch.
 long run_batch(const bcc_batch_item* items, size_t n, unsigned flags, int* ret_out,
                bitcoinconsensus_error* err_out) {
     using clk = std::chrono::steady_clock;
@@ -266,24 +323,49 @@ long run_batch(const bcc_batch_item* items, size_t n, unsigned flags, int* ret_o
     t_stats.items = n;
     double host_s = 0, gpu_s = 0;
     auto t0 = clk::now();
+    const unsigned T = n >= 256 ? std::min<unsigned>(host_threads(), (unsigned)(n / 64)) : 1u;
     BatchState b;
-    prepare(b, items, n, flags);
+    prepare(b, items, n, flags, T);
     auto& st = b.st;
     const int dev = current_device();
-    Round rd;
+    const auto shards = make_shards(b, T);
+    std::vector<Round> rds(T);
+    std::vector<size_t> row0(T + 1, 0);
+    SighashJobs mjobs;
+    TupleRows mrows;
     std::vector<uint8_t> verdict;
     long status = 0;
     for (size_t round = 0;; round++) {
-        rd.reset();
-        bool any = interpret_round(b, rd);
-        if (!any || rd.pending.empty()) break;
+        std::vector<char> ran(T, 0);
+        run_threads(T, [&](unsigned t) {
+            rds[t].reset();
+            ran[t] = interpret_shard(b, shards[t], rds[t]);
+        });
+        size_t npend = 0;
+        bool any = false;
+        for (unsigned t = 0; t < T; t++) {
+            row0[t] = npend;
+            npend += rds[t].pending.size();
+            any |= ran[t] != 0;
+        }
+        row0[T] = npend;
+        if (!any || npend == 0) break;
+        const SighashJobs* jobs = &rds[0].jobs;
+        const TupleRows* rows = &rds[0].rows;
+        if (T > 1) {  // one device batch for the whole round
+            mjobs.clear();
+            mrows.clear();
+            for (unsigned t = 0; t < T; t++) append_round(mjobs, mrows, rds[t].jobs, rds[t].rows);
+            jobs = &mjobs;
+            rows = &mrows;
+        }
         t_stats.rounds++;
-        t_stats.tuples += rd.rows.size();
-        t_stats.preimages += rd.jobs.pre_off.size();
-        t_stats.aux_messages += rd.jobs.aux_off.size();
+        t_stats.tuples += rows->size();
+        t_stats.preimages += jobs->pre_off.size();
+        t_stats.aux_messages += jobs->aux_off.size();
         auto g0 = clk::now();
-        verdict.assign(rd.rows.size(), 0);
-        int e = gpu_verify_batch(dev, rd.jobs, rd.rows, verdict.data());
+        verdict.assign(rows->size(), 0);
+        int e = gpu_verify_batch(dev, *jobs, *rows, verdict.data());
         gpu_s += std::chrono::duration<double>(clk::now() - g0).count();
         if (e != 0) {
             status = -1;
@@ -295,18 +377,21 @@ long run_batch(const bcc_batch_item* items, size_t n, unsigned flags, int* ret_o
                 }
             break;
         }
-        for (size_t k = 0; k < rd.pending.size(); k++) {
-            Item& it = st[rd.pending[k].item];
-            it.cache[rd.pending[k].key] = (int8_t)verdict[k];
-        }
-        for (auto& it : st) {
-            if (it.pending.empty()) continue;
-            bool all_true = true;
-            for (uint32_t k : it.pending) all_true &= verdict[k] != 0;
-            if (!all_true) it.active = true;  // speculation was wrong somewhere: re-run
-        }
+        run_threads(T, [&](unsigned t) {
+            const Round& rd = rds[t];
+            const uint8_t* v = verdict.data() + row0[t];
+            for (size_t k = 0; k < rd.pending.size(); k++)
+                st[rd.pending[k].item].cache[rd.pending[k].key] = (int8_t)v[k];
+            for (uint32_t i : shards[t]) {
+                Item& it = st[i];
+                if (it.pending.empty()) continue;
+                bool all_true = true;
+                for (uint32_t k : it.pending) all_true &= v[k] != 0;
+                if (!all_true) it.active = true;  // speculation was wrong somewhere: re-run
+            }
+        });
     }
-    t_stats.host_rejected = rd.host_rejected;
+    for (unsigned t = 0; t < T; t++) t_stats.host_rejected += rds[t].host_rejected;
     long valid = 0;
     for (size_t i = 0; i < n; i++) {
         Item& it = st[i];
@@ -326,9 +411,11 @@ long run_batch(const bcc_batch_item* items, size_t n, unsigned flags, int* ret_o
 size_t build_first_round(const bcc_batch_item* items, size_t n, unsigned flags, SighashJobs& jobs,
                          TupleRows& rows, std::vector<uint32_t>* tuple_item) {
     BatchState b;
-    prepare(b, items, n, flags);
+    prepare(b, items, n, flags, 1);
     Round rd;
-    interpret_round(b, rd);
+    std::vector<uint32_t> all(n);
+    for (size_t i = 0; i < n; i++) all[i] = (uint32_t)i;
+    interpret_shard(b, all, rd);
     if (tuple_item) {
         tuple_item->clear();
         for (const auto& p : rd.pending) tuple_item->push_back(p.item);

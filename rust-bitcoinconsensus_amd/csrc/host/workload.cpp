@@ -10,6 +10,7 @@
 // The staged device batch is exactly what bitcoinconsensus_verify_batch hands the GPU for these
 // inputs: the engine's own first-round interpreter pass (build_first_round) builds it.
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <thread>
 #include <vector>
@@ -19,15 +20,19 @@
 #include "engine.h"
 #include "hashes.h"
 #include "script.h"
+#include "sighash.h"
 #include "tx.h"
 
 struct bcc_workload {
     int device = 0;
-    size_t n = 0;
+    size_t n = 0;                // items (spends)
     std::vector<uint8_t> txblob;
-    std::vector<size_t> txoff;  // n + 1
-    std::vector<uint8_t> spk;   // 22 bytes per item
+    std::vector<size_t> txoff;   // per transaction, + 1
+    std::vector<uint8_t> spkblob;
+    std::vector<size_t> spkoff;  // per item, + 1
     std::vector<int64_t> amount;
+    std::vector<uint32_t> item_tx, item_nin;
+    std::vector<bcc_batch_item> items;  // borrowed pointers into the blobs above
     bcc::DeviceBatch* batch = nullptr;
 };
 
@@ -70,7 +75,7 @@ void put_le(std::vector<uint8_t>& o, uint64_t v, int k) {
 template <class F>
 void parallel_for(size_t n, F f) {
     unsigned T = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-    if (n < 4096) T = 1;
+    T = (unsigned)std::max<size_t>(1, std::min<size_t>(T, n / 64));
     std::vector<std::thread> th;
     for (unsigned t = 0; t < T; t++)
         th.emplace_back([=]() {
@@ -101,6 +106,62 @@ void der_encode(const uint8_t* r, const uint8_t* s, uint8_t hashtype, std::vecto
     out.push_back(hashtype);
 }
 
+void push_data(std::vector<uint8_t>& o, const uint8_t* p, size_t n) {
+    if (n < 76) {
+        o.push_back((uint8_t)n);
+    } else {
+        o.push_back(0x4c);  // OP_PUSHDATA1
+        o.push_back((uint8_t)n);
+    }
+    o.insert(o.end(), p, p + n);
+}
+
+// Items from the blobs, then the engine's first interpreter round over all of them (threaded,
+// merged in item order), staged in HBM: exactly the batch bitcoinconsensus_verify_batch hands the
+// GPU first.  Frees w and returns nonzero on failure.
+int finish(bcc_workload* w) {
+    const size_t n = w->n;
+    w->items.resize(n);
+    for (size_t i = 0; i < n; i++) {
+        size_t t = w->item_tx[i];
+        w->items[i] = bcc_batch_item{&w->spkblob[w->spkoff[i]],
+                                     (unsigned)(w->spkoff[i + 1] - w->spkoff[i]), w->amount[i],
+                                     &w->txblob[w->txoff[t]],
+                                     (unsigned)(w->txoff[t + 1] - w->txoff[t]), w->item_nin[i]};
+    }
+    unsigned T = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    std::vector<bcc::SighashJobs> pj(T);
+    std::vector<bcc::TupleRows> pr(T);
+    // split on transaction boundaries: items of one tx share its BIP143 aux messages
+    std::vector<size_t> cut(T + 1, n);
+    cut[0] = 0;
+    for (unsigned t = 1; t < T; t++) {
+        size_t c = std::max(cut[t - 1], n * t / T);
+        while (c > 0 && c < n && w->item_tx[c] == w->item_tx[c - 1]) c++;
+        cut[t] = c;
+    }
+    std::vector<std::thread> th;
+    for (unsigned t = 0; t < T; t++)
+        th.emplace_back([&, t]() {
+            build_first_round(w->items.data() + cut[t], cut[t + 1] - cut[t], FLAGS_VERIFY_ALL,
+                              pj[t], pr[t]);
+        });
+    for (auto& x : th) x.join();
+    bcc::SighashJobs jobs;
+    bcc::TupleRows rows;
+    for (unsigned t = 0; t < T; t++) {
+        append_round(jobs, rows, pj[t], pr[t]);
+        pj[t] = bcc::SighashJobs();
+        pr[t] = bcc::TupleRows();
+    }
+    w->batch = new bcc::DeviceBatch(w->device);
+    if (w->batch->stage(jobs, rows) != 0) {
+        bcc_workload_free(w);
+        return 1;
+    }
+    return 0;
+}
+
 }  // namespace
 
 extern "C" {
@@ -111,6 +172,7 @@ bcc_workload* bcc_workload_p2wpkh(size_t n, uint64_t seed, int device) {
     w->n = n;
     std::vector<uint8_t> d(32 * n), px(32 * n), py(32 * n), ok(n), m(32 * n), k(32 * n),
         r(32 * n), s(32 * n);
+    w->txoff.reserve(n + 1);
     // 1. keys
     parallel_for(n, [&](size_t lo, size_t hi, unsigned) {
         uint8_t buf[9 + 16];
@@ -126,7 +188,7 @@ bcc_workload* bcc_workload_p2wpkh(size_t n, uint64_t seed, int device) {
         return nullptr;
     }
     // 2. unsigned txs + BIP143 sighashes (host, generation only)
-    w->spk.resize(22 * n);
+    w->spkblob.resize(22 * n);
     w->amount.resize(n);
     std::vector<std::vector<uint8_t>> pubs(n);
     parallel_for(n, [&](size_t lo, size_t hi, unsigned) {
@@ -138,7 +200,7 @@ bcc_workload* bcc_workload_p2wpkh(size_t n, uint64_t seed, int device) {
             memcpy(&pub[1], &px[32 * i], 32);
             uint8_t h160[20];
             hash160(pub.data(), 33, h160);
-            uint8_t* spk = &w->spk[22 * i];
+            uint8_t* spk = &w->spkblob[22 * i];
             spk[0] = 0x00;
             spk[1] = 0x14;
             memcpy(spk + 2, h160, 20);
@@ -239,29 +301,12 @@ bcc_workload* bcc_workload_p2wpkh(size_t n, uint64_t seed, int device) {
     for (size_t i = 0; i < n; i++) memcpy(&w->txblob[w->txoff[i]], txs[i].data(), txs[i].size());
     txs.clear();
     pubs.clear();
-    // 5. the engine's first round over all items (threaded, merged in item order), staged in HBM
-    std::vector<bcc_batch_item> items(n);
-    for (size_t i = 0; i < n; i++)
-        items[i] = bcc_batch_item{&w->spk[22 * i], 22, w->amount[i], &w->txblob[w->txoff[i]],
-                                  (unsigned)(w->txoff[i + 1] - w->txoff[i]), 0};
-    unsigned T = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-    std::vector<bcc::SighashJobs> pj(T);
-    std::vector<bcc::TupleRows> pr(T);
-    parallel_for(n, [&](size_t lo, size_t hi, unsigned t) {
-        build_first_round(items.data() + lo, hi - lo, FLAGS_VERIFY_ALL, pj[t], pr[t]);
-    });
-    bcc::SighashJobs jobs;
-    bcc::TupleRows rows;
-    for (unsigned t = 0; t < T; t++) {
-        append_round(jobs, rows, pj[t], pr[t]);
-        pj[t] = bcc::SighashJobs();
-        pr[t] = bcc::TupleRows();
-    }
-    w->batch = new bcc::DeviceBatch(device);
-    if (w->batch->stage(jobs, rows) != 0) {
-        bcc_workload_free(w);
-        return nullptr;
-    }
+    w->spkoff.resize(n + 1);
+    w->item_tx.resize(n);
+    w->item_nin.assign(n, 0);
+    for (size_t i = 0; i <= n; i++) w->spkoff[i] = 22 * i;
+    for (size_t i = 0; i < n; i++) w->item_tx[i] = (uint32_t)i;
+    if (finish(w)) return nullptr;
     return w;
 }
 
@@ -291,12 +336,310 @@ void bcc_workload_shape(const bcc_workload* w, size_t* tuples, size_t* sighash_b
 size_t bcc_workload_item(const bcc_workload* w, size_t i, uint8_t* spk, size_t* spk_len,
                          int64_t* amount, uint8_t* tx, size_t cap) {
     if (!w || i >= w->n) return 0;
-    memcpy(spk, &w->spk[22 * i], 22);
-    *spk_len = 22;
-    *amount = w->amount[i];
-    size_t len = w->txoff[i + 1] - w->txoff[i];
-    memcpy(tx, &w->txblob[w->txoff[i]], std::min(len, cap));
-    return len;
+    const bcc_batch_item& it = w->items[i];
+    memcpy(spk, it.script_pubkey, std::min<size_t>(it.script_pubkey_len, 64));
+    *spk_len = it.script_pubkey_len;
+    *amount = it.amount;
+    memcpy(tx, it.tx_to, std::min<size_t>(it.tx_to_len, cap));
+    return it.tx_to_len;
+}
+
+const bcc_batch_item* bcc_workload_items(const bcc_workload* w, size_t* n) {
+    if (n) *n = w ? w->n : 0;
+    return w ? w->items.data() : nullptr;
 }
 
 }  // extern "C"
+
+// ------------------------------------------------------------------------------------------
+// C3: block replay.  Transactions with the (inputs, outputs) counts given by the
+// caller (the histogram of the reference's bench/data/block413567.raw, tests/golden/
+// block413567_shape.json), re-signed with synthetic keys because the block's prevouts are not
+// in the block.  Input type per input: 60 % P2PKH (legacy sighash), 30 % P2WPKH (BIP143),
+// 10 % P2SH 2-of-3 CHECKMULTISIG (legacy, signer pair uniform over {1,2}, {1,3}, {2,3}, so
+// 2-3 signature checks per input); outputs P2PKH : P2SH = 2841 : 737 as in the block.  All
+// signatures SIGHASH_ALL, low-S, strict DER; a transaction with a P2WPKH input is serialized
+// with witnesses (version 2), otherwise legacy (version 1).
+// ------------------------------------------------------------------------------------------
+namespace {
+
+enum InType : uint8_t { IN_P2PKH = 0, IN_P2WPKH = 1, IN_MS = 2 };
+
+struct PlanIn {
+    uint8_t type;
+    uint8_t pair;      // multisig signer pair: 0 {1,2}, 1 {1,3}, 2 {2,3}
+    uint32_t key0;     // first key index (multisig: 3 consecutive keys)
+    int64_t amount;
+    uint8_t m[32];     // sighash
+    uint32_t sig0;     // first signature index (multisig: 2)
+};
+
+}  // namespace
+
+extern "C" bcc_workload* bcc_workload_block(const uint32_t* tx_nin, const uint32_t* tx_nout,
+                                            size_t ntx, uint64_t seed, int device) {
+    auto* w = new bcc_workload();
+    w->device = device;
+    // ---- plan: input types, key indices ----
+    std::vector<std::vector<PlanIn>> plan(ntx);
+    std::vector<size_t> tx_key0(ntx + 1, 0), tx_sig0(ntx + 1, 0), tx_item0(ntx + 1, 0);
+    for (size_t j = 0; j < ntx; j++) {
+        plan[j].resize(tx_nin[j]);
+        size_t keys = 0, sigs = 0;
+        for (uint32_t i = 0; i < tx_nin[j]; i++) {
+            uint64_t r = splitmix64(seed ^ ((uint64_t)j << 20) ^ i ^ 0xC3C3C3C3ULL);
+            PlanIn& p = plan[j][i];
+            unsigned u = (unsigned)(r % 10);
+            p.type = u < 6 ? IN_P2PKH : u < 9 ? IN_P2WPKH : IN_MS;
+            p.pair = (uint8_t)((r >> 8) % 3);
+            p.key0 = (uint32_t)(tx_key0[j] + keys);
+            p.sig0 = (uint32_t)(tx_sig0[j] + sigs);
+            p.amount = 546 + (int64_t)((r >> 16) % (uint64_t)(50000000000LL));
+            keys += p.type == IN_MS ? 3 : 1;
+            sigs += p.type == IN_MS ? 2 : 1;
+        }
+        tx_key0[j + 1] = tx_key0[j] + keys;
+        tx_sig0[j + 1] = tx_sig0[j] + sigs;
+        tx_item0[j + 1] = tx_item0[j] + tx_nin[j];
+    }
+    const size_t K = tx_key0[ntx], S = tx_sig0[ntx], n = tx_item0[ntx];
+    w->n = n;
+    // ---- keys (GPU) ----
+    std::vector<uint8_t> d(32 * K), px(32 * K), py(32 * K), ok(std::max<size_t>(K, S));
+    parallel_for(K, [&](size_t lo, size_t hi, unsigned) {
+        uint8_t buf[9 + 16];
+        memcpy(buf, "mi355x-c3", 9);
+        for (size_t k = lo; k < hi; k++) {
+            for (int b = 0; b < 8; b++) buf[9 + b] = (uint8_t)(seed >> (8 * b));
+            for (int b = 0; b < 8; b++) buf[17 + b] = (uint8_t)((uint64_t)k >> (8 * b));
+            derive_scalar(buf, sizeof buf, &d[32 * k]);
+        }
+    });
+    if (mi_gen_pubkeys(d.data(), K, px.data(), py.data(), ok.data(), device) != 0) {
+        delete w;
+        return nullptr;
+    }
+    auto pub33 = [&](size_t k, uint8_t* o) {
+        o[0] = 0x02 | (py[32 * k + 31] & 1);
+        memcpy(o + 1, &px[32 * k], 32);
+    };
+    auto redeem = [&](const PlanIn& p, std::vector<uint8_t>& o) {  // OP_2 <k1> <k2> <k3> OP_3 OP_CMS
+        o.clear();
+        o.push_back(0x52);
+        for (int q = 0; q < 3; q++) {
+            uint8_t pk[33];
+            pub33(p.key0 + q, pk);
+            push_data(o, pk, 33);
+        }
+        o.push_back(0x53);
+        o.push_back(0xae);
+    };
+    auto spk_of = [&](const PlanIn& p, std::vector<uint8_t>& o) {
+        o.clear();
+        uint8_t h[20];
+        if (p.type == IN_MS) {
+            std::vector<uint8_t> rs;
+            redeem(p, rs);
+            hash160(rs.data(), rs.size(), h);
+            o.insert(o.end(), {0xa9, 0x14});
+            o.insert(o.end(), h, h + 20);
+            o.push_back(0x87);
+            return;
+        }
+        uint8_t pk[33];
+        pub33(p.key0, pk);
+        hash160(pk, 33, h);
+        if (p.type == IN_P2WPKH) {
+            o.insert(o.end(), {0x00, 0x14});
+            o.insert(o.end(), h, h + 20);
+        } else {
+            o.insert(o.end(), {0x76, 0xa9, 0x14});
+            o.insert(o.end(), h, h + 20);
+            o.insert(o.end(), {0x88, 0xac});
+        }
+    };
+    // ---- unsigned transactions + sighashes (host, generation only) ----
+    std::vector<std::vector<uint8_t>> outs(ntx);  // serialized vout section per tx
+    std::vector<uint8_t> sm(32 * S), sk(32 * S), sd(32 * S);
+    parallel_for(ntx, [&](size_t lo, size_t hi, unsigned) {
+        std::vector<uint8_t> un, pre, code, aux;
+        for (size_t j = lo; j < hi; j++) {
+            std::vector<uint8_t>& vo = outs[j];
+            vo.clear();
+            put_compact_size(vo, tx_nout[j]);
+            for (uint32_t o = 0; o < tx_nout[j]; o++) {
+                uint64_t r = splitmix64(seed * 31 + ((uint64_t)j << 24) + o);
+                put_le(vo, 1000 + r % 100000000ULL, 8);
+                uint8_t h[20], t[12];
+                for (int b = 0; b < 8; b++) t[b] = (uint8_t)(j >> (8 * b));
+                for (int b = 0; b < 4; b++) t[8 + b] = (uint8_t)(o >> (8 * b));
+                hash160(t, 12, h);
+                if ((r >> 40) % 3578 < 2841) {  // block413567: 2841 P2PKH : 737 P2SH outputs
+                    vo.push_back(25);
+                    vo.insert(vo.end(), {0x76, 0xa9, 0x14});
+                    vo.insert(vo.end(), h, h + 20);
+                    vo.insert(vo.end(), {0x88, 0xac});
+                } else {
+                    vo.push_back(23);
+                    vo.insert(vo.end(), {0xa9, 0x14});
+                    vo.insert(vo.end(), h, h + 20);
+                    vo.push_back(0x87);
+                }
+            }
+            bool seg = false;
+            for (const auto& p : plan[j]) seg |= p.type == IN_P2WPKH;
+            un.clear();
+            put_le(un, seg ? 2 : 1, 4);
+            put_compact_size(un, tx_nin[j]);
+            for (uint32_t i = 0; i < tx_nin[j]; i++) {
+                uint8_t t[20], op[32];
+                for (int b = 0; b < 8; b++) t[b] = (uint8_t)(j >> (8 * b));
+                for (int b = 0; b < 4; b++) t[8 + b] = (uint8_t)(i >> (8 * b));
+                for (int b = 0; b < 8; b++) t[12 + b] = (uint8_t)(seed >> (8 * b));
+                sha256(t, 20, op);
+                un.insert(un.end(), op, op + 32);
+                put_le(un, i % 3, 4);
+                un.push_back(0);  // scriptSig (other inputs' scriptSigs never enter a sighash)
+                put_le(un, 0xffffffffu, 4);
+            }
+            un.insert(un.end(), vo.begin(), vo.end());
+            put_le(un, 0, 4);
+            Tx tx;
+            if (!parse_tx(un.data(), un.size(), tx)) abort();
+            for (uint32_t i = 0; i < tx_nin[j]; i++) {
+                PlanIn& p = plan[j][i];
+                if (p.type == IN_MS) {
+                    redeem(p, code);
+                } else {
+                    uint8_t pk[33], h[20];
+                    pub33(p.key0, pk);
+                    hash160(pk, 33, h);
+                    code.assign({0x76, 0xa9, 0x14});
+                    code.insert(code.end(), h, h + 20);
+                    code.insert(code.end(), {0x88, 0xac});
+                }
+                if (p.type == IN_P2WPKH) {  // BIP143 (interpreter.cpp:1581-1625)
+                    Bip143Job job;
+                    build_bip143_preimage(tx, i, code, 1, p.amount, job);
+                    for (int k = 0; k < 3; k++) {
+                        if (!job.need[k]) continue;
+                        build_aux_message(tx, (AuxKind)k, aux);
+                        sha256d(aux.data(), aux.size(), &job.preimage[job.off[k]]);
+                    }
+                    sha256d(job.preimage.data(), job.preimage.size(), p.m);
+                } else {  // legacy (interpreter.cpp:1273-1364)
+                    if (!build_legacy_preimage(tx, i, code, 1, pre)) abort();
+                    sha256d(pre.data(), pre.size(), p.m);
+                }
+                const int nsig = p.type == IN_MS ? 2 : 1;
+                for (int q = 0; q < nsig; q++) {
+                    // signer keys: pair {1,2} {1,3} {2,3} -> key offsets
+                    const int ko = p.type != IN_MS ? 0 : (q == 0 ? (p.pair == 2 ? 1 : 0)
+                                                                  : (p.pair == 0 ? 1 : 2));
+                    size_t sgi = p.sig0 + q;
+                    memcpy(&sd[32 * sgi], &d[32 * (p.key0 + ko)], 32);
+                    memcpy(&sm[32 * sgi], p.m, 32);
+                    uint8_t nb[15 + 64];
+                    memcpy(nb, "mi355x-c3-nonce", 15);
+                    memcpy(nb + 15, &sd[32 * sgi], 32);
+                    memcpy(nb + 47, p.m, 32);
+                    derive_scalar(nb, sizeof nb, &sk[32 * sgi]);
+                }
+            }
+        }
+    });
+    // ---- signatures (GPU) ----
+    std::vector<uint8_t> r(32 * S), s(32 * S);
+    if (mi_gen_sign(sd.data(), sm.data(), sk.data(), S, r.data(), s.data(), ok.data(), device) != 0) {
+        delete w;
+        return nullptr;
+    }
+    // ---- final transactions, spent scripts, amounts ----
+    std::vector<std::vector<uint8_t>> txs(ntx), spks(n);
+    w->amount.resize(n);
+    w->item_tx.resize(n);
+    w->item_nin.resize(n);
+    parallel_for(ntx, [&](size_t lo, size_t hi, unsigned) {
+        std::vector<uint8_t> sig, sig2, ss, rs;
+        for (size_t j = lo; j < hi; j++) {
+            bool seg = false;
+            for (const auto& p : plan[j]) seg |= p.type == IN_P2WPKH;
+            std::vector<uint8_t>& t = txs[j];
+            put_le(t, seg ? 2 : 1, 4);
+            if (seg) t.insert(t.end(), {0x00, 0x01});
+            put_compact_size(t, tx_nin[j]);
+            for (uint32_t i = 0; i < tx_nin[j]; i++) {
+                const PlanIn& p = plan[j][i];
+                uint8_t tb[20], op[32];
+                for (int b = 0; b < 8; b++) tb[b] = (uint8_t)(j >> (8 * b));
+                for (int b = 0; b < 4; b++) tb[8 + b] = (uint8_t)(i >> (8 * b));
+                for (int b = 0; b < 8; b++) tb[12 + b] = (uint8_t)(seed >> (8 * b));
+                sha256(tb, 20, op);
+                t.insert(t.end(), op, op + 32);
+                put_le(t, i % 3, 4);
+                ss.clear();
+                der_encode(&r[32 * p.sig0], &s[32 * p.sig0], 0x01, sig);
+                if (p.type == IN_P2PKH) {
+                    uint8_t pk[33];
+                    pub33(p.key0, pk);
+                    push_data(ss, sig.data(), sig.size());
+                    push_data(ss, pk, 33);
+                } else if (p.type == IN_MS) {
+                    der_encode(&r[32 * (p.sig0 + 1)], &s[32 * (p.sig0 + 1)], 0x01, sig2);
+                    redeem(p, rs);
+                    ss.push_back(0x00);  // CHECKMULTISIG dummy (NULLDUMMY)
+                    push_data(ss, sig.data(), sig.size());
+                    push_data(ss, sig2.data(), sig2.size());
+                    push_data(ss, rs.data(), rs.size());
+                }
+                put_compact_size(t, ss.size());
+                t.insert(t.end(), ss.begin(), ss.end());
+                put_le(t, 0xffffffffu, 4);
+                size_t item = tx_item0[j] + i;
+                spk_of(p, spks[item]);
+                w->amount[item] = p.amount;
+                w->item_tx[item] = (uint32_t)j;
+                w->item_nin[item] = i;
+            }
+            t.insert(t.end(), outs[j].begin(), outs[j].end());
+            if (seg) {
+                for (uint32_t i = 0; i < tx_nin[j]; i++) {
+                    const PlanIn& p = plan[j][i];
+                    if (p.type != IN_P2WPKH) {
+                        t.push_back(0);
+                        continue;
+                    }
+                    uint8_t pk[33];
+                    pub33(p.key0, pk);
+                    der_encode(&r[32 * p.sig0], &s[32 * p.sig0], 0x01, sig);
+                    t.push_back(2);
+                    t.push_back((uint8_t)sig.size());
+                    t.insert(t.end(), sig.begin(), sig.end());
+                    t.push_back(33);
+                    t.insert(t.end(), pk, pk + 33);
+                }
+            }
+            put_le(t, 0, 4);
+        }
+    });
+    w->txoff.resize(ntx + 1);
+    size_t total = 0;
+    for (size_t j = 0; j < ntx; j++) {
+        w->txoff[j] = total;
+        total += txs[j].size();
+    }
+    w->txoff[ntx] = total;
+    w->txblob.resize(total);
+    for (size_t j = 0; j < ntx; j++) memcpy(&w->txblob[w->txoff[j]], txs[j].data(), txs[j].size());
+    w->spkoff.resize(n + 1);
+    total = 0;
+    for (size_t i = 0; i < n; i++) {
+        w->spkoff[i] = total;
+        total += spks[i].size();
+    }
+    w->spkoff[n] = total;
+    w->spkblob.resize(total);
+    for (size_t i = 0; i < n; i++) memcpy(&w->spkblob[w->spkoff[i]], spks[i].data(), spks[i].size());
+    if (finish(w)) return nullptr;
+    return w;
+}
