@@ -1,23 +1,34 @@
-"""bench.py — ECDSA verifies/s of the MI355X signature hot path (BASELINE.json metric, config C2).
+"""bench.py — ECDSA verifies/s of the MI355X signature hot path (BASELINE.json metric).
 
-    python bench.py [--gpus N --steps K --warmup W --n INPUTS_PER_GPU]
+    python bench.py [--gpus N --steps K --warmup W --config c2|c3|c4|c5 --n UNITS_PER_GPU]
     (N > 1: python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1
              --master-port P bench.py --gpus N ...)
 
-Workload (BASELINE.json configs[1]): n synthetic P2WPKH spends per GPU (default
-1,000,000), inputs resident in HBM (staged by the engine's own first-round interpreter pass).
-One step = one pass of the hot path over the batch: BIP143 sighash kernels (aux hashes, patch,
-preimage SHA-256d) + the ECDSA verify kernel (pubkey decompression, s^-1, GLV, Strauss ladder,
-x-check).  value = verifies of all ranks / max-over-ranks wall time of K steps.  Multi-GPU is
-weak scaling: every rank verifies its own shard (seed + rank), no collective in the timed loop.
+Default workload (BASELINE.json configs[1]): n synthetic P2WPKH spends per GPU
+(default 1,000,000), inputs resident in HBM (staged by the engine's own first-round interpreter
+pass).  One step = one pass of the hot path over the batch: BIP143 sighash kernels (aux hashes,
+patch, preimage SHA-256d) + the ECDSA kernels (batched s^-1, pubkey decompression + GLV + Q table,
+Strauss ladder + x-check).  value = verifies of all ranks / max-over-ranks wall time of K steps.
+Multi-GPU is weak scaling: every rank verifies its own shard (seed + rank), no collective in the
+timed loop.
+
+Other configs (run explicitly, results committed under profiles/):
+  c3  block replay: transactions shaped like the reference's bench block413567 (tiled to 4,000
+      txs), mixed P2PKH / P2WPKH / P2SH 2-of-3, through bitcoinconsensus_verify_batch end to end
+      (host buffers -> threaded host interpreter -> GPU sighash + ECDSA rounds -> verdicts); a
+      step is one verify_batch call.
+  c4  ECDSA tuples (pub, msg32, DER sig), 90 % valid + 18 adversarial classes, staged rows in HBM
+      (8M per GPU = the per-GPU shard of the 64M-tuple node batch); a step is the ECDSA kernels.
+  c5  BIP340 rows (GPU-signed + the 15 BIP340 vectors tiled), a step is the Schnorr kernels.
 
 Also reported:
-  roofline      the ECDSA kernel against the measured v_mad_u64_u32 issue rate (int-ALU bound:
-                MFMA is deliberately unused; SURVEY.md §8d W = 2,257 modmuls = 144,448 32x32->64
-                partial products per verify), kernel time from HIP events on the launch stream
-  cpu_baseline  the REFERENCE (oracle/_ref: Bitcoin Core v0.21 libbitcoinconsensus built from
-                /root/reference) bitcoinconsensus_verify_script_with_amount on a bounded sample of
-                the same inputs, std::thread pool over the host cores (rank 0, N = 1 only)
+  roofline      the signature kernels against the measured v_mad_u64_u32 issue rate (int-ALU
+                bound: MFMA is deliberately unused; SURVEY.md §8d W = 2,257 modmuls = 144,448
+                32x32->64 partial products per ECDSA verify; DESIGN.md §3 for BIP340), kernel time
+                from HIP events on the launch stream
+  cpu_baseline  the REFERENCE (oracle/_ref: Bitcoin Core v0.21 libbitcoinconsensus + libsecp256k1
+                built from /root/reference) on a bounded sample of the same inputs, std::thread
+                pool over the host cores (rank 0, N = 1 only)
 """
 import argparse
 import json
@@ -29,28 +40,32 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "rust-bitcoinconsensus_amd"))
 
 MADS_PER_VERIFY = 144448          # 2,257 modmuls x 64 (32x32->64) products
+MADS_PER_SCHNORR = 142848         # 2,232 modmuls x 64
 METRIC = "ECDSA verifies/sec (node) at 1/2/4/8 MI355X; % of int-ALU roofline"
+DEFAULT_N = {"c2": 1_000_000, "c3": 4000, "c4": 8_000_000, "c5": 4_000_000}
+SEEDS = {"c2": 0x5EED0001, "c3": 0x5EED0003, "c4": 0x5EED0004, "c5": 0x5EED0005}
+CPU_THREADS = 16                  # the GPU box's CPU share
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(wl, sample, threads):
-    """Reference libbitcoinconsensus on `sample` items of the workload (checker-side code)."""
+def _reference():
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from oracle_ctypes import Reference, reference_available
+    return Reference() if reference_available() else None
+
+
+def cpu_baseline_script(items, threads, what, unit="inputs/s"):
+    """Reference libbitcoinconsensus over (spk, amount, tx, nin) items (checker-side code)."""
     import ctypes
     ref = os.path.join(ROOT, "oracle", "_ref", "libref_consensus.so")
     if not os.path.exists(ref):
         return None
     L = ctypes.CDLL(ref)
     L.ref_bench_verify_script.restype = ctypes.c_double
-    spks, txs, amts, nins = [], [], [], []
-    for i in range(sample):
-        s, a, t, k = wl.item(i)
-        spks.append(s)
-        txs.append(t)
-        amts.append(a)
-        nins.append(k)
+    sample = len(items)
 
     def blob(parts):
         off = [0]
@@ -58,10 +73,10 @@ def cpu_baseline(wl, sample, threads):
             off.append(off[-1] + len(p))
         return b"".join(parts), (ctypes.c_long * len(off))(*off)
 
-    sb, so = blob(spks)
-    tb, to = blob(txs)
-    am = (ctypes.c_int64 * sample)(*amts)
-    nin = (ctypes.c_uint * sample)(*nins)
+    sb, so = blob([it[0] for it in items])
+    tb, to = blob([it[2] for it in items])
+    am = (ctypes.c_int64 * sample)(*[it[1] for it in items])
+    nin = (ctypes.c_uint * sample)(*[it[3] for it in items])
     ret = (ctypes.c_int * sample)()
     args = (ctypes.c_long(sample), sb, so, tb, to, am, nin, ctypes.c_uint(0xE15), ret)
     L.ref_bench_verify_script(ctypes.c_int(threads), ctypes.c_long(min(sample, 2000)), *args[1:])  # warm
@@ -69,9 +84,8 @@ def cpu_baseline(wl, sample, threads):
     ok = sum(ret[i] for i in range(sample))
     n1 = max(1, sample // 16)
     secs1 = L.ref_bench_verify_script(ctypes.c_int(1), ctypes.c_long(n1), *args[1:])
-    return dict(value=sample / secs, unit="verifies/s", cores=threads, kind="reference",
-                sample=f"{sample} C2 inputs (first {sample} of rank 0's workload), "
-                       f"bitcoinconsensus_verify_script_with_amount flags=0xE15, "
+    return dict(value=sample / secs, unit=unit, cores=threads, kind="reference",
+                sample=f"{sample} {what}, bitcoinconsensus_verify_script_with_amount flags=0xE15, "
                        f"std::thread pool x{threads}; reference accepted {ok}/{sample}",
                 single_core_value=n1 / secs1, cpu_seconds=secs * threads)
 
@@ -90,18 +104,214 @@ def aggregate(elapsed, n_valid, world, device="cuda"):
     return t.item(), int(c.item())
 
 
+# ---- per-config jobs: stage inputs, run one step, time the dominant kernels, CPU baseline ----
+
+class C2:
+    unit = "verifies/s"
+
+    def __init__(self, B, n, seed, dev):
+        self.wl = B.Workload(n, seed=seed, device=dev)
+        self.shape = self.wl.shape()
+        self.units = self.shape["tuples"]
+        self.n = n
+
+    def step(self, sp):
+        self.wl.run(sp)
+
+    def valid(self):
+        return sum(self.wl.verdicts())
+
+    def kernel_times(self, stream, reps):
+        import torch
+        e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+        sp = stream.cuda_stream
+        e[0].record(stream)
+        for _ in range(reps):
+            self.wl.run_sighash(sp)
+        e[1].record(stream)
+        for _ in range(reps):
+            self.wl.run_ecdsa(sp)
+        e[2].record(stream)
+        torch.cuda.synchronize()
+        return e[0].elapsed_time(e[1]) / reps, e[1].elapsed_time(e[2]) / reps
+
+    def extra(self, sighash_ms):
+        sh = self.shape
+        b = 64 * (sh["sighash_blocks"] + sh["aux_blocks"]) + 32 * (sh["preimages"] + sh["aux_messages"])
+        return {"sighash_stage": dict(kernels="sha256d aux + patch + sha256d preimage",
+                                      avg_ms=sighash_ms, algorithmic_bytes=b,
+                                      achieved_GBps=b / (sighash_ms * 1e-3) / 1e9, peak_GBps=8000.0)}
+
+    def cpu(self, sample):
+        sample = min(sample, self.n)
+        return cpu_baseline_script([self.wl.item(i) for i in range(sample)], CPU_THREADS,
+                                   f"C2 inputs (first {sample} of rank 0's workload)",
+                                   unit="verifies/s")
+
+    def config(self, world):
+        return {"workload": "C2: synthetic P2WPKH inputs, BIP143 sighash + ECDSA verify "
+                            "(BASELINE.json configs[1])",
+                "inputs_per_gpu": self.n, "global_inputs": self.n * world,
+                "parallelism": f"shard x{world} (independent tuples, no collective)"}
+
+    data = "synthetic (deterministic P2WPKH spends, GPU-generated keys/signatures)"
+    mads = MADS_PER_VERIFY
+    kernel = "ecdsa (batch_sinv + ecdsa_prep + ecdsa_ladder)"
+
+
+class C3(C2):
+    """Block replay through the drop-in batch ABI, end to end from host buffers."""
+    unit = "inputs/s"
+
+    def __init__(self, B, n, seed, dev):
+        self.B = B
+        shape = [tuple(t) for t in json.load(open(os.path.join(
+            ROOT, "tests", "golden", "block413567_shape.json")))["txs"]]
+        txs = (shape * (n // len(shape) + 1))[:n]
+        self.ntx = n
+        self.wl = B.Workload(kind="block", shape=txs, seed=seed, device=dev)
+        self.shape = self.wl.shape()
+        self.units = self.wl.n           # inputs
+        self.n = self.wl.n
+        self._valid = 0
+
+    def step(self, sp):
+        self._valid, _ = self.wl.verify_batch()
+
+    def valid(self):
+        self.step(None)
+        st = self.B.last_batch_stats()
+        self.stats = st
+        return self._valid
+
+    def extra(self, sighash_ms):
+        e = C2.extra(self, sighash_ms)
+        st = self.stats
+        e["batch_stats"] = {k: st[k] for k in ("items", "tuples", "rounds", "preimages",
+                                               "aux_messages", "host_rejected", "host_seconds",
+                                               "gpu_seconds", "prepare_seconds",
+                                               "interpret_seconds", "merge_seconds",
+                                               "stage_seconds", "total_seconds")}
+        e["note"] = ("value = inputs/s of bitcoinconsensus_verify_batch end to end from host "
+                     "buffers (host deserialize + interpreter + preimage building on up to 16 "
+                     "threads, H2D, GPU sighash + ECDSA, re-run rounds for CHECKMULTISIG key "
+                     "advance); roofline = the first round's staged ECDSA kernels in HBM")
+        return e
+
+    def cpu(self, sample):
+        sample = min(sample, self.n)
+        return cpu_baseline_script([self.wl.item(i) for i in range(sample)], CPU_THREADS,
+                                   f"C3 inputs (first {sample})")
+
+    def config(self, world):
+        return {"workload": f"C3: block replay, {self.ntx} txs with block413567's input/output "
+                            "histogram, 60% P2PKH / 30% P2WPKH / 10% P2SH 2-of-3, "
+                            "bitcoinconsensus_verify_batch end to end (BASELINE.json configs[2])",
+                "inputs_per_gpu": self.n, "global_inputs": self.n * world,
+                "parallelism": f"shard x{world} (independent batches, no collective)"}
+
+    data = "synthetic (block413567-shaped txs re-signed with GPU-generated keys/signatures)"
+
+
+class TupleJob:
+    def __init__(self, B, n, seed, dev, kind):
+        import bitcoinconsensus_amd as BB
+        vec = []
+        if kind == "c5":
+            sys.path.insert(0, os.path.join(ROOT, "tests"))
+            from fixtures import bip340_vectors
+            vec = [(t["sig"], t["msg"], t["pub"], t["verdict"]) for t in bip340_vectors()]
+        self.kind = kind
+        self.ts = BB.TupleSet(n, kind=kind, seed=seed, device=dev, vectors=vec)
+        self.units = self.n = n
+        self.unit = "verifies/s"
+        self.mads = MADS_PER_VERIFY if kind == "c4" else MADS_PER_SCHNORR
+        self.kernel = ("ecdsa (batch_sinv + ecdsa_prep + ecdsa_ladder)" if kind == "c4"
+                       else "schnorr (prep + ladder + y-parity batch inversion)")
+
+    def step(self, sp):
+        self.ts.run(sp)
+
+    def valid(self):
+        import numpy as np
+        v = np.frombuffer(self.ts.verdicts(), np.uint8)
+        h = self.ts.host()
+        self.mismatch_vs_construction = int((v != h["expect"]).sum())
+        return int(v.sum())
+
+    def kernel_times(self, stream, reps):
+        import torch
+        e = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        e[0].record(stream)
+        for _ in range(reps):
+            self.ts.run(stream.cuda_stream)
+        e[1].record(stream)
+        torch.cuda.synchronize()
+        return 0.0, e[0].elapsed_time(e[1]) / reps
+
+    def extra(self, sighash_ms):
+        import numpy as np
+        h = self.ts.host()
+        return {"expected_valid": int(h["expect"].sum()),
+                "mismatch_vs_construction": self.mismatch_vs_construction,
+                "class_counts": np.bincount(h["cls"]).tolist()}
+
+    def cpu(self, sample):
+        import numpy as np
+        R = _reference()
+        if R is None:
+            return None
+        sample = min(sample, self.n)
+        h = self.ts.host()
+        if self.kind == "c4":
+            args = (h["pub_blob"], h["pub_off"], h["msg32"], h["sig_blob"], h["sig_off"])
+            f, what = R.pubkey_verify_blob, "CPubKey::Verify"
+        else:
+            args = (h["sig64"], h["msg32"], h["xonly32"])
+            f, what = R.schnorr_verify_rows, "secp256k1_schnorrsig_verify"
+        f(*args, threads=CPU_THREADS, n=min(sample, 2000))  # warm
+        ref, secs = f(*args, threads=CPU_THREADS, n=sample)
+        n1 = max(1, sample // 16)
+        _, secs1 = f(*args, threads=1, n=n1)
+        v = np.frombuffer(self.ts.verdicts(), np.uint8)[:sample]
+        return dict(value=sample / secs, unit="verifies/s", cores=CPU_THREADS, kind="reference",
+                    sample=f"first {sample} {self.kind.upper()} tuples of rank 0, {what}, "
+                           f"std::thread pool x{CPU_THREADS}; reference accepted "
+                           f"{int(ref.sum())}/{sample}; GPU verdict mismatches on the sample: "
+                           f"{int((ref != v).sum())}",
+                    single_core_value=n1 / secs1, cpu_seconds=secs * CPU_THREADS)
+
+    def config(self, world):
+        if self.kind == "c4":
+            w = ("C4: ECDSA (pub, msg32, DER sig) tuples, 10% adversarial over 18 classes, "
+                 "CPubKey::Verify semantics (BASELINE.json configs[3]; node batch = 8 x per-GPU)")
+        else:
+            w = ("C5: BIP340 Schnorr rows, GPU-signed + the 15 BIP340 vectors tiled "
+                 "(BASELINE.json configs[4])")
+        return {"workload": w, "tuples_per_gpu": self.n, "global_tuples": self.n * world,
+                "parallelism": f"shard x{world} (independent tuples, no collective)"}
+
+    @property
+    def data(self):
+        return f"synthetic (deterministic {self.kind.upper()} tuples, GPU-generated keys/signatures)"
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--n", type=int, default=1_000_000, help="P2WPKH inputs per GPU")
-    ap.add_argument("--seed", type=int, default=0x5EED0001)
-    ap.add_argument("--cpu-sample", type=int, default=200_000)
+    ap.add_argument("--config", choices=("c2", "c3", "c4", "c5"), default="c2")
+    ap.add_argument("--n", type=int, default=None,
+                    help="units per GPU: inputs (c2), transactions (c3), tuples (c4, c5)")
+    ap.add_argument("--seed", type=int, default=None)
+    ap.add_argument("--cpu-sample", type=int, default=None)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--traffic", type=float, default=None,
                     help="HBM bytes per ECDSA launch from a rocprofv3 --pmc run (profiles/)")
     args = ap.parse_args()
+    n = args.n or DEFAULT_N[args.config]
+    seed = SEEDS[args.config] if args.seed is None else args.seed
 
     import torch
     import torch.distributed as dist
@@ -116,21 +326,25 @@ def main():
     else:
         torch.cuda.set_device(0)
     dev = torch.cuda.current_device()
+    B.set_device(dev)
 
     t0 = time.time()
-    wl = B.Workload(args.n, seed=args.seed + rank, device=dev)
-    shape = wl.shape()
-    log(f"[rank {rank}] staged {args.n} P2WPKH inputs in {time.time() - t0:.1f}s: {shape}")
-    stream = torch.cuda.current_stream()
+    if args.config in ("c2", "c3"):
+        job = (C2 if args.config == "c2" else C3)(B, n, seed + rank, dev)
+    else:
+        job = TupleJob(B, n, seed + rank, dev, args.config)
+    log(f"[rank {rank}] staged {args.config} x{n} in {time.time() - t0:.1f}s")
+    # a dedicated (non-null) stream: every launch of a step and the HIP events that time the
+    # kernels sit on it (torch's default stream is the null handle, which the engine maps to its
+    # own internal stream)
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
     sp = stream.cuda_stream
 
     for _ in range(args.warmup):
-        wl.run(sp)
+        job.step(sp)
     torch.cuda.synchronize()
-    v = wl.verdicts()
-    n_valid = sum(v)
-    if n_valid != len(v):
-        log(f"[rank {rank}] WARNING: {len(v) - n_valid} of {len(v)} verdicts invalid")
+    n_valid = job.valid()
 
     def barrier():
         if world > 1:
@@ -140,59 +354,43 @@ def main():
     torch.cuda.synchronize()
     ts = time.perf_counter()
     for _ in range(args.steps):
-        wl.run(sp)
+        job.step(sp)
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - ts
     elapsed, n_valid_all = aggregate(elapsed, n_valid, world)
 
     # per-kernel timing with HIP events on the launch stream (outside the timed region)
-    reps = max(3, args.steps)
-    e = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
-    e[0].record(stream)
-    for _ in range(reps):
-        wl.run_sighash(sp)
-    e[1].record(stream)
-    for _ in range(reps):
-        wl.run_ecdsa(sp)
-    e[2].record(stream)
-    torch.cuda.synchronize()
-    sighash_ms = e[0].elapsed_time(e[1]) / reps
-    ecdsa_ms = e[1].elapsed_time(e[2]) / reps
+    sighash_ms, sig_ms = job.kernel_times(stream, max(3, args.steps))
+    sig_units = job.shape["tuples"] if args.config in ("c2", "c3") else job.units
 
-    total = shape["tuples"] * world * args.steps
+    total = job.units * world * args.steps
     value = total / elapsed
     if rank == 0:
         peak = B.microbench(0, 4096)  # v_mad_u64_u32 lane-ops/s, measured on this GPU
-        achieved = shape["tuples"] * MADS_PER_VERIFY / (ecdsa_ms * 1e-3)
-        roof = dict(bound="int-alu", kernel="ecdsa_verify_kernel",
+        achieved = sig_units * job.mads / (sig_ms * 1e-3)
+        roof = dict(bound="int-alu", kernel=job.kernel,
                     achieved=achieved / 1e12, peak=peak / 1e12, unit="T(v_mad_u64_u32)/s",
                     frac=achieved / peak, traffic=args.traffic,
-                    per_launch=dict(verifies=shape["tuples"], mads=shape["tuples"] * MADS_PER_VERIFY,
-                                    avg_ms=ecdsa_ms))
-        sh_bytes = 64 * (shape["sighash_blocks"] + shape["aux_blocks"]) + 32 * (shape["preimages"] + shape["aux_messages"])
-        sighash = dict(kernels="sha256d aux + patch + sha256d preimage", avg_ms=sighash_ms,
-                       algorithmic_bytes=sh_bytes, achieved_GBps=sh_bytes / (sighash_ms * 1e-3) / 1e9,
-                       peak_GBps=8000.0)
+                    per_launch=dict(verifies=sig_units, mads=sig_units * job.mads, avg_ms=sig_ms,
+                                    verifies_per_s=sig_units / (sig_ms * 1e-3)))
         cpu = None
         if world == 1 and not args.no_cpu:
-            threads = min(16, os.cpu_count() or 1)
-            cpu = cpu_baseline(wl, min(args.cpu_sample, args.n), threads)
+            default_sample = {"c2": 200_000, "c3": 100_000, "c4": 400_000, "c5": 400_000}
+            cpu = job.cpu(args.cpu_sample or default_sample[args.config])
         out = {
-            "metric": METRIC, "value": value, "unit": "verifies/s", "n_gpus": world,
+            "metric": METRIC, "value": value, "unit": job.unit, "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "u32",
-            "data": "synthetic (deterministic P2WPKH spends, GPU-generated keys/signatures)",
-            "config": {"workload": "C2: synthetic P2WPKH inputs, BIP143 sighash + ECDSA verify "
-                                   "(BASELINE.json configs[1])",
-                       "inputs_per_gpu": args.n, "global_inputs": args.n * world,
-                       "parallelism": f"shard x{world} (independent tuples, no collective)"},
+            "data": job.data,
+            "config": job.config(world),
             "roofline": roof,
             "cpu_baseline": cpu,
-            "sighash_stage": sighash,
-            "verdicts_valid": n_valid_all, "verdicts_total": shape["tuples"] * world,
         }
+        out.update(job.extra(sighash_ms))
+        out["verdicts_valid"] = n_valid_all
+        out["verdicts_total"] = job.units * world
         if cpu:
             out["gpu_vs_cpu"] = value / cpu["value"]
         print(json.dumps(out), flush=True)

@@ -45,6 +45,42 @@ int mi_schnorr_verify_device(const uint8_t* d_sig64, const uint8_t* d_msg32,
                              const uint8_t* d_xonly32, uint8_t* d_verdict, size_t n,
                              void* stream);
 
+/* ---- tuple level with the CPubKey front end ---------------------------------------------------
+ * verdict[i] = CPubKey(pub_i).Verify(msg_i, sig_i) (depend/bitcoin/src/pubkey.cpp:191-207) for n
+ * tuples: pub_i = pub_blob[pub_off[i] .. pub_off[i+1]) (any length; the CPubKey length filter,
+ * pubkey.h:58-94, applies), sig_i = sig_blob[sig_off[i] .. sig_off[i+1]) = DER without the
+ * hashtype byte, parsed laxly (pubkey.cpp:28-168).  Synchronous on `device`.  0 or an error. */
+int bcc_pubkey_verify_batch(const uint8_t* pub_blob, const uint64_t* pub_off,
+                            const uint8_t* msg32, const uint8_t* sig_blob,
+                            const uint64_t* sig_off, uint8_t* verdict, size_t n, int device);
+
+/* ---- synthetic tuple sets (configs C4 / C5; bench.py / tests), staged in HBM ---------------- */
+typedef struct bcc_tupleset bcc_tupleset;
+/* C4: n (pub, msg32, DER sig) tuples from `seed`, 90 % valid, 10 % over 18 adversarial classes
+ * (bit-flipped r / s / msg, high-S, r or s >= n, r or s = 0, over-long and zero-padded r,
+ * compressed x without a square root, x >= p, 04 with a wrong y, 04, hybrid 06/07 with good and
+ * bad parity, bad header, wrong key).  The staged rows are those bcc_pubkey_verify_batch builds. */
+bcc_tupleset* bcc_tupleset_c4(size_t n, uint64_t seed, int device);
+/* C5: n BIP340 rows, fresh GPU-signed from `seed`, with the nvec caller vectors (sig64, msg32,
+ * xonly32, expected verdict) at rows i with i % 1024 == 1 + j. */
+bcc_tupleset* bcc_tupleset_c5(size_t n, uint64_t seed, const uint8_t* vec_sig64,
+                              const uint8_t* vec_msg32, const uint8_t* vec_xonly32,
+                              const uint8_t* vec_expect, size_t nvec, int device);
+void bcc_tupleset_free(bcc_tupleset* ts);
+size_t bcc_tupleset_size(const bcc_tupleset* ts);
+/* launch the verify kernels over the resident rows on `stream` (asynchronous) */
+int bcc_tupleset_run(bcc_tupleset* ts, void* stream);
+/* copy back the n verdicts of the last run (synchronous) */
+int bcc_tupleset_verdicts(bcc_tupleset* ts, uint8_t* out);
+/* host copies of the inputs (valid while ts lives); cls = generator class (0 = plain valid),
+ * expect = verdict by construction.  C4 fills pub / sig, C5 fills sig64 / xonly32. */
+typedef struct bcc_tupleset_host {
+    size_t n;
+    const uint8_t *pub_blob, *sig_blob, *msg32, *sig64, *xonly32, *cls, *expect;
+    const uint64_t *pub_off, *sig_off;
+} bcc_tupleset_host;
+void bcc_tupleset_view(const bcc_tupleset* ts, bcc_tupleset_host* v);
+
 /* ---- engine configuration / statistics ---------------------------------------------------- */
 /* Device used by the bitcoinconsensus_* entry points of the calling process (default 0, or the
  * BCC_DEVICE environment variable). */
@@ -53,6 +89,10 @@ int bcc_set_device(int device);
 typedef struct bcc_batch_stats {
     size_t items, tuples, rounds, preimages, aux_messages, host_rejected;
     double host_seconds, gpu_seconds;
+    /* breakdown: host deserialize + pre-checks, interpreter passes (preimage building
+     * included), merging the per-thread rounds, host -> HBM staging (part of gpu_seconds) */
+    double prepare_seconds, interpret_seconds, merge_seconds, stage_seconds;
+    double total_seconds; /* the whole call, teardown included */
 } bcc_batch_stats;
 /* Statistics of the calling thread's last bitcoinconsensus_verify_batch / verify call. */
 void bcc_last_batch_stats(bcc_batch_stats* out);

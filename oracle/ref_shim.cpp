@@ -235,4 +235,42 @@ double ref_bench_pubkey_verify(int nthreads, long n, const unsigned char* pub65,
     return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
 }
 
+// Tuple-level baseline / checker over blob inputs (uint64 offsets, n + 1 each): CPubKey::Verify.
+double ref_bench_pubkey_verify_blob(int nthreads, long n, const unsigned char* pub_blob,
+                                    const uint64_t* pub_off, const unsigned char* hash32,
+                                    const unsigned char* sig_blob, const uint64_t* sig_off,
+                                    unsigned char* ret) {
+    auto t0 = std::chrono::steady_clock::now();
+    std::vector<std::thread> pool;
+    for (int t = 0; t < nthreads; ++t) {
+        pool.emplace_back([=]() {
+            long lo = n * t / nthreads, hi = n * (t + 1) / nthreads;
+            for (long i = lo; i < hi; ++i)
+                ret[i] = (unsigned char)ref_pubkey_verify(
+                    pub_blob + pub_off[i], (size_t)(pub_off[i + 1] - pub_off[i]), hash32 + 32 * i,
+                    sig_blob + sig_off[i], (size_t)(sig_off[i + 1] - sig_off[i]));
+        });
+    }
+    for (auto& th : pool) th.join();
+    return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+}
+
+// BIP340 baseline / checker: secp256k1_xonly_pubkey_parse + secp256k1_schnorrsig_verify per row.
+double ref_bench_schnorr_verify(int nthreads, long n, const unsigned char* sig64,
+                                const unsigned char* msg32, const unsigned char* xonly32,
+                                unsigned char* ret) {
+    auto t0 = std::chrono::steady_clock::now();
+    std::vector<std::thread> pool;
+    for (int t = 0; t < nthreads; ++t) {
+        pool.emplace_back([=]() {
+            long lo = n * t / nthreads, hi = n * (t + 1) / nthreads;
+            for (long i = lo; i < hi; ++i)
+                ret[i] = (unsigned char)ref_schnorr_verify(sig64 + 64 * i, msg32 + 32 * i,
+                                                           xonly32 + 32 * i);
+        });
+    }
+    for (auto& th : pool) th.join();
+    return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+}
+
 }  // extern "C"

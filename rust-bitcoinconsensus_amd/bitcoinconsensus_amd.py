@@ -64,6 +64,18 @@ def lib():
         L.mi_schnorr_verify_tuples.argtypes = [u8p, u8p, u8p, u8p, sz, ctypes.c_int]
         L.mi_schnorr_verify_device.argtypes = [vp] * 4 + [sz, vp]
         L.mi_microbench.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_double)]
+        u64p = ctypes.POINTER(ctypes.c_uint64)
+        L.bcc_pubkey_verify_batch.argtypes = [u8p, u64p, u8p, u8p, u64p, u8p, sz, ctypes.c_int]
+        L.bcc_tupleset_c4.argtypes = [sz, ctypes.c_uint64, ctypes.c_int]
+        L.bcc_tupleset_c4.restype = vp
+        L.bcc_tupleset_c5.argtypes = [sz, ctypes.c_uint64, u8p, u8p, u8p, u8p, sz, ctypes.c_int]
+        L.bcc_tupleset_c5.restype = vp
+        L.bcc_tupleset_free.argtypes = [vp]
+        L.bcc_tupleset_size.argtypes = [vp]
+        L.bcc_tupleset_size.restype = sz
+        L.bcc_tupleset_run.argtypes = [vp, vp]
+        L.bcc_tupleset_verdicts.argtypes = [vp, u8p]
+        L.bcc_tupleset_view.argtypes = [vp, ctypes.POINTER(TuplesetHost)]
         _bind_consensus(L)
         _lib = L
     return _lib
@@ -76,11 +88,21 @@ class BatchItem(ctypes.Structure):
                 ("tx_to_len", ctypes.c_uint), ("n_in", ctypes.c_uint)]
 
 
+class TuplesetHost(ctypes.Structure):
+    """struct bcc_tupleset_host (include/bcc_amd.h)."""
+    _fields_ = [("n", ctypes.c_size_t)] + [
+        (f, ctypes.c_void_p) for f in ("pub_blob", "sig_blob", "msg32", "sig64", "xonly32", "cls",
+                                       "expect", "pub_off", "sig_off")]
+
+
 class BatchStats(ctypes.Structure):
     _fields_ = [("items", ctypes.c_size_t), ("tuples", ctypes.c_size_t),
                 ("rounds", ctypes.c_size_t), ("preimages", ctypes.c_size_t),
                 ("aux_messages", ctypes.c_size_t), ("host_rejected", ctypes.c_size_t),
-                ("host_seconds", ctypes.c_double), ("gpu_seconds", ctypes.c_double)]
+                ("host_seconds", ctypes.c_double), ("gpu_seconds", ctypes.c_double),
+                ("prepare_seconds", ctypes.c_double), ("interpret_seconds", ctypes.c_double),
+                ("merge_seconds", ctypes.c_double), ("stage_seconds", ctypes.c_double),
+                ("total_seconds", ctypes.c_double)]
 
 
 def _bind_consensus(L):
@@ -148,7 +170,7 @@ class Workload:
         rc = lib().bitcoinconsensus_verify_batch(items, cnt.value, flags & 0xffffffff, ret, None)
         if rc < 0:
             raise RuntimeError("bitcoinconsensus_verify_batch: device pipeline failed")
-        return rc, bytes(ret[i] for i in range(cnt.value))
+        return rc, bytes(memoryview(ret).cast("B"))[:: ctypes.sizeof(ctypes.c_int)][: cnt.value]
 
     def run(self, stream=None):
         rc = lib().bcc_workload_run(self.h, stream)
@@ -276,6 +298,115 @@ def height_to_flags(height):
     if height >= 481824:
         flag |= VERIFY_NULLDUMMY | VERIFY_WITNESS
     return flag
+
+
+def _blob(parts):
+    off = [0]
+    for p in parts:
+        off.append(off[-1] + len(p))
+    return b"".join(parts), (ctypes.c_uint64 * len(off))(*off)
+
+
+def pubkey_verify_batch(tuples, device=0):
+    """[CPubKey(pub).Verify(hash32, der_sig) for (pub, hash32, der_sig) in tuples] as a bytes of
+    0/1 (depend/bitcoin/src/pubkey.cpp:191-207): length filter + lax DER on the host, the
+    secp256k1 work on the GPU (include/bcc_amd.h bcc_pubkey_verify_batch)."""
+    n = len(tuples)
+    if n == 0:
+        return b""
+    pb, po = _blob([bytes(t[0]) for t in tuples])
+    sb, so = _blob([bytes(t[2]) for t in tuples])
+    msg = b"".join(bytes(t[1]) for t in tuples)
+    assert len(msg) == 32 * n
+    out = ctypes.create_string_buffer(n)
+    rc = lib().bcc_pubkey_verify_batch(pb, po, msg, sb, so, out, n, device)
+    if rc != 0:
+        raise RuntimeError(f"bcc_pubkey_verify_batch failed: {rc}")
+    return out.raw[:n]
+
+
+class TupleSet:
+    """Synthetic signature tuples staged in HBM (include/bcc_amd.h, bcc_tupleset_*).
+
+    kind "c4": n ECDSA (pub, msg32, DER sig) tuples, 90 % valid + 18 adversarial classes.
+    kind "c5": n BIP340 rows; `vectors` = [(sig64, msg32, xonly32, expected)] tiled in."""
+
+    C4_CLASSES = ("valid", "flip_r", "flip_s", "flip_msg", "high_s", "r_ge_n", "s_ge_n", "r_zero",
+                  "s_zero", "r_overlong", "r_zeropad", "pub_no_sqrt", "pub_x_ge_p",
+                  "pub_04_bad_y", "pub_04", "pub_hybrid_ok", "pub_hybrid_bad", "pub_bad_header",
+                  "wrong_key")
+
+    def __init__(self, n, kind="c4", seed=None, device=0, vectors=()):
+        L = lib()
+        if kind == "c4":
+            self.h = L.bcc_tupleset_c4(n, 0x5EED0004 if seed is None else seed, device)
+        elif kind == "c5":
+            v = list(vectors)
+            self.h = L.bcc_tupleset_c5(n, 0x5EED0005 if seed is None else seed,
+                                       b"".join(x[0] for x in v), b"".join(x[1] for x in v),
+                                       b"".join(x[2] for x in v), bytes(int(x[3]) for x in v),
+                                       len(v), device)
+        else:
+            raise ValueError(kind)
+        if not self.h:
+            raise RuntimeError(f"bcc_tupleset_{kind} failed")
+        self.kind, self.n = kind, n
+
+    def run(self, stream=None):
+        rc = lib().bcc_tupleset_run(self.h, stream)
+        if rc != 0:
+            raise RuntimeError(f"bcc_tupleset_run failed: {rc}")
+
+    def verdicts(self):
+        out = ctypes.create_string_buffer(max(self.n, 1))
+        if lib().bcc_tupleset_verdicts(self.h, out) != 0:
+            raise RuntimeError("bcc_tupleset_verdicts failed")
+        return out.raw[: self.n]
+
+    def host(self):
+        """numpy views of the host inputs: dict with msg32, cls, expect and pub/sig blobs +
+        offsets (c4) or sig64/xonly32 (c5).  Valid while the set lives."""
+        import numpy as np
+        v = TuplesetHost()
+        lib().bcc_tupleset_view(self.h, ctypes.byref(v))
+        n = v.n
+
+        def arr(ptr, count, dt=np.uint8):
+            if not ptr:
+                return None
+            c = ctypes.c_uint64 if dt == np.uint64 else ctypes.c_uint8
+            return np.ctypeslib.as_array(ctypes.cast(ptr, ctypes.POINTER(c)), shape=(count,))
+
+        d = dict(msg32=arr(v.msg32, 32 * n), cls=arr(v.cls, n), expect=arr(v.expect, n))
+        if self.kind == "c4":
+            d["pub_off"] = arr(v.pub_off, n + 1, np.uint64)
+            d["sig_off"] = arr(v.sig_off, n + 1, np.uint64)
+            d["pub_blob"] = arr(v.pub_blob, int(d["pub_off"][-1]))
+            d["sig_blob"] = arr(v.sig_blob, int(d["sig_off"][-1]))
+        else:
+            d["sig64"] = arr(v.sig64, 64 * n)
+            d["xonly32"] = arr(v.xonly32, 32 * n)
+        return d
+
+    def tuple(self, i):
+        d = self.host()
+        if self.kind == "c4":
+            po, so = d["pub_off"], d["sig_off"]
+            return (d["pub_blob"][po[i]:po[i + 1]].tobytes(), d["msg32"][32 * i:32 * i + 32].tobytes(),
+                    d["sig_blob"][so[i]:so[i + 1]].tobytes())
+        return (d["sig64"][64 * i:64 * i + 64].tobytes(), d["msg32"][32 * i:32 * i + 32].tobytes(),
+                d["xonly32"][32 * i:32 * i + 32].tobytes())
+
+    def free(self):
+        if self.h:
+            lib().bcc_tupleset_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
 
 
 def ecdsa_verify_tuples(pub65, msg32, r32, s32, device=0):

@@ -48,6 +48,8 @@ struct TxEntry {
     Tx tx;
     bool ok = false;
     int32_t aux[3] = {-1, -1, -1};  // aux message index per AuxKind in the current round
+    int64_t tpl = -1;               // legacy template offset in the current round (-1: none)
+    uint32_t tpl_len = 0;
 };
 
 struct Item {
@@ -57,8 +59,9 @@ struct Item {
     bitcoinconsensus_error err = bitcoinconsensus_ERR_OK;
     bool active = false;  // needs (another) interpreter run
     bool result = false;
-    std::unordered_map<std::string, int8_t> cache;  // tuple key -> 0/1, -1 = deferred
-    std::vector<uint32_t> pending;                  // tuple rows deferred in the last run
+    // tuple key -> 0/1 known verdict, or -2 - r: deferred as row r of the current round
+    std::unordered_map<std::string, int32_t> cache;
+    std::vector<uint32_t> pending;  // deferred rows the last run consulted (answered "true")
 };
 
 struct Pending {
@@ -88,6 +91,7 @@ class DeferringChecker : public SigChecker {
 public:
     DeferringChecker(Round& rd, uint32_t idx, Item& it) : rd_(rd), idx_(idx), it_(it) {}
     bool check_ecdsa(const Bytes& sig, const Bytes& pub, const Bytes& code, SigVersion sv) override;
+    void hint_ecdsa(const Bytes& sig, const Bytes& pub, const Bytes& code, SigVersion sv) override;
     bool check_locktime(int64_t n) override { return tx_check_locktime(it_.tx->tx, it_.in->n_in, n); }
     bool check_sequence(int64_t n) override { return tx_check_sequence(it_.tx->tx, it_.in->n_in, n); }
 
@@ -109,11 +113,17 @@ public:
 
     // GenericTransactionSignatureChecker::CheckECDSASignature (interpreter.cpp:1656-1676) up to
     // the point where the sighash + secp256k1 verify would run; those become a GPU tuple.
+    // consult = false queues a check the run may reach later (a CHECKMULTISIG candidate pair)
+    // without making the item's finality depend on it.
     bool defer(uint32_t item_idx, Item& it, const Bytes& sig, const Bytes& pub, const Bytes& code,
-               SigVersion sv) {
+               SigVersion sv, bool consult) {
         std::string key = tuple_key(pub, sig, code, sv);
         auto f = it.cache.find(key);
-        if (f != it.cache.end()) return f->second != 0;  // known (or already deferred: true)
+        if (f != it.cache.end()) {
+            if (f->second >= 0) return f->second != 0;  // known
+            if (consult) it.pending.push_back((uint32_t)(-2 - f->second));
+            return true;                                // deferred this round: speculate
+        }
         // CPubKey filter, empty signature, lax-DER: decided on the host (no secp work)
         uint8_t r[32], s[32];
         bool reject = !pubkey_size_valid(pub.data(), pub.size()) || sig.empty() ||
@@ -139,7 +149,26 @@ public:
         uint8_t ybuf[32] = {0};
         const uint8_t* y = pub.size() == 65 ? pub.data() + 33 : ybuf;  // y unused for 02/03
         uint32_t row = rows.add(pub[0], pub.data() + 1, y, r, s, one);
-        if (sv == SIGVERSION_BASE) {
+        if (sv == SIGVERSION_BASE && legacy_all_type(hashtype)) {
+            // device-assembled from the tx template (pipeline.h TplJob)
+            if (it.tx->tpl < 0) {
+                build_legacy_template(tx, scratch);
+                it.tx->tpl = jobs.add_tpl(scratch.data(), scratch.size());
+                it.tx->tpl_len = (uint32_t)scratch.size();
+                touched.push_back(it.tx);
+            }
+            build_script_code_field(code, scratch);
+            TplJob tj;
+            tj.tpl_off = (uint32_t)it.tx->tpl;
+            tj.tpl_len = it.tx->tpl_len;
+            tj.pos = (uint32_t)legacy_template_pos(tx, nin);
+            tj.code_off = jobs.add_code(scratch.data(), scratch.size());
+            tj.code_len = (uint32_t)scratch.size();
+            tj.hashtype = (uint32_t)hashtype;
+            tj.row = row;
+            tj.nblk = SighashJobs::tpl_nblk(tj.tpl_len, tj.code_len);
+            jobs.tjobs.push_back(tj);
+        } else if (sv == SIGVERSION_BASE) {
             if (build_legacy_preimage(tx, nin, code, hashtype, scratch))
                 jobs.add_pre(scratch.data(), scratch.size(), row);
             // else: SIGHASH_SINGLE bug, msg stays ONE
@@ -165,8 +194,8 @@ public:
                 jobs.patches.push_back(PatchRec{(uint32_t)(base + job.off[k]), (uint32_t)aux});
             }
         }
-        it.cache.emplace(key, (int8_t)-1);
-        it.pending.push_back((uint32_t)pending.size());
+        it.cache.emplace(key, -2 - (int32_t)pending.size());
+        if (consult) it.pending.push_back((uint32_t)pending.size());
         pending.push_back(Pending{item_idx, std::move(key)});
         return true;  // speculative
     }
@@ -175,14 +204,22 @@ public:
         jobs.clear();
         rows.clear();
         pending.clear();
-        for (auto* t : touched) t->aux[0] = t->aux[1] = t->aux[2] = -1;
+        for (auto* t : touched) {
+            t->aux[0] = t->aux[1] = t->aux[2] = -1;
+            t->tpl = -1;
+        }
         touched.clear();
     }
 };
 
 bool DeferringChecker::check_ecdsa(const Bytes& sig, const Bytes& pub, const Bytes& code,
                                    SigVersion sv) {
-    return rd_.defer(idx_, it_, sig, pub, code, sv);
+    return rd_.defer(idx_, it_, sig, pub, code, sv, true);
+}
+
+void DeferringChecker::hint_ecdsa(const Bytes& sig, const Bytes& pub, const Bytes& code,
+                                  SigVersion sv) {
+    rd_.defer(idx_, it_, sig, pub, code, sv, false);
 }
 
 int set_err(bitcoinconsensus_error* e, bitcoinconsensus_error v) {
@@ -193,6 +230,8 @@ int set_err(bitcoinconsensus_error* e, bitcoinconsensus_error v) {
 struct BatchState {
     std::vector<Item> st;
     std::unordered_map<std::string, TxEntry> txs;  // parse each distinct tx buffer once
+    std::vector<std::pair<const bcc_batch_item*, TxEntry*>> fresh;  // parse order
+    unsigned parse_threads = 1;
     unsigned flags = 0;
 };
 
@@ -227,7 +266,7 @@ void prepare(BatchState& b, const bcc_batch_item* items, size_t n, unsigned flag
     auto& st = b.st;
     auto& txs = b.txs;
     const bool flags_ok = (flags & ~(unsigned)FLAGS_VERIFY_ALL) == 0;
-    std::vector<std::pair<const bcc_batch_item*, TxEntry*>> fresh;
+    auto& fresh = b.fresh;
     for (size_t i = 0; i < n; i++) {
         Item& it = st[i];
         it.in = &items[i];
@@ -242,6 +281,7 @@ void prepare(BatchState& b, const bcc_batch_item* items, size_t n, unsigned flag
         it.tx = &f->second;
     }
     if (fresh.size() < 64) T = 1;
+    b.parse_threads = T;
     run_threads(T, [&](unsigned t) {
         for (size_t k = t; k < fresh.size(); k += T) {
             const bcc_batch_item* in = fresh[k].first;
@@ -326,6 +366,8 @@ long run_batch(const bcc_batch_item* items, size_t n, unsigned flags, int* ret_o
     const unsigned T = n >= 256 ? std::min<unsigned>(host_threads(), (unsigned)(n / 64)) : 1u;
     BatchState b;
     prepare(b, items, n, flags, T);
+    auto since = [](clk::time_point a) { return std::chrono::duration<double>(clk::now() - a).count(); };
+    t_stats.prepare_seconds = since(t0);
     auto& st = b.st;
     const int dev = current_device();
     const auto shards = make_shards(b, T);
@@ -337,10 +379,12 @@ long run_batch(const bcc_batch_item* items, size_t n, unsigned flags, int* ret_o
     long status = 0;
     for (size_t round = 0;; round++) {
         std::vector<char> ran(T, 0);
+        auto i0 = clk::now();
         run_threads(T, [&](unsigned t) {
             rds[t].reset();
             ran[t] = interpret_shard(b, shards[t], rds[t]);
         });
+        t_stats.interpret_seconds += since(i0);
         size_t npend = 0;
         bool any = false;
         for (unsigned t = 0; t < T; t++) {
@@ -353,11 +397,13 @@ long run_batch(const bcc_batch_item* items, size_t n, unsigned flags, int* ret_o
         const SighashJobs* jobs = &rds[0].jobs;
         const TupleRows* rows = &rds[0].rows;
         if (T > 1) {  // one device batch for the whole round
+            auto m0 = clk::now();
             mjobs.clear();
             mrows.clear();
             for (unsigned t = 0; t < T; t++) append_round(mjobs, mrows, rds[t].jobs, rds[t].rows);
             jobs = &mjobs;
             rows = &mrows;
+            t_stats.merge_seconds += since(m0);
         }
         t_stats.rounds++;
         t_stats.tuples += rows->size();
@@ -365,7 +411,9 @@ long run_batch(const bcc_batch_item* items, size_t n, unsigned flags, int* ret_o
         t_stats.aux_messages += jobs->aux_off.size();
         auto g0 = clk::now();
         verdict.assign(rows->size(), 0);
-        int e = gpu_verify_batch(dev, *jobs, *rows, verdict.data());
+        double stage_s = 0;
+        int e = gpu_verify_batch(dev, *jobs, *rows, verdict.data(), &stage_s);
+        t_stats.stage_seconds += stage_s;
         gpu_s += std::chrono::duration<double>(clk::now() - g0).count();
         if (e != 0) {
             status = -1;
@@ -381,7 +429,7 @@ long run_batch(const bcc_batch_item* items, size_t n, unsigned flags, int* ret_o
             const Round& rd = rds[t];
             const uint8_t* v = verdict.data() + row0[t];
             for (size_t k = 0; k < rd.pending.size(); k++)
-                st[rd.pending[k].item].cache[rd.pending[k].key] = (int8_t)v[k];
+                st[rd.pending[k].item].cache[rd.pending[k].key] = v[k] ? 1 : 0;
             for (uint32_t i : shards[t]) {
                 Item& it = st[i];
                 if (it.pending.empty()) continue;
@@ -400,6 +448,19 @@ long run_batch(const bcc_batch_item* items, size_t n, unsigned flags, int* ret_o
         if (err_out) err_out[i] = it.err;
         valid += ret;
     }
+    // Teardown on the threads that allocated: the per-item verdict caches, the rounds and the
+    // parsed txs were built by the worker threads, and freeing them all from this thread (other
+    // malloc arenas) costs more than the interpreter pass itself.
+    run_threads(T, [&](unsigned t) {
+        for (uint32_t i : shards[t]) {
+            decltype(st[i].cache)().swap(st[i].cache);
+            std::vector<uint32_t>().swap(st[i].pending);
+        }
+        rds[t] = Round();
+    });
+    run_threads(b.parse_threads, [&](unsigned t) {
+        for (size_t k = t; k < b.fresh.size(); k += b.parse_threads) b.fresh[k].second->tx = Tx();
+    });
     host_s = std::chrono::duration<double>(clk::now() - t0).count() - gpu_s;
     t_stats.host_seconds = host_s;
     t_stats.gpu_seconds = gpu_s;
@@ -450,6 +511,15 @@ void append_round(SighashJobs& dst, TupleRows& drows, const SighashJobs& src,
     }
     for (const auto& p : src.patches)
         dst.patches.push_back(PatchRec{p.pre_byte + pre_blk0 * 64, p.aux + aux_idx0});
+    const uint32_t tpl0 = (uint32_t)dst.tpl.size(), code0 = (uint32_t)dst.code.size();
+    cat(dst.tpl, src.tpl);
+    cat(dst.code, src.code);
+    for (TplJob t : src.tjobs) {
+        t.tpl_off += tpl0;
+        t.code_off += code0;
+        t.row += row0;
+        dst.tjobs.push_back(t);
+    }
 }
 
 }  // namespace host
@@ -492,7 +562,11 @@ unsigned int bitcoinconsensus_version(void) { return BITCOINCONSENSUS_API_VER; }
 long bitcoinconsensus_verify_batch(const bcc_batch_item* items, size_t n, unsigned int flags,
                                    int* ret_out, bitcoinconsensus_error* err_out) {
     try {
-        return run_batch(items, n, flags, ret_out, err_out);
+        auto t0 = std::chrono::steady_clock::now();
+        long r = run_batch(items, n, flags, ret_out, err_out);
+        t_stats.total_seconds =
+            std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        return r;
     } catch (...) {
         for (size_t i = 0; i < n; i++) {
             ret_out[i] = 0;

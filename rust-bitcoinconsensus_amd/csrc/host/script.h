@@ -79,6 +79,9 @@ public:
     virtual ~SigChecker() {}
     virtual bool check_ecdsa(const Bytes& sig, const Bytes& pub, const Bytes& script_code,
                              SigVersion sv) = 0;
+    // A check the script may consult later in the same CHECKMULTISIG (a candidate (sig, key)
+    // pair); a batching checker may queue it now.  Must not change any verdict.
+    virtual void hint_ecdsa(const Bytes&, const Bytes&, const Bytes&, SigVersion) {}
     virtual bool check_locktime(int64_t n) = 0;
     virtual bool check_sequence(int64_t n) = 0;
 };

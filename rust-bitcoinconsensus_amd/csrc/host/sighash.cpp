@@ -108,6 +108,31 @@ bool build_legacy_preimage(const Tx& tx, unsigned nin, const Bytes& sc, int hash
     return true;
 }
 
+void build_legacy_template(const Tx& tx, std::vector<uint8_t>& o) {
+    o.clear();
+    put_le(o, (uint32_t)tx.version, 4);
+    put_compact_size(o, tx.vin.size());
+    for (const auto& in : tx.vin) {
+        put(o, in.prevout, 36);
+        o.push_back(0);
+        put_le(o, in.sequence, 4);
+    }
+    put_compact_size(o, tx.vout.size());
+    for (const auto& out : tx.vout) put(o, out.ser.p, out.ser.n);
+    put_le(o, tx.locktime, 4);
+}
+
+size_t legacy_template_pos(const Tx& tx, unsigned nin) {
+    const size_t n = tx.vin.size();
+    const size_t cs = n < 0xfd ? 1 : n <= 0xffff ? 3 : n <= 0xffffffffu ? 5 : 9;
+    return 4 + cs + 41 * (size_t)nin + 36;
+}
+
+void build_script_code_field(const Bytes& sc, std::vector<uint8_t>& o) {
+    o.clear();
+    put_script_code(o, sc);
+}
+
 void build_bip143_preimage(const Tx& tx, unsigned nin, const Bytes& sc, int hashtype,
                            int64_t amount, Bip143Job& job) {
     const bool acp = (hashtype & 0x80) != 0;

@@ -30,6 +30,18 @@ void build_aux_message(const Tx& tx, AuxKind kind, std::vector<uint8_t>& out);
 bool build_legacy_preimage(const Tx& tx, unsigned nin, const Bytes& script_code, int hashtype,
                            std::vector<uint8_t>& out);
 
+// The device-assembled form of a legacy SIGHASH_ALL preimage (pipeline.h TplJob):
+// legacy_template = the tx serialized with every scriptSig empty (no witness, no hashtype);
+// legacy_template_pos = offset of input nin's empty-script length byte in it;
+// script_code_field = compactsize || scriptCode without OP_CODESEPARATORs (SerializeScriptCode).
+// legacy_all_type: hashtypes whose preimage has that form (not NONE / SINGLE / ANYONECANPAY).
+void build_legacy_template(const Tx& tx, std::vector<uint8_t>& out);
+size_t legacy_template_pos(const Tx& tx, unsigned nin);
+void build_script_code_field(const Bytes& script_code, std::vector<uint8_t>& out);
+inline bool legacy_all_type(int hashtype) {
+    return (hashtype & 0x80) == 0 && (hashtype & 0x1f) != 2 && (hashtype & 0x1f) != 3;
+}
+
 // BIP143 preimage with zeroed 32-byte slots for hashPrevouts (offset 4), hashSequence (offset 36)
 // and hashOutputs (offset len-40).  need[k] says whether slot k must be patched with aux digest k
 // (AuxKind order; for SIGHASH_SINGLE with nin < vout.size() slot 2 takes the digest of the

@@ -1,0 +1,81 @@
+// Tuple level of the hot path, without a script around it: bcc_pubkey_verify_batch =
+// N x CPubKey(pub).Verify(hash, sig) (pubkey.cpp:191-207).  The CPubKey length filter
+// (pubkey.h:58-94), lax DER (pubkey.cpp:28-168) and the r / s == 0 rule are decided on the host,
+// threaded; every surviving tuple goes to the GPU ECDSA kernels (normalisation is implicit: the
+// verdict is invariant under s -> n - s).
+#include "tuples.h"
+
+#include <algorithm>
+#include <cstring>
+#include <thread>
+#include <vector>
+
+#include "bcc_amd.h"
+#include "sighash.h"
+
+namespace bcc {
+namespace host {
+
+unsigned pool_threads(size_t n, size_t grain) {
+    unsigned T = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    return (unsigned)std::max<size_t>(1, std::min<size_t>(T, n / grain));
+}
+
+// One tuple's host half of CPubKey::Verify into row i of preallocated rows.  A tuple the host
+// already rejects keeps tag 0 (the kernel's "rejected" header) and zero r / s.
+static void parse_row(const uint8_t* pub, size_t publen, const uint8_t* m32, const uint8_t* sig,
+                      size_t siglen, bcc::TupleRows& rows, size_t i) {
+    uint8_t* tag = &rows.tag[i];
+    uint8_t *x = &rows.x[32 * i], *y = &rows.y[32 * i], *r = &rows.r[32 * i], *s = &rows.s[32 * i];
+    memcpy(&rows.msg[32 * i], m32, 32);
+    *tag = 0;
+    memset(x, 0, 32);
+    memset(y, 0, 32);
+    memset(r, 0, 32);
+    memset(s, 0, 32);
+    if (!pubkey_size_valid(pub, publen)) return;     // CPubKey::IsValid
+    if (!der_parse_lax(sig, siglen, r, s)) return;   // ecdsa_signature_parse_der_lax
+    bool rz = true, sz = true;
+    for (int k = 0; k < 32; k++) {
+        rz &= r[k] == 0;
+        sz &= s[k] == 0;
+    }
+    if (rz || sz) return;                             // ecdsa_sig_verify: r, s != 0
+    *tag = pub[0];
+    memcpy(x, pub + 1, 32);
+    if (publen == 65) memcpy(y, pub + 33, 32);
+}
+
+static void rows_resize(bcc::TupleRows& rows, size_t n) {
+    rows.tag.resize(n);
+    rows.x.resize(32 * n);
+    rows.y.resize(32 * n);
+    rows.r.resize(32 * n);
+    rows.s.resize(32 * n);
+    rows.msg.resize(32 * n);
+}
+
+void parse_rows(const uint8_t* pub_blob, const uint64_t* pub_off, const uint8_t* msg32,
+                const uint8_t* sig_blob, const uint64_t* sig_off, size_t n, bcc::TupleRows& rows) {
+    rows_resize(rows, n);
+    pfor(n, 4096, [&](size_t lo, size_t hi) {
+        for (size_t i = lo; i < hi; i++)
+            parse_row(pub_blob + pub_off[i], pub_off[i + 1] - pub_off[i], msg32 + 32 * i,
+                      sig_blob + sig_off[i], sig_off[i + 1] - sig_off[i], rows, i);
+    });
+}
+
+}  // namespace host
+}  // namespace bcc
+
+extern "C" int bcc_pubkey_verify_batch(const uint8_t* pub_blob, const uint64_t* pub_off,
+                                       const uint8_t* msg32, const uint8_t* sig_blob,
+                                       const uint64_t* sig_off, uint8_t* verdict, size_t n,
+                                       int device) {
+    if (n == 0) return 0;
+    if (!pub_off || !sig_off || !msg32 || !verdict) return -1;
+    bcc::TupleRows rows;
+    bcc::host::parse_rows(pub_blob, pub_off, msg32, sig_blob, sig_off, n, rows);
+    bcc::SighashJobs none;
+    return bcc::gpu_verify_batch(device, none, rows, verdict);
+}

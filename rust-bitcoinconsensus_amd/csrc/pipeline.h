@@ -2,6 +2,7 @@
 //   K1 sha256d(aux messages)        BIP143 hashPrevouts / hashSequence / hashOutputs per tx
 //   K2 patch(aux digests -> preimages)
 //   K3 sha256d(preimages)           legacy + BIP143 sighashes, written as the tuple msg rows
+//   K3' sha256d(template jobs)      legacy SIGHASH_ALL sighashes assembled from per-tx templates
 //   K4 ecdsa_verify(tuples)         csrc/ecdsa_verify.hip
 // All four launch back-to-back on one stream with inputs resident in HBM.
 #pragma once
@@ -28,11 +29,46 @@ inline void sha_append_padded(std::vector<uint8_t>& buf, const uint8_t* m, size_
     for (int i = 0; i < 8; i++) buf[base + L - 1 - i] = (uint8_t)(bits >> (8 * i));
 }
 
+// A legacy SIGHASH_ALL job (interpreter.cpp:1273-1364) built on the device from its tx's
+// template instead of a host preimage: message = T[0, pos) || code || T[pos + 1, tpl_len) ||
+// le32(hashtype), where T is the tx serialized with every scriptSig empty (the byte at pos is the
+// signing input's empty-script length byte) and code = compactsize || scriptCode without
+// OP_CODESEPARATORs.  A tx's template is uploaded once per round; the O(nIn^2) preimage bytes of
+// a many-input tx never exist on the host.
+struct TplJob {
+    uint32_t tpl_off;   // byte offset of T in the template blob (4-aligned)
+    uint32_t tpl_len;
+    uint32_t pos;
+    uint32_t code_off;  // byte offset of code in the code blob (4-aligned)
+    uint32_t code_len;
+    uint32_t hashtype;
+    uint32_t row;       // tuple row whose msg receives the sighash
+    uint32_t nblk;      // padded message length in 64-byte blocks
+};
+
 struct SighashJobs {
     std::vector<uint8_t> aux, pre;                  // padded messages, back to back
     std::vector<uint32_t> aux_off, aux_nblk;        // offsets / lengths in 64-byte blocks
     std::vector<uint32_t> pre_off, pre_nblk, pre_row;
     std::vector<PatchRec> patches;
+    std::vector<uint8_t> tpl, code;                 // templates / code segments (4-aligned,
+                                                    // templates followed by 8 zero bytes)
+    std::vector<TplJob> tjobs;
+    uint32_t add_tpl(const uint8_t* m, size_t n) {
+        uint32_t off = (uint32_t)tpl.size();
+        tpl.insert(tpl.end(), m, m + n);
+        tpl.resize(off + ((n + 3) & ~(size_t)3) + 8, 0);
+        return off;
+    }
+    uint32_t add_code(const uint8_t* m, size_t n) {
+        uint32_t off = (uint32_t)code.size();
+        code.insert(code.end(), m, m + n);
+        code.resize(off + ((n + 3) & ~(size_t)3), 0);
+        return off;
+    }
+    static uint32_t tpl_nblk(uint32_t tpl_len, uint32_t code_len) {
+        return (uint32_t)(sha_padded_len(tpl_len - 1 + code_len + 4) / 64);
+    }
     uint32_t add_aux(const uint8_t* m, size_t n) {
         aux_off.push_back((uint32_t)(aux.size() / 64));
         sha_append_padded(aux, m, n);
@@ -49,6 +85,7 @@ struct SighashJobs {
     void clear() {
         aux.clear(); pre.clear(); aux_off.clear(); aux_nblk.clear();
         pre_off.clear(); pre_nblk.clear(); pre_row.clear(); patches.clear();
+        tpl.clear(); code.clear(); tjobs.clear();
     }
 };
 
@@ -108,9 +145,9 @@ public:
     int fetch_verdicts(uint8_t* out);            // synchronous D2H (waits for the last run)
     int fetch_msgs(uint8_t* out);                // synchronous D2H (tests)
     size_t n_tuples() const { return n_rows_; }
-    size_t n_pre() const { return n_pre_; }
+    size_t n_pre() const { return n_pre_ + n_tjob_; }     // sighash messages (both kinds)
     size_t n_aux() const { return n_aux_; }
-    size_t pre_blocks() const { return pre_blocks_; }
+    size_t pre_blocks() const { return pre_blocks_ + tjob_blocks_; }
     size_t aux_blocks() const { return aux_blocks_; }
     int device() const { return dev_; }
     // raw device pointers (bench / profiling)
@@ -131,9 +168,14 @@ private:
     uint32_t *d_aux_off_ = nullptr, *d_aux_nblk_ = nullptr, *d_pre_off_ = nullptr,
              *d_pre_nblk_ = nullptr, *d_pre_row_ = nullptr;
     PatchRec* d_patch_ = nullptr;
+    size_t n_tjob_ = 0, tjob_blocks_ = 0;
+    uint8_t *d_tpl_ = nullptr, *d_code_ = nullptr;
+    TplJob* d_tjob_ = nullptr;
 };
 
 // One-shot helper: stage + run + fetch on `device` (synchronous).
-int gpu_verify_batch(int device, const SighashJobs& jobs, const TupleRows& rows, uint8_t* verdict);
+// *stage_seconds (optional) receives the host -> HBM staging time.
+int gpu_verify_batch(int device, const SighashJobs& jobs, const TupleRows& rows, uint8_t* verdict,
+                     double* stage_seconds = nullptr);
 
 }  // namespace bcc

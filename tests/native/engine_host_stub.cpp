@@ -19,7 +19,7 @@ static size_t unpadded_len(const uint8_t* m, size_t padded) {
     return (size_t)(bits / 8);
 }
 
-int gpu_verify_batch(int, const SighashJobs& j, const TupleRows& rows, uint8_t* verdict) {
+int gpu_verify_batch(int, const SighashJobs& j, const TupleRows& rows, uint8_t* verdict, double*) {
     std::vector<uint8_t> auxd(32 * j.aux_off.size());
     for (size_t a = 0; a < j.aux_off.size(); a++) {
         const uint8_t* m = &j.aux[(size_t)j.aux_off[a] * 64];
@@ -33,6 +33,14 @@ int gpu_verify_batch(int, const SighashJobs& j, const TupleRows& rows, uint8_t* 
         const uint8_t* m = &pre[(size_t)j.pre_off[k] * 64];
         size_t L = (size_t)j.pre_nblk[k] * 64;
         bcco_sha256d(m, unpadded_len(m, L), &msg[32 * j.pre_row[k]]);
+    }
+    for (const TplJob& t : j.tjobs) {  // template jobs: assemble the preimage, then hash
+        std::vector<uint8_t> m(j.tpl.begin() + t.tpl_off, j.tpl.begin() + t.tpl_off + t.pos);
+        m.insert(m.end(), j.code.begin() + t.code_off, j.code.begin() + t.code_off + t.code_len);
+        m.insert(m.end(), j.tpl.begin() + t.tpl_off + t.pos + 1,
+                 j.tpl.begin() + t.tpl_off + t.tpl_len);
+        for (int b = 0; b < 4; b++) m.push_back((uint8_t)(t.hashtype >> (8 * b)));
+        bcco_sha256d(m.data(), m.size(), &msg[32 * t.row]);
     }
     for (size_t i = 0; i < rows.size(); i++) {
         uint8_t pub[65];

@@ -109,6 +109,11 @@ class Reference:
                                          c_u8p, i32p, c_u8p, i32p, i32p, i32p]
         L.ref_bench_verify_script.restype = ctypes.c_double
         L.ref_bench_pubkey_verify.restype = ctypes.c_double
+        vp = ctypes.c_void_p
+        L.ref_bench_pubkey_verify_blob.argtypes = [ctypes.c_int, ctypes.c_long] + [vp] * 6
+        L.ref_bench_pubkey_verify_blob.restype = ctypes.c_double
+        L.ref_bench_schnorr_verify.argtypes = [ctypes.c_int, ctypes.c_long] + [vp] * 4
+        L.ref_bench_schnorr_verify.restype = ctypes.c_double
 
     def verify_script_with_amount(self, spk, amount, tx, nin, flags):
         e = ctypes.c_int(0)
@@ -126,6 +131,26 @@ class Reference:
 
     def schnorr_verify(self, sig64, msg32, xonly32):
         return self.L.ref_schnorr_verify(sig64, msg32, xonly32)
+
+    def pubkey_verify_blob(self, pub_blob, pub_off, msg32, sig_blob, sig_off, threads=1, n=None):
+        """CPubKey::Verify over numpy blob inputs (uint64 offsets) on `threads` host threads.
+        Returns (verdicts as a uint8 numpy array, wall seconds)."""
+        import numpy as np
+        n = len(pub_off) - 1 if n is None else n
+        out = np.zeros(max(n, 1), np.uint8)
+        p = lambda a: a.ctypes.data  # noqa: E731
+        t = self.L.ref_bench_pubkey_verify_blob(threads, n, p(pub_blob), p(pub_off), p(msg32),
+                                                p(sig_blob), p(sig_off), p(out))
+        return out[:n], t
+
+    def schnorr_verify_rows(self, sig64, msg32, xonly32, threads=1, n=None):
+        """secp256k1_schnorrsig_verify over numpy row arrays.  Returns (verdicts, seconds)."""
+        import numpy as np
+        n = len(msg32) // 32 if n is None else n
+        out = np.zeros(max(n, 1), np.uint8)
+        p = lambda a: a.ctypes.data  # noqa: E731
+        t = self.L.ref_bench_schnorr_verify(threads, n, p(sig64), p(msg32), p(xonly32), p(out))
+        return out[:n], t
 
     def pubkey_create(self, sk, compressed=True):
         out = ctypes.create_string_buffer(65)

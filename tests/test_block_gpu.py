@@ -33,7 +33,7 @@ def test_block_workload_all_valid_and_matches_reference(wl):
     n_valid, ret = wl.verify_batch()
     st = B.last_batch_stats()
     assert n_valid == wl.n and all(r == 1 for r in ret)
-    assert st["rounds"] >= 2          # multisig pairs {1,3} / {2,3} need the key-advance re-run
+    assert st["rounds"] == 1          # multisig candidate pairs are queued up front: no re-run
     assert st["tuples"] > wl.n        # multisig inputs verify 2-3 signatures
     if reference_available():
         R = Reference()

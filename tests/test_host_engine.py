@@ -31,7 +31,7 @@ def eng():
     srcs = [os.path.join(HERE, "native", "engine_host_stub.cpp")]
     hostdir = os.path.join(ROOT, "rust-bitcoinconsensus_amd", "csrc", "host")
     srcs += [os.path.join(hostdir, f) for f in sorted(os.listdir(hostdir))
-             if f.endswith(".cpp") and f != "workload.cpp"]  # workload needs the GPU generator
+             if f.endswith(".cpp") and f not in ("workload.cpp", "tupleset.cpp")]  # GPU generators
     deps = srcs + [os.path.join(hostdir, f) for f in os.listdir(hostdir) if f.endswith(".h")]
     deps += [os.path.join(ROOT, "oracle", "bcc_oracle.c"),
              os.path.join(ROOT, "rust-bitcoinconsensus_amd", "csrc", "pipeline.h")]
@@ -105,3 +105,28 @@ def test_script_cases_as_batches(eng):
         got = list(zip(ret, err))
         assert got == exp
         assert nvalid == sum(r for r, _ in exp)
+
+
+def test_pubkey_verify_batch_front_end(eng):
+    """bcc_pubkey_verify_batch's host front end (CPubKey length filter, lax DER, r/s == 0; the
+    curve work stubbed by the oracle) on the reference-labelled adversarial tuple fixtures."""
+    from fixtures import ecdsa_tuples
+    ts = ecdsa_tuples()
+
+    def blob(parts):
+        off = [0]
+        for p in parts:
+            off.append(off[-1] + len(p))
+        return b"".join(parts), (ctypes.c_uint64 * len(off))(*off)
+
+    pb, po = blob([t["pub"] for t in ts])
+    sb, so = blob([t["sig"] for t in ts])
+    msg = b"".join(t["hash"] for t in ts)
+    out = ctypes.create_string_buffer(len(ts))
+    u64p = ctypes.POINTER(ctypes.c_uint64)
+    eng.bcc_pubkey_verify_batch.argtypes = [ctypes.c_char_p, u64p, ctypes.c_char_p,
+                                            ctypes.c_char_p, u64p, ctypes.c_char_p,
+                                            ctypes.c_size_t, ctypes.c_int]
+    assert eng.bcc_pubkey_verify_batch(pb, po, msg, sb, so, out, len(ts), 0) == 0
+    bad = [(t["cls"], i) for i, t in enumerate(ts) if out.raw[i] != t["verdict"]]
+    assert not bad, bad[:20]

@@ -1,0 +1,85 @@
+"""GPU parity of the tuple level (configs C4 / C5) through the product C ABI:
+
+* bcc_pubkey_verify_batch (N x CPubKey::Verify, pubkey.cpp:191-207) against the reference
+  verdicts of the committed adversarial fixtures (tests/golden/ecdsa_tuples.npz);
+* the C4 tuple set (90 % valid + 18 adversarial classes, include/bcc_amd.h bcc_tupleset_c4)
+  against the reference's CPubKey::Verify on every tuple, and against the verdict by construction;
+* the C5 BIP340 set (fresh GPU-signed rows + the 15 BIP340 vectors tiled) against the
+  reference's secp256k1_schnorrsig_verify on every row."""
+import numpy as np
+import pytest
+
+from fixtures import bip340_vectors, ecdsa_tuples
+from oracle_ctypes import Reference, reference_available
+
+pytestmark = pytest.mark.gpu
+THREADS = 16
+
+
+def test_pubkey_verify_batch_matches_reference_fixtures():
+    import bitcoinconsensus_amd as B
+    ts = ecdsa_tuples()
+    v = B.pubkey_verify_batch([(t["pub"], t["hash"], t["sig"]) for t in ts])  # CPubKey level
+    bad = [(t["cls"], i, v[i], t["verdict"]) for i, t in enumerate(ts) if v[i] != t["verdict"]]
+    assert not bad, bad[:20]
+
+
+def test_pubkey_verify_batch_empty_and_garbage():
+    import bitcoinconsensus_amd as B
+    assert B.pubkey_verify_batch([]) == b""
+    rows = [(b"", bytes(32), b""), (b"\x02" + bytes(32), bytes(32), b"\x30\x00"),
+            (b"\x04" * 65, bytes(32), b"\x30" * 70), (b"\x03" * 33, b"\xff" * 32, b"")]
+    assert B.pubkey_verify_batch(rows) == bytes(4)
+
+
+@pytest.fixture(scope="module")
+def c4():
+    import bitcoinconsensus_amd as B
+    ts = B.TupleSet(300_000, kind="c4", seed=0x5EED0004)
+    ts.run()
+    return ts
+
+
+def test_c4_classes_and_construction(c4):
+    import bitcoinconsensus_amd as B
+    h = c4.host()
+    cls = h["cls"]
+    counts = np.bincount(cls, minlength=len(B.TupleSet.C4_CLASSES))
+    assert len(counts) == len(B.TupleSet.C4_CLASSES) and counts.min() > 0
+    assert 0.88 < counts[0] / c4.n < 0.92
+    v = np.frombuffer(c4.verdicts(), np.uint8)
+    bad = np.nonzero(v != h["expect"])[0]
+    assert len(bad) == 0, [(int(i), B.TupleSet.C4_CLASSES[cls[i]]) for i in bad[:20]]
+
+
+@pytest.mark.skipif(not reference_available(), reason="oracle/_ref not built")
+def test_c4_matches_reference_every_tuple(c4):
+    h = c4.host()
+    ref, _ = Reference().pubkey_verify_blob(h["pub_blob"], h["pub_off"], h["msg32"],
+                                            h["sig_blob"], h["sig_off"], threads=THREADS)
+    v = np.frombuffer(c4.verdicts(), np.uint8)
+    assert np.array_equal(v, ref), np.nonzero(v != ref)[0][:20]
+    assert np.array_equal(ref, h["expect"])
+
+
+def test_c4_through_pubkey_verify_batch(c4):
+    """The staged rows are exactly what the host front end builds: the one-shot entry point over
+    the same tuples gives the same verdicts."""
+    import bitcoinconsensus_amd as B
+    m = 20_000
+    tup = [c4.tuple(i) for i in range(m)]
+    assert B.pubkey_verify_batch(tup) == c4.verdicts()[:m]
+
+
+@pytest.mark.skipif(not reference_available(), reason="oracle/_ref not built")
+def test_c5_matches_reference_every_row():
+    import bitcoinconsensus_amd as B
+    vec = [(t["sig"], t["msg"], t["pub"], t["verdict"]) for t in bip340_vectors()]
+    ts = B.TupleSet(100_000, kind="c5", seed=0x5EED0005, vectors=vec)
+    ts.run()
+    v = np.frombuffer(ts.verdicts(), np.uint8)
+    h = ts.host()
+    ref, _ = Reference().schnorr_verify_rows(h["sig64"], h["msg32"], h["xonly32"], threads=THREADS)
+    assert np.array_equal(v, ref), np.nonzero(v != ref)[0][:20]
+    assert np.array_equal(v, h["expect"])
+    assert (h["cls"] > 0).sum() >= len(vec) * (100_000 // 1024)
