@@ -369,9 +369,15 @@ def main():
     if rank == 0:
         peak = B.microbench(0, 4096)  # v_mad_u64_u32 lane-ops/s, measured on this GPU
         achieved = sig_units * job.mads / (sig_ms * 1e-3)
+        traffic, tsrc = args.traffic, "--traffic" if args.traffic else None
+        tf = os.path.join(ROOT, "profiles", "traffic.json")
+        if traffic is None and os.path.exists(tf):
+            t = json.load(open(tf)).get(args.config)
+            if t and t.get("units") == sig_units:
+                traffic, tsrc = t["traffic_bytes"], t["source"]
         roof = dict(bound="int-alu", kernel=job.kernel,
                     achieved=achieved / 1e12, peak=peak / 1e12, unit="T(v_mad_u64_u32)/s",
-                    frac=achieved / peak, traffic=args.traffic,
+                    frac=achieved / peak, traffic=traffic, traffic_source=tsrc,
                     per_launch=dict(verifies=sig_units, mads=sig_units * job.mads, avg_ms=sig_ms,
                                     verifies_per_s=sig_units / (sig_ms * 1e-3)))
         cpu = None

@@ -86,6 +86,10 @@ void bcc_tupleset_view(const bcc_tupleset* ts, bcc_tupleset_host* v);
  * BCC_DEVICE environment variable). */
 int bcc_set_device(int device);
 
+/* Lanes per signature-kernel launch (0 = default: 4M, or the BCC_CHUNK environment variable).
+ * Bounds the per-caller device scratch (900 B per lane); results do not depend on it. */
+int bcc_set_chunk_lanes(size_t lanes);
+
 typedef struct bcc_batch_stats {
     size_t items, tuples, rounds, preimages, aux_messages, host_rejected;
     double host_seconds, gpu_seconds;

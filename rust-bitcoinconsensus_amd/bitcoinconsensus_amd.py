@@ -451,6 +451,11 @@ def gen_schnorr_sign(d32, m32, k32, device=0):
     return sig.raw[: 64 * n], xo.raw[: 32 * n], ok.raw[:n]
 
 
+def set_chunk_lanes(lanes):
+    """Lanes per signature-kernel launch (0 restores the default); results never depend on it."""
+    lib().bcc_set_chunk_lanes(ctypes.c_size_t(lanes))
+
+
 def microbench(op, iters=4096):
     r = ctypes.c_double(0)
     rc = lib().mi_microbench(op, iters, ctypes.byref(r))

@@ -70,11 +70,19 @@ def test_schnorr_kernel_multi_chunk_property():
     import bitcoinconsensus_amd as B
     n = 600_000
     sig, msg, pk = _gen(n, 12)
-    v = np.frombuffer(B.schnorr_verify_tuples(sig.tobytes(), msg.tobytes(), pk.tobytes()), np.uint8)
-    assert v.all()
-    bad = np.arange(0, n, 7)
-    msg[bad, 5] ^= 0x10
-    v = np.frombuffer(B.schnorr_verify_tuples(sig.tobytes(), msg.tobytes(), pk.tobytes()), np.uint8)
-    want = np.ones(n, np.uint8)
-    want[bad] = 0
-    assert np.array_equal(v, want)
+    B.set_chunk_lanes(262_144)  # 3 launches of the kernel pair (the default chunk holds 4M)
+    try:
+        v = np.frombuffer(B.schnorr_verify_tuples(sig.tobytes(), msg.tobytes(), pk.tobytes()), np.uint8)
+        assert v.all()
+        bad = np.arange(0, n, 7)
+        msg[bad, 5] ^= 0x10
+        v = np.frombuffer(B.schnorr_verify_tuples(sig.tobytes(), msg.tobytes(), pk.tobytes()), np.uint8)
+        want = np.ones(n, np.uint8)
+        want[bad] = 0
+        assert np.array_equal(v, want)
+        # the same rows in one chunk give the same verdicts
+        B.set_chunk_lanes(0)
+        v1 = np.frombuffer(B.schnorr_verify_tuples(sig.tobytes(), msg.tobytes(), pk.tobytes()), np.uint8)
+        assert np.array_equal(v1, want)
+    finally:
+        B.set_chunk_lanes(0)

@@ -83,3 +83,16 @@ def test_c5_matches_reference_every_row():
     assert np.array_equal(v, ref), np.nonzero(v != ref)[0][:20]
     assert np.array_equal(v, h["expect"])
     assert (h["cls"] > 0).sum() >= len(vec) * (100_000 // 1024)
+
+
+def test_c4_chunking_invariance(c4):
+    """The ECDSA kernels over the same staged rows in 65,536-lane chunks (5 launch pairs) and in
+    one chunk give identical verdicts."""
+    import bitcoinconsensus_amd as B
+    one = c4.verdicts()
+    B.set_chunk_lanes(65_536)
+    try:
+        c4.run()
+        assert c4.verdicts() == one
+    finally:
+        B.set_chunk_lanes(0)

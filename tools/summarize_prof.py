@@ -1,0 +1,65 @@
+"""Summarise a tools/profile_round.sh output directory: per-kernel launches / average duration
+from the --kernel-trace --stats pass and per-launch FETCH_SIZE / WRITE_SIZE from the --pmc passes
+(rocprofv3 reports both in KB; gfx950 FETCH_SIZE counts 128-B requests as 64 B for wide
+coalesced reads, MI355X_MICROARCH.md "HBM", so `fetch_bytes_x2` doubles it)."""
+import collections
+import csv
+import glob
+import json
+import os
+import sys
+
+
+def short(name):
+    n = name.split("(")[0]
+    return n.replace("bcc::", "").replace("(anonymous namespace)::", "")
+
+
+def main(d):
+    out = {"kernels": {}}
+    stats = glob.glob(os.path.join(d, "trace", "**", "*kernel_stats.csv"), recursive=True)
+    for f in stats:
+        for r in csv.DictReader(open(f)):
+            out["kernels"].setdefault(short(r["Name"]), {}).update(
+                calls=int(r["Calls"]), avg_ns=float(r["AverageNs"]), total_ns=float(r["TotalDurationNs"]))
+    for tag, ctr in (("pmc_fetch", "FETCH_SIZE"), ("pmc_write", "WRITE_SIZE")):
+        agg, cnt = collections.defaultdict(float), collections.Counter()
+        for f in glob.glob(os.path.join(d, tag, "**", "*counter_collection.csv"), recursive=True):
+            for r in csv.DictReader(open(f)):
+                if r["Counter_Name"] != ctr:
+                    continue
+                k = short(r["Kernel_Name"])
+                agg[k] += float(r["Counter_Value"])
+                cnt[k] += 1
+        for k in agg:
+            e = out["kernels"].setdefault(k, {})
+            e[ctr.lower() + "_bytes_per_launch"] = agg[k] * 1024 / cnt[k]
+            e[ctr.lower() + "_launches"] = cnt[k]
+            e[ctr.lower() + "_bytes_total"] = agg[k] * 1024
+    for k, e in out["kernels"].items():
+        if "fetch_size_bytes_per_launch" in e:
+            e["fetch_bytes_x2_per_launch"] = 2 * e["fetch_size_bytes_per_launch"]
+    # per signature stage = all launches of one run_ecdsa / schnorr call.  The PMC passes run
+    # bench.py --steps 1 --warmup 0: one timed step + 3 HIP-event timing repetitions = 4 stages.
+    stages = {"ecdsa": ["batch_sinv_kernel", "ecdsa_prep_kernel", "ecdsa_ladder_kernel"],
+              "schnorr": ["schnorr_prep_kernel", "schnorr_ladder_kernel", "schnorr_parity_kernel"]}
+    K = out["kernels"]
+    n_stage = 4
+    for st, ks in stages.items():
+        if not any("fetch_size_launches" in K.get(k, {}) for k in ks):
+            continue
+        fb = sum(K[k].get("fetch_size_bytes_total", 0) for k in ks if k in K) / n_stage
+        wb = sum(K[k].get("write_size_bytes_total", 0) for k in ks if k in K) / n_stage
+        out.setdefault("stages", {})[st] = dict(executions=n_stage, fetch_bytes=fb, fetch_bytes_x2=2 * fb,
+                                               write_bytes=wb, traffic_bytes=2 * fb + wb)
+    bench = os.path.join(d, "bench_under_rocprof.json")
+    if os.path.exists(bench):
+        try:
+            out["bench_under_rocprof"] = json.loads(open(bench).read().strip().splitlines()[-1])
+        except (ValueError, IndexError):
+            pass
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])
