@@ -28,8 +28,20 @@
 
 namespace bcc {
 
-// Per-tuple Q table, word-interleaved: word (entry i, field f, limb j) of tuple t at
-// base[((i*3 + f)*8 + j) * stride + t].
+// Per-lane scratch words in wave blocks: word w of lane t at
+//   base[(t / 64) * (W * 64) + w * 64 + t % 64]
+// so one wave's access to one word is 256 contiguous bytes and all W words of a wave's 64 lanes
+// are one contiguous W * 256-byte block (few DRAM pages / TLB entries per wave, unlike a
+// chunk-wide stride that puts consecutive words of a lane C * 4 bytes apart).
+constexpr size_t LANE_STRIDE = 64;
+__device__ __forceinline__ u32* lane_words(u32* base, size_t t, int W) {
+    return base + (t >> 6) * (size_t)(W * 64) + (t & 63);
+}
+__device__ __forceinline__ const u32* lane_words(const u32* base, size_t t, int W) {
+    return base + (t >> 6) * (size_t)(W * 64) + (t & 63);
+}
+
+// Per-tuple Q table: word (entry i, field f, limb j) at base[((i*3 + f)*8 + j) * stride].
 struct QTableGlobal {
     u32* base;
     size_t stride;
@@ -51,8 +63,14 @@ constexpr int STATE_WORDS = 16 + 1 + 8 + 8;  // LadderState
 struct GTableLDS {
     const fe* xy;
     __device__ void get(int tab, int i, fe& x, fe& y) const {
-        x = xy[(tab * GTAB + i) * 2 + 0];
-        y = xy[(tab * GTAB + i) * 2 + 1];
+        // LDS address space explicitly: ds_read instead of flat loads
+        const __attribute__((address_space(3))) u32* l = (const __attribute__((address_space(3))) u32*)xy;
+        const int b = (tab * GTAB + i) * 16;
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            x.v[j] = l[b + j];
+            y.v[j] = l[b + 8 + j];
+        }
     }
 };
 
@@ -160,7 +178,9 @@ struct LadderStateView {
     __device__ __forceinline__ u32 kword(int s, int w) const {
         const u32* q = p;
         asm volatile("" : "+v"(q));
-        return q[(size_t)(s * 4 + w) * C];
+        // the asm hides the address space too: restore it so this is a global (not flat) load
+        const __attribute__((address_space(1))) u32* g = (const __attribute__((address_space(1))) u32*)q;
+        return g[(size_t)(s * 4 + w) * C];
     }
     __device__ __forceinline__ void get_r(sc& o) const {
 #pragma unroll
@@ -184,10 +204,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
     load_be32(s, ps + 32 * i);
     load_be32(m, pm + 32 * i);
     load_limbs(si, psinv + 8 * i);
-    QTableGlobal qt{qtab + t, C};
+    QTableGlobal qt{lane_words(qtab, t, QTABLE_WORDS), LANE_STRIDE};
     LadderState st;
     ecdsa_prep_lane(tag[i], x, y, r, s, m, &si, qt, st);
-    store_state(state + t, C, st);
+    store_state(lane_words(state, t, STATE_WORDS), LANE_STRIDE, st);
 }
 
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) void ecdsa_ladder_kernel(const u32* __restrict__ state,
@@ -201,12 +221,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= cnt) return;
     LadderStateView st;
-    st.p = state + t;
-    st.C = C;
-    st.flags = st.p[16 * C];
+    st.p = lane_words(state, t, STATE_WORDS);
+    st.C = LANE_STRIDE;
+    st.flags = st.p[16 * LANE_STRIDE];
 #pragma unroll
-    for (int j = 0; j < 8; j++) st.sigma.v[j] = st.p[(17 + j) * C];
-    QTableGlobal qt{const_cast<u32*>(qtab) + t, C};
+    for (int j = 0; j < 8; j++) st.sigma.v[j] = st.p[(17 + j) * LANE_STRIDE];
+    QTableGlobal qt{lane_words(const_cast<u32*>(qtab), t, QTABLE_WORDS), LANE_STRIDE};
     GTableLDS gt{g_lds};
     verdict[base + t] = (uint8_t)ecdsa_ladder_lane(st, qt, gt);
 }
@@ -230,10 +250,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
     load_be32(s, psig + 64 * i + 32);
     load_be32(m, pm + 32 * i);
     load_be32(px, ppk + 32 * i);
-    QTableGlobal qt{qtab + t, C};
+    QTableGlobal qt{lane_words(qtab, t, QTABLE_WORDS), LANE_STRIDE};
     LadderState st;
     schnorr_prep_lane(px, rx, s, m, qt, st);
-    store_state(state + t, C, st);
+    store_state(lane_words(state, t, STATE_WORDS), LANE_STRIDE, st);
 }
 
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) void schnorr_ladder_kernel(
@@ -245,12 +265,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= cnt) return;
     LadderStateView st;
-    st.p = state + t;
-    st.C = C;
-    st.flags = st.p[16 * C];
+    st.p = lane_words(state, t, STATE_WORDS);
+    st.C = LANE_STRIDE;
+    st.flags = st.p[16 * LANE_STRIDE];
 #pragma unroll
-    for (int j = 0; j < 8; j++) st.sigma.v[j] = st.p[(17 + j) * C];
-    QTableGlobal qt{qtab + t, C};
+    for (int j = 0; j < 8; j++) st.sigma.v[j] = st.p[(17 + j) * LANE_STRIDE];
+    QTableGlobal qt{lane_words(qtab, t, QTABLE_WORDS), LANE_STRIDE};
     GTableLDS gt{g_lds};
     fe ye, ze;
     int ok = schnorr_ladder_lane(st, qt, gt, ye, ze);
@@ -273,12 +293,12 @@ __global__ __launch_bounds__(256) void schnorr_parity_kernel(u32* __restrict__ q
     const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= cnt || t >= T) return;
     fe acc, z, ye;
-    QTableGlobal q0{qtab + t, C};
+    QTableGlobal q0{lane_words(qtab, t, QTABLE_WORDS), LANE_STRIDE};
     q0.get(0, 1, acc);
     q0.put(0, 2, acc);
     size_t last = t;
     for (size_t i = t + T; i < cnt; i += T) {
-        QTableGlobal qi{qtab + i, C};
+        QTableGlobal qi{lane_words(qtab, i, QTABLE_WORDS), LANE_STRIDE};
         qi.get(0, 1, z);
         fe_mul(acc, acc, z);
         qi.put(0, 2, acc);  // Z_t * ... * Z_i
@@ -287,7 +307,8 @@ __global__ __launch_bounds__(256) void schnorr_parity_kernel(u32* __restrict__ q
     fe inv;
     fe_inv(inv, acc);
     for (size_t i = last; i >= t + T; i -= T) {
-        QTableGlobal qi{qtab + i, C}, qp{qtab + i - T, C};
+        QTableGlobal qi{lane_words(qtab, i, QTABLE_WORDS), LANE_STRIDE},
+            qp{lane_words(qtab, i - T, QTABLE_WORDS), LANE_STRIDE};
         fe prev, zi;
         qp.get(0, 2, prev);
         fe_mul(zi, inv, prev);  // Z_i^-1
