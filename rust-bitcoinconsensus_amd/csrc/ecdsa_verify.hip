@@ -411,22 +411,39 @@ static int ensure_scratch(SigScratch& sc, int dev, size_t n, bool with_sinv, siz
     return 0;
 }
 
-int ecdsa_launch(SigScratch& sc, const uint8_t* d_tag, const uint8_t* d_x, const uint8_t* d_y,
-                 const uint8_t* d_r, const uint8_t* d_s, const uint8_t* d_m, uint8_t* d_verdict,
-                 size_t n, void* stream) {
+int ecdsa_launch_sinv(SigScratch& sc, const uint8_t* d_s, size_t n, void* stream) {
     if (n == 0) return 0;
     int dev = 0, cus = 0;
     fe* gtab = nullptr;
     size_t C = 0;
     if (int e = device_tables(&dev, &gtab, &cus)) return e;
     if (int e = ensure_scratch(sc, dev, n, true, &C)) return e;
-    hipStream_t sm = (hipStream_t)stream;
-    u32* sinv = (u32*)sc.sinv;
     // K_inv: chunks of <= 16 tuples, but at least one wave per SIMD
     size_t T = std::max<size_t>((n + 15) / 16, std::min<size_t>(n, (size_t)cus * 256));
-    hipLaunchKernelGGL(batch_sinv_kernel, dim3((unsigned)((T + 255) / 256)), dim3(256), 0, sm, d_s,
-                       sinv, n, T);
+    hipLaunchKernelGGL(batch_sinv_kernel, dim3((unsigned)((T + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)stream, d_s, (u32*)sc.sinv, n, T);
     BCC_HIP_TRY(hipGetLastError());
+    return 0;
+}
+
+int ecdsa_launch(SigScratch& sc, const uint8_t* d_tag, const uint8_t* d_x, const uint8_t* d_y,
+                 const uint8_t* d_r, const uint8_t* d_s, const uint8_t* d_m, uint8_t* d_verdict,
+                 size_t n, void* stream) {
+    if (int e = ecdsa_launch_sinv(sc, d_s, n, stream)) return e;
+    return ecdsa_launch_after_sinv(sc, d_tag, d_x, d_y, d_r, d_s, d_m, d_verdict, n, stream);
+}
+
+int ecdsa_launch_after_sinv(SigScratch& sc, const uint8_t* d_tag, const uint8_t* d_x,
+                            const uint8_t* d_y, const uint8_t* d_r, const uint8_t* d_s,
+                            const uint8_t* d_m, uint8_t* d_verdict, size_t n, void* stream) {
+    if (n == 0) return 0;
+    int dev = 0, cus = 0;
+    fe* gtab = nullptr;
+    size_t C = 0;
+    if (int e = device_tables(&dev, &gtab, &cus)) return e;
+    if (int e = ensure_scratch(sc, dev, n, true, &C)) return e;  // sized by ecdsa_launch_sinv
+    hipStream_t sm = (hipStream_t)stream;
+    u32* sinv = (u32*)sc.sinv;
     u32* qtab = (u32*)sc.chunk;
     u32* state = qtab + C * QTABLE_WORDS;
     for (size_t base = 0; base < n; base += C) {

@@ -128,6 +128,12 @@ struct SigScratch {
 int ecdsa_launch(SigScratch& sc, const uint8_t* d_tag, const uint8_t* d_x, const uint8_t* d_y,
                  const uint8_t* d_r, const uint8_t* d_s, const uint8_t* d_m, uint8_t* d_verdict,
                  size_t n, void* stream);
+// The same in two parts: K_inv (reads only the s rows, so it can run beside the sighash
+// kernels on another stream) and everything after it (must be ordered after K_inv).
+int ecdsa_launch_sinv(SigScratch& sc, const uint8_t* d_s, size_t n, void* stream);
+int ecdsa_launch_after_sinv(SigScratch& sc, const uint8_t* d_tag, const uint8_t* d_x,
+                            const uint8_t* d_y, const uint8_t* d_r, const uint8_t* d_s,
+                            const uint8_t* d_m, uint8_t* d_verdict, size_t n, void* stream);
 int schnorr_launch(SigScratch& sc, const uint8_t* d_sig64, const uint8_t* d_msg32,
                    const uint8_t* d_xonly32, uint8_t* d_verdict, size_t n, void* stream);
 
@@ -160,6 +166,9 @@ private:
     int dev_;
     void* own_stream_ = nullptr;   // hipStream_t, created on first use
     void* last_stream_ = nullptr;  // stream of the last run
+    void* side_stream_ = nullptr;  // K_inv beside the sighash kernels (run())
+    void* ev_fork_ = nullptr;      // hipEvent_t: run() start on the main stream
+    void* ev_join_ = nullptr;      // hipEvent_t: K_inv done on the side stream
     SigScratch scratch_;
     void* arena_ = nullptr;
     size_t cap_ = 0;

@@ -157,11 +157,30 @@ __global__ __launch_bounds__(256) void patch_digests_kernel(uint8_t* __restrict_
                                                             const PatchRec* __restrict__ patches,
                                                             const uint8_t* __restrict__ auxd,
                                                             uint32_t npatch) {
+    // one lane per patch: the 32-byte digest with the widest stores the slot's alignment allows
+    // (BIP143 slots sit at preimage offsets 4, 36 and len - 40)
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= npatch * 32) return;
-    PatchRec p = patches[i >> 5];
-    uint32_t k = i & 31;
-    pre[(size_t)p.pre_byte + k] = auxd[(size_t)p.aux * 32 + k];
+    if (i >= npatch) return;
+    const PatchRec p = patches[i];
+    const uint4* src = reinterpret_cast<const uint4*>(auxd + (size_t)p.aux * 32);
+    const uint4 d0 = src[0], d1 = src[1];
+    const uint32_t w[8] = {d0.x, d0.y, d0.z, d0.w, d1.x, d1.y, d1.z, d1.w};
+    uint8_t* dst = pre + p.pre_byte;
+    if ((p.pre_byte & 3) == 0) {
+        uint32_t* o = reinterpret_cast<uint32_t*>(dst);
+#pragma unroll
+        for (int k = 0; k < 8; k++) o[k] = w[k];
+    } else if ((p.pre_byte & 1) == 0) {
+        uint16_t* o = reinterpret_cast<uint16_t*>(dst);
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            o[2 * k] = (uint16_t)w[k];
+            o[2 * k + 1] = (uint16_t)(w[k] >> 16);
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < 32; k++) dst[k] = (uint8_t)(w[k >> 2] >> (8 * (k & 3)));
+    }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -170,6 +189,9 @@ DeviceBatch::DeviceBatch(int device) : dev_(device) {}
 DeviceBatch::~DeviceBatch() {
     (void)hipSetDevice(dev_);
     if (own_stream_) (void)hipStreamDestroy((hipStream_t)own_stream_);
+    if (side_stream_) (void)hipStreamDestroy((hipStream_t)side_stream_);
+    if (ev_fork_) (void)hipEventDestroy((hipEvent_t)ev_fork_);
+    if (ev_join_) (void)hipEventDestroy((hipEvent_t)ev_join_);
     if (arena_) (void)hipFree(arena_);
 }
 
@@ -255,7 +277,7 @@ int DeviceBatch::run_sighash(void* stream) {
         BCC_HIP_TRY(hipGetLastError());
     }
     if (n_patch_) {
-        size_t th = n_patch_ * 32;
+        size_t th = n_patch_;
         hipLaunchKernelGGL(patch_digests_kernel, dim3((unsigned)((th + 255) / 256)), dim3(256), 0, st,
                            d_pre_, d_patch_, d_auxd_, (uint32_t)n_patch_);
         BCC_HIP_TRY(hipGetLastError());
@@ -275,9 +297,34 @@ int DeviceBatch::run_ecdsa(void* stream) {
     return ecdsa_launch(scratch_, d_tag, d_x, d_y, d_r, d_s, d_m, d_v, n_rows_, st);
 }
 
+// K_inv reads only the s rows, so it runs on a side stream beside the sighash kernels
+// (fork / join by events: graph-capturable); prep + ladder wait for both.
 int DeviceBatch::run(void* stream) {
-    if (int e = run_sighash(stream)) return e;
-    return run_ecdsa(stream);
+    BCC_HIP_TRY(hipSetDevice(dev_));
+    hipStream_t st = (hipStream_t)pick(stream);
+    if (!st) return (int)hipErrorOutOfMemory;
+    if (n_rows_ == 0 || n_aux_ + n_tjob_ + n_pre_ == 0) {
+        if (int e = run_sighash(st)) return e;
+        return run_ecdsa(st);
+    }
+    if (!side_stream_) {
+        hipStream_t s = nullptr;
+        hipEvent_t a = nullptr, b = nullptr;
+        BCC_HIP_TRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+        BCC_HIP_TRY(hipEventCreateWithFlags(&a, hipEventDisableTiming));
+        BCC_HIP_TRY(hipEventCreateWithFlags(&b, hipEventDisableTiming));
+        side_stream_ = s;
+        ev_fork_ = a;
+        ev_join_ = b;
+    }
+    hipStream_t side = (hipStream_t)side_stream_;
+    BCC_HIP_TRY(hipEventRecord((hipEvent_t)ev_fork_, st));
+    BCC_HIP_TRY(hipStreamWaitEvent(side, (hipEvent_t)ev_fork_, 0));
+    if (int e = ecdsa_launch_sinv(scratch_, d_s, n_rows_, side)) return e;
+    BCC_HIP_TRY(hipEventRecord((hipEvent_t)ev_join_, side));
+    if (int e = run_sighash(st)) return e;
+    BCC_HIP_TRY(hipStreamWaitEvent(st, (hipEvent_t)ev_join_, 0));
+    return ecdsa_launch_after_sinv(scratch_, d_tag, d_x, d_y, d_r, d_s, d_m, d_v, n_rows_, st);
 }
 
 int DeviceBatch::fetch_verdicts(uint8_t* out) {
