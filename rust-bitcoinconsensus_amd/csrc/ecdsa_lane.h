@@ -202,32 +202,50 @@ BCC_HD void curve_rhs(fe& r, const fe& x) {
 // tag = pubkey header byte (0 for "length invalid"), px/py as parsed from the big-endian bytes
 // (py ignored for compressed keys), r/s/m as raw integers from big-endian bytes.
 // sinv_pre: s^-1 mod n from the batched-inversion kernel (nullptr: invert here).
+// Pubkey parse (eckey_impl.h:17-35, ge_set_xo_var / ge_is_valid_var): tag = header byte (0 for
+// "length invalid"), px/py as parsed from the big-endian bytes (py ignored for compressed keys).
+// On success qy is the affine y (normalized for compressed keys).
+BCC_HD bool pubkey_load(u32 tag, const fe& px, const fe& py_in, fe& qy) {
+    bool compressed = (tag == 2u || tag == 3u);
+    bool full = (tag == 4u || tag == 6u || tag == 7u);
+    if (!compressed && !full) return false;
+    if (!fe_lt_p(px)) return false;
+    qy = py_in;
+    fe x3, t;
+    curve_rhs(x3, px);                       // x^3 + 7
+    if (compressed) {
+        if (!fe_sqrt(qy, x3)) return false;  // ge_set_xo_var: no square root
+        fe_normalize(qy);
+        if ((qy.v[0] & 1u) != (tag == 3u ? 1u : 0u)) fe_neg(qy, qy);
+        return true;
+    }
+    if (!fe_lt_p(qy)) return false;
+    if (tag != 4u && (qy.v[0] & 1u) != (tag == 7u ? 1u : 0u)) return false;  // hybrid parity
+    fe_sqr(t, qy);
+    return fe_equal(t, x3);                  // ge_is_valid_var
+}
+
+// Prep after the pubkey parse: scalar checks, u1/u2, GLV split, odd fix-ups and the Q table for
+// an already loaded key (qx, qy).
+template <class QT>
+BCC_HD bool ecdsa_prep_loaded(const fe& qx, const fe& qy, const sc& r_in, const sc& s_in,
+                              const sc& m_in, const sc* sinv_pre, QT& qt, LadderState& st);
+
 template <class QT>
 BCC_HD bool ecdsa_prep_lane(u32 tag, const fe& px_in, const fe& py_in, const sc& r_in,
                             const sc& s_in, const sc& m_in, const sc* sinv_pre, QT& qt,
                             LadderState& st) {
+    st.flags = 0;
+    fe qy;
+    if (!pubkey_load(tag, px_in, py_in, qy)) return false;
+    return ecdsa_prep_loaded(px_in, qy, r_in, s_in, m_in, sinv_pre, qt, st);
+}
+
+template <class QT>
+BCC_HD bool ecdsa_prep_loaded(const fe& qx, const fe& qy, const sc& r_in, const sc& s_in,
+                              const sc& m_in, const sc* sinv_pre, QT& qt, LadderState& st) {
     const u32 N[8] = BCC_N_LIMBS;
     st.flags = 0;
-    // ---- pubkey parse (eckey_impl.h:17-35) ----
-    bool compressed = (tag == 2u || tag == 3u);
-    bool full = (tag == 4u || tag == 6u || tag == 7u);
-    if (!compressed && !full) return false;
-    fe qx = px_in, qy = py_in;
-    if (!fe_lt_p(qx)) return false;
-    {
-        fe x3, t;
-        curve_rhs(x3, qx);                       // x^3 + 7
-        if (compressed) {
-            if (!fe_sqrt(qy, x3)) return false;  // ge_set_xo_var: no square root
-            fe_normalize(qy);
-            if ((qy.v[0] & 1u) != (tag == 3u ? 1u : 0u)) fe_neg(qy, qy);
-        } else {
-            if (!fe_lt_p(qy)) return false;
-            if (tag != 4u && (qy.v[0] & 1u) != (tag == 7u ? 1u : 0u)) return false;  // hybrid parity
-            fe_sqr(t, qy);
-            if (!fe_equal(t, x3)) return false;  // ge_is_valid_var
-        }
-    }
     // ---- scalars (ecdsa_impl.h:216-222) ----
     if (u256_is_zero(r_in.v) || u256_is_zero(s_in.v)) return false;
     if (!u256_lt(r_in.v, N) || !u256_lt(s_in.v, N)) return false;

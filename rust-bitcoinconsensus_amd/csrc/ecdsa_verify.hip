@@ -1,13 +1,15 @@
-// ECDSA verify on gfx950: stage (c) of the hot path, with stage (b) (pubkey decompression)
-// in its prep phase.  One lane = one tuple; the per-lane algorithm is ecdsa_lane.h.
+// ECDSA verify on gfx950: stages (b) and (c) of the hot path.  One lane = one tuple; the
+// per-lane algorithm is ecdsa_lane.h.
 //
 //   K_inv     batch_sinv_kernel     s^-1 mod n by Montgomery's trick over strided chunks of <= 16
 //                                   tuples (3 mults/tuple + one Fermat inversion per chunk)
-//   K_prep    ecdsa_prep_kernel     pubkey parse/decompress, u1/u2, GLV split, Q table
+//   K_key     ecdsa_key_kernel      pubkey parse / decompression (square root), high occupancy
+//   K_prep    ecdsa_prep_kernel     scalar checks, u1/u2, GLV split, Q table
 //   K_ladder  ecdsa_ladder_kernel   Strauss ladder (shared doublings) + inversion-free x-check
-// K_prep and K_ladder are separate launches so that each gets its own register allocation: the
-// ladder, which is ~85% of the work, then runs at 3+ waves per SIMD instead of 1.  Tuples are
-// processed in chunks so the per-tuple scratch (Q table + ladder state, ~900 B) stays bounded.
+// K_inv and K_key need only the s and key rows: DeviceBatch::run launches them on a side stream
+// beside the sighash kernels.  K_prep and K_ladder are separate launches so that each gets its
+// own register allocation (ladder: 4 waves per SIMD).  Tuples are processed in chunks of up to
+// 4M lanes so the per-tuple scratch (Q table + ladder state, ~900 B) stays bounded.
 //
 // HBM layout (all device-resident):
 //   tag[n]            u8   pubkey header byte (0 = rejected by the host length filter)
@@ -15,9 +17,10 @@
 //   r[n][32], s[n][32]     signature scalars after lax-DER (zero on overflow)
 //   m[n][32]               sighash (raw SHA-256d bytes == big-endian integer)
 //   verdict[n]        u8   1 = valid
-//   scratch                s^-1 [n][8] u32; per chunk: Q table [24 fe words][C], state [33][C]
-// Row loads are two 16-byte loads per lane (a wave covers one contiguous 2 KiB span); scratch is
-// word-interleaved by tuple ([word][C]) so every scratch access of a wave is one 256-byte line.
+//   scratch                per tuple s^-1, key y, key status; per chunk lane Q table (192 words)
+//                          and ladder state (33 words) in wave blocks (lane_words below)
+// Row loads are two 16-byte loads per lane (a wave covers one contiguous 2 KiB span); every
+// scratch access of a wave is one 256-byte span.
 #include <atomic>
 #include <cstdlib>
 #include <memory>
@@ -58,6 +61,7 @@ struct QTableGlobal {
 };
 constexpr int QTABLE_WORDS = QTAB * 3 * 8;  // 192
 constexpr int STATE_WORDS = 16 + 1 + 8 + 8;  // LadderState
+constexpr int PRE_WORDS = 8 + 8 + 1;          // per tuple: s^-1, key y, key status
 
 // G tables staged in LDS (16 KiB per workgroup).
 struct GTableLDS {
@@ -188,25 +192,52 @@ struct LadderStateView {
     }
 };
 
+// Stage b (pubkey parse + decompression, eckey_impl.h:17-35) for every tuple, before and apart
+// from the prep kernel: the square root (266 of prep's ~420 modmuls) needs few registers, so it
+// runs at high occupancy here, and it reads only the key rows, so it runs on the side stream
+// beside the sighash kernels.  Writes y (8 limbs) and the parse status per tuple.
+__global__ __launch_bounds__(256) void ecdsa_key_kernel(const uint8_t* __restrict__ tag,
+                                                        const uint8_t* __restrict__ px,
+                                                        const uint8_t* __restrict__ py, size_t n,
+                                                        u32* __restrict__ keyy,
+                                                        u32* __restrict__ kok) {
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    fe x, y, qy;
+    load_be32(x, px + 32 * i);
+    load_be32(y, py + 32 * i);
+    const bool ok = pubkey_load(tag[i], x, y, qy);
+    sc o;
+#pragma unroll
+    for (int k = 0; k < 8; k++) o.v[k] = ok ? qy.v[k] : 0u;
+    store_limbs(keyy + 8 * i, o);
+    kok[i] = ok ? 1u : 0u;
+}
+
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void ecdsa_prep_kernel(
-    const uint8_t* __restrict__ tag, const uint8_t* __restrict__ px, const uint8_t* __restrict__ py,
-    const uint8_t* __restrict__ pr, const uint8_t* __restrict__ ps, const uint8_t* __restrict__ pm,
-    const u32* __restrict__ psinv, size_t base, size_t cnt, size_t C, u32* __restrict__ qtab,
+    const uint8_t* __restrict__ px, const uint8_t* __restrict__ pr, const uint8_t* __restrict__ ps,
+    const uint8_t* __restrict__ pm, const u32* __restrict__ psinv, const u32* __restrict__ keyy,
+    const u32* __restrict__ kok, size_t base, size_t cnt, u32* __restrict__ qtab,
     u32* __restrict__ state) {
     const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= cnt) return;
     const size_t i = base + t;
-    fe x, y;
-    sc r, s, m, si;
-    load_be32(x, px + 32 * i);
-    load_be32(y, py + 32 * i);
-    load_be32(r, pr + 32 * i);
-    load_be32(s, ps + 32 * i);
-    load_be32(m, pm + 32 * i);
-    load_limbs(si, psinv + 8 * i);
-    QTableGlobal qt{lane_words(qtab, t, QTABLE_WORDS), LANE_STRIDE};
     LadderState st;
-    ecdsa_prep_lane(tag[i], x, y, r, s, m, &si, qt, st);
+    st.flags = 0;
+    QTableGlobal qt{lane_words(qtab, t, QTABLE_WORDS), LANE_STRIDE};
+    if (kok[i]) {
+        fe x, y;
+        sc r, s, m, si, yl;
+        load_be32(x, px + 32 * i);
+        load_limbs(yl, keyy + 8 * i);
+#pragma unroll
+        for (int k = 0; k < 8; k++) y.v[k] = yl.v[k];
+        load_be32(r, pr + 32 * i);
+        load_be32(s, ps + 32 * i);
+        load_be32(m, pm + 32 * i);
+        load_limbs(si, psinv + 8 * i);
+        ecdsa_prep_loaded(x, y, r, s, m, &si, qt, st);
+    }
     store_state(lane_words(state, t, STATE_WORDS), LANE_STRIDE, st);
 }
 
@@ -404,24 +435,31 @@ static int ensure_scratch(SigScratch& sc, int dev, size_t n, bool with_sinv, siz
         sc.sinv = nullptr;
         sc.sinv_cap = 0;
         size_t cap = std::max<size_t>(n, 1 << 12);
-        BCC_HIP_TRY(hipMalloc(&sc.sinv, cap * 8 * sizeof(u32)));
+        // per tuple: s^-1 (8 words), the loaded key's y (8 words) and its parse status (1 word)
+        BCC_HIP_TRY(hipMalloc(&sc.sinv, cap * PRE_WORDS * sizeof(u32)));
         sc.sinv_cap = cap;
     }
     *C = want;
     return 0;
 }
 
-int ecdsa_launch_sinv(SigScratch& sc, const uint8_t* d_s, size_t n, void* stream) {
+int ecdsa_launch_pre(SigScratch& sc, const uint8_t* d_tag, const uint8_t* d_x,
+                     const uint8_t* d_y, const uint8_t* d_s, size_t n, void* stream) {
     if (n == 0) return 0;
     int dev = 0, cus = 0;
     fe* gtab = nullptr;
     size_t C = 0;
     if (int e = device_tables(&dev, &gtab, &cus)) return e;
     if (int e = ensure_scratch(sc, dev, n, true, &C)) return e;
+    u32* sinv = (u32*)sc.sinv;
     // K_inv: chunks of <= 16 tuples, but at least one wave per SIMD
     size_t T = std::max<size_t>((n + 15) / 16, std::min<size_t>(n, (size_t)cus * 256));
     hipLaunchKernelGGL(batch_sinv_kernel, dim3((unsigned)((T + 255) / 256)), dim3(256), 0,
-                       (hipStream_t)stream, d_s, (u32*)sc.sinv, n, T);
+                       (hipStream_t)stream, d_s, sinv, n, T);
+    BCC_HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(ecdsa_key_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)stream, d_tag, d_x, d_y, n, sinv + 8 * sc.sinv_cap,
+                       sinv + 16 * sc.sinv_cap);
     BCC_HIP_TRY(hipGetLastError());
     return 0;
 }
@@ -429,28 +467,30 @@ int ecdsa_launch_sinv(SigScratch& sc, const uint8_t* d_s, size_t n, void* stream
 int ecdsa_launch(SigScratch& sc, const uint8_t* d_tag, const uint8_t* d_x, const uint8_t* d_y,
                  const uint8_t* d_r, const uint8_t* d_s, const uint8_t* d_m, uint8_t* d_verdict,
                  size_t n, void* stream) {
-    if (int e = ecdsa_launch_sinv(sc, d_s, n, stream)) return e;
-    return ecdsa_launch_after_sinv(sc, d_tag, d_x, d_y, d_r, d_s, d_m, d_verdict, n, stream);
+    if (int e = ecdsa_launch_pre(sc, d_tag, d_x, d_y, d_s, n, stream)) return e;
+    return ecdsa_launch_after_pre(sc, d_x, d_r, d_s, d_m, d_verdict, n, stream);
 }
 
-int ecdsa_launch_after_sinv(SigScratch& sc, const uint8_t* d_tag, const uint8_t* d_x,
-                            const uint8_t* d_y, const uint8_t* d_r, const uint8_t* d_s,
-                            const uint8_t* d_m, uint8_t* d_verdict, size_t n, void* stream) {
+int ecdsa_launch_after_pre(SigScratch& sc, const uint8_t* d_x, const uint8_t* d_r,
+                           const uint8_t* d_s, const uint8_t* d_m, uint8_t* d_verdict, size_t n,
+                           void* stream) {
     if (n == 0) return 0;
     int dev = 0, cus = 0;
     fe* gtab = nullptr;
     size_t C = 0;
     if (int e = device_tables(&dev, &gtab, &cus)) return e;
-    if (int e = ensure_scratch(sc, dev, n, true, &C)) return e;  // sized by ecdsa_launch_sinv
+    if (int e = ensure_scratch(sc, dev, n, true, &C)) return e;  // sized by ecdsa_launch_pre
     hipStream_t sm = (hipStream_t)stream;
     u32* sinv = (u32*)sc.sinv;
+    const u32* keyy = sinv + 8 * sc.sinv_cap;
+    const u32* kok = sinv + 16 * sc.sinv_cap;
     u32* qtab = (u32*)sc.chunk;
     u32* state = qtab + C * QTABLE_WORDS;
     for (size_t base = 0; base < n; base += C) {
         size_t cnt = std::min(C, n - base);
         unsigned blocks = (unsigned)((cnt + 255) / 256);
-        hipLaunchKernelGGL(ecdsa_prep_kernel, dim3(blocks), dim3(256), 0, sm, d_tag, d_x, d_y, d_r,
-                           d_s, d_m, sinv, base, cnt, C, qtab, state);
+        hipLaunchKernelGGL(ecdsa_prep_kernel, dim3(blocks), dim3(256), 0, sm, d_x, d_r, d_s, d_m,
+                           sinv, keyy, kok, base, cnt, qtab, state);
         BCC_HIP_TRY(hipGetLastError());
         hipLaunchKernelGGL(ecdsa_ladder_kernel, dim3(blocks), dim3(256), 0, sm, state, qtab, gtab,
                            d_verdict, base, cnt, C);

@@ -128,12 +128,14 @@ struct SigScratch {
 int ecdsa_launch(SigScratch& sc, const uint8_t* d_tag, const uint8_t* d_x, const uint8_t* d_y,
                  const uint8_t* d_r, const uint8_t* d_s, const uint8_t* d_m, uint8_t* d_verdict,
                  size_t n, void* stream);
-// The same in two parts: K_inv (reads only the s rows, so it can run beside the sighash
-// kernels on another stream) and everything after it (must be ordered after K_inv).
-int ecdsa_launch_sinv(SigScratch& sc, const uint8_t* d_s, size_t n, void* stream);
-int ecdsa_launch_after_sinv(SigScratch& sc, const uint8_t* d_tag, const uint8_t* d_x,
-                            const uint8_t* d_y, const uint8_t* d_r, const uint8_t* d_s,
-                            const uint8_t* d_m, uint8_t* d_verdict, size_t n, void* stream);
+// The same in two parts: K_inv + K_key (s^-1 and the pubkey parse / decompression read only the
+// s and key rows, so they can run beside the sighash kernels on another stream) and everything
+// after them (must be ordered after both, and after the sighash kernels that write m).
+int ecdsa_launch_pre(SigScratch& sc, const uint8_t* d_tag, const uint8_t* d_x,
+                     const uint8_t* d_y, const uint8_t* d_s, size_t n, void* stream);
+int ecdsa_launch_after_pre(SigScratch& sc, const uint8_t* d_x, const uint8_t* d_r,
+                           const uint8_t* d_s, const uint8_t* d_m, uint8_t* d_verdict, size_t n,
+                           void* stream);
 int schnorr_launch(SigScratch& sc, const uint8_t* d_sig64, const uint8_t* d_msg32,
                    const uint8_t* d_xonly32, uint8_t* d_verdict, size_t n, void* stream);
 

@@ -297,8 +297,8 @@ int DeviceBatch::run_ecdsa(void* stream) {
     return ecdsa_launch(scratch_, d_tag, d_x, d_y, d_r, d_s, d_m, d_v, n_rows_, st);
 }
 
-// K_inv reads only the s rows, so it runs on a side stream beside the sighash kernels
-// (fork / join by events: graph-capturable); prep + ladder wait for both.
+// K_inv and K_key read only the s and key rows, so they run on a side stream beside the sighash
+// kernels (fork / join by events: graph-capturable); prep + ladder wait for both.
 int DeviceBatch::run(void* stream) {
     BCC_HIP_TRY(hipSetDevice(dev_));
     hipStream_t st = (hipStream_t)pick(stream);
@@ -320,11 +320,11 @@ int DeviceBatch::run(void* stream) {
     hipStream_t side = (hipStream_t)side_stream_;
     BCC_HIP_TRY(hipEventRecord((hipEvent_t)ev_fork_, st));
     BCC_HIP_TRY(hipStreamWaitEvent(side, (hipEvent_t)ev_fork_, 0));
-    if (int e = ecdsa_launch_sinv(scratch_, d_s, n_rows_, side)) return e;
+    if (int e = ecdsa_launch_pre(scratch_, d_tag, d_x, d_y, d_s, n_rows_, side)) return e;
     BCC_HIP_TRY(hipEventRecord((hipEvent_t)ev_join_, side));
     if (int e = run_sighash(st)) return e;
     BCC_HIP_TRY(hipStreamWaitEvent(st, (hipEvent_t)ev_join_, 0));
-    return ecdsa_launch_after_sinv(scratch_, d_tag, d_x, d_y, d_r, d_s, d_m, d_v, n_rows_, st);
+    return ecdsa_launch_after_pre(scratch_, d_x, d_r, d_s, d_m, d_v, n_rows_, st);
 }
 
 int DeviceBatch::fetch_verdicts(uint8_t* out) {
