@@ -59,14 +59,21 @@ struct Item {
     bitcoinconsensus_error err = bitcoinconsensus_ERR_OK;
     bool active = false;  // needs (another) interpreter run
     bool result = false;
-    // tuple key -> 0/1 known verdict, or -2 - r: deferred as row r of the current round
-    std::unordered_map<std::string, int32_t> cache;
+    // checks seen by this item's runs: tuple key -> 0/1 known verdict, or -2 - r: deferred as
+    // row r of the current round.  A flat list: an input makes a handful of checks, so a linear
+    // scan beats a hash map and costs no bucket allocation per item.
+    std::vector<std::pair<std::string, int32_t>> cache;
     std::vector<uint32_t> pending;  // deferred rows the last run consulted (answered "true")
+    int32_t* find(const std::string& k) {
+        for (auto& e : cache)
+            if (e.first == k) return &e.second;
+        return nullptr;
+    }
 };
 
 struct Pending {
     uint32_t item;
-    std::string key;
+    uint32_t slot;  // index of the check in the item's cache
 };
 
 std::string tuple_key(const Bytes& pub, const Bytes& sig, const Bytes& code, SigVersion sv) {
@@ -108,6 +115,7 @@ public:
     TupleRows rows;
     std::vector<Pending> pending;
     std::vector<uint8_t> scratch;
+    Bip143Job bip143;
     std::vector<TxEntry*> touched;
     size_t host_rejected = 0;
 
@@ -118,10 +126,9 @@ public:
     bool defer(uint32_t item_idx, Item& it, const Bytes& sig, const Bytes& pub, const Bytes& code,
                SigVersion sv, bool consult) {
         std::string key = tuple_key(pub, sig, code, sv);
-        auto f = it.cache.find(key);
-        if (f != it.cache.end()) {
-            if (f->second >= 0) return f->second != 0;  // known
-            if (consult) it.pending.push_back((uint32_t)(-2 - f->second));
+        if (int32_t* f = it.find(key)) {
+            if (*f >= 0) return *f != 0;                // known
+            if (consult) it.pending.push_back((uint32_t)(-2 - *f));
             return true;                                // deferred this round: speculate
         }
         // CPubKey filter, empty signature, lax-DER: decided on the host (no secp work)
@@ -137,7 +144,7 @@ public:
             reject = rz || sz;  // secp256k1_ecdsa_sig_verify rejects r == 0 || s == 0
         }
         if (reject) {
-            it.cache.emplace(std::move(key), 0);
+            it.cache.emplace_back(std::move(key), 0);
             host_rejected++;
             return false;
         }
@@ -173,7 +180,7 @@ public:
                 jobs.add_pre(scratch.data(), scratch.size(), row);
             // else: SIGHASH_SINGLE bug, msg stays ONE
         } else {
-            Bip143Job job;
+            Bip143Job& job = bip143;
             build_bip143_preimage(tx, nin, code, hashtype, it.in->amount, job);
             uint32_t pre = jobs.add_pre(job.preimage.data(), job.preimage.size(), row);
             size_t base = (size_t)jobs.pre_off[pre] * 64;
@@ -194,9 +201,9 @@ public:
                 jobs.patches.push_back(PatchRec{(uint32_t)(base + job.off[k]), (uint32_t)aux});
             }
         }
-        it.cache.emplace(key, -2 - (int32_t)pending.size());
+        it.cache.emplace_back(std::move(key), -2 - (int32_t)pending.size());
         if (consult) it.pending.push_back((uint32_t)pending.size());
-        pending.push_back(Pending{item_idx, std::move(key)});
+        pending.push_back(Pending{item_idx, (uint32_t)(it.cache.size() - 1)});
         return true;  // speculative
     }
 
@@ -229,9 +236,11 @@ int set_err(bitcoinconsensus_error* e, bitcoinconsensus_error v) {
 
 struct BatchState {
     std::vector<Item> st;
-    std::unordered_map<std::string, TxEntry> txs;  // parse each distinct tx buffer once
-    std::vector<std::pair<const bcc_batch_item*, TxEntry*>> fresh;  // parse order
-    unsigned parse_threads = 1;
+    // one entry per run of adjacent items with the same tx buffer (the inputs of one tx are
+    // passed together): each tx is deserialized once and its BIP143 hashes computed once; a
+    // buffer repeated non-adjacently is merely parsed again (same result)
+    std::vector<TxEntry> txs;
+    std::vector<uint32_t> tx_first;  // first item of each entry
     unsigned flags = 0;
 };
 
@@ -258,58 +267,43 @@ void run_threads(unsigned T, F f) {
     for (auto& x : th) x.join();
 }
 
-// verify_script's pre-checks (bitcoinconsensus.cpp:83-95) in reference order.  Distinct tx
-// buffers are deserialized once each, in parallel over T threads.
+// Contiguous [lo, hi) share t of T over n units.
+inline size_t share_lo(size_t n, unsigned t, unsigned T) { return n * t / T; }
+
+// verify_script's pre-checks (bitcoinconsensus.cpp:83-95) in reference order.  Tx buffers are
+// deserialized once per adjacent run of items, in parallel over T threads.
 void prepare(BatchState& b, const bcc_batch_item* items, size_t n, unsigned flags, unsigned T) {
-    b.st.assign(n, Item());
+    b.st.resize(n);
     b.flags = flags;
     auto& st = b.st;
-    auto& txs = b.txs;
     const bool flags_ok = (flags & ~(unsigned)FLAGS_VERIFY_ALL) == 0;
-    auto& fresh = b.fresh;
-    for (size_t i = 0; i < n; i++) {
-        Item& it = st[i];
-        it.in = &items[i];
-        if (!flags_ok) continue;
-        std::string tk((const char*)&items[i].tx_to, sizeof(void*));
-        tk.append((const char*)&items[i].tx_to_len, sizeof(unsigned));
-        auto f = txs.find(tk);
-        if (f == txs.end()) {
-            f = txs.emplace(tk, TxEntry()).first;
-            fresh.emplace_back(&items[i], &f->second);
-        }
-        it.tx = &f->second;
-    }
-    if (fresh.size() < 64) T = 1;
-    b.parse_threads = T;
+    b.tx_first.clear();
+    for (size_t i = 0; i < n; i++)
+        if (i == 0 || items[i].tx_to != items[i - 1].tx_to || items[i].tx_to_len != items[i - 1].tx_to_len)
+            b.tx_first.push_back((uint32_t)i);
+    const size_t E = b.tx_first.size();
+    b.txs.resize(E);
     run_threads(T, [&](unsigned t) {
-        for (size_t k = t; k < fresh.size(); k += T) {
-            const bcc_batch_item* in = fresh[k].first;
-            TxEntry* e = fresh[k].second;
-            e->ok = in->tx_to != nullptr && parse_tx(in->tx_to, in->tx_to_len, e->tx);
+        for (size_t k = share_lo(E, t, T); k < share_lo(E, t + 1, T); k++) {
+            const bcc_batch_item* in = &items[b.tx_first[k]];
+            TxEntry& e = b.txs[k];
+            e.ok = flags_ok && in->tx_to != nullptr && parse_tx(in->tx_to, in->tx_to_len, e.tx);
+            const size_t end = k + 1 < E ? b.tx_first[k + 1] : n;
+            for (size_t i = b.tx_first[k]; i < end; i++) {
+                Item& it = st[i];
+                it.in = &items[i];
+                it.tx = &e;
+                if (!flags_ok) it.err = bitcoinconsensus_ERR_INVALID_FLAGS;
+                else if (!e.ok) it.err = bitcoinconsensus_ERR_TX_DESERIALIZE;
+                else if (items[i].n_in >= e.tx.vin.size()) it.err = bitcoinconsensus_ERR_TX_INDEX;
+                else if (e.tx.ser_size != items[i].tx_to_len) it.err = bitcoinconsensus_ERR_TX_SIZE_MISMATCH;
+                else {
+                    it.err = bitcoinconsensus_ERR_OK;
+                    it.active = true;
+                }
+            }
         }
     });
-    for (size_t i = 0; i < n; i++) {
-        Item& it = st[i];
-        if (!flags_ok) {
-            it.err = bitcoinconsensus_ERR_INVALID_FLAGS;
-            continue;
-        }
-        if (!it.tx->ok) {
-            it.err = bitcoinconsensus_ERR_TX_DESERIALIZE;
-            continue;
-        }
-        if (items[i].n_in >= it.tx->tx.vin.size()) {
-            it.err = bitcoinconsensus_ERR_TX_INDEX;
-            continue;
-        }
-        if (it.tx->tx.ser_size != items[i].tx_to_len) {
-            it.err = bitcoinconsensus_ERR_TX_SIZE_MISMATCH;
-            continue;
-        }
-        it.err = bitcoinconsensus_ERR_OK;
-        it.active = true;
-    }
 }
 
 // Interpreter pass over the active items of one shard; deferred checks land in rd.  Returns
@@ -337,17 +331,19 @@ bool interpret_shard(BatchState& b, const std::vector<uint32_t>& idx, Round& rd)
     return any;
 }
 
-// Splits the items into T shards of whole transactions (items of one tx share its TxEntry, whose
-// BIP143 aux slots the shard's Round owns), balanced by item count.
+// Splits the items into T contiguous shards of whole transactions (items of one tx share its
+// TxEntry, whose BIP143 aux slots and legacy template the shard's Round owns), balanced by count.
 std::vector<std::vector<uint32_t>> make_shards(const BatchState& b, unsigned T) {
-    const size_t n = b.st.size();
+    const size_t n = b.st.size(), E = b.tx_first.size();
     std::vector<std::vector<uint32_t>> sh(T);
-    std::unordered_map<const TxEntry*, unsigned> owner;
-    for (size_t i = 0; i < n; i++) {
-        const TxEntry* e = b.st[i].tx;
-        unsigned t = (unsigned)(i * T / std::max<size_t>(n, 1));
-        if (e) t = owner.emplace(e, t).first->second;
-        sh[t].push_back((uint32_t)i);
+    size_t k = 0;
+    for (unsigned t = 0; t < T; t++) {
+        const size_t want = share_lo(n, t + 1, T);
+        size_t lo = k < E ? b.tx_first[k] : n;
+        while (k < E && (t + 1 == T || b.tx_first[k] < want)) k++;
+        size_t hi = k < E ? b.tx_first[k] : n;
+        sh[t].reserve(hi - lo);
+        for (size_t i = lo; i < hi; i++) sh[t].push_back((uint32_t)i);
     }
     return sh;
 }
@@ -373,8 +369,6 @@ long run_batch(const bcc_batch_item* items, size_t n, unsigned flags, int* ret_o
     const auto shards = make_shards(b, T);
     std::vector<Round> rds(T);
     std::vector<size_t> row0(T + 1, 0);
-    SighashJobs mjobs;
-    TupleRows mrows;
     std::vector<uint8_t> verdict;
     long status = 0;
     for (size_t round = 0;; round++) {
@@ -394,25 +388,22 @@ long run_batch(const bcc_batch_item* items, size_t n, unsigned flags, int* ret_o
         }
         row0[T] = npend;
         if (!any || npend == 0) break;
-        const SighashJobs* jobs = &rds[0].jobs;
-        const TupleRows* rows = &rds[0].rows;
-        if (T > 1) {  // one device batch for the whole round
-            auto m0 = clk::now();
-            mjobs.clear();
-            mrows.clear();
-            for (unsigned t = 0; t < T; t++) append_round(mjobs, mrows, rds[t].jobs, rds[t].rows);
-            jobs = &mjobs;
-            rows = &mrows;
-            t_stats.merge_seconds += since(m0);
+        // one device batch for the whole round: the shards' jobs are concatenated straight into
+        // the pinned staging image (DeviceBatch::stage_parts), no merged host copy
+        std::vector<const SighashJobs*> pj(T);
+        std::vector<const TupleRows*> pr(T);
+        for (unsigned t = 0; t < T; t++) {
+            pj[t] = &rds[t].jobs;
+            pr[t] = &rds[t].rows;
+            t_stats.preimages += rds[t].jobs.pre_off.size() + rds[t].jobs.tjobs.size();
+            t_stats.aux_messages += rds[t].jobs.aux_off.size();
         }
         t_stats.rounds++;
-        t_stats.tuples += rows->size();
-        t_stats.preimages += jobs->pre_off.size();
-        t_stats.aux_messages += jobs->aux_off.size();
+        t_stats.tuples += npend;
         auto g0 = clk::now();
-        verdict.assign(rows->size(), 0);
+        verdict.assign(npend, 0);
         double stage_s = 0;
-        int e = gpu_verify_batch(dev, *jobs, *rows, verdict.data(), &stage_s);
+        int e = gpu_verify_parts(dev, pj.data(), pr.data(), T, verdict.data(), &stage_s);
         t_stats.stage_seconds += stage_s;
         gpu_s += std::chrono::duration<double>(clk::now() - g0).count();
         if (e != 0) {
@@ -429,7 +420,7 @@ long run_batch(const bcc_batch_item* items, size_t n, unsigned flags, int* ret_o
             const Round& rd = rds[t];
             const uint8_t* v = verdict.data() + row0[t];
             for (size_t k = 0; k < rd.pending.size(); k++)
-                st[rd.pending[k].item].cache[rd.pending[k].key] = v[k] ? 1 : 0;
+                st[rd.pending[k].item].cache[rd.pending[k].slot].second = v[k] ? 1 : 0;
             for (uint32_t i : shards[t]) {
                 Item& it = st[i];
                 if (it.pending.empty()) continue;
@@ -458,8 +449,9 @@ long run_batch(const bcc_batch_item* items, size_t n, unsigned flags, int* ret_o
         }
         rds[t] = Round();
     });
-    run_threads(b.parse_threads, [&](unsigned t) {
-        for (size_t k = t; k < b.fresh.size(); k += b.parse_threads) b.fresh[k].second->tx = Tx();
+    run_threads(T, [&](unsigned t) {
+        const size_t E = b.txs.size();
+        for (size_t k = share_lo(E, t, T); k < share_lo(E, t + 1, T); k++) b.txs[k].tx = Tx();
     });
     host_s = std::chrono::duration<double>(clk::now() - t0).count() - gpu_s;
     t_stats.host_seconds = host_s;

@@ -2,7 +2,11 @@
 // algorithms (FIPS 180-4 SHA-256 / SHA-1, Dobbertin-Bosselaers-Preneel RIPEMD-160).
 #include "hashes.h"
 
+#include <cstdlib>
 #include <cstring>
+#if defined(__x86_64__)
+#include <immintrin.h>
+#endif
 
 namespace bcc {
 namespace host {
@@ -28,7 +32,7 @@ const uint32_t K256[64] = {
     0x19a4c116, 0x1e376c08, 0x2748774c, 0x34b0bcb5, 0x391c0cb3, 0x4ed8aa4a, 0x5b9cca4f, 0x682e6ff3,
     0x748f82ee, 0x78a5636f, 0x84c87814, 0x8cc70208, 0x90befffa, 0xa4506ceb, 0xbef9a3f7, 0xc67178f2};
 
-void sha256_block(uint32_t s[8], const uint8_t* blk) {
+void sha256_block_portable(uint32_t s[8], const uint8_t* blk) {
     uint32_t w[64];
     for (int i = 0; i < 16; i++) w[i] = be32(blk + 4 * i);
     for (int i = 16; i < 64; i++) {
@@ -45,7 +49,58 @@ void sha256_block(uint32_t s[8], const uint8_t* blk) {
     s[0] += a; s[1] += b; s[2] += c; s[3] += d; s[4] += e; s[5] += f; s[6] += g; s[7] += h;
 }
 
+#if defined(__x86_64__)
+// The same compression with the x86 SHA extensions (sha256rnds2 / sha256msg1 / sha256msg2),
+// selected at run time when the host CPU has them.  State in the ABEF / CDGH register layout
+// the instructions use; message words scheduled four at a time.
+__attribute__((target("sha,sse4.1"))) void sha256_block_shani(uint32_t s[8], const uint8_t* blk) {
+    const __m128i BSWAP = _mm_set_epi64x(0x0c0d0e0f08090a0bULL, 0x0405060700010203ULL);
+    __m128i tmp = _mm_loadu_si128((const __m128i*)&s[0]);
+    __m128i st1 = _mm_loadu_si128((const __m128i*)&s[4]);
+    tmp = _mm_shuffle_epi32(tmp, 0xB1);              // CDAB
+    st1 = _mm_shuffle_epi32(st1, 0x1B);              // EFGH
+    __m128i st0 = _mm_alignr_epi8(tmp, st1, 8);      // ABEF
+    st1 = _mm_blend_epi16(st1, tmp, 0xF0);           // CDGH
+    const __m128i save0 = st0, save1 = st1;
+    __m128i w[4];
+    for (int g = 0; g < 16; g++) {
+        if (g < 4) {
+            w[g] = _mm_shuffle_epi8(_mm_loadu_si128((const __m128i*)(blk + 16 * g)), BSWAP);
+        } else {
+            __m128i t = _mm_sha256msg1_epu32(w[(g - 4) & 3], w[(g - 3) & 3]);
+            t = _mm_add_epi32(t, _mm_alignr_epi8(w[(g - 1) & 3], w[(g - 2) & 3], 4));
+            w[g & 3] = _mm_sha256msg2_epu32(t, w[(g - 1) & 3]);
+        }
+        __m128i m = _mm_add_epi32(w[g & 3], _mm_loadu_si128((const __m128i*)&K256[4 * g]));
+        st1 = _mm_sha256rnds2_epu32(st1, st0, m);
+        m = _mm_shuffle_epi32(m, 0x0E);
+        st0 = _mm_sha256rnds2_epu32(st0, st1, m);
+    }
+    st0 = _mm_add_epi32(st0, save0);
+    st1 = _mm_add_epi32(st1, save1);
+    tmp = _mm_shuffle_epi32(st0, 0x1B);              // FEBA
+    st1 = _mm_shuffle_epi32(st1, 0xB1);              // DCHG
+    st0 = _mm_blend_epi16(tmp, st1, 0xF0);           // DCBA
+    st1 = _mm_alignr_epi8(st1, tmp, 8);              // HGFE
+    _mm_storeu_si128((__m128i*)&s[0], st0);
+    _mm_storeu_si128((__m128i*)&s[4], st1);
+}
+#endif
+
+using BlockFn = void (*)(uint32_t*, const uint8_t*);
+BlockFn pick_sha256_block() {
+#if defined(__x86_64__)
+    __builtin_cpu_init();
+    if (__builtin_cpu_supports("sha") && __builtin_cpu_supports("sse4.1") && !getenv("BCC_NO_SHANI"))
+        return sha256_block_shani;
+#endif
+    return sha256_block_portable;
+}
+const BlockFn sha256_block = pick_sha256_block();
+
 }  // namespace
+
+bool sha256_uses_shani() { return sha256_block != sha256_block_portable; }
 
 Sha256::Sha256() : bytes(0) {
     static const uint32_t iv[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a,
@@ -170,40 +225,43 @@ inline uint32_t rf(int j, uint32_t x, uint32_t y, uint32_t z) {
         default: return x ^ (y | ~z);
     }
 }
+
+// One compression; fully unrolled so every selector, index and rotation is a constant.
+void ripemd160_block(uint32_t h[5], const uint8_t* blk) {
+    uint32_t X[16];
+    for (int i = 0; i < 16; i++) X[i] = le32(blk + 4 * i);
+    uint32_t al = h[0], bl = h[1], cl = h[2], dl = h[3], el = h[4];
+    uint32_t ar = h[0], br = h[1], cr = h[2], dr = h[3], er = h[4];
+#pragma GCC unroll 80
+    for (int j = 0; j < 80; j++) {
+        uint32_t t = rotl(al + rf(j, bl, cl, dl) + X[RL[j]] + KL[j / 16], SL[j]) + el;
+        al = el; el = dl; dl = rotl(cl, 10); cl = bl; bl = t;
+        t = rotl(ar + rf(79 - j, br, cr, dr) + X[RR[j]] + KR[j / 16], SR[j]) + er;
+        ar = er; er = dr; dr = rotl(cr, 10); cr = br; br = t;
+    }
+    uint32_t t = h[1] + cl + dr;
+    h[1] = h[2] + dl + er;
+    h[2] = h[3] + el + ar;
+    h[3] = h[4] + al + br;
+    h[4] = h[0] + bl + cr;
+    h[0] = t;
+}
 }  // namespace
 
 void ripemd160(const uint8_t* p, size_t n, uint8_t out[20]) {
     uint32_t h[5] = {0x67452301, 0xEFCDAB89, 0x98BADCFE, 0x10325476, 0xC3D2E1F0};
-    uint64_t bits = (uint64_t)n * 8;
-    size_t total = ((n + 8) / 64 + 1) * 64;
-    for (size_t off = 0; off < total; off += 64) {
-        uint8_t blk[64];
-        for (int i = 0; i < 64; i++) {
-            size_t k = off + i;
-            uint8_t v;
-            if (k < n) v = p[k];
-            else if (k == n) v = 0x80;
-            else if (k >= total - 8) v = (uint8_t)(bits >> (8 * (k - (total - 8))));  // little-endian
-            else v = 0;
-            blk[i] = v;
-        }
-        uint32_t X[16];
-        for (int i = 0; i < 16; i++) X[i] = le32(blk + 4 * i);
-        uint32_t al = h[0], bl = h[1], cl = h[2], dl = h[3], el = h[4];
-        uint32_t ar = h[0], br = h[1], cr = h[2], dr = h[3], er = h[4];
-        for (int j = 0; j < 80; j++) {
-            uint32_t t = rotl(al + rf(j, bl, cl, dl) + X[RL[j]] + KL[j / 16], SL[j]) + el;
-            al = el; el = dl; dl = rotl(cl, 10); cl = bl; bl = t;
-            t = rotl(ar + rf(79 - j, br, cr, dr) + X[RR[j]] + KR[j / 16], SR[j]) + er;
-            ar = er; er = dr; dr = rotl(cr, 10); cr = br; br = t;
-        }
-        uint32_t t = h[1] + cl + dr;
-        h[1] = h[2] + dl + er;
-        h[2] = h[3] + el + ar;
-        h[3] = h[4] + al + br;
-        h[4] = h[0] + bl + cr;
-        h[0] = t;
-    }
+    size_t full = n / 64;
+    for (size_t b = 0; b < full; b++) ripemd160_block(h, p + 64 * b);
+    // tail + padding (one or two blocks), length little-endian
+    uint8_t tail[128];
+    const size_t rem = n - 64 * full, tl = rem < 56 ? 64 : 128;
+    memset(tail, 0, tl);
+    if (rem) memcpy(tail, p + 64 * full, rem);
+    tail[rem] = 0x80;
+    const uint64_t bits = (uint64_t)n * 8;
+    for (int i = 0; i < 8; i++) tail[tl - 8 + i] = (uint8_t)(bits >> (8 * i));
+    ripemd160_block(h, tail);
+    if (tl == 128) ripemd160_block(h, tail + 64);
     for (int i = 0; i < 5; i++) {
         out[4 * i] = (uint8_t)h[i];
         out[4 * i + 1] = (uint8_t)(h[i] >> 8);

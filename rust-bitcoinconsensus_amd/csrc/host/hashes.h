@@ -22,6 +22,7 @@ void sha256(const uint8_t* p, size_t n, uint8_t out[32]);
 void sha256d(const uint8_t* p, size_t n, uint8_t out[32]);              // CHash256
 void sha1(const uint8_t* p, size_t n, uint8_t out[20]);
 void ripemd160(const uint8_t* p, size_t n, uint8_t out[20]);
+bool sha256_uses_shani();                                                 // x86 SHA extensions in use
 void hash160(const uint8_t* p, size_t n, uint8_t out[20]);              // RIPEMD160(SHA256(x))
 
 }  // namespace host

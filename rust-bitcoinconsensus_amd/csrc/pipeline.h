@@ -147,6 +147,8 @@ public:
     explicit DeviceBatch(int device);
     ~DeviceBatch();
     int stage(const SighashJobs& jobs, const TupleRows& rows);
+    // the concatenation of P parts (row / message / job indices fixed up per part)
+    int stage_parts(const SighashJobs* const* jobs, const TupleRows* const* rows, size_t P);
     int run(void* stream);                       // K1..K4
     int run_sighash(void* stream);               // K1..K3 only
     int run_ecdsa(void* stream);                 // K4 only
@@ -174,6 +176,8 @@ private:
     SigScratch scratch_;
     void* arena_ = nullptr;
     size_t cap_ = 0;
+    void* host_image_ = nullptr;  // pinned host image of the arena (staging)
+    size_t host_cap_ = 0;
     size_t n_rows_ = 0, n_pre_ = 0, n_aux_ = 0, n_patch_ = 0, pre_blocks_ = 0, aux_blocks_ = 0;
     uint8_t *d_aux_ = nullptr, *d_pre_ = nullptr, *d_auxd_ = nullptr;
     uint32_t *d_aux_off_ = nullptr, *d_aux_nblk_ = nullptr, *d_pre_off_ = nullptr,
@@ -188,5 +192,8 @@ private:
 // *stage_seconds (optional) receives the host -> HBM staging time.
 int gpu_verify_batch(int device, const SighashJobs& jobs, const TupleRows& rows, uint8_t* verdict,
                      double* stage_seconds = nullptr);
+// The same over the concatenation of `parts` (jobs[p], rows[p]) pairs: verdict rows in order.
+int gpu_verify_parts(int device, const SighashJobs* const* jobs, const TupleRows* const* rows,
+                     size_t parts, uint8_t* verdict, double* stage_seconds = nullptr);
 
 }  // namespace bcc

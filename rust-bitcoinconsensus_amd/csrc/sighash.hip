@@ -6,6 +6,9 @@
 // bench.py as the algorithmic bytes (message bytes in + 32 B out per message).
 #include <chrono>
 #include <memory>
+#include <thread>
+#include <vector>
+#include <cstring>
 
 #include "gpu_common.h"
 #include "pipeline.h"
@@ -193,6 +196,7 @@ DeviceBatch::~DeviceBatch() {
     if (ev_fork_) (void)hipEventDestroy((hipEvent_t)ev_fork_);
     if (ev_join_) (void)hipEventDestroy((hipEvent_t)ev_join_);
     if (arena_) (void)hipFree(arena_);
+    if (host_image_) (void)hipHostFree(host_image_);
 }
 
 void* DeviceBatch::pick(void* stream) {
@@ -217,25 +221,52 @@ int DeviceBatch::sync() {
 static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 int DeviceBatch::stage(const SighashJobs& j, const TupleRows& rows) {
-    if (int e = sync()) return e;  // the previous run may still read the arena
-    n_rows_ = rows.size();
-    n_pre_ = j.pre_off.size();
-    n_aux_ = j.aux_off.size();
-    n_patch_ = j.patches.size();
-    pre_blocks_ = j.pre.size() / 64;
-    aux_blocks_ = j.aux.size() / 64;
-    n_tjob_ = j.tjobs.size();
-    tjob_blocks_ = 0;
-    for (const auto& t : j.tjobs) tjob_blocks_ += t.nblk;
+    const SighashJobs* jp = &j;
+    const TupleRows* rp = &rows;
+    return stage_parts(&jp, &rp, 1);
+}
+
+// The parts (one per host interpreter thread) are concatenated in order straight into a pinned
+// host image of the device arena, each part by its own thread with its index fix-ups (the
+// append_round rules), then the image goes to HBM in one DMA copy: no merged host copy of the
+// jobs and no pageable-memory staging.
+int DeviceBatch::stage_parts(const SighashJobs* const* J, const TupleRows* const* Rw, size_t P) {
+    if (int e = sync()) return e;  // the previous run may still read the arena / the image
+    std::vector<size_t> row0(P + 1, 0), auxb0(P + 1, 0), preb0(P + 1, 0), auxi0(P + 1, 0),
+        prei0(P + 1, 0), pat0(P + 1, 0), tpl0(P + 1, 0), code0(P + 1, 0), tj0(P + 1, 0);
+    size_t tjblk = 0;
+    for (size_t p = 0; p < P; p++) {
+        row0[p + 1] = row0[p] + Rw[p]->size();
+        auxb0[p + 1] = auxb0[p] + J[p]->aux.size();
+        preb0[p + 1] = preb0[p] + J[p]->pre.size();
+        auxi0[p + 1] = auxi0[p] + J[p]->aux_off.size();
+        prei0[p + 1] = prei0[p] + J[p]->pre_off.size();
+        pat0[p + 1] = pat0[p] + J[p]->patches.size();
+        tpl0[p + 1] = tpl0[p] + J[p]->tpl.size();
+        code0[p + 1] = code0[p] + J[p]->code.size();
+        tj0[p + 1] = tj0[p] + J[p]->tjobs.size();
+        for (const auto& t : J[p]->tjobs) tjblk += t.nblk;
+    }
+    n_rows_ = row0[P];
+    n_pre_ = prei0[P];
+    n_aux_ = auxi0[P];
+    n_patch_ = pat0[P];
+    pre_blocks_ = preb0[P] / 64;
+    aux_blocks_ = auxb0[P] / 64;
+    n_tjob_ = tj0[P];
+    tjob_blocks_ = tjblk;
     const size_t R = n_rows_;
     size_t sizes[] = {R,         32 * R,           32 * R,         32 * R,        32 * R,
-                      32 * R,    R,                j.aux.size(),   j.pre.size(),  32 * n_aux_,
+                      32 * R,    R,                auxb0[P],       preb0[P],      32 * n_aux_,
                       4 * n_aux_, 4 * n_aux_,      4 * n_pre_,     4 * n_pre_,    4 * n_pre_,
-                      sizeof(PatchRec) * n_patch_, j.tpl.size(),   j.code.size(),
+                      sizeof(PatchRec) * n_patch_, tpl0[P],        code0[P],
                       sizeof(TplJob) * n_tjob_};
     const int NB = sizeof(sizes) / sizeof(sizes[0]);
-    size_t total = 0;
-    for (int i = 0; i < NB; i++) total += align256(sizes[i]);
+    size_t off[NB], total = 0;
+    for (int i = 0; i < NB; i++) {
+        off[i] = total;
+        total += align256(sizes[i]);
+    }
     if (total > cap_) {
         if (arena_) BCC_HIP_TRY(hipFree(arena_));
         arena_ = nullptr;
@@ -243,25 +274,71 @@ int DeviceBatch::stage(const SighashJobs& j, const TupleRows& rows) {
         BCC_HIP_TRY(hipMalloc(&arena_, total));
         cap_ = total;
     }
-    uint8_t* p = (uint8_t*)arena_;
-    uint8_t* ptr[NB];
-    for (int i = 0; i < NB; i++) {
-        ptr[i] = p;
-        p += align256(sizes[i]);
+    if (total > host_cap_) {
+        if (host_image_) BCC_HIP_TRY(hipHostFree(host_image_));
+        host_image_ = nullptr;
+        host_cap_ = 0;
+        BCC_HIP_TRY(hipHostMalloc(&host_image_, total, hipHostMallocDefault));
+        host_cap_ = total;
     }
-    d_tag = ptr[0]; d_x = ptr[1]; d_y = ptr[2]; d_r = ptr[3]; d_s = ptr[4]; d_m = ptr[5];
-    d_v = ptr[6]; d_aux_ = ptr[7]; d_pre_ = ptr[8]; d_auxd_ = ptr[9];
-    d_aux_off_ = (uint32_t*)ptr[10]; d_aux_nblk_ = (uint32_t*)ptr[11];
-    d_pre_off_ = (uint32_t*)ptr[12]; d_pre_nblk_ = (uint32_t*)ptr[13];
-    d_pre_row_ = (uint32_t*)ptr[14]; d_patch_ = (PatchRec*)ptr[15];
-    d_tpl_ = ptr[16]; d_code_ = ptr[17]; d_tjob_ = (TplJob*)ptr[18];
-    const void* src[] = {rows.tag.data(), rows.x.data(), rows.y.data(), rows.r.data(),
-                         rows.s.data(), rows.msg.data(), nullptr, j.aux.data(), j.pre.data(),
-                         nullptr, j.aux_off.data(), j.aux_nblk.data(), j.pre_off.data(),
-                         j.pre_nblk.data(), j.pre_row.data(), j.patches.data(), j.tpl.data(),
-                         j.code.data(), j.tjobs.data()};
-    for (int i = 0; i < NB; i++)
-        if (src[i] && sizes[i]) BCC_HIP_TRY(hipMemcpy(ptr[i], src[i], sizes[i], hipMemcpyHostToDevice));
+    uint8_t* a = (uint8_t*)arena_;
+    d_tag = a + off[0]; d_x = a + off[1]; d_y = a + off[2]; d_r = a + off[3]; d_s = a + off[4];
+    d_m = a + off[5]; d_v = a + off[6]; d_aux_ = a + off[7]; d_pre_ = a + off[8]; d_auxd_ = a + off[9];
+    d_aux_off_ = (uint32_t*)(a + off[10]); d_aux_nblk_ = (uint32_t*)(a + off[11]);
+    d_pre_off_ = (uint32_t*)(a + off[12]); d_pre_nblk_ = (uint32_t*)(a + off[13]);
+    d_pre_row_ = (uint32_t*)(a + off[14]); d_patch_ = (PatchRec*)(a + off[15]);
+    d_tpl_ = a + off[16]; d_code_ = a + off[17]; d_tjob_ = (TplJob*)(a + off[18]);
+    uint8_t* h = (uint8_t*)host_image_;
+    auto fill = [&](size_t p) {
+        const SighashJobs& j = *J[p];
+        const TupleRows& rw = *Rw[p];
+        const size_t nr = rw.size(), r0 = row0[p];
+        auto cp = [&](int b, size_t at, const void* src, size_t len) {
+            if (len) memcpy(h + off[b] + at, src, len);
+        };
+        cp(0, r0, rw.tag.data(), nr);
+        cp(1, 32 * r0, rw.x.data(), 32 * nr);
+        cp(2, 32 * r0, rw.y.data(), 32 * nr);
+        cp(3, 32 * r0, rw.r.data(), 32 * nr);
+        cp(4, 32 * r0, rw.s.data(), 32 * nr);
+        cp(5, 32 * r0, rw.msg.data(), 32 * nr);
+        cp(7, auxb0[p], j.aux.data(), j.aux.size());
+        cp(8, preb0[p], j.pre.data(), j.pre.size());
+        const uint32_t ablk = (uint32_t)(auxb0[p] / 64), pblk = (uint32_t)(preb0[p] / 64);
+        uint32_t* ao = (uint32_t*)(h + off[10]) + auxi0[p];
+        for (size_t k = 0; k < j.aux_off.size(); k++) ao[k] = j.aux_off[k] + ablk;
+        cp(11, 4 * auxi0[p], j.aux_nblk.data(), 4 * j.aux_nblk.size());
+        uint32_t* po = (uint32_t*)(h + off[12]) + prei0[p];
+        uint32_t* pr = (uint32_t*)(h + off[14]) + prei0[p];
+        for (size_t k = 0; k < j.pre_off.size(); k++) {
+            po[k] = j.pre_off[k] + pblk;
+            pr[k] = j.pre_row[k] + (uint32_t)r0;
+        }
+        cp(13, 4 * prei0[p], j.pre_nblk.data(), 4 * j.pre_nblk.size());
+        PatchRec* pt = (PatchRec*)(h + off[15]) + pat0[p];
+        for (size_t k = 0; k < j.patches.size(); k++)
+            pt[k] = PatchRec{j.patches[k].pre_byte + pblk * 64, j.patches[k].aux + (uint32_t)auxi0[p]};
+        cp(16, tpl0[p], j.tpl.data(), j.tpl.size());
+        cp(17, code0[p], j.code.data(), j.code.size());
+        TplJob* tj = (TplJob*)(h + off[18]) + tj0[p];
+        for (size_t k = 0; k < j.tjobs.size(); k++) {
+            TplJob t = j.tjobs[k];
+            t.tpl_off += (uint32_t)tpl0[p];
+            t.code_off += (uint32_t)code0[p];
+            t.row += (uint32_t)r0;
+            tj[k] = t;
+        }
+    };
+    if (P == 1 || total < ((size_t)1 << 20)) {
+        for (size_t p = 0; p < P; p++) fill(p);
+    } else {
+        std::vector<std::thread> th;
+        for (size_t p = 1; p < P; p++) th.emplace_back(fill, p);
+        fill(0);
+        for (auto& x : th) x.join();
+    }
+    BCC_HIP_TRY(hipSetDevice(dev_));
+    BCC_HIP_TRY(hipMemcpy(arena_, host_image_, total, hipMemcpyHostToDevice));
     return 0;
 }
 
@@ -341,16 +418,25 @@ int DeviceBatch::fetch_msgs(uint8_t* out) {
 
 int gpu_verify_batch(int device, const SighashJobs& jobs, const TupleRows& rows, uint8_t* verdict,
                      double* stage_seconds) {
-    if (rows.size() == 0) return 0;
-    // one cached batch per (thread, device): repeated calls reuse the device arena, scratch and
-    // stream, and concurrent callers never share any of them
+    const SighashJobs* jp = &jobs;
+    const TupleRows* rp = &rows;
+    return gpu_verify_parts(device, &jp, &rp, 1, verdict, stage_seconds);
+}
+
+int gpu_verify_parts(int device, const SighashJobs* const* jobs, const TupleRows* const* rows,
+                     size_t parts, uint8_t* verdict, double* stage_seconds) {
+    size_t n = 0;
+    for (size_t p = 0; p < parts; p++) n += rows[p]->size();
+    if (n == 0) return 0;
+    // one cached batch per (thread, device): repeated calls reuse the device arena, the pinned
+    // host image, scratch and streams, and concurrent callers never share any of them
     thread_local std::vector<std::unique_ptr<DeviceBatch>> cache;
     if (device < 0) return (int)hipErrorInvalidDevice;
     if ((int)cache.size() <= device) cache.resize(device + 1);
     if (!cache[device]) cache[device] = std::make_unique<DeviceBatch>(device);
     DeviceBatch& b = *cache[device];
     auto t0 = std::chrono::steady_clock::now();
-    if (int e = b.stage(jobs, rows)) return e;
+    if (int e = b.stage_parts(jobs, rows, parts)) return e;
     if (stage_seconds)
         *stage_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     if (int e = b.run(nullptr)) return e;

@@ -19,6 +19,17 @@ static size_t unpadded_len(const uint8_t* m, size_t padded) {
     return (size_t)(bits / 8);
 }
 
+int gpu_verify_batch(int, const SighashJobs& j, const TupleRows& rows, uint8_t* verdict, double*);
+int gpu_verify_parts(int dev, const SighashJobs* const* jobs, const TupleRows* const* rows, size_t parts,
+                     uint8_t* verdict, double*) {
+    size_t r0 = 0;
+    for (size_t p = 0; p < parts; p++) {
+        gpu_verify_batch(dev, *jobs[p], *rows[p], verdict + r0, nullptr);
+        r0 += rows[p]->size();
+    }
+    return 0;
+}
+
 int gpu_verify_batch(int, const SighashJobs& j, const TupleRows& rows, uint8_t* verdict, double*) {
     std::vector<uint8_t> auxd(32 * j.aux_off.size());
     for (size_t a = 0; a < j.aux_off.size(); a++) {

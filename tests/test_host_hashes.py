@@ -1,0 +1,78 @@
+"""CPU: the engine's host hash functions (csrc/host/hashes.cpp: SHA-256 portable and x86
+SHA-extension paths, SHA-1, RIPEMD-160, HASH160) against hashlib and the published RIPEMD-160
+test vectors, across message lengths that exercise every padding case."""
+import ctypes
+import hashlib
+import os
+import random
+import subprocess
+import sys
+
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+SO = os.path.join(HERE, "native", "_build", "hash_test.so")
+SRC = [os.path.join(HERE, "native", "hash_test.cpp"),
+       os.path.join(ROOT, "rust-bitcoinconsensus_amd", "csrc", "host", "hashes.cpp")]
+
+# Dobbertin-Bosselaers-Preneel, "RIPEMD-160: A Strengthened Version of RIPEMD", test vectors
+RIPEMD_VECTORS = [
+    (b"", "9c1185a5c5e9fc54612808977ee8f548b2258d31"),
+    (b"a", "0bdc9d2d256b3ee9daae347be6f4dc835a467ffe"),
+    (b"abc", "8eb208f7e05d987a9b044a8e98c6b087f15a0bfc"),
+    (b"message digest", "5d0689ef49d2fae572b881b123a85ffa21595f36"),
+    (b"abcdefghijklmnopqrstuvwxyz", "f71c27109c692c1b56bbdceb5b9d2865b3708dbc"),
+    (b"abcdbcdecdefdefgefghfghighijhijkijkljklmklmnlmnomnopnopq",
+     "12a053384a9c0c88e405a06c27dcf49ada62eb2b"),
+    (b"ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789",
+     "b0e20b6e3116640286ed3a87a5713079b21f5189"),
+    (b"1234567890" * 8, "9b752e45573d4b39f4dbd3323cab82bf63326bfb"),
+]
+
+
+@pytest.fixture(scope="module")
+def so():
+    if not os.path.exists(SO) or any(os.path.getmtime(s) > os.path.getmtime(SO) for s in SRC):
+        os.makedirs(os.path.dirname(SO), exist_ok=True)
+        subprocess.check_call(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-o", SO] + SRC)
+    return SO
+
+
+def _check(so_path):
+    L = ctypes.CDLL(so_path)
+    rng = random.Random(11)
+    out = ctypes.create_string_buffer(32)
+    for n in list(range(0, 200)) + [255, 256, 257, 1000, 4096, 10007]:
+        m = bytes(rng.getrandbits(8) for _ in range(n))
+        L.th_sha256(m, n, out)
+        assert out.raw == hashlib.sha256(m).digest(), n
+        L.th_sha1(m, n, out)
+        assert out.raw[:20] == hashlib.sha1(m).digest(), n
+    for m, h in RIPEMD_VECTORS:
+        L.th_ripemd160(m, len(m), out)
+        assert out.raw[:20].hex() == h, m
+    try:
+        hashlib.new("ripemd160")
+    except ValueError:
+        return L.th_shani()
+    for n in (0, 1, 33, 55, 56, 63, 64, 65, 119, 120, 128, 500):
+        m = bytes(rng.getrandbits(8) for _ in range(n))
+        L.th_ripemd160(m, n, out)
+        assert out.raw[:20] == hashlib.new("ripemd160", m).digest(), n
+        L.th_hash160(m, n, out)
+        assert out.raw[:20] == hashlib.new("ripemd160", hashlib.sha256(m).digest()).digest(), n
+    return L.th_shani()
+
+
+def test_host_hashes_default_path(so):
+    _check(so)
+
+
+def test_host_sha256_portable_path(so):
+    """The portable SHA-256 compression (forced with BCC_NO_SHANI) in a fresh process."""
+    code = f"import sys; sys.path.insert(0, {HERE!r}); import test_host_hashes as t; print(t._check({so!r}))"
+    env = dict(os.environ, BCC_NO_SHANI="1")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.strip() == "0"

@@ -1,0 +1,83 @@
+// Dev tool: profile the HOST half of bitcoinconsensus_verify_batch (deserialize, pre-checks,
+// interpreter, sighash job building) on N synthetic P2WPKH spends, with the device pipeline
+// replaced by a stub that answers "valid" for every deferred check.  Not part of the library.
+//   g++ -O2 -pg ... (see tools/host_prof/run.sh)
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "../../include/bitcoinconsensus.h"
+#include "../../rust-bitcoinconsensus_amd/csrc/host/hashes.h"
+#include "../../rust-bitcoinconsensus_amd/csrc/pipeline.h"
+
+namespace bcc {
+int gpu_verify_batch(int, const SighashJobs&, const TupleRows& rows, uint8_t* verdict, double*) {
+    memset(verdict, 1, rows.size());
+    return 0;
+}
+int gpu_verify_parts(int, const SighashJobs* const*, const TupleRows* const* rows, size_t parts,
+                     uint8_t* verdict, double*) {
+    size_t n = 0;
+    for (size_t p = 0; p < parts; p++) n += rows[p]->size();
+    memset(verdict, 1, n);
+    return 0;
+}
+}  // namespace bcc
+
+static void le(std::vector<uint8_t>& o, uint64_t v, int k) {
+    for (int i = 0; i < k; i++) o.push_back((uint8_t)(v >> (8 * i)));
+}
+
+int main(int argc, char** argv) {
+    size_t n = argc > 1 ? (size_t)atol(argv[1]) : 200000;
+    std::vector<std::vector<uint8_t>> txs(n), spks(n);
+    for (size_t i = 0; i < n; i++) {
+        uint8_t pub[33], h[20], sig[72];
+        pub[0] = 2;
+        for (int k = 1; k < 33; k++) pub[k] = (uint8_t)(i * 131 + k * 7);
+        bcc::host::hash160(pub, 33, h);
+        spks[i] = {0x00, 0x14};
+        spks[i].insert(spks[i].end(), h, h + 20);
+        // strict-DER (r, s) of 32 bytes each, + SIGHASH_ALL
+        sig[0] = 0x30; sig[1] = 68; sig[2] = 0x02; sig[3] = 32;
+        for (int k = 0; k < 32; k++) sig[4 + k] = (uint8_t)(0x11 + i + k);
+        sig[4] &= 0x7f;
+        sig[36] = 0x02; sig[37] = 32;
+        for (int k = 0; k < 32; k++) sig[38 + k] = (uint8_t)(0x22 + i * 3 + k);
+        sig[38] &= 0x7f;
+        sig[70] = 0x01;
+        auto& t = txs[i];
+        le(t, 2, 4);
+        t.push_back(0); t.push_back(1);
+        t.push_back(1);
+        for (int k = 0; k < 32; k++) t.push_back((uint8_t)(i >> (k % 8)));
+        le(t, 0, 4);
+        t.push_back(0);
+        le(t, 0xffffffffu, 4);
+        t.push_back(1);
+        le(t, 1000 + i, 8);
+        t.push_back(22); t.push_back(0); t.push_back(0x14);
+        for (int k = 0; k < 20; k++) t.push_back((uint8_t)k);
+        t.push_back(2);
+        t.push_back(71);
+        t.insert(t.end(), sig, sig + 71);
+        t.push_back(33);
+        t.insert(t.end(), pub, pub + 33);
+        le(t, 0, 4);
+    }
+    std::vector<bcc_batch_item> items(n);
+    for (size_t i = 0; i < n; i++)
+        items[i] = bcc_batch_item{spks[i].data(), (unsigned)spks[i].size(), (int64_t)(5000 + i),
+                                  txs[i].data(), (unsigned)txs[i].size(), 0};
+    std::vector<int> ret(n);
+    std::vector<bitcoinconsensus_error> err(n);
+    for (int rep = 0; rep < 3; rep++) {
+        auto t0 = std::chrono::steady_clock::now();
+        long v = bitcoinconsensus_verify_batch(items.data(), n, 0xE15, ret.data(), err.data());
+        double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        printf("n %zu valid %ld  %.1f ms  %.2f M items/s\n", n, v, 1e3 * s, n / s / 1e6);
+    }
+    return 0;
+}
