@@ -60,15 +60,14 @@ struct Item {
     bool active = false;  // needs (another) interpreter run
     bool result = false;
     // checks seen by this item's runs: tuple key -> 0/1 known verdict, or -2 - r: deferred as
-    // row r of the current round.  A flat list: an input makes a handful of checks, so a linear
-    // scan beats a hash map and costs no bucket allocation per item.
-    std::vector<std::pair<std::string, int32_t>> cache;
+    // row r of the current round.  A flat list (an input makes a handful of checks, so a linear
+    // scan beats a hash map); the key bytes live in the item's shard's key arena (Round::keys).
+    struct Check {
+        uint32_t off, len;
+        int32_t v;
+    };
+    std::vector<Check> cache;
     std::vector<uint32_t> pending;  // deferred rows the last run consulted (answered "true")
-    int32_t* find(const std::string& k) {
-        for (auto& e : cache)
-            if (e.first == k) return &e.second;
-        return nullptr;
-    }
 };
 
 struct Pending {
@@ -76,19 +75,21 @@ struct Pending {
     uint32_t slot;  // index of the check in the item's cache
 };
 
-std::string tuple_key(const Bytes& pub, const Bytes& sig, const Bytes& code, SigVersion sv) {
-    std::string k;
-    k.reserve(pub.size() + sig.size() + code.size() + 16);
+// Appends the identity of a signature check (sigversion, pubkey, signature, scriptCode) to the
+// key arena; returns its length.
+uint32_t append_key(std::vector<uint8_t>& a, const Bytes& pub, const Bytes& sig, const Bytes& code,
+                    SigVersion sv) {
+    const size_t k0 = a.size();
     auto put = [&](const Bytes& b) {
         uint32_t n = (uint32_t)b.size();
-        k.append((const char*)&n, 4);
-        k.append((const char*)b.data(), b.size());
+        a.insert(a.end(), (const uint8_t*)&n, (const uint8_t*)&n + 4);
+        a.insert(a.end(), b.begin(), b.end());
     };
-    k.push_back((char)sv);
+    a.push_back((uint8_t)sv);
     put(pub);
     put(sig);
     put(code);
-    return k;
+    return (uint32_t)(a.size() - k0);
 }
 
 class Round;
@@ -115,6 +116,7 @@ public:
     TupleRows rows;
     std::vector<Pending> pending;
     std::vector<uint8_t> scratch;
+    std::vector<uint8_t> keys;  // check identities of this shard's items (whole call, all rounds)
     Bip143Job bip143;
     std::vector<TxEntry*> touched;
     size_t host_rejected = 0;
@@ -125,10 +127,13 @@ public:
     // without making the item's finality depend on it.
     bool defer(uint32_t item_idx, Item& it, const Bytes& sig, const Bytes& pub, const Bytes& code,
                SigVersion sv, bool consult) {
-        std::string key = tuple_key(pub, sig, code, sv);
-        if (int32_t* f = it.find(key)) {
-            if (*f >= 0) return *f != 0;                // known
-            if (consult) it.pending.push_back((uint32_t)(-2 - *f));
+        const uint32_t koff = (uint32_t)keys.size();
+        const uint32_t klen = append_key(keys, pub, sig, code, sv);
+        for (const Item::Check& c : it.cache) {
+            if (c.len != klen || memcmp(&keys[c.off], &keys[koff], klen) != 0) continue;
+            keys.resize(koff);                          // seen before: drop the copy
+            if (c.v >= 0) return c.v != 0;              // known
+            if (consult) it.pending.push_back((uint32_t)(-2 - c.v));
             return true;                                // deferred this round: speculate
         }
         // CPubKey filter, empty signature, lax-DER: decided on the host (no secp work)
@@ -144,7 +149,7 @@ public:
             reject = rz || sz;  // secp256k1_ecdsa_sig_verify rejects r == 0 || s == 0
         }
         if (reject) {
-            it.cache.emplace_back(std::move(key), 0);
+            it.cache.push_back(Item::Check{koff, klen, 0});
             host_rejected++;
             return false;
         }
@@ -201,7 +206,7 @@ public:
                 jobs.patches.push_back(PatchRec{(uint32_t)(base + job.off[k]), (uint32_t)aux});
             }
         }
-        it.cache.emplace_back(std::move(key), -2 - (int32_t)pending.size());
+        it.cache.push_back(Item::Check{koff, klen, -2 - (int32_t)pending.size()});
         if (consult) it.pending.push_back((uint32_t)pending.size());
         pending.push_back(Pending{item_idx, (uint32_t)(it.cache.size() - 1)});
         return true;  // speculative
@@ -273,7 +278,7 @@ inline size_t share_lo(size_t n, unsigned t, unsigned T) { return n * t / T; }
 // verify_script's pre-checks (bitcoinconsensus.cpp:83-95) in reference order.  Tx buffers are
 // deserialized once per adjacent run of items, in parallel over T threads.
 void prepare(BatchState& b, const bcc_batch_item* items, size_t n, unsigned flags, unsigned T) {
-    b.st.resize(n);
+    b.st.resize(n);  // the state is reused across calls: every field is (re)set below
     b.flags = flags;
     auto& st = b.st;
     const bool flags_ok = (flags & ~(unsigned)FLAGS_VERIFY_ALL) == 0;
@@ -287,12 +292,19 @@ void prepare(BatchState& b, const bcc_batch_item* items, size_t n, unsigned flag
         for (size_t k = share_lo(E, t, T); k < share_lo(E, t + 1, T); k++) {
             const bcc_batch_item* in = &items[b.tx_first[k]];
             TxEntry& e = b.txs[k];
+            e.aux[0] = e.aux[1] = e.aux[2] = -1;
+            e.tpl = -1;
             e.ok = flags_ok && in->tx_to != nullptr && parse_tx(in->tx_to, in->tx_to_len, e.tx);
             const size_t end = k + 1 < E ? b.tx_first[k + 1] : n;
             for (size_t i = b.tx_first[k]; i < end; i++) {
                 Item& it = st[i];
                 it.in = &items[i];
                 it.tx = &e;
+                it.ret = 0;
+                it.active = false;
+                it.result = false;
+                it.cache.clear();
+                it.pending.clear();
                 if (!flags_ok) it.err = bitcoinconsensus_ERR_INVALID_FLAGS;
                 else if (!e.ok) it.err = bitcoinconsensus_ERR_TX_DESERIALIZE;
                 else if (items[i].n_in >= e.tx.vin.size()) it.err = bitcoinconsensus_ERR_TX_INDEX;
@@ -360,14 +372,24 @@ long run_batch(const bcc_batch_item* items, size_t n, unsigned flags, int* ret_o
     double host_s = 0, gpu_s = 0;
     auto t0 = clk::now();
     const unsigned T = n >= 256 ? std::min<unsigned>(host_threads(), (unsigned)(n / 64)) : 1u;
-    BatchState b;
+    // per calling thread, reused across calls (capacity kept: no per-call allocation storm)
+    // (plain references: a lambda run on a worker thread must not name the thread_locals, which
+    // would resolve to that worker's own instances)
+    thread_local BatchState tl_state;
+    thread_local std::vector<Round> tl_rounds;
+    BatchState& b = tl_state;
+    std::vector<Round>& rds = tl_rounds;
     prepare(b, items, n, flags, T);
     auto since = [](clk::time_point a) { return std::chrono::duration<double>(clk::now() - a).count(); };
     t_stats.prepare_seconds = since(t0);
     auto& st = b.st;
     const int dev = current_device();
     const auto shards = make_shards(b, T);
-    std::vector<Round> rds(T);
+    if (rds.size() < T) rds.resize(T);
+    for (unsigned t = 0; t < T; t++) {
+        rds[t].keys.clear();
+        rds[t].touched.clear();  // pointers into the previous call's tx entries: never followed
+    }
     std::vector<size_t> row0(T + 1, 0);
     std::vector<uint8_t> verdict;
     long status = 0;
@@ -420,7 +442,7 @@ long run_batch(const bcc_batch_item* items, size_t n, unsigned flags, int* ret_o
             const Round& rd = rds[t];
             const uint8_t* v = verdict.data() + row0[t];
             for (size_t k = 0; k < rd.pending.size(); k++)
-                st[rd.pending[k].item].cache[rd.pending[k].slot].second = v[k] ? 1 : 0;
+                st[rd.pending[k].item].cache[rd.pending[k].slot].v = v[k] ? 1 : 0;
             for (uint32_t i : shards[t]) {
                 Item& it = st[i];
                 if (it.pending.empty()) continue;
@@ -439,20 +461,22 @@ long run_batch(const bcc_batch_item* items, size_t n, unsigned flags, int* ret_o
         if (err_out) err_out[i] = it.err;
         valid += ret;
     }
-    // Teardown on the threads that allocated: the per-item verdict caches, the rounds and the
-    // parsed txs were built by the worker threads, and freeing them all from this thread (other
-    // malloc arenas) costs more than the interpreter pass itself.
-    run_threads(T, [&](unsigned t) {
-        for (uint32_t i : shards[t]) {
-            decltype(st[i].cache)().swap(st[i].cache);
-            std::vector<uint32_t>().swap(st[i].pending);
-        }
-        rds[t] = Round();
-    });
-    run_threads(T, [&](unsigned t) {
-        const size_t E = b.txs.size();
-        for (size_t k = share_lo(E, t, T); k < share_lo(E, t + 1, T); k++) b.txs[k].tx = Tx();
-    });
+    // The state stays with the calling thread for its next call, except after a very large batch:
+    // then it is released, in parallel (freeing from one thread costs more than the
+    // interpreter pass itself).
+    if (n > ((size_t)1 << 22)) {
+        run_threads(T, [&](unsigned t) {
+            for (uint32_t i : shards[t]) {
+                decltype(st[i].cache)().swap(st[i].cache);
+                std::vector<uint32_t>().swap(st[i].pending);
+            }
+            rds[t] = Round();
+            const size_t E = b.txs.size();
+            for (size_t k = share_lo(E, t, T); k < share_lo(E, t + 1, T); k++) b.txs[k].tx = Tx();
+        });
+        b = BatchState();
+        rds = std::vector<Round>();
+    }
     host_s = std::chrono::duration<double>(clk::now() - t0).count() - gpu_s;
     t_stats.host_seconds = host_s;
     t_stats.gpu_seconds = gpu_s;

@@ -89,7 +89,11 @@ bool read_vout(Reader& r, std::vector<TxOut>& vout) {
 
 bool parse_tx(const uint8_t* data, size_t len, Tx& tx) {
     Reader r{data, len};
-    tx = Tx();
+    tx.vin.clear();   // keep capacity: callers reuse Tx objects across batches
+    tx.vout.clear();
+    tx.version = 0;
+    tx.locktime = 0;
+    tx.ser_size = 0;
     tx.version = (int32_t)(uint32_t)r.le(4);
     if (r.bad) return false;
     uint8_t flags = 0;
