@@ -90,6 +90,11 @@ int bcc_set_device(int device);
  * Bounds the per-caller device scratch (900 B per lane); results do not depend on it. */
 int bcc_set_chunk_lanes(size_t lanes);
 
+/* bitcoinconsensus_verify_batch keeps its host-side state (items, parsed transactions, job
+ * buffers) with the calling thread for reuse by its next call; batches above 4M items release it
+ * on return.  This releases the calling thread's state now. */
+void bcc_release_thread_state(void);
+
 typedef struct bcc_batch_stats {
     size_t items, tuples, rounds, preimages, aux_messages, host_rejected;
     double host_seconds, gpu_seconds;

@@ -360,6 +360,10 @@ std::vector<std::vector<uint32_t>> make_shards(const BatchState& b, unsigned T) 
     return sh;
 }
 
+// Host state of bitcoinconsensus_verify_batch, per calling thread, reused across its calls.
+thread_local BatchState tl_state;
+thread_local std::vector<Round> tl_rounds;
+
 // Runs the batch; fills ret/err per item.  Returns -1 if the device pipeline failed.
 // Host work (deserialization, interpreter passes, preimage building) runs on up to
 // host_threads() threads over whole-transaction shards; each round's deferred checks of all
@@ -375,8 +379,6 @@ long run_batch(const bcc_batch_item* items, size_t n, unsigned flags, int* ret_o
     // per calling thread, reused across calls (capacity kept: no per-call allocation storm)
     // (plain references: a lambda run on a worker thread must not name the thread_locals, which
     // would resolve to that worker's own instances)
-    thread_local BatchState tl_state;
-    thread_local std::vector<Round> tl_rounds;
     BatchState& b = tl_state;
     std::vector<Round>& rds = tl_rounds;
     prepare(b, items, n, flags, T);
@@ -590,6 +592,11 @@ long bitcoinconsensus_verify_batch(const bcc_batch_item* items, size_t n, unsign
         }
         return -1;
     }
+}
+
+void bcc_release_thread_state(void) {
+    tl_state = BatchState();
+    tl_rounds = std::vector<Round>();
 }
 
 int bcc_set_device(int device) {
