@@ -56,6 +56,10 @@ struct QTableArray {
     fe e[QTAB][3];
     BCC_HD void put(int i, int f, const fe& a) { e[i][f] = a; }
     BCC_HD void get(int i, int f, fe& a) const { a = e[i][f]; }
+    BCC_HD void get_pair(int i, int which, fe& x, fe& y) const {
+        x = e[i][which];
+        y = e[i][2];
+    }
 };
 
 // Host version of the G tables: affine (2i+1) * 2^(128 tab) * G.
@@ -314,8 +318,7 @@ BCC_HD bool ladder_accumulate(const ST& st, const QT& qt, const GT& gt, gej& acc
             if (isg) {
                 gt.get(slot - 2, (int)idx, px, py);
             } else {
-                qt.get((int)idx, slot == 0 ? 0 : 1, px);
-                qt.get((int)idx, 2, py);
+                qt.get_pair((int)idx, slot == 0 ? 0 : 1, px, py);  // (x or beta*x, y)
             }
             if (sneg) fe_neg(py, py);
             acc_add(acc, inf, px, py, st.sigma, isg);

@@ -44,22 +44,45 @@ __device__ __forceinline__ const u32* lane_words(const u32* base, size_t t, int 
     return base + (t >> 6) * (size_t)(W * 64) + (t & 63);
 }
 
-// Per-tuple Q table: word (entry i, field f, limb j) at base[((i*3 + f)*8 + j) * stride].
+// Per-lane Q table, lane-major: lane t's 1 KiB table is contiguous at base + t * QTABLE_WORDS,
+// entry i at 32 words [x | y | beta*x | y] (y stored twice), so an addition reads its point
+// (x, y) or (beta*x, y) as one aligned 64-byte piece with four 16-byte loads.  The ladder gathers
+// by a per-lane digit index: with the entry words interleaved across lanes instead (word-major),
+// each of those loads hit up to 8 table rows per wave and the L2 fetched ~3.7x the bytes used
+// (rocprofv3 TCP_TCC_READ_REQ / SQ_INSTS_VMEM_RD = 14.7, 90 % L2 misses, profiles/r01g_pmc).
+// Fields for put / get: 0 = x, 1 = beta*x (an H value while the table is built), 2 = y.
 struct QTableGlobal {
     u32* base;
-    size_t stride;
+    __device__ static int field_off(int f) { return f == 0 ? 0 : f == 1 ? 16 : 8; }
     __device__ void put(int i, int f, const fe& a) {
-        u32* p = base + (size_t)((i * 3 + f) * 8) * stride;
-#pragma unroll
-        for (int j = 0; j < 8; j++) p[(size_t)j * stride] = a.v[j];
+        uint4* p = reinterpret_cast<uint4*>(base + i * 32 + field_off(f));
+        p[0] = make_uint4(a.v[0], a.v[1], a.v[2], a.v[3]);
+        p[1] = make_uint4(a.v[4], a.v[5], a.v[6], a.v[7]);
+        if (f == 2) {
+            uint4* q = reinterpret_cast<uint4*>(base + i * 32 + 24);
+            q[0] = p[0];
+            q[1] = p[1];
+        }
     }
     __device__ void get(int i, int f, fe& a) const {
-        const u32* p = base + (size_t)((i * 3 + f) * 8) * stride;
-#pragma unroll
-        for (int j = 0; j < 8; j++) a.v[j] = p[(size_t)j * stride];
+        const uint4* p = reinterpret_cast<const uint4*>(base + i * 32 + field_off(f));
+        const uint4 u = p[0], v = p[1];
+        a.v[0] = u.x; a.v[1] = u.y; a.v[2] = u.z; a.v[3] = u.w;
+        a.v[4] = v.x; a.v[5] = v.y; a.v[6] = v.z; a.v[7] = v.w;
+    }
+    // (x, y) for which == 0, (beta*x, y) for which == 1: one 64-byte piece
+    __device__ void get_pair(int i, int which, fe& x, fe& y) const {
+        const uint4* p = reinterpret_cast<const uint4*>(base + i * 32 + 16 * which);
+        const uint4 a = p[0], b = p[1], c = p[2], d = p[3];
+        x.v[0] = a.x; x.v[1] = a.y; x.v[2] = a.z; x.v[3] = a.w;
+        x.v[4] = b.x; x.v[5] = b.y; x.v[6] = b.z; x.v[7] = b.w;
+        y.v[0] = c.x; y.v[1] = c.y; y.v[2] = c.z; y.v[3] = c.w;
+        y.v[4] = d.x; y.v[5] = d.y; y.v[6] = d.z; y.v[7] = d.w;
     }
 };
-constexpr int QTABLE_WORDS = QTAB * 3 * 8;  // 192
+__device__ __forceinline__ u32* lane_table(u32* qtab, size_t t);
+constexpr int QTABLE_WORDS = QTAB * 32;     // 256 words = 1 KiB per lane
+__device__ __forceinline__ u32* lane_table(u32* qtab, size_t t) { return qtab + t * QTABLE_WORDS; }
 constexpr int STATE_WORDS = 16 + 1 + 8 + 8;  // LadderState
 constexpr int PRE_WORDS = 8 + 8 + 1;          // per tuple: s^-1, key y, key status
 
@@ -174,17 +197,24 @@ __device__ __forceinline__ void load_state(LadderState& s, const u32* st, size_t
 // The ladder's view of its state: flags and sigma live in registers; the scalar words and r
 // are loaded where they are used (store_state layout), which keeps 24 VGPRs free across the
 // loop.  The empty asm hides the address from LICM so the loads stay at their use.
+// The ladder's scalar words live in LDS for the whole ladder: 16 words x 256 lanes = 16 KiB per
+// workgroup beside the 16 KiB G tables (4 workgroups per CU: 128 of 160 KiB), word w of lane l at
+// w * 256 + l, so a wave's read of one word is 64 consecutive dwords (no bank conflict).  They are
+// read at every addition (digit extraction); from HBM scratch that was ~1.5 KB per verify.
+constexpr int KLDS_STRIDE = 256;
+
 struct LadderStateView {
     const u32* p;
     size_t C;
     u32 flags;
     fe sigma;
+    const u32* klds;  // this lane's 16 scalar words in LDS, stride KLDS_STRIDE
     __device__ __forceinline__ u32 kword(int s, int w) const {
-        const u32* q = p;
+        const u32* q = klds;
         asm volatile("" : "+v"(q));
-        // the asm hides the address space too: restore it so this is a global (not flat) load
-        const __attribute__((address_space(1))) u32* g = (const __attribute__((address_space(1))) u32*)q;
-        return g[(size_t)(s * 4 + w) * C];
+        // the asm hides the address space too: restore it so this is an LDS (not flat) read
+        const __attribute__((address_space(3))) u32* l = (const __attribute__((address_space(3))) u32*)q;
+        return l[(s * 4 + w) * KLDS_STRIDE];
     }
     __device__ __forceinline__ void get_r(sc& o) const {
 #pragma unroll
@@ -224,7 +254,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
     const size_t i = base + t;
     LadderState st;
     st.flags = 0;
-    QTableGlobal qt{lane_words(qtab, t, QTABLE_WORDS), LANE_STRIDE};
+    QTableGlobal qt{lane_table(qtab, t)};
     if (kok[i]) {
         fe x, y;
         sc r, s, m, si, yl;
@@ -247,6 +277,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
                                                            uint8_t* __restrict__ verdict,
                                                            size_t base, size_t cnt, size_t C) {
     __shared__ fe g_lds[2 * GTAB * 2];
+    __shared__ u32 k_lds[16 * KLDS_STRIDE];
     for (int i = threadIdx.x; i < 2 * GTAB * 2; i += blockDim.x) g_lds[i] = gtab[i];
     __syncthreads();
     const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -257,7 +288,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     st.flags = st.p[16 * LANE_STRIDE];
 #pragma unroll
     for (int j = 0; j < 8; j++) st.sigma.v[j] = st.p[(17 + j) * LANE_STRIDE];
-    QTableGlobal qt{lane_words(const_cast<u32*>(qtab), t, QTABLE_WORDS), LANE_STRIDE};
+#pragma unroll
+    for (int w = 0; w < 16; w++) k_lds[w * KLDS_STRIDE + threadIdx.x] = st.p[w * LANE_STRIDE];
+    st.klds = k_lds + threadIdx.x;  // each lane reads only its own words: no barrier
+    QTableGlobal qt{lane_table(const_cast<u32*>(qtab), t)};
     GTableLDS gt{g_lds};
     verdict[base + t] = (uint8_t)ecdsa_ladder_lane(st, qt, gt);
 }
@@ -281,7 +315,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
     load_be32(s, psig + 64 * i + 32);
     load_be32(m, pm + 32 * i);
     load_be32(px, ppk + 32 * i);
-    QTableGlobal qt{lane_words(qtab, t, QTABLE_WORDS), LANE_STRIDE};
+    QTableGlobal qt{lane_table(qtab, t)};
     LadderState st;
     schnorr_prep_lane(px, rx, s, m, qt, st);
     store_state(lane_words(state, t, STATE_WORDS), LANE_STRIDE, st);
@@ -291,6 +325,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     const u32* __restrict__ state, u32* __restrict__ qtab, const fe* __restrict__ gtab,
     uint8_t* __restrict__ verdict, size_t base, size_t cnt, size_t C) {
     __shared__ fe g_lds[2 * GTAB * 2];
+    __shared__ u32 k_lds[16 * KLDS_STRIDE];
     for (int i = threadIdx.x; i < 2 * GTAB * 2; i += blockDim.x) g_lds[i] = gtab[i];
     __syncthreads();
     const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -301,7 +336,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     st.flags = st.p[16 * LANE_STRIDE];
 #pragma unroll
     for (int j = 0; j < 8; j++) st.sigma.v[j] = st.p[(17 + j) * LANE_STRIDE];
-    QTableGlobal qt{lane_words(qtab, t, QTABLE_WORDS), LANE_STRIDE};
+#pragma unroll
+    for (int w = 0; w < 16; w++) k_lds[w * KLDS_STRIDE + threadIdx.x] = st.p[w * LANE_STRIDE];
+    st.klds = k_lds + threadIdx.x;  // each lane reads only its own words: no barrier
+    QTableGlobal qt{lane_table(qtab, t)};
     GTableLDS gt{g_lds};
     fe ye, ze;
     int ok = schnorr_ladder_lane(st, qt, gt, ye, ze);
@@ -324,12 +362,12 @@ __global__ __launch_bounds__(256) void schnorr_parity_kernel(u32* __restrict__ q
     const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= cnt || t >= T) return;
     fe acc, z, ye;
-    QTableGlobal q0{lane_words(qtab, t, QTABLE_WORDS), LANE_STRIDE};
+    QTableGlobal q0{lane_table(qtab, t)};
     q0.get(0, 1, acc);
     q0.put(0, 2, acc);
     size_t last = t;
     for (size_t i = t + T; i < cnt; i += T) {
-        QTableGlobal qi{lane_words(qtab, i, QTABLE_WORDS), LANE_STRIDE};
+        QTableGlobal qi{lane_table(qtab, i)};
         qi.get(0, 1, z);
         fe_mul(acc, acc, z);
         qi.put(0, 2, acc);  // Z_t * ... * Z_i
@@ -338,8 +376,7 @@ __global__ __launch_bounds__(256) void schnorr_parity_kernel(u32* __restrict__ q
     fe inv;
     fe_inv(inv, acc);
     for (size_t i = last; i >= t + T; i -= T) {
-        QTableGlobal qi{lane_words(qtab, i, QTABLE_WORDS), LANE_STRIDE},
-            qp{lane_words(qtab, i - T, QTABLE_WORDS), LANE_STRIDE};
+        QTableGlobal qi{lane_table(qtab, i)}, qp{lane_table(qtab, i - T)};
         fe prev, zi;
         qp.get(0, 2, prev);
         fe_mul(zi, inv, prev);  // Z_i^-1
