@@ -19,13 +19,17 @@ namespace bcc {
 
 // window widths
 constexpr int WQ = 4;                         // Q / lambda*Q digits: table of 8 odd multiples
-constexpr int WG = 8;                         // G / 2^128*G digits: tables of 128 odd multiples
+#ifndef BCC_WG_BITS
+#define BCC_WG_BITS 10
+#endif
+constexpr int WG = BCC_WG_BITS;               // G / 2^128*G digits: tables of 2^(WG-1) odd multiples
 constexpr int QTAB = 1 << (WQ - 1);           // 8
-constexpr int GTAB = 1 << (WG - 1);           // 128
+constexpr int GTAB = 1 << (WG - 1);
 constexpr int TOPQ = 124;                     // WQ * 31: top digit position for 128-bit scalars
-constexpr int TOPG = 120;                     // WG * 15
+constexpr int TOPG = (127 / WG) * WG;         // top G digit position: 120 for WG = 8, 10, 12
+static_assert(TOPG + WG >= 128 && TOPG <= TOPQ, "top G digit must cover bit 127 inside the ladder");
 
-// (k >> pos) & (2^w - 1) for a 128-bit k (4 limbs), 0 <= pos < 128, w <= 8
+// (k >> pos) & (2^w - 1) for a 128-bit k (4 limbs), 0 <= pos < 128, w <= 31
 BCC_HD u32 bits_at(u32 l0, u32 l1, u32 l2, u32 l3, int pos, int w) {
     int li = pos >> 5, sh = pos & 31;
     u32 a = li == 0 ? l0 : li == 1 ? l1 : li == 2 ? l2 : l3;

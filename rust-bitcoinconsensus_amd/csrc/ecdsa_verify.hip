@@ -86,7 +86,7 @@ __device__ __forceinline__ u32* lane_table(u32* qtab, size_t t) { return qtab + 
 constexpr int STATE_WORDS = 16 + 1 + 8 + 8;  // LadderState
 constexpr int PRE_WORDS = 8 + 8 + 1;          // per tuple: s^-1, key y, key status
 
-// G tables staged in LDS (16 KiB per workgroup).
+// G tables staged in LDS (64 KiB per workgroup).
 struct GTableLDS {
     const fe* xy;
     __device__ void get(int tab, int i, fe& x, fe& y) const {
@@ -197,11 +197,23 @@ __device__ __forceinline__ void load_state(LadderState& s, const u32* st, size_t
 // The ladder's view of its state: flags and sigma live in registers; the scalar words and r
 // are loaded where they are used (store_state layout), which keeps 24 VGPRs free across the
 // loop.  The empty asm hides the address from LICM so the loads stay at their use.
-// The ladder's scalar words live in LDS for the whole ladder: 16 words x 256 lanes = 16 KiB per
-// workgroup beside the 16 KiB G tables (4 workgroups per CU: 128 of 160 KiB), word w of lane l at
-// w * 256 + l, so a wave's read of one word is 64 consecutive dwords (no bank conflict).  They are
-// read at every addition (digit extraction); from HBM scratch that was ~1.5 KB per verify.
-constexpr int KLDS_STRIDE = 256;
+// Ladder workgroups are 512 lanes (8 waves), two per CU (4 waves per SIMD), each with its own
+// copy of the 64 KiB w = 10 G tables (128 of 160 KiB).  Measured on MI355X, C2 1M, ECDSA stage
+// (variants built by tools/variants/build.sh): w = 8 / 256-lane groups 77.3 M/s; w = 10 /
+// 512-lane groups 78.9 M/s (13 instead of 16 G additions per 128-bit half); w = 10 / 1024-lane
+// groups (one per CU, one shared table) 72.5 M/s and w = 8 / 1024 71.3 M/s: a CU whose only
+// workgroup has stragglers idles until the whole group retires.  The scalar words can also be
+// staged in LDS (BCC_K_IN_LDS: 16 words per lane, word w of lane l at w * LADDER_WG + l); at
+// w = 8 that measured the same as reading them from the wave-blocked scratch (77.3 vs 77.5 M/s),
+// and at w = 10 it would leave room for one workgroup per CU only, so it is off.
+#ifndef BCC_LADDER_WG
+#define BCC_LADDER_WG 512
+#endif
+constexpr int LADDER_WG = BCC_LADDER_WG;
+#ifndef BCC_K_IN_LDS
+#define BCC_K_IN_LDS 0
+#endif
+[[maybe_unused]] constexpr int KLDS_STRIDE = BCC_K_IN_LDS ? LADDER_WG : 1;
 
 struct LadderStateView {
     const u32* p;
@@ -210,11 +222,18 @@ struct LadderStateView {
     fe sigma;
     const u32* klds;  // this lane's 16 scalar words in LDS, stride KLDS_STRIDE
     __device__ __forceinline__ u32 kword(int s, int w) const {
+#if BCC_K_IN_LDS
         const u32* q = klds;
         asm volatile("" : "+v"(q));
         // the asm hides the address space too: restore it so this is an LDS (not flat) read
         const __attribute__((address_space(3))) u32* l = (const __attribute__((address_space(3))) u32*)q;
         return l[(s * 4 + w) * KLDS_STRIDE];
+#else
+        const u32* q = p;
+        asm volatile("" : "+v"(q));
+        const __attribute__((address_space(1))) u32* g = (const __attribute__((address_space(1))) u32*)q;
+        return g[(size_t)(s * 4 + w) * C];
+#endif
     }
     __device__ __forceinline__ void get_r(sc& o) const {
 #pragma unroll
@@ -271,13 +290,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
     store_state(lane_words(state, t, STATE_WORDS), LANE_STRIDE, st);
 }
 
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) void ecdsa_ladder_kernel(const u32* __restrict__ state,
+__global__ __launch_bounds__(LADDER_WG) __attribute__((amdgpu_waves_per_eu(4, 4))) void ecdsa_ladder_kernel(const u32* __restrict__ state,
                                                            const u32* __restrict__ qtab,
                                                            const fe* __restrict__ gtab,
                                                            uint8_t* __restrict__ verdict,
                                                            size_t base, size_t cnt, size_t C) {
     __shared__ fe g_lds[2 * GTAB * 2];
+#if BCC_K_IN_LDS
     __shared__ u32 k_lds[16 * KLDS_STRIDE];
+#endif
     for (int i = threadIdx.x; i < 2 * GTAB * 2; i += blockDim.x) g_lds[i] = gtab[i];
     __syncthreads();
     const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -288,9 +309,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     st.flags = st.p[16 * LANE_STRIDE];
 #pragma unroll
     for (int j = 0; j < 8; j++) st.sigma.v[j] = st.p[(17 + j) * LANE_STRIDE];
+#if BCC_K_IN_LDS
 #pragma unroll
     for (int w = 0; w < 16; w++) k_lds[w * KLDS_STRIDE + threadIdx.x] = st.p[w * LANE_STRIDE];
     st.klds = k_lds + threadIdx.x;  // each lane reads only its own words: no barrier
+#endif
     QTableGlobal qt{lane_table(const_cast<u32*>(qtab), t)};
     GTableLDS gt{g_lds};
     verdict[base + t] = (uint8_t)ecdsa_ladder_lane(st, qt, gt);
@@ -321,11 +344,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
     store_state(lane_words(state, t, STATE_WORDS), LANE_STRIDE, st);
 }
 
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) void schnorr_ladder_kernel(
+__global__ __launch_bounds__(LADDER_WG) __attribute__((amdgpu_waves_per_eu(4, 4))) void schnorr_ladder_kernel(
     const u32* __restrict__ state, u32* __restrict__ qtab, const fe* __restrict__ gtab,
     uint8_t* __restrict__ verdict, size_t base, size_t cnt, size_t C) {
     __shared__ fe g_lds[2 * GTAB * 2];
+#if BCC_K_IN_LDS
     __shared__ u32 k_lds[16 * KLDS_STRIDE];
+#endif
     for (int i = threadIdx.x; i < 2 * GTAB * 2; i += blockDim.x) g_lds[i] = gtab[i];
     __syncthreads();
     const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -336,9 +361,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 4))) voi
     st.flags = st.p[16 * LANE_STRIDE];
 #pragma unroll
     for (int j = 0; j < 8; j++) st.sigma.v[j] = st.p[(17 + j) * LANE_STRIDE];
+#if BCC_K_IN_LDS
 #pragma unroll
     for (int w = 0; w < 16; w++) k_lds[w * KLDS_STRIDE + threadIdx.x] = st.p[w * LANE_STRIDE];
     st.klds = k_lds + threadIdx.x;  // each lane reads only its own words: no barrier
+#endif
     QTableGlobal qt{lane_table(qtab, t)};
     GTableLDS gt{g_lds};
     fe ye, ze;
@@ -529,7 +556,8 @@ int ecdsa_launch_after_pre(SigScratch& sc, const uint8_t* d_x, const uint8_t* d_
         hipLaunchKernelGGL(ecdsa_prep_kernel, dim3(blocks), dim3(256), 0, sm, d_x, d_r, d_s, d_m,
                            sinv, keyy, kok, base, cnt, qtab, state);
         BCC_HIP_TRY(hipGetLastError());
-        hipLaunchKernelGGL(ecdsa_ladder_kernel, dim3(blocks), dim3(256), 0, sm, state, qtab, gtab,
+        hipLaunchKernelGGL(ecdsa_ladder_kernel, dim3((unsigned)((cnt + LADDER_WG - 1) / LADDER_WG)),
+                           dim3(LADDER_WG), 0, sm, state, qtab, gtab,
                            d_verdict, base, cnt, C);
         BCC_HIP_TRY(hipGetLastError());
     }
@@ -553,7 +581,8 @@ int schnorr_launch(SigScratch& sc, const uint8_t* d_sig64, const uint8_t* d_msg3
         hipLaunchKernelGGL(schnorr_prep_kernel, dim3(blocks), dim3(256), 0, sm, d_sig64, d_msg32,
                            d_xonly32, base, cnt, C, qtab, state);
         BCC_HIP_TRY(hipGetLastError());
-        hipLaunchKernelGGL(schnorr_ladder_kernel, dim3(blocks), dim3(256), 0, sm, state, qtab, gtab,
+        hipLaunchKernelGGL(schnorr_ladder_kernel, dim3((unsigned)((cnt + LADDER_WG - 1) / LADDER_WG)),
+                           dim3(LADDER_WG), 0, sm, state, qtab, gtab,
                            d_verdict, base, cnt, C);
         BCC_HIP_TRY(hipGetLastError());
         // parity: sub-chunks of <= 16 lanes, at least one wave per SIMD
