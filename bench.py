@@ -42,7 +42,7 @@ sys.path.insert(0, os.path.join(ROOT, "rust-bitcoinconsensus_amd"))
 MADS_PER_VERIFY = 144448          # 2,257 modmuls x 64 (32x32->64) products
 MADS_PER_SCHNORR = 142848         # 2,232 modmuls x 64
 METRIC = "ECDSA verifies/sec (node) at 1/2/4/8 MI355X; % of int-ALU roofline"
-DEFAULT_N = {"c2": 1_000_000, "c3": 4000, "c4": 8_000_000, "c5": 4_000_000}
+DEFAULT_N = {"c2": 1_000_000, "c3": 4000, "c4": 8_000_000, "c5": 16_000_000}
 SEEDS = {"c2": 0x5EED0001, "c3": 0x5EED0003, "c4": 0x5EED0004, "c5": 0x5EED0005}
 CPU_THREADS = 16                  # the GPU box's CPU share
 
@@ -391,7 +391,8 @@ def main():
         traffic, tsrc = args.traffic, "--traffic" if args.traffic else None
         tf = os.path.join(ROOT, "profiles", "traffic.json")
         if traffic is None and os.path.exists(tf):
-            t = json.load(open(tf)).get(args.config)
+            tj = json.load(open(tf))
+            t = tj.get(f"{args.config}@{sig_units}") or tj.get(args.config)
             if t and t.get("units") == sig_units:
                 traffic, tsrc = t["traffic_bytes"], t["source"]
         roof = dict(bound="int-alu", kernel=job.kernel,

@@ -40,11 +40,19 @@ def main(d):
         if "fetch_size_bytes_per_launch" in e:
             e["fetch_bytes_x2_per_launch"] = 2 * e["fetch_size_bytes_per_launch"]
     # per signature stage = all launches of one run_ecdsa / schnorr call.  The PMC passes run
-    # bench.py --steps 1 --warmup 0: one timed step + 3 HIP-event timing repetitions = 4 stages.
+    # bench.py --steps 1 --warmup 0: one timed step + 3 HIP-event timing repetitions = 4 stages,
+    # plus, for the C2 line (which carries drop_in_end_to_end), 3 drop-in verify_batch runs over
+    # the same inputs = 7.  A stage may launch a kernel once per lane chunk (C4 at 8M, C5 at 16M).
     stages = {"ecdsa": ["batch_sinv_kernel", "ecdsa_prep_kernel", "ecdsa_ladder_kernel"],
               "schnorr": ["schnorr_prep_kernel", "schnorr_ladder_kernel", "schnorr_parity_kernel"]}
     K = out["kernels"]
-    n_stage = 4
+    bench = os.path.join(d, "bench_under_rocprof.json")
+    if os.path.exists(bench):
+        try:
+            out["bench_under_rocprof"] = json.loads(open(bench).read().strip().splitlines()[-1])
+        except (ValueError, IndexError):
+            pass
+    n_stage = 7 if "drop_in_end_to_end" in out.get("bench_under_rocprof", {}) else 4
     for st, ks in stages.items():
         if not any("fetch_size_launches" in K.get(k, {}) for k in ks):
             continue
@@ -52,12 +60,6 @@ def main(d):
         wb = sum(K[k].get("write_size_bytes_total", 0) for k in ks if k in K) / n_stage
         out.setdefault("stages", {})[st] = dict(executions=n_stage, fetch_bytes=fb, fetch_bytes_x2=2 * fb,
                                                write_bytes=wb, traffic_bytes=2 * fb + wb)
-    bench = os.path.join(d, "bench_under_rocprof.json")
-    if os.path.exists(bench):
-        try:
-            out["bench_under_rocprof"] = json.loads(open(bench).read().strip().splitlines()[-1])
-        except (ValueError, IndexError):
-            pass
     print(json.dumps(out, indent=1))
 
 
