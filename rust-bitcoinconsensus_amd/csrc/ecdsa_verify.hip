@@ -205,11 +205,16 @@ __device__ __forceinline__ void load_state(LadderState& s, const u32* st, size_t
 // workgroup has stragglers idles until the whole group retires.  The scalar words can also be
 // staged in LDS (BCC_K_IN_LDS: 16 words per lane, word w of lane l at w * LADDER_WG + l); at
 // w = 8 that measured the same as reading them from the wave-blocked scratch (77.3 vs 77.5 M/s),
-// and at w = 10 it would leave room for one workgroup per CU only, so it is off.
+// and at w = 10 it would leave room for one workgroup per CU only, so it is off.  Five waves per
+// SIMD (640-lane groups, BCC_LADDER_WAVES=5) caps the ladder at 96 VGPRs and spills 25 of them:
+// 67.4 M/s (C2) and 77.7 M/s (C5) against 79.3 / 87.2 M/s at four waves.
 #ifndef BCC_LADDER_WG
 #define BCC_LADDER_WG 512
 #endif
 constexpr int LADDER_WG = BCC_LADDER_WG;
+#ifndef BCC_LADDER_WAVES
+#define BCC_LADDER_WAVES 4  // waves per SIMD the ladder kernels are register-allocated for
+#endif
 #ifndef BCC_K_IN_LDS
 #define BCC_K_IN_LDS 0
 #endif
@@ -290,7 +295,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
     store_state(lane_words(state, t, STATE_WORDS), LANE_STRIDE, st);
 }
 
-__global__ __launch_bounds__(LADDER_WG) __attribute__((amdgpu_waves_per_eu(4, 4))) void ecdsa_ladder_kernel(const u32* __restrict__ state,
+__global__ __launch_bounds__(LADDER_WG) __attribute__((amdgpu_waves_per_eu(BCC_LADDER_WAVES, BCC_LADDER_WAVES))) void ecdsa_ladder_kernel(const u32* __restrict__ state,
                                                            const u32* __restrict__ qtab,
                                                            const fe* __restrict__ gtab,
                                                            uint8_t* __restrict__ verdict,
@@ -344,7 +349,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
     store_state(lane_words(state, t, STATE_WORDS), LANE_STRIDE, st);
 }
 
-__global__ __launch_bounds__(LADDER_WG) __attribute__((amdgpu_waves_per_eu(4, 4))) void schnorr_ladder_kernel(
+__global__ __launch_bounds__(LADDER_WG) __attribute__((amdgpu_waves_per_eu(BCC_LADDER_WAVES, BCC_LADDER_WAVES))) void schnorr_ladder_kernel(
     const u32* __restrict__ state, u32* __restrict__ qtab, const fe* __restrict__ gtab,
     uint8_t* __restrict__ verdict, size_t base, size_t cnt, size_t C) {
     __shared__ fe g_lds[2 * GTAB * 2];
