@@ -175,7 +175,7 @@ class C2:
 
     data = "synthetic (deterministic P2WPKH spends, GPU-generated keys/signatures)"
     mads = MADS_PER_VERIFY
-    kernel = "ecdsa (batch_sinv + ecdsa_prep + ecdsa_ladder)"
+    kernel = "ecdsa (batch_sinv + ecdsa_key + ecdsa_prep + ecdsa_ladder)"
 
 
 class C3(C2):
@@ -245,7 +245,7 @@ class TupleJob:
         self.units = self.n = n
         self.unit = "verifies/s"
         self.mads = MADS_PER_VERIFY if kind == "c4" else MADS_PER_SCHNORR
-        self.kernel = ("ecdsa (batch_sinv + ecdsa_prep + ecdsa_ladder)" if kind == "c4"
+        self.kernel = ("ecdsa (batch_sinv + ecdsa_key + ecdsa_prep + ecdsa_ladder)" if kind == "c4"
                        else "schnorr (prep + ladder + y-parity batch inversion)")
 
     def step(self, sp):
