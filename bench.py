@@ -41,10 +41,16 @@ sys.path.insert(0, os.path.join(ROOT, "rust-bitcoinconsensus_amd"))
 
 MADS_PER_VERIFY = 144448          # 2,257 modmuls x 64 (32x32->64) products
 MADS_PER_SCHNORR = 142848         # 2,232 modmuls x 64
+UBENCH_OPS = {0: "v_mad_u64_u32", 1: "v_mul_lo_u32", 2: "v_mul_hi_u32", 3: "v_add_co_u32 (sgpr)",
+              4: "v_addc_co_u32", 5: "v_mad_u32_u24", 6: "v_lshl_add_u64", 7: "v_fma_f64",
+              8: "v_add_u32", 9: "v_add3_u32", 10: "v_mul_u32_u24", 11: "v_mul_hi_u32_u24",
+              12: "v_alignbit_b32", 13: "v_lshrrev_b64", 14: "v_add_co_u32 (vcc)",
+              15: "v_cndmask_b32", 16: "mad_u64_u32+addc pair", 17: "mul_lo+mul_hi pair",
+              18: "mad_u64_u32+add_u32 pair"}
 METRIC = "ECDSA verifies/sec (node) at 1/2/4/8 MI355X; % of int-ALU roofline"
 DEFAULT_N = {"c2": 1_000_000, "c3": 4000, "c4": 8_000_000, "c5": 16_000_000}
 SEEDS = {"c2": 0x5EED0001, "c3": 0x5EED0003, "c4": 0x5EED0004, "c5": 0x5EED0005}
-CPU_THREADS = 16                  # the GPU box's CPU share
+CPU_PASSES = 3                    # timed passes of the CPU baseline (median), after 1 warm-up
 
 
 def log(*a):
@@ -57,8 +63,60 @@ def _reference():
     return Reference() if reference_available() else None
 
 
-def cpu_baseline_script(items, threads, what, unit="inputs/s"):
-    """Reference libbitcoinconsensus over (spk, amount, tx, nin) items (checker-side code)."""
+def host_cpu_info():
+    """CPU model, logical / physical counts and the threads the baseline uses: the smaller of the
+    affinity mask and the cgroup CPU quota (on a shared GPU box os.cpu_count() shows the whole
+    machine, the quota is the share this process may use).  BASELINE.md §3: rayon's default is
+    one worker per logical CPU the process can run on."""
+    info = {"logical_cpus_visible": os.cpu_count()}
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count() or 1
+    info["affinity_cpus"] = aff
+    quota = None
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(round(int(q) / int(p))))
+    except (OSError, ValueError):
+        pass
+    info["cgroup_cpu_quota"] = quota
+    model, cores = None, set()
+    try:
+        phys = core = None
+        for line in open("/proc/cpuinfo"):
+            k, _, v = line.partition(":")
+            k, v = k.strip(), v.strip()
+            if k == "model name" and model is None:
+                model = v
+            elif k == "physical id":
+                phys = v
+            elif k == "core id":
+                core = v
+            elif not k and phys is not None:
+                cores.add((phys, core))
+                phys = core = None
+    except OSError:
+        pass
+    info["model"] = model
+    info["physical_cores_visible"] = len(cores) or None
+    info["threads_used"] = min(aff, quota) if quota else aff
+    return info
+
+
+def median_rate(run, n, passes=CPU_PASSES):
+    """1 warm-up + `passes` timed runs of run() (returns seconds); median items/s and all passes."""
+    run()
+    secs = sorted(run() for _ in range(passes))
+    return n / secs[len(secs) // 2], [round(n / s, 1) for s in secs]
+
+
+def cpu_baseline_script(items, what, unit="inputs/s", gpu_verdicts=None):
+    """Reference libbitcoinconsensus over (spk, amount, tx, nin) items (checker-side code):
+    bitcoinconsensus_verify_script_with_amount per item on a dynamically chunked std::thread
+    pool (oracle/ref_shim.cpp), median of CPU_PASSES passes; the single-core rate beside it.
+    gpu_verdicts: the GPU's per-item verdicts on the same items (0/1 bytes) -> mismatch count."""
     import ctypes
     ref = os.path.join(ROOT, "oracle", "_ref", "libref_consensus.so")
     if not os.path.exists(ref):
@@ -66,6 +124,8 @@ def cpu_baseline_script(items, threads, what, unit="inputs/s"):
     L = ctypes.CDLL(ref)
     L.ref_bench_verify_script.restype = ctypes.c_double
     sample = len(items)
+    hw = host_cpu_info()
+    threads = hw["threads_used"]
 
     def blob(parts):
         off = [0]
@@ -78,16 +138,24 @@ def cpu_baseline_script(items, threads, what, unit="inputs/s"):
     am = (ctypes.c_int64 * sample)(*[it[1] for it in items])
     nin = (ctypes.c_uint * sample)(*[it[3] for it in items])
     ret = (ctypes.c_int * sample)()
-    args = (ctypes.c_long(sample), sb, so, tb, to, am, nin, ctypes.c_uint(0xE15), ret)
-    L.ref_bench_verify_script(ctypes.c_int(threads), ctypes.c_long(min(sample, 2000)), *args[1:])  # warm
-    secs = L.ref_bench_verify_script(ctypes.c_int(threads), *args)
+    args = (sb, so, tb, to, am, nin, ctypes.c_uint(0xE15), ret)
+    rate, passes = median_rate(
+        lambda: L.ref_bench_verify_script(ctypes.c_int(threads), ctypes.c_long(sample), *args),
+        sample)
     ok = sum(ret[i] for i in range(sample))
     n1 = max(1, sample // 16)
-    secs1 = L.ref_bench_verify_script(ctypes.c_int(1), ctypes.c_long(n1), *args[1:])
-    return dict(value=sample / secs, unit=unit, cores=threads, kind="reference",
+    rate1, _ = median_rate(
+        lambda: L.ref_bench_verify_script(ctypes.c_int(1), ctypes.c_long(n1), *args), n1, passes=1)
+    mism = None
+    if gpu_verdicts is not None:
+        mism = sum(1 for i in range(sample) if (ret[i] == 1) != (gpu_verdicts[i] == 1))
+    return dict(value=rate, unit=unit, cores=threads, kind="reference",
                 sample=f"{sample} {what}, bitcoinconsensus_verify_script_with_amount flags=0xE15, "
-                       f"std::thread pool x{threads}; reference accepted {ok}/{sample}",
-                single_core_value=n1 / secs1, cpu_seconds=secs * threads)
+                       f"dynamically chunked std::thread pool x{threads}, median of "
+                       f"{CPU_PASSES} passes after 1 warm-up; reference accepted {ok}/{sample}"
+                       + ("" if mism is None else f"; GPU verdict mismatches on the sample: {mism}"),
+                passes=passes, single_core_value=rate1, host=hw,
+                gpu_verdict_mismatches=mism)
 
 
 def aggregate(elapsed, n_valid, world, device="cuda"):
@@ -163,9 +231,14 @@ class C2:
 
     def cpu(self, sample):
         sample = min(sample, self.n)
-        return cpu_baseline_script([self.wl.item(i) for i in range(sample)], CPU_THREADS,
+        # per-item GPU verdicts of the benchmarked staged path (one tuple per P2WPKH item)
+        v = self.wl.verdicts()
+        item_v = bytearray(self.n)
+        for t, i in enumerate(self.wl.tuple_items()):
+            item_v[i] = v[t]
+        return cpu_baseline_script([self.wl.item(i) for i in range(sample)],
                                    f"C2 inputs (first {sample} of rank 0's workload)",
-                                   unit="verifies/s")
+                                   unit="verifies/s", gpu_verdicts=item_v[:sample])
 
     def config(self, world):
         return {"workload": "C2: synthetic P2WPKH inputs, BIP143 sighash + ECDSA verify "
@@ -219,8 +292,9 @@ class C3(C2):
 
     def cpu(self, sample):
         sample = min(sample, self.n)
-        return cpu_baseline_script([self.wl.item(i) for i in range(sample)], CPU_THREADS,
-                                   f"C3 inputs (first {sample})")
+        _, ret = self.wl.verify_batch()
+        return cpu_baseline_script([self.wl.item(i) for i in range(sample)],
+                                   f"C3 inputs (first {sample})", gpu_verdicts=ret[:sample])
 
     def config(self, world):
         return {"workload": f"C3: block replay, {self.ntx} txs with block413567's input/output "
@@ -288,17 +362,27 @@ class TupleJob:
         else:
             args = (h["sig64"], h["msg32"], h["xonly32"])
             f, what = R.schnorr_verify_rows, "secp256k1_schnorrsig_verify"
-        f(*args, threads=CPU_THREADS, n=min(sample, 2000))  # warm
-        ref, secs = f(*args, threads=CPU_THREADS, n=sample)
+        hw = host_cpu_info()
+        threads = hw["threads_used"]
+        box = {}
+
+        def run():
+            box["ref"], secs = f(*args, threads=threads, n=sample)
+            return secs
+
+        rate, passes = median_rate(run, sample)
+        ref = box["ref"]
         n1 = max(1, sample // 16)
-        _, secs1 = f(*args, threads=1, n=n1)
+        rate1, _ = median_rate(lambda: f(*args, threads=1, n=n1)[1], n1, passes=1)
         v = np.frombuffer(self.ts.verdicts(), np.uint8)[:sample]
-        return dict(value=sample / secs, unit="verifies/s", cores=CPU_THREADS, kind="reference",
+        mism = int((ref != v).sum())
+        return dict(value=rate, unit="verifies/s", cores=threads, kind="reference",
                     sample=f"first {sample} {self.kind.upper()} tuples of rank 0, {what}, "
-                           f"std::thread pool x{CPU_THREADS}; reference accepted "
+                           f"dynamically chunked std::thread pool x{threads}, median of "
+                           f"{CPU_PASSES} passes after 1 warm-up; reference accepted "
                            f"{int(ref.sum())}/{sample}; GPU verdict mismatches on the sample: "
-                           f"{int((ref != v).sum())}",
-                    single_core_value=n1 / secs1, cpu_seconds=secs * CPU_THREADS)
+                           f"{mism}",
+                    passes=passes, single_core_value=rate1, host=hw, gpu_verdict_mismatches=mism)
 
     def config(self, world):
         if self.kind == "c4":
@@ -387,6 +471,7 @@ def main():
     value = total / elapsed
     if rank == 0:
         peak = B.microbench(0, 4096)  # v_mad_u64_u32 lane-ops/s, measured on this GPU
+        rates = {UBENCH_OPS[op]: round(B.microbench(op, 2048) / 1e12, 2) for op in UBENCH_OPS}
         achieved = sig_units * job.mads / (sig_ms * 1e-3)
         traffic, tsrc = args.traffic, "--traffic" if args.traffic else None
         tf = os.path.join(ROOT, "profiles", "traffic.json")
@@ -398,6 +483,7 @@ def main():
         roof = dict(bound="int-alu", kernel=job.kernel,
                     achieved=achieved / 1e12, peak=peak / 1e12, unit="T(v_mad_u64_u32)/s",
                     frac=achieved / peak, traffic=traffic, traffic_source=tsrc,
+                    issue_rates_T_per_s=rates,
                     per_launch=dict(verifies=sig_units, mads=sig_units * job.mads, avg_ms=sig_ms,
                                     verifies_per_s=sig_units / (sig_ms * 1e-3)))
         cpu = None
@@ -415,6 +501,7 @@ def main():
             "cpu_baseline": cpu,
         }
         out.update(job.extra(sighash_ms))
+        out["source_hash"] = B.source_hash()
         out["verdicts_valid"] = n_valid_all
         out["verdicts_total"] = job.units * world
         if cpu:

@@ -54,34 +54,11 @@ int bcc_pubkey_verify_batch(const uint8_t* pub_blob, const uint64_t* pub_off,
                             const uint8_t* msg32, const uint8_t* sig_blob,
                             const uint64_t* sig_off, uint8_t* verdict, size_t n, int device);
 
-/* ---- synthetic tuple sets (configs C4 / C5; bench.py / tests), staged in HBM ---------------- */
-typedef struct bcc_tupleset bcc_tupleset;
-/* C4: n (pub, msg32, DER sig) tuples from `seed`, 90 % valid, 10 % over 18 adversarial classes
- * (bit-flipped r / s / msg, high-S, r or s >= n, r or s = 0, over-long and zero-padded r,
- * compressed x without a square root, x >= p, 04 with a wrong y, 04, hybrid 06/07 with good and
- * bad parity, bad header, wrong key).  The staged rows are those bcc_pubkey_verify_batch builds. */
-bcc_tupleset* bcc_tupleset_c4(size_t n, uint64_t seed, int device);
-/* C5: n BIP340 rows, fresh GPU-signed from `seed`, with the nvec caller vectors (sig64, msg32,
- * xonly32, expected verdict) at rows i with i % 1024 == 1 + j. */
-bcc_tupleset* bcc_tupleset_c5(size_t n, uint64_t seed, const uint8_t* vec_sig64,
-                              const uint8_t* vec_msg32, const uint8_t* vec_xonly32,
-                              const uint8_t* vec_expect, size_t nvec, int device);
-void bcc_tupleset_free(bcc_tupleset* ts);
-size_t bcc_tupleset_size(const bcc_tupleset* ts);
-/* launch the verify kernels over the resident rows on `stream` (asynchronous) */
-int bcc_tupleset_run(bcc_tupleset* ts, void* stream);
-/* copy back the n verdicts of the last run (synchronous) */
-int bcc_tupleset_verdicts(bcc_tupleset* ts, uint8_t* out);
-/* host copies of the inputs (valid while ts lives); cls = generator class (0 = plain valid),
- * expect = verdict by construction.  C4 fills pub / sig, C5 fills sig64 / xonly32. */
-typedef struct bcc_tupleset_host {
-    size_t n;
-    const uint8_t *pub_blob, *sig_blob, *msg32, *sig64, *xonly32, *cls, *expect;
-    const uint64_t *pub_off, *sig_off;
-} bcc_tupleset_host;
-void bcc_tupleset_view(const bcc_tupleset* ts, bcc_tupleset_host* v);
-
 /* ---- engine configuration / statistics ---------------------------------------------------- */
+/* Hash of the sources this library was built from (rust-bitcoinconsensus_amd/source_hash.py):
+ * callers can check that the library they loaded matches the tree they test. */
+const char* bcc_source_hash(void);
+
 /* Device used by the bitcoinconsensus_* entry points of the calling process (default 0, or the
  * BCC_DEVICE environment variable). */
 int bcc_set_device(int device);
@@ -102,57 +79,17 @@ typedef struct bcc_batch_stats {
      * included), merging the per-thread rounds, host -> HBM staging (part of gpu_seconds) */
     double prepare_seconds, interpret_seconds, merge_seconds, stage_seconds;
     double total_seconds; /* the whole call, teardown included */
+    size_t device_retries; /* device rounds that failed once and were re-run on a fresh batch */
 } bcc_batch_stats;
 /* Statistics of the calling thread's last bitcoinconsensus_verify_batch / verify call. */
 void bcc_last_batch_stats(bcc_batch_stats* out);
 
-/* ---- synthetic workloads (bench.py / tests): built and staged on the device ---------------- */
-typedef struct bcc_workload bcc_workload;
-
-/* C2: n synthetic P2WPKH spends (1-in/1-out v2 txs, BIP143 SIGHASH_ALL, low-S DER), keys,
- * nonces and amounts derived from `seed`.  Keys and signatures are produced by
- * the engine's own GPU kernels; txs / sighash jobs are staged in HBM. */
-bcc_workload* bcc_workload_p2wpkh(size_t n, uint64_t seed, int device);
-/* C3: block replay.  ntx transactions with tx_nin[j] inputs / tx_nout[j] outputs (the histogram
- * of the reference's bench/data/block413567.raw), inputs 60 % P2PKH / 30 % P2WPKH / 10 % P2SH
- * 2-of-3 multisig, re-signed with synthetic keys from `seed`.  One item per
- * input, in transaction order. */
-bcc_workload* bcc_workload_block(const uint32_t* tx_nin, const uint32_t* tx_nout, size_t ntx,
-                                 uint64_t seed, int device);
-void bcc_workload_free(bcc_workload* w);
-/* the workload's items (valid while w lives), e.g. for bitcoinconsensus_verify_batch */
-const bcc_batch_item* bcc_workload_items(const bcc_workload* w, size_t* n);
-size_t bcc_workload_size(const bcc_workload* w);
-/* launch the full hot path (sighash kernels + ECDSA kernel) on the staged inputs */
-int bcc_workload_run(bcc_workload* w, void* stream);
-int bcc_workload_run_sighash(bcc_workload* w, void* stream);
-int bcc_workload_run_ecdsa(bcc_workload* w, void* stream);
-/* copy back verdicts (n bytes) */
-int bcc_workload_verdicts(bcc_workload* w, uint8_t* out);
-/* algorithmic work of one run: bytes hashed + written by the sighash stage, tuples verified */
-void bcc_workload_shape(const bcc_workload* w, size_t* tuples, size_t* sighash_blocks,
-                        size_t* aux_blocks, size_t* preimages, size_t* aux_messages);
-/* export item i as (spk, amount, tx) for CPU-baseline / parity checks: returns tx length and
- * copies up to cap bytes; *spk_len <= 64 */
-size_t bcc_workload_item(const bcc_workload* w, size_t i, uint8_t* spk, size_t* spk_len,
-                         int64_t* amount, uint8_t* tx, size_t cap);
-
-/* ---- generator kernels (synthetic inputs; not on the verification path) -------------------- */
-int mi_gen_pubkeys(const uint8_t* d32, size_t n, uint8_t* x32, uint8_t* y32, uint8_t* ok,
-                   int device);
-int mi_gen_sign(const uint8_t* d32, const uint8_t* m32, const uint8_t* k32, size_t n,
-                uint8_t* r32, uint8_t* s32, uint8_t* ok, int device);
-/* BIP340 sig64 (nonce k given) + the x-only key of d, for n (d, m, k) rows. */
-int mi_gen_schnorr_sign(const uint8_t* d32, const uint8_t* m32, const uint8_t* k32, size_t n,
-                        uint8_t* sig64, uint8_t* xonly32, uint8_t* ok, int device);
-
-/* ---- integer-ALU microbenchmark (the roofline peak) ---------------------------------------- */
-int mi_microbench(int op, int iters, double* rate);
-
-/* ---- field self-test (tests only): one device Fp operation over n operand pairs ------------
- * a, b, out: n x 8 little-endian u32 limbs.  op: 0 add, 1 sub, 2 mul, 3 sqr, 4/5/6 shift by
- * 1/2/3, 7 neg, 8 is_zero (out[0]), 9 normalize.  Results are weak (< 2^256) except 8, 9. */
-int mi_fe_selftest(int op, const uint32_t* a, const uint32_t* b, uint32_t* out, size_t n);
+/* Fault injection (tests): the next `rounds` device rounds of any thread fail as if the HIP
+ * runtime had returned an error, without touching the GPU (also: BCC_FAULT_INJECT=rounds in the
+ * environment at load time).  A failed round is retried once on a fresh device batch; a second
+ * failure makes bitcoinconsensus_verify_batch return -1 (unfinished items: BCC_ERR_DEVICE_FAILURE)
+ * and the single-item ABI abort (see bitcoinconsensus.h). */
+void bcc_debug_fail_device_rounds(int rounds);
 
 #ifdef __cplusplus
 }

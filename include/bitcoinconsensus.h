@@ -17,7 +17,14 @@
  * Return convention: 1 = valid, 0 = invalid or error; *err is written only when err != NULL.
  * Check order: flags -> deserialize -> nIn -> size -> (ERR_OK) -> script.
  * Every signature check runs on the GPU (HIP, gfx950); there is no CPU verification fallback.
- * Thread safety: reentrant; concurrent callers share the device under an internal lock.
+ * Thread safety: reentrant.  Each calling thread gets its own HIP stream, device arena, pinned
+ * staging buffer and kernel scratch per device (created on its first call, reused afterwards), so
+ * concurrent callers never share mutable device state; the only shared state is the read-only
+ * G table per device, built once under a lock.
+ * Device failure: a failed device round is retried once on a fresh batch.  If it fails again,
+ * bitcoinconsensus_verify_script[_with_amount] abort() the process (there is no verdict, and
+ * returning 0 would report a consensus failure for a transaction that may be valid);
+ * bitcoinconsensus_verify_batch returns -1 instead (see below).
  */
 #ifndef BCC_AMD_BITCOINCONSENSUS_H
 #define BCC_AMD_BITCOINCONSENSUS_H
@@ -80,10 +87,15 @@ typedef struct bcc_batch_item {
     unsigned int n_in;
 } bcc_batch_item;
 
+/* Engine-specific error code, written ONLY by bitcoinconsensus_verify_batch, for items whose
+ * verdict the device could not deliver (never by the single-item ABI, which aborts instead). */
+#define BCC_ERR_DEVICE_FAILURE 6
+
 /* Verifies n items with `flags`.  ret_out[i] / err_out[i] (err_out may be NULL) receive exactly
  * what bitcoinconsensus_verify_script_with_amount would return / write for item i.
- * Returns the number of valid items, or -1 if the device pipeline failed (then ret_out is 0 and
- * err_out is bitcoinconsensus_ERR_TX_DESERIALIZE for the unfinished items). */
+ * Returns the number of valid items, or -1 if the device pipeline failed twice in a row: then
+ * items the failed round left unfinished get ret_out 0 and err_out BCC_ERR_DEVICE_FAILURE, and
+ * every other item carries its final result. */
 long bitcoinconsensus_verify_batch(const bcc_batch_item* items, size_t n, unsigned int flags,
                                    int* ret_out, bitcoinconsensus_error* err_out);
 

@@ -13,7 +13,8 @@
 //                             depend/bitcoin/src/script/interpreter.cpp:1644-1676)
 //   * ref_schnorr_verify  -> secp256k1_schnorrsig_verify            secp256k1/src/modules/schnorrsig/main_impl.h:190-237
 //   * ref_sign / ref_pubkey_create / ref_schnorr_sign: fixture generation only
-//   * ref_bench_*         -> std::thread pool timing of the reference entry points (cpu_baseline)
+//   * ref_bench_* / ref_bulk_* -> dynamically chunked std::thread pool over the reference entry
+//                            points (cpu_baseline timing, bulk agreement checks)
 //
 // The shim contains no consensus logic of its own: every verdict comes from the reference.
 #include <script/bitcoinconsensus.h>
@@ -85,6 +86,32 @@ protected:
         return ok;
     }
 };
+
+// ---- CPU baseline timing: std::thread pool with DYNAMIC chunking ----
+// Workers pull chunks of CHUNK consecutive items from one atomic counter (rayon's work stealing
+// restated for a flat index space), so one long item (a many-input legacy tx) does not leave the
+// other threads idle behind a static partition.  Returns wall seconds; the per-item results are
+// written so the caller can cross-check verdicts.
+constexpr long CHUNK = 64;
+
+template <class F>
+double run_pool(int nthreads, long n, F f) {
+    auto t0 = std::chrono::steady_clock::now();
+    std::atomic<long> next{0};
+    std::vector<std::thread> pool;
+    auto worker = [&]() {
+        for (;;) {
+            long lo = next.fetch_add(CHUNK, std::memory_order_relaxed);
+            if (lo >= n) break;
+            long hi = lo + CHUNK < n ? lo + CHUNK : n;
+            for (long i = lo; i < hi; ++i) f(i);
+        }
+    };
+    for (int t = 1; t < nthreads; ++t) pool.emplace_back(worker);
+    worker();
+    for (auto& th : pool) th.join();
+    return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+}
 
 }  // namespace
 
@@ -192,28 +219,33 @@ int ref_schnorr_sign(const unsigned char* seckey32, const unsigned char* msg32,
     return secp256k1_schnorrsig_sign(sign_ctx(), sig64, msg32, &kp, nullptr, (void*)aux32);
 }
 
-// ---- CPU baseline timing: std::thread pool, static contiguous chunks (rayon-like) ----
-// items are given as concatenated blobs with offset arrays. Returns wall seconds; writes the
-// per-item return codes into ret (so the caller can also cross-check verdicts).
+// items are given as concatenated blobs with offset arrays (bitcoinconsensus_verify_script_
+// with_amount per item, exactly what the crate's verify() calls).
 double ref_bench_verify_script(int nthreads, long n, const unsigned char* spk_blob,
                                const long* spk_off, const unsigned char* tx_blob,
                                const long* tx_off, const int64_t* amounts,
                                const unsigned int* nin, unsigned int flags, int* ret) {
-    auto t0 = std::chrono::steady_clock::now();
-    std::vector<std::thread> pool;
-    for (int t = 0; t < nthreads; ++t) {
-        pool.emplace_back([=]() {
-            long lo = n * t / nthreads, hi = n * (t + 1) / nthreads;
-            for (long i = lo; i < hi; ++i) {
-                bitcoinconsensus_error e;
-                ret[i] = bitcoinconsensus_verify_script_with_amount(
-                    spk_blob + spk_off[i], (unsigned)(spk_off[i + 1] - spk_off[i]), amounts[i],
-                    tx_blob + tx_off[i], (unsigned)(tx_off[i + 1] - tx_off[i]), nin[i], flags, &e);
-            }
-        });
-    }
-    for (auto& th : pool) th.join();
-    return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    return run_pool(nthreads, n, [=](long i) {
+        bitcoinconsensus_error e;
+        ret[i] = bitcoinconsensus_verify_script_with_amount(
+            spk_blob + spk_off[i], (unsigned)(spk_off[i + 1] - spk_off[i]), amounts[i],
+            tx_blob + tx_off[i], (unsigned)(tx_off[i + 1] - tx_off[i]), nin[i], flags, &e);
+    });
+}
+
+// The same with the error code per item: ret[i] = result, err[i] = bitcoinconsensus_error
+// (bulk script-level agreement checks).
+double ref_bulk_verify_script(int nthreads, long n, const unsigned char* spk_blob,
+                              const long* spk_off, const unsigned char* tx_blob, const long* tx_off,
+                              const int64_t* amounts, const unsigned int* nin, unsigned int flags,
+                              int* ret, int* err) {
+    return run_pool(nthreads, n, [=](long i) {
+        bitcoinconsensus_error e = bitcoinconsensus_ERR_OK;
+        ret[i] = bitcoinconsensus_verify_script_with_amount(
+            spk_blob + spk_off[i], (unsigned)(spk_off[i + 1] - spk_off[i]), amounts[i],
+            tx_blob + tx_off[i], (unsigned)(tx_off[i + 1] - tx_off[i]), nin[i], flags, &e);
+        err[i] = (int)e;
+    });
 }
 
 // Tuple-level baseline: CPubKey::Verify over (pub, hash, sig) tuples. pub in 65-B slots with
@@ -221,18 +253,10 @@ double ref_bench_verify_script(int nthreads, long n, const unsigned char* spk_bl
 double ref_bench_pubkey_verify(int nthreads, long n, const unsigned char* pub65, const int* publen,
                                const unsigned char* hash32, const unsigned char* sig80,
                                const int* siglen, int* ret) {
-    auto t0 = std::chrono::steady_clock::now();
-    std::vector<std::thread> pool;
-    for (int t = 0; t < nthreads; ++t) {
-        pool.emplace_back([=]() {
-            long lo = n * t / nthreads, hi = n * (t + 1) / nthreads;
-            for (long i = lo; i < hi; ++i)
-                ret[i] = ref_pubkey_verify(pub65 + 65 * i, (size_t)publen[i], hash32 + 32 * i,
-                                           sig80 + 80 * i, (size_t)siglen[i]);
-        });
-    }
-    for (auto& th : pool) th.join();
-    return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    return run_pool(nthreads, n, [=](long i) {
+        ret[i] = ref_pubkey_verify(pub65 + 65 * i, (size_t)publen[i], hash32 + 32 * i,
+                                   sig80 + 80 * i, (size_t)siglen[i]);
+    });
 }
 
 // Tuple-level baseline / checker over blob inputs (uint64 offsets, n + 1 each): CPubKey::Verify.
@@ -240,37 +264,21 @@ double ref_bench_pubkey_verify_blob(int nthreads, long n, const unsigned char* p
                                     const uint64_t* pub_off, const unsigned char* hash32,
                                     const unsigned char* sig_blob, const uint64_t* sig_off,
                                     unsigned char* ret) {
-    auto t0 = std::chrono::steady_clock::now();
-    std::vector<std::thread> pool;
-    for (int t = 0; t < nthreads; ++t) {
-        pool.emplace_back([=]() {
-            long lo = n * t / nthreads, hi = n * (t + 1) / nthreads;
-            for (long i = lo; i < hi; ++i)
-                ret[i] = (unsigned char)ref_pubkey_verify(
-                    pub_blob + pub_off[i], (size_t)(pub_off[i + 1] - pub_off[i]), hash32 + 32 * i,
-                    sig_blob + sig_off[i], (size_t)(sig_off[i + 1] - sig_off[i]));
-        });
-    }
-    for (auto& th : pool) th.join();
-    return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    return run_pool(nthreads, n, [=](long i) {
+        ret[i] = (unsigned char)ref_pubkey_verify(
+            pub_blob + pub_off[i], (size_t)(pub_off[i + 1] - pub_off[i]), hash32 + 32 * i,
+            sig_blob + sig_off[i], (size_t)(sig_off[i + 1] - sig_off[i]));
+    });
 }
 
 // BIP340 baseline / checker: secp256k1_xonly_pubkey_parse + secp256k1_schnorrsig_verify per row.
 double ref_bench_schnorr_verify(int nthreads, long n, const unsigned char* sig64,
                                 const unsigned char* msg32, const unsigned char* xonly32,
                                 unsigned char* ret) {
-    auto t0 = std::chrono::steady_clock::now();
-    std::vector<std::thread> pool;
-    for (int t = 0; t < nthreads; ++t) {
-        pool.emplace_back([=]() {
-            long lo = n * t / nthreads, hi = n * (t + 1) / nthreads;
-            for (long i = lo; i < hi; ++i)
-                ret[i] = (unsigned char)ref_schnorr_verify(sig64 + 64 * i, msg32 + 32 * i,
-                                                           xonly32 + 32 * i);
-        });
-    }
-    for (auto& th : pool) th.join();
-    return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    return run_pool(nthreads, n, [=](long i) {
+        ret[i] = (unsigned char)ref_schnorr_verify(sig64 + 64 * i, msg32 + 32 * i,
+                                                   xonly32 + 32 * i);
+    });
 }
 
 }  // extern "C"

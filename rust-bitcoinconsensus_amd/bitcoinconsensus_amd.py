@@ -18,6 +18,7 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "librbc_amd.so")
+BENCH_LIB_PATH = os.path.join(_HERE, "librbc_bench.so")
 
 VERIFY_NONE = 0
 VERIFY_P2SH = 1 << 0
@@ -38,6 +39,11 @@ class Error(enum.IntEnum):
     ERR_TX_DESERIALIZE = 3
     ERR_AMOUNT_REQUIRED = 4
     ERR_INVALID_FLAGS = 5
+
+
+# Engine-specific code (include/bitcoinconsensus.h BCC_ERR_DEVICE_FAILURE), outside the mirrored
+# enum: only verify_batch_raw can report it, for items the device left without a verdict.
+ERR_DEVICE_FAILURE = 6
 
 
 class ConsensusError(Exception):
@@ -63,9 +69,28 @@ def lib():
         L.mi_ecdsa_verify_device.argtypes = [vp] * 7 + [sz, vp]
         L.mi_schnorr_verify_tuples.argtypes = [u8p, u8p, u8p, u8p, sz, ctypes.c_int]
         L.mi_schnorr_verify_device.argtypes = [vp] * 4 + [sz, vp]
-        L.mi_microbench.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_double)]
         u64p = ctypes.POINTER(ctypes.c_uint64)
         L.bcc_pubkey_verify_batch.argtypes = [u8p, u64p, u8p, u8p, u64p, u8p, sz, ctypes.c_int]
+        _bind_consensus(L)
+        L.bcc_source_hash.restype = ctypes.c_char_p
+        _lib = L
+    return _lib
+
+
+_blib = None
+
+
+def blib():
+    """Load librbc_bench.so (synthetic workloads, generators, microbenchmark: include/bcc_bench.h),
+    which links the product library; raises if it has not been built."""
+    global _blib
+    if _blib is None:
+        lib()
+        if not os.path.exists(BENCH_LIB_PATH):
+            raise ImportError(f"{BENCH_LIB_PATH} missing: build with `make -C {_HERE}`")
+        L = ctypes.CDLL(BENCH_LIB_PATH)
+        u8p, sz, vp, ui = ctypes.c_char_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_uint
+        L.mi_microbench.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_double)]
         L.bcc_tupleset_c4.argtypes = [sz, ctypes.c_uint64, ctypes.c_int]
         L.bcc_tupleset_c4.restype = vp
         L.bcc_tupleset_c5.argtypes = [sz, ctypes.c_uint64, u8p, u8p, u8p, u8p, sz, ctypes.c_int]
@@ -76,9 +101,38 @@ def lib():
         L.bcc_tupleset_run.argtypes = [vp, vp]
         L.bcc_tupleset_verdicts.argtypes = [vp, u8p]
         L.bcc_tupleset_view.argtypes = [vp, ctypes.POINTER(TuplesetHost)]
-        _bind_consensus(L)
-        _lib = L
-    return _lib
+        L.bcc_workload_p2wpkh.argtypes = [sz, ctypes.c_uint64, ctypes.c_int]
+        L.bcc_workload_p2wpkh.restype = vp
+        u32p = ctypes.POINTER(ctypes.c_uint32)
+        L.bcc_workload_block.argtypes = [u32p, u32p, sz, ctypes.c_uint64, ctypes.c_int]
+        L.bcc_workload_block.restype = vp
+        L.bcc_workload_items.argtypes = [vp, ctypes.POINTER(sz)]
+        L.bcc_workload_items.restype = ctypes.POINTER(BatchItem)
+        L.bcc_workload_free.argtypes = [vp]
+        L.bcc_workload_size.argtypes = [vp]
+        L.bcc_workload_size.restype = sz
+        for f in (L.bcc_workload_run, L.bcc_workload_run_sighash, L.bcc_workload_run_ecdsa):
+            f.argtypes = [vp, vp]
+        L.bcc_workload_verdicts.argtypes = [vp, u8p]
+        L.bcc_workload_from_items.argtypes = [ctypes.POINTER(BatchItem), sz, ui, ctypes.c_int]
+        L.bcc_workload_from_items.restype = vp
+        L.bcc_workload_tuple_items.argtypes = [vp, ctypes.POINTER(ctypes.c_uint32)]
+        L.bcc_workload_msgs.argtypes = [vp, u8p]
+        szp = ctypes.POINTER(sz)
+        L.bcc_workload_shape.argtypes = [vp, szp, szp, szp, szp, szp]
+        L.bcc_workload_item.argtypes = [vp, sz, u8p, szp, ctypes.POINTER(ctypes.c_int64), u8p, sz]
+        L.bcc_workload_item.restype = sz
+        L.mi_gen_pubkeys.argtypes = [u8p, sz, u8p, u8p, u8p, ctypes.c_int]
+        L.mi_gen_sign.argtypes = [u8p, u8p, u8p, sz, u8p, u8p, u8p, ctypes.c_int]
+        L.mi_gen_schnorr_sign.argtypes = [u8p, u8p, u8p, sz, u8p, u8p, u8p, ctypes.c_int]
+
+        _blib = L
+    return _blib
+
+
+def source_hash():
+    """Hash of the sources the loaded library was built from (Makefile / source_hash.py)."""
+    return lib().bcc_source_hash().decode()
 
 
 class BatchItem(ctypes.Structure):
@@ -116,28 +170,8 @@ def _bind_consensus(L):
                                                 ip, ip]
     L.bitcoinconsensus_verify_batch.restype = ctypes.c_long
     L.bcc_set_device.argtypes = [ctypes.c_int]
+    L.bcc_debug_fail_device_rounds.argtypes = [ctypes.c_int]
     L.bcc_last_batch_stats.argtypes = [ctypes.POINTER(BatchStats)]
-    vp, sz = ctypes.c_void_p, ctypes.c_size_t
-    L.bcc_workload_p2wpkh.argtypes = [sz, ctypes.c_uint64, ctypes.c_int]
-    L.bcc_workload_p2wpkh.restype = vp
-    u32p = ctypes.POINTER(ctypes.c_uint32)
-    L.bcc_workload_block.argtypes = [u32p, u32p, sz, ctypes.c_uint64, ctypes.c_int]
-    L.bcc_workload_block.restype = vp
-    L.bcc_workload_items.argtypes = [vp, ctypes.POINTER(sz)]
-    L.bcc_workload_items.restype = ctypes.POINTER(BatchItem)
-    L.bcc_workload_free.argtypes = [vp]
-    L.bcc_workload_size.argtypes = [vp]
-    L.bcc_workload_size.restype = sz
-    for f in (L.bcc_workload_run, L.bcc_workload_run_sighash, L.bcc_workload_run_ecdsa):
-        f.argtypes = [vp, vp]
-    L.bcc_workload_verdicts.argtypes = [vp, u8p]
-    szp = ctypes.POINTER(sz)
-    L.bcc_workload_shape.argtypes = [vp, szp, szp, szp, szp, szp]
-    L.bcc_workload_item.argtypes = [vp, sz, u8p, szp, ctypes.POINTER(ctypes.c_int64), u8p, sz]
-    L.bcc_workload_item.restype = sz
-    L.mi_gen_pubkeys.argtypes = [u8p, sz, u8p, u8p, u8p, ctypes.c_int]
-    L.mi_gen_sign.argtypes = [u8p, u8p, u8p, sz, u8p, u8p, u8p, ctypes.c_int]
-    L.mi_gen_schnorr_sign.argtypes = [u8p, u8p, u8p, sz, u8p, u8p, u8p, ctypes.c_int]
 
 
 class Workload:
@@ -147,25 +181,29 @@ class Workload:
     kind "block":  config C3, transactions shaped by `shape` = [(n_inputs, n_outputs), ...]
                    (one item per input)."""
 
-    def __init__(self, n=0, seed=0x5EED0001, device=0, kind="p2wpkh", shape=None):
-        if kind == "p2wpkh":
-            self.h = lib().bcc_workload_p2wpkh(n, seed, device)
+    def __init__(self, n=0, seed=0x5EED0001, device=0, kind="p2wpkh", shape=None, items=None,
+                 flags=VERIFY_ALL):
+        if kind == "items":  # any caller items, staged through the same first-round pass
+            arr, keep = _batch_items(items)
+            self.h = blib().bcc_workload_from_items(arr, len(keep[0]), flags & 0xffffffff, device)
+        elif kind == "p2wpkh":
+            self.h = blib().bcc_workload_p2wpkh(n, seed, device)
         elif kind == "block":
             nin = (ctypes.c_uint32 * len(shape))(*[a for a, _ in shape])
             nout = (ctypes.c_uint32 * len(shape))(*[b for _, b in shape])
-            self.h = lib().bcc_workload_block(nin, nout, len(shape), seed, device)
+            self.h = blib().bcc_workload_block(nin, nout, len(shape), seed, device)
         else:
             raise ValueError(kind)
         if not self.h:
             raise RuntimeError(f"bcc_workload_{kind} failed")
-        self.n = lib().bcc_workload_size(self.h)
+        self.n = blib().bcc_workload_size(self.h)
         self.kind = kind
 
     def verify_batch(self, flags=VERIFY_ALL):
         """bitcoinconsensus_verify_batch over all items (host interpreter + GPU rounds, end to
         end, host buffers as the drop-in receives them).  Returns (n_valid, ret bytes)."""
         cnt = ctypes.c_size_t(0)
-        items = lib().bcc_workload_items(self.h, ctypes.byref(cnt))
+        items = blib().bcc_workload_items(self.h, ctypes.byref(cnt))
         ret = (ctypes.c_int * max(1, cnt.value))()
         rc = lib().bitcoinconsensus_verify_batch(items, cnt.value, flags & 0xffffffff, ret, None)
         if rc < 0:
@@ -173,43 +211,59 @@ class Workload:
         return rc, bytes(memoryview(ret).cast("B"))[:: ctypes.sizeof(ctypes.c_int)][: cnt.value]
 
     def run(self, stream=None):
-        rc = lib().bcc_workload_run(self.h, stream)
+        rc = blib().bcc_workload_run(self.h, stream)
         if rc:
             raise RuntimeError(f"bcc_workload_run: {rc}")
 
     def run_sighash(self, stream=None):
-        rc = lib().bcc_workload_run_sighash(self.h, stream)
+        rc = blib().bcc_workload_run_sighash(self.h, stream)
         if rc:
             raise RuntimeError(f"bcc_workload_run_sighash: {rc}")
 
     def run_ecdsa(self, stream=None):
-        rc = lib().bcc_workload_run_ecdsa(self.h, stream)
+        rc = blib().bcc_workload_run_ecdsa(self.h, stream)
         if rc:
             raise RuntimeError(f"bcc_workload_run_ecdsa: {rc}")
 
     def verdicts(self):
         out = ctypes.create_string_buffer(max(1, self.n))
-        rc = lib().bcc_workload_verdicts(self.h, out)
+        rc = blib().bcc_workload_verdicts(self.h, out)
         if rc:
             raise RuntimeError(f"bcc_workload_verdicts: {rc}")
         return out.raw[: self.shape()["tuples"]]
 
+    def tuple_items(self):
+        """Item index of every staged tuple row."""
+        t = self.shape()["tuples"]
+        out = (ctypes.c_uint32 * max(1, t))()
+        if blib().bcc_workload_tuple_items(self.h, out):
+            raise RuntimeError("bcc_workload_tuple_items failed")
+        return list(out)[:t]
+
+    def msgs(self):
+        """The sighash rows (32 bytes per staged tuple) of the last run."""
+        t = self.shape()["tuples"]
+        out = ctypes.create_string_buffer(max(1, 32 * t))
+        if blib().bcc_workload_msgs(self.h, out):
+            raise RuntimeError("bcc_workload_msgs failed")
+        return out.raw[: 32 * t]
+
     def shape(self):
         v = [ctypes.c_size_t() for _ in range(5)]
-        lib().bcc_workload_shape(self.h, *[ctypes.byref(x) for x in v])
+        blib().bcc_workload_shape(self.h, *[ctypes.byref(x) for x in v])
         return dict(zip(("tuples", "sighash_blocks", "aux_blocks", "preimages", "aux_messages"),
                         (x.value for x in v)))
 
     def item(self, i):
         """(spent script, amount, tx bytes, input index) of item i."""
         cnt = ctypes.c_size_t(0)
-        it = lib().bcc_workload_items(self.h, ctypes.byref(cnt))[i]
+        it = blib().bcc_workload_items(self.h, ctypes.byref(cnt))[i]
         return (ctypes.string_at(it.script_pubkey, it.script_pubkey_len), it.amount,
                 ctypes.string_at(it.tx_to, it.tx_to_len), it.n_in)
 
     def free(self):
         if self.h:
-            lib().bcc_workload_free(self.h)
+            blib().bcc_workload_free(self.h)
             self.h = None
 
     def __del__(self):
@@ -248,10 +302,8 @@ def verify(spent_output, amount, spending_transaction, input_index):
     verify_with_flags(spent_output, amount, spending_transaction, input_index, VERIFY_ALL)
 
 
-def verify_batch(items, flags=VERIFY_ALL):
-    """items: iterable of (spent_output_script, amount, spending_transaction, input_index).
-    Returns a list of (ret, Error) equal to calling the C ABI once per item; all signature work
-    of the batch runs on the GPU in as few device rounds as the scripts allow."""
+def _batch_items(items):
+    """(BatchItem array, keep-alive buffers) for (spk, amount, tx, nin) tuples."""
     items = list(items)
     n = len(items)
     arr = (BatchItem * max(n, 1))()
@@ -266,18 +318,41 @@ def verify_batch(items, flags=VERIFY_ALL):
         keep.append(bs)
         arr[i] = BatchItem(ctypes.addressof(bs), len(spk), amount, ctypes.addressof(bt), len(tx),
                            nin & 0xffffffff)
+    return arr, (keep, txbufs)
+
+
+def verify_batch_raw(items, flags=VERIFY_ALL):
+    """bitcoinconsensus_verify_batch as is: (return code, [(ret, err int)]); rc is the number of
+    valid items, or -1 when the device failed (items it left unfinished carry
+    ERR_DEVICE_FAILURE)."""
+    arr, keep = _batch_items(items)
+    n = len(keep[0])
     ret = (ctypes.c_int * max(n, 1))()
     err = (ctypes.c_int * max(n, 1))()
     rc = lib().bitcoinconsensus_verify_batch(arr, n, flags & 0xffffffff, ret, err)
+    return rc, [(ret[i], err[i]) for i in range(n)]
+
+
+def verify_batch(items, flags=VERIFY_ALL):
+    """items: iterable of (spent_output_script, amount, spending_transaction, input_index).
+    Returns a list of (ret, Error) equal to calling the C ABI once per item; all signature work
+    of the batch runs on the GPU in as few device rounds as the scripts allow.  Raises
+    RuntimeError when the device failed (no verdict is ever reported for a device error)."""
+    rc, res = verify_batch_raw(items, flags)
     if rc < 0:
         raise RuntimeError("bitcoinconsensus_verify_batch: device pipeline failed")
-    return [(ret[i], Error(err[i])) for i in range(n)]
+    return [(r, Error(e)) for r, e in res]
 
 
 def last_batch_stats():
     s = BatchStats()
     lib().bcc_last_batch_stats(ctypes.byref(s))
     return {k: getattr(s, k) for k, _ in BatchStats._fields_}
+
+
+def debug_fail_device_rounds(rounds):
+    """Fault injection (tests): the next `rounds` device rounds fail (include/bcc_amd.h)."""
+    lib().bcc_debug_fail_device_rounds(rounds)
 
 
 def set_device(device):
@@ -337,7 +412,7 @@ class TupleSet:
                   "wrong_key")
 
     def __init__(self, n, kind="c4", seed=None, device=0, vectors=()):
-        L = lib()
+        L = blib()
         if kind == "c4":
             self.h = L.bcc_tupleset_c4(n, 0x5EED0004 if seed is None else seed, device)
         elif kind == "c5":
@@ -353,13 +428,13 @@ class TupleSet:
         self.kind, self.n = kind, n
 
     def run(self, stream=None):
-        rc = lib().bcc_tupleset_run(self.h, stream)
+        rc = blib().bcc_tupleset_run(self.h, stream)
         if rc != 0:
             raise RuntimeError(f"bcc_tupleset_run failed: {rc}")
 
     def verdicts(self):
         out = ctypes.create_string_buffer(max(self.n, 1))
-        if lib().bcc_tupleset_verdicts(self.h, out) != 0:
+        if blib().bcc_tupleset_verdicts(self.h, out) != 0:
             raise RuntimeError("bcc_tupleset_verdicts failed")
         return out.raw[: self.n]
 
@@ -368,7 +443,7 @@ class TupleSet:
         offsets (c4) or sig64/xonly32 (c5).  Valid while the set lives."""
         import numpy as np
         v = TuplesetHost()
-        lib().bcc_tupleset_view(self.h, ctypes.byref(v))
+        blib().bcc_tupleset_view(self.h, ctypes.byref(v))
         n = v.n
 
         def arr(ptr, count, dt=np.uint8):
@@ -399,7 +474,7 @@ class TupleSet:
 
     def free(self):
         if self.h:
-            lib().bcc_tupleset_free(self.h)
+            blib().bcc_tupleset_free(self.h)
             self.h = None
 
     def __del__(self):
@@ -445,7 +520,7 @@ def gen_schnorr_sign(d32, m32, k32, device=0):
     sig = ctypes.create_string_buffer(64 * max(n, 1))
     xo = ctypes.create_string_buffer(32 * max(n, 1))
     ok = ctypes.create_string_buffer(max(n, 1))
-    rc = lib().mi_gen_schnorr_sign(d32, m32, k32, n, sig, xo, ok, device)
+    rc = blib().mi_gen_schnorr_sign(d32, m32, k32, n, sig, xo, ok, device)
     if rc != 0:
         raise RuntimeError(f"mi_gen_schnorr_sign failed: hip error {rc}")
     return sig.raw[: 64 * n], xo.raw[: 32 * n], ok.raw[:n]
@@ -458,7 +533,7 @@ def set_chunk_lanes(lanes):
 
 def microbench(op, iters=4096):
     r = ctypes.c_double(0)
-    rc = lib().mi_microbench(op, iters, ctypes.byref(r))
+    rc = blib().mi_microbench(op, iters, ctypes.byref(r))
     if rc != 0:
         raise RuntimeError(f"mi_microbench failed: {rc}")
     return r.value

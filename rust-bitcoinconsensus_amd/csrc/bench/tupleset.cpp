@@ -14,10 +14,11 @@
 #include <thread>
 #include <vector>
 
-#include "../pipeline.h"
+#include "pipeline.h"
 #include "bcc_amd.h"
-#include "hashes.h"
-#include "tuples.h"
+#include "bcc_bench.h"
+#include "host/hashes.h"
+#include "host/tuples.h"
 
 using namespace bcc::host;
 

@@ -15,13 +15,14 @@
 #include <thread>
 #include <vector>
 
-#include "../pipeline.h"
+#include "pipeline.h"
 #include "bcc_amd.h"
-#include "engine.h"
-#include "hashes.h"
-#include "script.h"
-#include "sighash.h"
-#include "tx.h"
+#include "bcc_bench.h"
+#include "host/engine.h"
+#include "host/hashes.h"
+#include "host/script.h"
+#include "host/sighash.h"
+#include "host/tx.h"
 
 struct bcc_workload {
     int device = 0;
@@ -33,6 +34,8 @@ struct bcc_workload {
     std::vector<int64_t> amount;
     std::vector<uint32_t> item_tx, item_nin;
     std::vector<bcc_batch_item> items;  // borrowed pointers into the blobs above
+    unsigned flags = bcc::host::FLAGS_VERIFY_ALL;
+    std::vector<uint32_t> tuple_item;  // staged tuple row -> item
     bcc::DeviceBatch* batch = nullptr;
 };
 
@@ -132,6 +135,7 @@ int finish(bcc_workload* w) {
     unsigned T = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
     std::vector<bcc::SighashJobs> pj(T);
     std::vector<bcc::TupleRows> pr(T);
+    std::vector<std::vector<uint32_t>> ti(T);
     // split on transaction boundaries: items of one tx share its BIP143 aux messages
     std::vector<size_t> cut(T + 1, n);
     cut[0] = 0;
@@ -143,13 +147,15 @@ int finish(bcc_workload* w) {
     std::vector<std::thread> th;
     for (unsigned t = 0; t < T; t++)
         th.emplace_back([&, t]() {
-            build_first_round(w->items.data() + cut[t], cut[t + 1] - cut[t], FLAGS_VERIFY_ALL,
-                              pj[t], pr[t]);
+            build_first_round(w->items.data() + cut[t], cut[t + 1] - cut[t], w->flags, pj[t],
+                              pr[t], &ti[t]);
         });
     for (auto& x : th) x.join();
     bcc::SighashJobs jobs;
     bcc::TupleRows rows;
+    w->tuple_item.clear();
     for (unsigned t = 0; t < T; t++) {
+        for (uint32_t i : ti[t]) w->tuple_item.push_back(i + (uint32_t)cut[t]);
         append_round(jobs, rows, pj[t], pr[t]);
         pj[t] = bcc::SighashJobs();
         pr[t] = bcc::TupleRows();
@@ -347,6 +353,47 @@ size_t bcc_workload_item(const bcc_workload* w, size_t i, uint8_t* spk, size_t* 
 const bcc_batch_item* bcc_workload_items(const bcc_workload* w, size_t* n) {
     if (n) *n = w ? w->n : 0;
     return w ? w->items.data() : nullptr;
+}
+
+int bcc_workload_tuple_items(const bcc_workload* w, uint32_t* out) {
+    if (!w) return -1;
+    if (!w->tuple_item.empty()) memcpy(out, w->tuple_item.data(), 4 * w->tuple_item.size());
+    return 0;
+}
+
+int bcc_workload_msgs(bcc_workload* w, uint8_t* out) { return w->batch->fetch_msgs(out); }
+
+// Any caller items (copied): the engine's first interpreter round over them under `flags`,
+// staged like the synthetic workloads, so tests can run the exact benchmarked path on mutated
+// inputs.  Adjacent items with the same tx buffer share one copy (and its BIP143 aux hashes).
+bcc_workload* bcc_workload_from_items(const bcc_batch_item* items, size_t n, unsigned flags,
+                                      int device) {
+    auto* w = new bcc_workload();
+    w->device = device;
+    w->n = n;
+    w->flags = flags;
+    w->spkoff.assign(1, 0);
+    w->txoff.assign(1, 0);
+    w->amount.resize(n);
+    w->item_tx.resize(n);
+    w->item_nin.resize(n);
+    for (size_t i = 0; i < n; i++) {
+        const bcc_batch_item& it = items[i];
+        if (it.script_pubkey_len)
+            w->spkblob.insert(w->spkblob.end(), it.script_pubkey, it.script_pubkey + it.script_pubkey_len);
+        w->spkoff.push_back(w->spkblob.size());
+        if (i == 0 || it.tx_to != items[i - 1].tx_to || it.tx_to_len != items[i - 1].tx_to_len) {
+            if (it.tx_to_len) w->txblob.insert(w->txblob.end(), it.tx_to, it.tx_to + it.tx_to_len);
+            w->txoff.push_back(w->txblob.size());
+        }
+        w->item_tx[i] = (uint32_t)(w->txoff.size() - 2);
+        w->amount[i] = it.amount;
+        w->item_nin[i] = it.n_in;
+    }
+    w->spkblob.push_back(0);  // keep data() valid for empty blobs
+    w->txblob.push_back(0);
+    if (finish(w)) return nullptr;
+    return w;
 }
 
 }  // extern "C"

@@ -613,11 +613,39 @@ static SigScratch* shared_scratch() {
     return g_shared[dev];
 }
 
+// Per (thread, device) context of the synchronous host-buffer entries: a stream, kernel scratch
+// and one device + one pinned host buffer, grown on demand and reused by every later call (no
+// per-call allocation; inputs go to HBM in one DMA copy from the pinned image).
 struct ThreadCtx {
     SigScratch sc;
     hipStream_t stream = nullptr;
+    int dev = -1;
+    void* dbuf = nullptr;
+    size_t dcap = 0;
+    void* hbuf = nullptr;
+    size_t hcap = 0;
     ~ThreadCtx() {
+        if (dev >= 0) (void)hipSetDevice(dev);
         if (stream) (void)hipStreamDestroy(stream);
+        if (dbuf) (void)hipFree(dbuf);
+        if (hbuf) (void)hipHostFree(hbuf);
+    }
+    int reserve(size_t bytes) {
+        if (bytes > dcap) {
+            if (dbuf) BCC_HIP_TRY(hipFree(dbuf));
+            dbuf = nullptr;
+            dcap = 0;
+            BCC_HIP_TRY(hipMalloc(&dbuf, bytes));
+            dcap = bytes;
+        }
+        if (bytes > hcap) {
+            if (hbuf) BCC_HIP_TRY(hipHostFree(hbuf));
+            hbuf = nullptr;
+            hcap = 0;
+            BCC_HIP_TRY(hipHostMalloc(&hbuf, bytes, hipHostMallocDefault));
+            hcap = bytes;
+        }
+        return 0;
     }
 };
 
@@ -626,6 +654,7 @@ static int thread_ctx(int device, ThreadCtx** out) {
     if (device < 0 || device >= 64) return (int)hipErrorInvalidDevice;
     if (!ctx[device]) {
         auto c = std::make_unique<ThreadCtx>();
+        c->dev = device;
         BCC_HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
         ctx[device] = std::move(c);
     }
@@ -667,68 +696,71 @@ int mi_schnorr_verify_device(const uint8_t* d_sig64, const uint8_t* d_msg32,
     return schnorr_launch(*sc, d_sig64, d_msg32, d_xonly32, d_verdict, n, stream);
 }
 
+static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
 // BIP340 host-buffer entry: n rows of sig64 / msg32 / xonly32; synchronous on `device`.
 int mi_schnorr_verify_tuples(const uint8_t* sig64, const uint8_t* msg32, const uint8_t* xonly32,
                              uint8_t* verdict, size_t n, int device) {
     if (n == 0) return 0;
     BCC_HIP_TRY(hipSetDevice(device));
-    uint8_t* d = nullptr;
-    size_t vbytes = (n + 255) & ~(size_t)255;
-    BCC_HIP_TRY(hipMalloc(&d, 128 * n + vbytes));
-    uint8_t *d_sig = d, *d_m = d + 64 * n, *d_pk = d_m + 32 * n, *d_v = d_pk + 32 * n;
-    int rc = 0;
     ThreadCtx* ctx = nullptr;
-    if ((rc = (int)hipMemcpy(d_sig, sig64, 64 * n, hipMemcpyHostToDevice)) ||
-        (rc = (int)hipMemcpy(d_m, msg32, 32 * n, hipMemcpyHostToDevice)) ||
-        (rc = (int)hipMemcpy(d_pk, xonly32, 32 * n, hipMemcpyHostToDevice)) ||
-        (rc = thread_ctx(device, &ctx)) ||
-        (rc = schnorr_launch(ctx->sc, d_sig, d_m, d_pk, d_v, n, ctx->stream)) ||
-        (rc = (int)hipStreamSynchronize(ctx->stream)) ||
-        (rc = (int)hipMemcpy(verdict, d_v, n, hipMemcpyDeviceToHost))) {
+    if (int e = thread_ctx(device, &ctx)) return e;
+    const size_t o_m = align256(64 * n), o_pk = o_m + align256(32 * n), o_v = o_pk + align256(32 * n);
+    const size_t total = o_v + align256(n);
+    if (int e = ctx->reserve(total)) return e;
+    uint8_t* h = (uint8_t*)ctx->hbuf;
+    uint8_t* d = (uint8_t*)ctx->dbuf;
+    memcpy(h, sig64, 64 * n);
+    memcpy(h + o_m, msg32, 32 * n);
+    memcpy(h + o_pk, xonly32, 32 * n);
+    int rc = 0;
+    if ((rc = (int)hipMemcpyAsync(d, h, o_v, hipMemcpyHostToDevice, ctx->stream)) ||
+        (rc = schnorr_launch(ctx->sc, d, d + o_m, d + o_pk, d + o_v, n, ctx->stream)) ||
+        (rc = (int)hipMemcpyAsync(h + o_v, d + o_v, n, hipMemcpyDeviceToHost, ctx->stream)) ||
+        (rc = (int)hipStreamSynchronize(ctx->stream))) {
         fprintf(stderr, "[bcc] mi_schnorr_verify_tuples failed: %d\n", rc);
+        return rc;
     }
-    (void)hipFree(d);
-    return rc;
+    memcpy(verdict, h + o_v, n);
+    return 0;
 }
 
 // Host-buffer entry (the inner C ABI of SURVEY §8b): pub65[n] = header byte || x || y (y ignored
 // for 02/03; header 0 = rejected by the caller's CPubKey length filter), msg32/r32/s32 big-endian.
-// Copies in, verifies on `device`, copies verdicts out. Synchronous and reentrant: each calling
-// thread has its own stream and scratch.
+// Copies in (one DMA copy from the thread's pinned image), verifies on `device`, copies verdicts
+// out. Synchronous and reentrant: each calling thread has its own stream, scratch and buffers.
 int mi_ecdsa_verify_tuples(const uint8_t* pub65, const uint8_t* msg32, const uint8_t* r32,
                            const uint8_t* s32, uint8_t* verdict, size_t n, int device) {
     if (n == 0) return 0;
     BCC_HIP_TRY(hipSetDevice(device));
-    uint8_t* d = nullptr;
-    // layout: tag | x | y | r | s | m | verdict  (32-byte rows 256-byte aligned)
-    size_t tag_bytes = (n + 255) & ~(size_t)255;
-    size_t row = 32 * n;
-    size_t total = tag_bytes + 5 * row + tag_bytes;
-    BCC_HIP_TRY(hipMalloc(&d, total));
-    uint8_t *d_tag = d, *d_x = d + tag_bytes, *d_y = d_x + row, *d_r = d_y + row, *d_s = d_r + row,
-            *d_m = d_s + row, *d_v = d_m + row;
-    std::vector<uint8_t> tag(n), xs(row), ys(row);
-    for (size_t i = 0; i < n; i++) {
-        tag[i] = pub65[65 * i];
-        memcpy(&xs[32 * i], pub65 + 65 * i + 1, 32);
-        memcpy(&ys[32 * i], pub65 + 65 * i + 33, 32);
-    }
-    int rc = 0;
     ThreadCtx* ctx = nullptr;
-    if ((rc = (int)hipMemcpy(d_tag, tag.data(), n, hipMemcpyHostToDevice)) ||
-        (rc = (int)hipMemcpy(d_x, xs.data(), row, hipMemcpyHostToDevice)) ||
-        (rc = (int)hipMemcpy(d_y, ys.data(), row, hipMemcpyHostToDevice)) ||
-        (rc = (int)hipMemcpy(d_r, r32, row, hipMemcpyHostToDevice)) ||
-        (rc = (int)hipMemcpy(d_s, s32, row, hipMemcpyHostToDevice)) ||
-        (rc = (int)hipMemcpy(d_m, msg32, row, hipMemcpyHostToDevice)) ||
-        (rc = thread_ctx(device, &ctx)) ||
-        (rc = ecdsa_launch(ctx->sc, d_tag, d_x, d_y, d_r, d_s, d_m, d_v, n, ctx->stream)) ||
-        (rc = (int)hipStreamSynchronize(ctx->stream)) ||
-        (rc = (int)hipMemcpy(verdict, d_v, n, hipMemcpyDeviceToHost))) {
-        fprintf(stderr, "[bcc] mi_ecdsa_verify_tuples failed: %d\n", rc);
+    if (int e = thread_ctx(device, &ctx)) return e;
+    // layout: tag | x | y | r | s | m | verdict  (rows 256-byte aligned)
+    const size_t tagb = align256(n), row = align256(32 * n);
+    const size_t o_x = tagb, o_y = o_x + row, o_r = o_y + row, o_s = o_r + row, o_m = o_s + row,
+                 o_v = o_m + row, total = o_v + tagb;
+    if (int e = ctx->reserve(total)) return e;
+    uint8_t* h = (uint8_t*)ctx->hbuf;
+    uint8_t* d = (uint8_t*)ctx->dbuf;
+    for (size_t i = 0; i < n; i++) {
+        h[i] = pub65[65 * i];
+        memcpy(h + o_x + 32 * i, pub65 + 65 * i + 1, 32);
+        memcpy(h + o_y + 32 * i, pub65 + 65 * i + 33, 32);
     }
-    (void)hipFree(d);
-    return rc;
+    memcpy(h + o_r, r32, 32 * n);
+    memcpy(h + o_s, s32, 32 * n);
+    memcpy(h + o_m, msg32, 32 * n);
+    int rc = 0;
+    if ((rc = (int)hipMemcpyAsync(d, h, o_v, hipMemcpyHostToDevice, ctx->stream)) ||
+        (rc = ecdsa_launch(ctx->sc, d, d + o_x, d + o_y, d + o_r, d + o_s, d + o_m, d + o_v, n,
+                           ctx->stream)) ||
+        (rc = (int)hipMemcpyAsync(h + o_v, d + o_v, n, hipMemcpyDeviceToHost, ctx->stream)) ||
+        (rc = (int)hipStreamSynchronize(ctx->stream))) {
+        fprintf(stderr, "[bcc] mi_ecdsa_verify_tuples failed: %d\n", rc);
+        return rc;
+    }
+    memcpy(verdict, h + o_v, n);
+    return 0;
 }
 
 }  // extern "C"

@@ -9,7 +9,9 @@
 // seen (e.g. the next multisig key), until a run needs no unknown verdict.  This reproduces the
 // reference's verdict-dependent control flow (CHECKMULTISIG key advance, CHECKSIG NOT) exactly.
 #include <algorithm>
+#include <atomic>
 #include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -22,6 +24,7 @@
 #include "bcc_amd.h"
 #include "bitcoinconsensus.h"
 #include "engine.h"
+#include "hashes.h"
 #include "script.h"
 #include "sighash.h"
 
@@ -44,6 +47,17 @@ int current_device() {
 
 thread_local bcc_batch_stats t_stats;
 
+// Fault injection (tests): the next N device rounds of any thread fail as if the HIP runtime had
+// returned an error (bcc_debug_fail_device_rounds, or BCC_FAULT_INJECT at load time).
+std::atomic<int> g_fail_rounds{[] {
+    const char* e = getenv("BCC_FAULT_INJECT");
+    return e ? atoi(e) : 0;
+}()};
+
+// Largest padded-message / template / code blob one device round may stage: the device job
+// records address them with 32-bit byte offsets (pipeline.h PatchRec / TplJob).
+constexpr size_t ROUND_BLOB_LIMIT = ((size_t)1 << 32) - ((size_t)1 << 24);
+
 struct TxEntry {
     Tx tx;
     bool ok = false;
@@ -59,11 +73,13 @@ struct Item {
     bitcoinconsensus_error err = bitcoinconsensus_ERR_OK;
     bool active = false;  // needs (another) interpreter run
     bool result = false;
+    uint32_t runs = 0;    // interpreter runs so far in this call
     // checks seen by this item's runs: tuple key -> 0/1 known verdict, or -2 - r: deferred as
     // row r of the current round.  A flat list (an input makes a handful of checks, so a linear
     // scan beats a hash map); the key bytes live in the item's shard's key arena (Round::keys).
     struct Check {
-        uint32_t off, len;
+        uint64_t off;  // into the shard's key arena (whole call: may exceed 4 GiB)
+        uint32_t len;
         int32_t v;
     };
     std::vector<Check> cache;
@@ -76,19 +92,30 @@ struct Pending {
 };
 
 // Appends the identity of a signature check (sigversion, pubkey, signature, scriptCode) to the
-// key arena; returns its length.
+// key arena; returns its length.  A scriptCode longer than 64 bytes enters as its SHA-256 (the
+// reference's own signature cache keys entries by a SHA-256 over the check's inputs,
+// script/sigcache.cpp ComputeEntryECDSA), so a key costs at most ~1.1 KB however large the
+// script: pushes are <= 520 bytes (script.h MAX_SCRIPT_ELEMENT_SIZE).
 uint32_t append_key(std::vector<uint8_t>& a, const Bytes& pub, const Bytes& sig, const Bytes& code,
                     SigVersion sv) {
     const size_t k0 = a.size();
-    auto put = [&](const Bytes& b) {
-        uint32_t n = (uint32_t)b.size();
+    auto put = [&](const uint8_t* p, size_t len) {
+        uint32_t n = (uint32_t)len;
         a.insert(a.end(), (const uint8_t*)&n, (const uint8_t*)&n + 4);
-        a.insert(a.end(), b.begin(), b.end());
+        a.insert(a.end(), p, p + len);
     };
     a.push_back((uint8_t)sv);
-    put(pub);
-    put(sig);
-    put(code);
+    put(pub.data(), pub.size());
+    put(sig.data(), sig.size());
+    if (code.size() > 64) {
+        uint8_t d[32];
+        sha256(code.data(), code.size(), d);
+        a.push_back(1);
+        put(d, 32);
+    } else {
+        a.push_back(0);
+        put(code.data(), code.size());
+    }
     return (uint32_t)(a.size() - k0);
 }
 
@@ -100,6 +127,7 @@ public:
     DeferringChecker(Round& rd, uint32_t idx, Item& it) : rd_(rd), idx_(idx), it_(it) {}
     bool check_ecdsa(const Bytes& sig, const Bytes& pub, const Bytes& code, SigVersion sv) override;
     void hint_ecdsa(const Bytes& sig, const Bytes& pub, const Bytes& code, SigVersion sv) override;
+    bool hint_all() const override { return it_.runs > 1; }  // a re-run: queue every pair
     bool check_locktime(int64_t n) override { return tx_check_locktime(it_.tx->tx, it_.in->n_in, n); }
     bool check_sequence(int64_t n) override { return tx_check_sequence(it_.tx->tx, it_.in->n_in, n); }
 
@@ -127,7 +155,7 @@ public:
     // without making the item's finality depend on it.
     bool defer(uint32_t item_idx, Item& it, const Bytes& sig, const Bytes& pub, const Bytes& code,
                SigVersion sv, bool consult) {
-        const uint32_t koff = (uint32_t)keys.size();
+        const uint64_t koff = keys.size();
         const uint32_t klen = append_key(keys, pub, sig, code, sv);
         for (const Item::Check& c : it.cache) {
             if (c.len != klen || memcmp(&keys[c.off], &keys[koff], klen) != 0) continue;
@@ -303,6 +331,7 @@ void prepare(BatchState& b, const bcc_batch_item* items, size_t n, unsigned flag
                 it.ret = 0;
                 it.active = false;
                 it.result = false;
+                it.runs = 0;
                 it.cache.clear();
                 it.pending.clear();
                 if (!flags_ok) it.err = bitcoinconsensus_ERR_INVALID_FLAGS;
@@ -318,14 +347,15 @@ void prepare(BatchState& b, const bcc_batch_item* items, size_t n, unsigned flag
     });
 }
 
-// Interpreter pass over the active items of one shard; deferred checks land in rd.  Returns
-// whether any item ran.
+// Interpreter pass over the active items of one shard (idx: the shard's items that need a run);
+// deferred checks land in rd.  Returns whether any item ran.
 bool interpret_shard(BatchState& b, const std::vector<uint32_t>& idx, Round& rd) {
     bool any = false;
     for (uint32_t i : idx) {
         Item& it = b.st[i];
         if (!it.active) continue;
         any = true;
+        it.runs++;
         it.pending.clear();
         DeferringChecker chk(rd, i, it);
         const TxIn& in = it.tx->tx.vin[it.in->n_in];
@@ -364,10 +394,66 @@ std::vector<std::vector<uint32_t>> make_shards(const BatchState& b, unsigned T) 
 thread_local BatchState tl_state;
 thread_local std::vector<Round> tl_rounds;
 
-// Runs the batch; fills ret/err per item.  Returns -1 if the device pipeline failed.
+// One device round over the parts [p0, p1): fault injection first, then the device pipeline.
+int device_round(int dev, const SighashJobs* const* pj, const TupleRows* const* pr, size_t P,
+                 uint8_t* verdict, double* stage_s) {
+    for (int f = g_fail_rounds.load(); f > 0;)
+        if (g_fail_rounds.compare_exchange_weak(f, f - 1)) return 719;  // hipErrorLaunchFailure
+    return gpu_verify_parts(dev, pj, pr, P, verdict, stage_s);
+}
+
+// The round's shards as device batches whose blobs stay under ROUND_BLOB_LIMIT (the device job
+// records use 32-bit byte offsets): consecutive shards are grouped greedily; a single shard above
+// the limit is an error (reported, never silently truncated).  A failed group is retried once on
+// a fresh device batch (gpu_verify_parts drops the failed one).  Returns 0 or the error.
+int run_device_round(int dev, const std::vector<Round>& rds, unsigned T,
+                     const std::vector<size_t>& row0, uint8_t* verdict, double* stage_total) {
+    unsigned g0 = 0;
+    while (g0 < T) {
+        size_t sz[4] = {0, 0, 0, 0};
+        unsigned g1 = g0;
+        for (; g1 < T; g1++) {
+            const SighashJobs& j = rds[g1].jobs;
+            const size_t add[4] = {j.aux.size(), j.pre.size(), j.tpl.size(), j.code.size()};
+            bool fits = true;
+            for (int k = 0; k < 4; k++) fits &= sz[k] + add[k] <= ROUND_BLOB_LIMIT;
+            if (!fits) break;
+            for (int k = 0; k < 4; k++) sz[k] += add[k];
+        }
+        if (g1 == g0) {
+            fprintf(stderr, "[bcc] verify_batch: one shard's sighash jobs exceed %zu bytes\n",
+                    ROUND_BLOB_LIMIT);
+            return (int)1;  // hipErrorInvalidValue
+        }
+        std::vector<const SighashJobs*> pj;
+        std::vector<const TupleRows*> pr;
+        for (unsigned t = g0; t < g1; t++) {
+            pj.push_back(&rds[t].jobs);
+            pr.push_back(&rds[t].rows);
+        }
+        double st = 0;
+        int e = device_round(dev, pj.data(), pr.data(), pj.size(), verdict + row0[g0], &st);
+        if (e != 0) {
+            fprintf(stderr, "[bcc] verify_batch: device round failed (hip error %d), retrying\n", e);
+            t_stats.device_retries++;
+            e = device_round(dev, pj.data(), pr.data(), pj.size(), verdict + row0[g0], &st);
+            if (e != 0) {
+                fprintf(stderr, "[bcc] verify_batch: device round failed again (hip error %d)\n", e);
+                return e;
+            }
+        }
+        *stage_total += st;
+        g0 = g1;
+    }
+    return 0;
+}
+
+// Runs the batch; fills ret/err per item.  Returns -1 if the device pipeline failed twice in a
+// row for some round: the items that round left unfinished get ret 0 and BCC_ERR_DEVICE_FAILURE
+// (never a consensus verdict); all other items carry their final results.
 // Host work (deserialization, interpreter passes, preimage building) runs on up to
 // host_threads() threads over whole-transaction shards; each round's deferred checks of all
-// shards go to the GPU as one batch.
+// shards go to the GPU together.  Only the items that need another run take part in a round.
 long run_batch(const bcc_batch_item* items, size_t n, unsigned flags, int* ret_out,
                bitcoinconsensus_error* err_out) {
     using clk = std::chrono::steady_clock;
@@ -387,6 +473,10 @@ long run_batch(const bcc_batch_item* items, size_t n, unsigned flags, int* ret_o
     auto& st = b.st;
     const int dev = current_device();
     const auto shards = make_shards(b, T);
+    std::vector<std::vector<uint32_t>> run_list(T), next_list(T);
+    for (unsigned t = 0; t < T; t++)
+        for (uint32_t i : shards[t])
+            if (st[i].active) run_list[t].push_back(i);
     if (rds.size() < T) rds.resize(T);
     for (unsigned t = 0; t < T; t++) {
         rds[t].keys.clear();
@@ -400,7 +490,7 @@ long run_batch(const bcc_batch_item* items, size_t n, unsigned flags, int* ret_o
         auto i0 = clk::now();
         run_threads(T, [&](unsigned t) {
             rds[t].reset();
-            ran[t] = interpret_shard(b, shards[t], rds[t]);
+            ran[t] = interpret_shard(b, run_list[t], rds[t]);
         });
         t_stats.interpret_seconds += since(i0);
         size_t npend = 0;
@@ -412,13 +502,7 @@ long run_batch(const bcc_batch_item* items, size_t n, unsigned flags, int* ret_o
         }
         row0[T] = npend;
         if (!any || npend == 0) break;
-        // one device batch for the whole round: the shards' jobs are concatenated straight into
-        // the pinned staging image (DeviceBatch::stage_parts), no merged host copy
-        std::vector<const SighashJobs*> pj(T);
-        std::vector<const TupleRows*> pr(T);
         for (unsigned t = 0; t < T; t++) {
-            pj[t] = &rds[t].jobs;
-            pr[t] = &rds[t].rows;
             t_stats.preimages += rds[t].jobs.pre_off.size() + rds[t].jobs.tjobs.size();
             t_stats.aux_messages += rds[t].jobs.aux_off.size();
         }
@@ -427,15 +511,17 @@ long run_batch(const bcc_batch_item* items, size_t n, unsigned flags, int* ret_o
         auto g0 = clk::now();
         verdict.assign(npend, 0);
         double stage_s = 0;
-        int e = gpu_verify_parts(dev, pj.data(), pr.data(), T, verdict.data(), &stage_s);
+        int e = run_device_round(dev, rds, T, row0, verdict.data(), &stage_s);
         t_stats.stage_seconds += stage_s;
         gpu_s += std::chrono::duration<double>(clk::now() - g0).count();
         if (e != 0) {
             status = -1;
-            for (auto& it : st)
-                if (!it.pending.empty()) {
+            for (unsigned t = 0; t < T; t++)
+                for (uint32_t i : run_list[t]) {
+                    Item& it = st[i];
+                    if (it.pending.empty()) continue;  // this run consulted no deferred check
                     it.result = false;
-                    it.err = bitcoinconsensus_ERR_TX_DESERIALIZE;
+                    it.err = (bitcoinconsensus_error)BCC_ERR_DEVICE_FAILURE;
                     it.pending.clear();
                 }
             break;
@@ -445,13 +531,18 @@ long run_batch(const bcc_batch_item* items, size_t n, unsigned flags, int* ret_o
             const uint8_t* v = verdict.data() + row0[t];
             for (size_t k = 0; k < rd.pending.size(); k++)
                 st[rd.pending[k].item].cache[rd.pending[k].slot].v = v[k] ? 1 : 0;
-            for (uint32_t i : shards[t]) {
+            next_list[t].clear();
+            for (uint32_t i : run_list[t]) {
                 Item& it = st[i];
                 if (it.pending.empty()) continue;
                 bool all_true = true;
                 for (uint32_t k : it.pending) all_true &= v[k] != 0;
-                if (!all_true) it.active = true;  // speculation was wrong somewhere: re-run
+                if (!all_true) {  // speculation was wrong somewhere: re-run
+                    it.active = true;
+                    next_list[t].push_back(i);
+                }
             }
+            run_list[t].swap(next_list[t]);
         });
     }
     for (unsigned t = 0; t < T; t++) t_stats.host_rejected += rds[t].host_rejected;
@@ -555,10 +646,21 @@ int bitcoinconsensus_verify_script_with_amount(const unsigned char* scriptPubKey
     bcc_batch_item item{scriptPubKey, scriptPubKeyLen, amount, txTo, txToLen, nIn};
     int ret = 0;
     bitcoinconsensus_error e = bitcoinconsensus_ERR_OK;
+    long rc;
     try {
-        run_batch(&item, 1, flags, &ret, &e);
+        rc = run_batch(&item, 1, flags, &ret, &e);
     } catch (...) {
         return set_err(err, bitcoinconsensus_ERR_TX_DESERIALIZE);
+    }
+    if (rc < 0) {
+        // The device failed twice in a row: there is no verdict, and the reference ABI has no
+        // code for "no verdict" (every error it reports is about the transaction, bitcoinconsensus.cpp
+        // :83-100).  Reporting 0 would reject a possibly valid spend as a consensus failure, so the
+        // call fails loudly instead, as libsecp256k1's illegal-argument callback does
+        // (secp256k1.c:45-54).  bitcoinconsensus_verify_batch reports the same condition as -1.
+        fprintf(stderr, "[bcc] bitcoinconsensus_verify_script_with_amount: GPU unavailable, no "
+                        "verdict; aborting\n");
+        abort();
     }
     // set_error semantics (bitcoinconsensus.cpp:58-63): errors return 0 and write *err;
     // a completed script run writes ERR_OK
@@ -593,6 +695,8 @@ long bitcoinconsensus_verify_batch(const bcc_batch_item* items, size_t n, unsign
         return -1;
     }
 }
+
+void bcc_debug_fail_device_rounds(int rounds) { g_fail_rounds.store(rounds > 0 ? rounds : 0); }
 
 void bcc_release_thread_state(void) {
     tl_state = BatchState();

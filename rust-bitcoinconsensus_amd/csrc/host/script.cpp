@@ -522,9 +522,10 @@ bool eval_script(std::vector<Bytes>& stack, const uint8_t* script, size_t script
                         }
                         // candidate pairs: sig k can only meet keys k .. k + nkeys - nsigs
                         // (the loop below never skips a signature); queue them all at once when
-                        // that is at most 2 x nkeys checks, so a batching checker needs no
-                        // extra round for the key advance
-                        if (nsigs > 0 && (long)nsigs * (nkeys - nsigs + 1) <= 2L * nkeys) {
+                        // that is at most 2 x nkeys checks (or the checker asks for all), so a
+                        // batching checker needs no extra round for the key advance
+                        if (nsigs > 0 && (checker.hint_all() ||
+                                          (long)nsigs * (nkeys - nsigs + 1) <= 2L * nkeys)) {
                             for (int k = 0; k < nsigs; k++) {
                                 const Bytes& sg = STACKTOP(-isig - k);
                                 if (sg.empty() || ((flags & FLAG_DERSIG) && !is_valid_signature_encoding(sg)))

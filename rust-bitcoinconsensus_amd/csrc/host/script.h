@@ -82,6 +82,10 @@ public:
     // A check the script may consult later in the same CHECKMULTISIG (a candidate (sig, key)
     // pair); a batching checker may queue it now.  Must not change any verdict.
     virtual void hint_ecdsa(const Bytes&, const Bytes&, const Bytes&, SigVersion) {}
+    // Offer EVERY candidate pair of a CHECKMULTISIG, not only when there are few: a batching
+    // checker turns this on for items that already needed a re-run, so that the key advance of
+    // an m-of-n with many keys costs at most one more device round.
+    virtual bool hint_all() const { return false; }
     virtual bool check_locktime(int64_t n) = 0;
     virtual bool check_sequence(int64_t n) = 0;
 };

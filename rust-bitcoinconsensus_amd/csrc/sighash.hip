@@ -9,6 +9,7 @@
 #include <thread>
 #include <vector>
 #include <cstring>
+#include <cstdio>
 
 #include "gpu_common.h"
 #include "pipeline.h"
@@ -247,6 +248,13 @@ int DeviceBatch::stage_parts(const SighashJobs* const* J, const TupleRows* const
         tj0[p + 1] = tj0[p] + J[p]->tjobs.size();
         for (const auto& t : J[p]->tjobs) tjblk += t.nblk;
     }
+    if (auxb0[P] >= ((size_t)1 << 32) || preb0[P] >= ((size_t)1 << 32) ||
+        tpl0[P] >= ((size_t)1 << 32) || code0[P] >= ((size_t)1 << 32) ||
+        row0[P] >= ((size_t)1 << 32)) {
+        // the job records (PatchRec, TplJob, offsets) are 32-bit: refuse, never wrap
+        fprintf(stderr, "[bcc] DeviceBatch::stage_parts: a job blob exceeds 4 GiB; split the round\n");
+        return (int)hipErrorInvalidValue;
+    }
     n_rows_ = row0[P];
     n_pre_ = prei0[P];
     n_aux_ = auxi0[P];
@@ -436,11 +444,13 @@ int gpu_verify_parts(int device, const SighashJobs* const* jobs, const TupleRows
     if (!cache[device]) cache[device] = std::make_unique<DeviceBatch>(device);
     DeviceBatch& b = *cache[device];
     auto t0 = std::chrono::steady_clock::now();
-    if (int e = b.stage_parts(jobs, rows, parts)) return e;
-    if (stage_seconds)
+    int e = b.stage_parts(jobs, rows, parts);
+    if (!e && stage_seconds)
         *stage_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-    if (int e = b.run(nullptr)) return e;
-    return b.fetch_verdicts(verdict);
+    if (!e) e = b.run(nullptr);
+    if (!e) e = b.fetch_verdicts(verdict);
+    if (e) cache[device].reset();  // a retry starts from a fresh batch (streams, arena, scratch)
+    return e;
 }
 
 }  // namespace bcc

@@ -114,6 +114,9 @@ class Reference:
         L.ref_bench_pubkey_verify_blob.restype = ctypes.c_double
         L.ref_bench_schnorr_verify.argtypes = [ctypes.c_int, ctypes.c_long] + [vp] * 4
         L.ref_bench_schnorr_verify.restype = ctypes.c_double
+        L.ref_bulk_verify_script.argtypes = [ctypes.c_int, ctypes.c_long] + [vp] * 6 + [
+            ctypes.c_uint, vp, vp]
+        L.ref_bulk_verify_script.restype = ctypes.c_double
 
     def verify_script_with_amount(self, spk, amount, tx, nin, flags):
         e = ctypes.c_int(0)
@@ -131,6 +134,32 @@ class Reference:
 
     def schnorr_verify(self, sig64, msg32, xonly32):
         return self.L.ref_schnorr_verify(sig64, msg32, xonly32)
+
+    def bulk_verify_script(self, items, flags, threads=None):
+        """bitcoinconsensus_verify_script_with_amount over (spk, amount, tx, nin) items on a
+        dynamically chunked thread pool.  Returns ([(ret, err)], wall seconds)."""
+        import numpy as np
+        items = list(items)
+        n = len(items)
+        if threads is None:
+            threads = max(1, min(16, len(os.sched_getaffinity(0))))
+
+        def blob(parts):
+            off = np.zeros(len(parts) + 1, np.int64)
+            off[1:] = np.cumsum([len(p) for p in parts])
+            return np.frombuffer(b"".join(parts) + b"\0", np.uint8), off
+
+        sb, so = blob([bytes(it[0]) for it in items])
+        tb, to = blob([bytes(it[2]) for it in items])
+        am = np.array([it[1] - (1 << 64) if it[1] >= (1 << 63) else it[1] for it in items],
+                      np.int64)
+        nin = np.array([it[3] & 0xffffffff for it in items], np.uint32)
+        ret = np.zeros(max(n, 1), np.int32)
+        err = np.zeros(max(n, 1), np.int32)
+        p = lambda a: a.ctypes.data  # noqa: E731
+        secs = self.L.ref_bulk_verify_script(threads, n, p(sb), p(so), p(tb), p(to), p(am), p(nin),
+                                             flags & 0xffffffff, p(ret), p(err))
+        return [(int(ret[i]), int(err[i])) for i in range(n)], secs
 
     def pubkey_verify_blob(self, pub_blob, pub_off, msg32, sig_blob, sig_off, threads=1, n=None):
         """CPubKey::Verify over numpy blob inputs (uint64 offsets) on `threads` host threads.

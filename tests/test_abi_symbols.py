@@ -9,11 +9,12 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB = os.path.join(ROOT, "rust-bitcoinconsensus_amd", "librbc_amd.so")
+BENCH_LIB = os.path.join(ROOT, "rust-bitcoinconsensus_amd", "librbc_bench.so")
 
 
-def declared_functions():
+def declared_functions(headers=("bitcoinconsensus.h", "bcc_amd.h")):
     names = set()
-    for h in ("bitcoinconsensus.h", "bcc_amd.h"):
+    for h in headers:
         src = open(os.path.join(ROOT, "include", h)).read()
         src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
         for m in re.finditer(r"\b([a-z_][a-z0-9_]*)\s*\([^;{]*\)\s*;", src):
@@ -35,6 +36,29 @@ def test_exports_every_declared_symbol(lib):
             "mi_ecdsa_verify_tuples"} <= names
     missing = [n for n in sorted(names) if not hasattr(lib, n)]
     assert not missing, missing
+
+
+def test_bench_library_exports_its_header():
+    """librbc_bench.so (synthetic workloads / generators / microbenchmark, include/bcc_bench.h)
+    exports everything its header declares; the product library exports none of it."""
+    if not os.path.exists(BENCH_LIB):
+        subprocess.check_call(["make", "-s", "-C", os.path.dirname(LIB), "-j8"])
+    b = ctypes.CDLL(BENCH_LIB)
+    p = ctypes.CDLL(LIB)
+    names = declared_functions(("bcc_bench.h",))
+    assert {"bcc_workload_p2wpkh", "bcc_workload_from_items", "bcc_tupleset_c4",
+            "mi_microbench"} <= names
+    assert not [n for n in sorted(names) if not hasattr(b, n)]
+    assert not [n for n in sorted(names) if hasattr(p, n)]
+
+
+def test_source_hash_matches_tree(lib):
+    """Provenance: the library embeds the hash of the sources it was built from."""
+    import sys
+    sys.path.insert(0, os.path.dirname(LIB))
+    from source_hash import source_hash
+    lib.bcc_source_hash.restype = ctypes.c_char_p
+    assert lib.bcc_source_hash().decode() == source_hash()
 
 
 def test_version_and_flag_check_need_no_gpu(lib):

@@ -46,8 +46,8 @@ def operand_pairs(seed=7, nrand=6000):
 
 
 def run(op, pairs):
-    from bitcoinconsensus_amd import lib
-    L = lib()
+    from bitcoinconsensus_amd import blib
+    L = blib()
     n = len(pairs)
     a = pack([x for x, _ in pairs])
     b = pack([y for _, y in pairs])

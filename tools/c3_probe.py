@@ -14,7 +14,7 @@ shape = [tuple(t) for t in json.load(open(os.path.join(ROOT, "tests", "golden", 
 ntx = int(sys.argv[1]) if len(sys.argv) > 1 else 4000
 txs = (shape * (ntx // len(shape) + 1))[:ntx]
 wl = B.Workload(kind="block", shape=txs, seed=0x5EED0003)
-L = B.lib()
+L = B.blib()
 cnt = ctypes.c_size_t(0)
 items = L.bcc_workload_items(wl.h, ctypes.byref(cnt))
 ret = (ctypes.c_int * cnt.value)()

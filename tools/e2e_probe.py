@@ -11,7 +11,7 @@ import bitcoinconsensus_amd as B  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 1_000_000
 wl = B.Workload(n, seed=0x5EED0001)
-L = B.lib()
+L = B.blib()
 cnt = ctypes.c_size_t(0)
 items = L.bcc_workload_items(wl.h, ctypes.byref(cnt))
 ret = (ctypes.c_int * cnt.value)()

@@ -1,5 +1,5 @@
 // Dev tool: field-multiply variant microbenchmark + cross-check (not part of the library).
-// hipcc --offload-arch=gfx950 -O3 -shared -fPIC -I rust-bitcoinconsensus_amd/csrc tools/fe_bench.hip -o tools/_build/fe_bench.so
+// hipcc --offload-arch=gfx950 -O3 -shared -fPIC -I rust-bitcoinconsensus_amd/csrc -I tools tools/fe_bench.hip -o tools/_build/fe_bench.so
 #include "ecdsa_lane.h"
 #include "fe_asm.h"
 #include "fe_asm_gen.h"

@@ -36,6 +36,21 @@ def main(d):
             e[ctr.lower() + "_bytes_per_launch"] = agg[k] * 1024 / cnt[k]
             e[ctr.lower() + "_launches"] = cnt[k]
             e[ctr.lower() + "_bytes_total"] = agg[k] * 1024
+    # SQ / GRBM issue counters (pmc_sq pass): per launch, per kernel
+    sq, sqn = collections.defaultdict(float), collections.Counter()
+    for f in glob.glob(os.path.join(d, "pmc_sq", "**", "*counter_collection.csv"), recursive=True):
+        seen = set()
+        for r in csv.DictReader(open(f)):
+            k = short(r["Kernel_Name"])
+            sq[(k, r["Counter_Name"])] += float(r["Counter_Value"])
+            key = (k, r.get("Dispatch_Id", r.get("Correlation_Id", "")))
+            if key not in seen:
+                seen.add(key)
+                sqn[k] += 1
+    for (k, c), v in sq.items():
+        e = out["kernels"].setdefault(k, {})
+        e.setdefault("pmc_per_launch", {})[c] = v / max(1, sqn[k])
+        e["pmc_launches"] = sqn[k]
     for k, e in out["kernels"].items():
         if "fetch_size_bytes_per_launch" in e:
             e["fetch_bytes_x2_per_launch"] = 2 * e["fetch_size_bytes_per_launch"]
