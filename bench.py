@@ -9,8 +9,9 @@ Default workload (BASELINE.json configs[1]): n synthetic P2WP
 pass).  One step = one pass of the hot path over the batch: BIP143 sighash kernels (aux hashes,
 patch, preimage SHA-256d) + the ECDSA kernels (batched s^-1, pubkey decompression + GLV + Q table,
 Strauss ladder + x-check).  value = verifies of all ranks / max-over-ranks wall time of K steps.
-Multi-GPU is weak scaling: every rank verifies its own shard (seed + rank), no collective in the
-timed loop.
+Multi-GPU is weak scaling: the N ranks partition ONE global input set of N x n units from the
+config's seed (rank r takes units [r n, (r + 1) n)), no collective in the timed
+loop; afterwards the validity bitmaps are all-gathered over RCCL and checked.
 
 Other configs (run explicitly, results committed under profiles/):
   c3  block replay: transactions shaped like the reference's bench block413567 (tiled to 4,000
@@ -172,14 +173,39 @@ def aggregate(elapsed, n_valid, world, device="cuda"):
     return t.item(), int(c.item())
 
 
+def gather_verdicts(local, world, device="cuda"):
+    """All-gather every rank's verdicts as packed validity bitmaps (1 bit per input) and return
+    the global verdict array in rank order.  The only data collective of a sharded run (SURVEY.md
+    §8e: RCCL all_gather on the GPUs, gloo in the CPU tests); it sits outside the timed loop."""
+    import numpy as np
+    local = np.asarray(local, dtype=np.uint8)
+    if world <= 1:
+        return local
+    import torch
+    import torch.distributed as dist
+    n = torch.tensor([len(local)], device=device, dtype=torch.int64)
+    ns = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(ns, n)
+    ns = [int(x.item()) for x in ns]
+    nbytes = (max(ns) + 7) // 8
+    bits = np.zeros(nbytes, np.uint8)
+    pk = np.packbits(local)
+    bits[: len(pk)] = pk
+    t = torch.from_numpy(bits).to(device)
+    out = torch.empty(world * nbytes, dtype=torch.uint8, device=device)
+    dist.all_gather_into_tensor(out, t)
+    allb = out.cpu().numpy().reshape(world, nbytes)
+    return np.concatenate([np.unpackbits(allb[r])[: ns[r]] for r in range(world)])
+
+
 # ---- per-config jobs: stage inputs, run one step, time the dominant kernels, CPU baseline ----
 
 class C2:
     unit = "verifies/s"
 
-    def __init__(self, B, n, seed, dev):
+    def __init__(self, B, n, seed, dev, first=0, total=None):
         self.B = B
-        self.wl = B.Workload(n, seed=seed, device=dev)
+        self.wl = B.Workload(n, seed=seed, device=dev, first=first)
         self.shape = self.wl.shape()
         self.units = self.shape["tuples"]
         self.n = n
@@ -189,6 +215,13 @@ class C2:
 
     def valid(self):
         return sum(self.wl.verdicts())
+
+    def item_verdicts(self):
+        v = self.wl.verdicts()
+        out = bytearray(self.n)
+        for t, i in enumerate(self.wl.tuple_items()):
+            out[i] = v[t]
+        return out
 
     def kernel_times(self, stream, reps):
         import torch
@@ -255,8 +288,9 @@ class C3(C2):
     """Block replay through the drop-in batch ABI, end to end from host buffers."""
     unit = "inputs/s"
 
-    def __init__(self, B, n, seed, dev):
+    def __init__(self, B, n, seed, dev, first=0, total=None):
         self.B = B
+        seed += first  # block shards: independent batches (a block's txs stay on one GPU)
         shape = [tuple(t) for t in json.load(open(os.path.join(
             ROOT, "tests", "golden", "block413567_shape.json")))["txs"]]
         txs = (shape * (n // len(shape) + 1))[:n]
@@ -270,8 +304,11 @@ class C3(C2):
     def step(self, sp):
         self._valid, _ = self.wl.verify_batch()
 
+    def item_verdicts(self):
+        return self._ret
+
     def valid(self):
-        self.step(None)
+        self._valid, self._ret = self.wl.verify_batch()
         st = self.B.last_batch_stats()
         self.stats = st
         return self._valid
@@ -307,7 +344,7 @@ class C3(C2):
 
 
 class TupleJob:
-    def __init__(self, B, n, seed, dev, kind):
+    def __init__(self, B, n, seed, dev, kind, first=0, total=None):
         import bitcoinconsensus_amd as BB
         vec = []
         if kind == "c5":
@@ -315,7 +352,8 @@ class TupleJob:
             from fixtures import bip340_vectors
             vec = [(t["sig"], t["msg"], t["pub"], t["verdict"]) for t in bip340_vectors()]
         self.kind = kind
-        self.ts = BB.TupleSet(n, kind=kind, seed=seed, device=dev, vectors=vec)
+        self.ts = BB.TupleSet(n, kind=kind, seed=seed, device=dev, vectors=vec, first=first,
+                              total=total)
         self.units = self.n = n
         self.unit = "verifies/s"
         self.mads = MADS_PER_VERIFY if kind == "c4" else MADS_PER_SCHNORR
@@ -331,6 +369,9 @@ class TupleJob:
         h = self.ts.host()
         self.mismatch_vs_construction = int((v != h["expect"]).sum())
         return int(v.sum())
+
+    def item_verdicts(self):
+        return self.ts.verdicts()
 
     def kernel_times(self, stream, reps):
         import torch
@@ -432,10 +473,12 @@ def main():
     B.set_device(dev)
 
     t0 = time.time()
+    # one global set of world x n units from `seed`; this rank's contiguous range
+    first, total = rank * n, world * n
     if args.config in ("c2", "c3"):
-        job = (C2 if args.config == "c2" else C3)(B, n, seed + rank, dev)
+        job = (C2 if args.config == "c2" else C3)(B, n, seed, dev, first=first, total=total)
     else:
-        job = TupleJob(B, n, seed + rank, dev, args.config)
+        job = TupleJob(B, n, seed, dev, args.config, first=first, total=total)
     log(f"[rank {rank}] staged {args.config} x{n} in {time.time() - t0:.1f}s")
     # a dedicated (non-null) stream: every launch of a step and the HIP events that time the
     # kernels sit on it (torch's default stream is the null handle, which the engine maps to its
@@ -462,6 +505,10 @@ def main():
     barrier()
     elapsed = time.perf_counter() - ts
     elapsed, n_valid_all = aggregate(elapsed, n_valid, world)
+    # the global validity bitmap (RCCL all-gather, outside the timed loop)
+    gathered = gather_verdicts(bytearray(job.item_verdicts()), world)
+    bitmap = dict(units=int(len(gathered)), valid=int(gathered.sum()),
+                  collective="all_gather_into_tensor (RCCL)" if world > 1 else "none (1 rank)")
 
     # per-kernel timing with HIP events on the launch stream (outside the timed region)
     sighash_ms, sig_ms = job.kernel_times(stream, max(3, args.steps))
@@ -503,6 +550,7 @@ def main():
         out.update(job.extra(sighash_ms))
         out["source_hash"] = B.source_hash()
         out["verdicts_valid"] = n_valid_all
+        out["validity_bitmap"] = bitmap
         out["verdicts_total"] = job.units * world
         if cpu:
             out["gpu_vs_cpu"] = value / cpu["value"]

@@ -49,7 +49,8 @@ int mi_schnorr_verify_device(const uint8_t* d_sig64, const uint8_t* d_msg32,
  * verdict[i] = CPubKey(pub_i).Verify(msg_i, sig_i) (depend/bitcoin/src/pubkey.cpp:191-207) for n
  * tuples: pub_i = pub_blob[pub_off[i] .. pub_off[i+1]) (any length; the CPubKey length filter,
  * pubkey.h:58-94, applies), sig_i = sig_blob[sig_off[i] .. sig_off[i+1]) = DER without the
- * hashtype byte, parsed laxly (pubkey.cpp:28-168).  Synchronous on `device`.  0 or an error. */
+ * hashtype byte, parsed laxly (pubkey.cpp:28-168).  Synchronous on `device`, or, for device = -1,
+ * sharded in contiguous equal ranges over the bcc_set_devices() GPUs.  0 or an error. */
 int bcc_pubkey_verify_batch(const uint8_t* pub_blob, const uint64_t* pub_off,
                             const uint8_t* msg32, const uint8_t* sig_blob,
                             const uint64_t* sig_off, uint8_t* verdict, size_t n, int device);
@@ -62,6 +63,17 @@ const char* bcc_source_hash(void);
 /* Device used by the bitcoinconsensus_* entry points of the calling process (default 0, or the
  * BCC_DEVICE environment variable). */
 int bcc_set_device(int device);
+
+/* Node sharding: spread every device round of bitcoinconsensus_verify_batch, and
+ * bcc_pubkey_verify_batch(..., device = -1), over these GPUs (default: the single device above,
+ * or BCC_DEVICES="0,1,2,..." in the environment; n = 0 restores the default).  A round is cut
+ * into contiguous groups of whole transactions with about equal signature counts, one per GPU;
+ * the groups run concurrently, each GPU from its own persistent host worker thread (its own HIP
+ * stream, device arena and kernel scratch), and the verdicts are gathered on the host.  Results
+ * never depend on the device set.  Returns 0, or -1 for a negative device id. */
+int bcc_set_devices(const int* devices, int n);
+/* Writes up to cap configured device ids to out; returns how many there are. */
+int bcc_get_devices(int* out, int cap);
 
 /* Lanes per signature-kernel launch (0 = default: 4M, or the BCC_CHUNK environment variable).
  * Bounds the per-caller device scratch (900 B per lane); results do not depend on it. */
@@ -80,6 +92,7 @@ typedef struct bcc_batch_stats {
     double prepare_seconds, interpret_seconds, merge_seconds, stage_seconds;
     double total_seconds; /* the whole call, teardown included */
     size_t device_retries; /* device rounds that failed once and were re-run on a fresh batch */
+    size_t devices;        /* GPUs a device round was spread over (max over the call's rounds) */
 } bcc_batch_stats;
 /* Statistics of the calling thread's last bitcoinconsensus_verify_batch / verify call. */
 void bcc_last_batch_stats(bcc_batch_stats* out);

@@ -23,11 +23,20 @@ typedef struct bcc_tupleset bcc_tupleset;
  * compressed x without a square root, x >= p, 04 with a wrong y, 04, hybrid 06/07 with good and
  * bad parity, bad header, wrong key).  The staged rows are those bcc_pubkey_verify_batch builds. */
 bcc_tupleset* bcc_tupleset_c4(size_t n, uint64_t seed, int device);
+/* Tuples [first, first + n) of the global C4 set of `total` tuples from `seed` (the node batch
+ * partitioned by rank: every tuple depends only on (seed, its global index, total)). */
+bcc_tupleset* bcc_tupleset_c4_range(size_t n, uint64_t seed, size_t first, size_t total,
+                                    int device);
 /* C5: n BIP340 rows, fresh GPU-signed from `seed`, with the nvec caller vectors (sig64, msg32,
  * xonly32, expected verdict) at rows i with i % 1024 == 1 + j. */
 bcc_tupleset* bcc_tupleset_c5(size_t n, uint64_t seed, const uint8_t* vec_sig64,
                               const uint8_t* vec_msg32, const uint8_t* vec_xonly32,
                               const uint8_t* vec_expect, size_t nvec, int device);
+/* Rows [first, first + n) of the global C5 set (vectors tiled by global index). */
+bcc_tupleset* bcc_tupleset_c5_range(size_t n, uint64_t seed, size_t first,
+                                    const uint8_t* vec_sig64, const uint8_t* vec_msg32,
+                                    const uint8_t* vec_xonly32, const uint8_t* vec_expect,
+                                    size_t nvec, int device);
 void bcc_tupleset_free(bcc_tupleset* ts);
 size_t bcc_tupleset_size(const bcc_tupleset* ts);
 /* launch the verify kernels over the resident rows on `stream` (asynchronous) */
@@ -50,6 +59,8 @@ typedef struct bcc_workload bcc_workload;
  * nonces and amounts derived from `seed`.  Keys and signatures are produced by
  * the engine's own GPU kernels; txs / sighash jobs are staged in HBM. */
 bcc_workload* bcc_workload_p2wpkh(size_t n, uint64_t seed, int device);
+/* Spends [first, first + n) of the global C2 set from `seed` (rank partitions of one set). */
+bcc_workload* bcc_workload_p2wpkh_range(size_t n, uint64_t seed, size_t first, int device);
 /* C3: block replay.  ntx transactions with tx_nin[j] inputs / tx_nout[j] outputs (the histogram
  * of the reference's bench/data/block413567.raw), inputs 60 % P2PKH / 30 % P2WPKH / 10 % P2SH
  * 2-of-3 multisig, re-signed with synthetic keys from `seed`.  One item per

@@ -93,8 +93,13 @@ def blib():
         L.mi_microbench.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_double)]
         L.bcc_tupleset_c4.argtypes = [sz, ctypes.c_uint64, ctypes.c_int]
         L.bcc_tupleset_c4.restype = vp
+        L.bcc_tupleset_c4_range.argtypes = [sz, ctypes.c_uint64, sz, sz, ctypes.c_int]
+        L.bcc_tupleset_c4_range.restype = vp
         L.bcc_tupleset_c5.argtypes = [sz, ctypes.c_uint64, u8p, u8p, u8p, u8p, sz, ctypes.c_int]
         L.bcc_tupleset_c5.restype = vp
+        L.bcc_tupleset_c5_range.argtypes = [sz, ctypes.c_uint64, sz, u8p, u8p, u8p, u8p, sz,
+                                            ctypes.c_int]
+        L.bcc_tupleset_c5_range.restype = vp
         L.bcc_tupleset_free.argtypes = [vp]
         L.bcc_tupleset_size.argtypes = [vp]
         L.bcc_tupleset_size.restype = sz
@@ -103,6 +108,8 @@ def blib():
         L.bcc_tupleset_view.argtypes = [vp, ctypes.POINTER(TuplesetHost)]
         L.bcc_workload_p2wpkh.argtypes = [sz, ctypes.c_uint64, ctypes.c_int]
         L.bcc_workload_p2wpkh.restype = vp
+        L.bcc_workload_p2wpkh_range.argtypes = [sz, ctypes.c_uint64, sz, ctypes.c_int]
+        L.bcc_workload_p2wpkh_range.restype = vp
         u32p = ctypes.POINTER(ctypes.c_uint32)
         L.bcc_workload_block.argtypes = [u32p, u32p, sz, ctypes.c_uint64, ctypes.c_int]
         L.bcc_workload_block.restype = vp
@@ -171,6 +178,8 @@ def _bind_consensus(L):
     L.bitcoinconsensus_verify_batch.restype = ctypes.c_long
     L.bcc_set_device.argtypes = [ctypes.c_int]
     L.bcc_debug_fail_device_rounds.argtypes = [ctypes.c_int]
+    L.bcc_set_devices.argtypes = [ctypes.POINTER(ctypes.c_int), ctypes.c_int]
+    L.bcc_get_devices.argtypes = [ctypes.POINTER(ctypes.c_int), ctypes.c_int]
     L.bcc_last_batch_stats.argtypes = [ctypes.POINTER(BatchStats)]
 
 
@@ -182,12 +191,12 @@ class Workload:
                    (one item per input)."""
 
     def __init__(self, n=0, seed=0x5EED0001, device=0, kind="p2wpkh", shape=None, items=None,
-                 flags=VERIFY_ALL):
+                 flags=VERIFY_ALL, first=0):
         if kind == "items":  # any caller items, staged through the same first-round pass
             arr, keep = _batch_items(items)
             self.h = blib().bcc_workload_from_items(arr, len(keep[0]), flags & 0xffffffff, device)
-        elif kind == "p2wpkh":
-            self.h = blib().bcc_workload_p2wpkh(n, seed, device)
+        elif kind == "p2wpkh":  # spends [first, first + n) of the global set from `seed`
+            self.h = blib().bcc_workload_p2wpkh_range(n, seed, first, device)
         elif kind == "block":
             nin = (ctypes.c_uint32 * len(shape))(*[a for a, _ in shape])
             nout = (ctypes.c_uint32 * len(shape))(*[b for _, b in shape])
@@ -359,6 +368,21 @@ def set_device(device):
     lib().bcc_set_device(device)
 
 
+def set_devices(devices):
+    """Node sharding (include/bcc_amd.h bcc_set_devices): spread verify_batch's device rounds and
+    pubkey_verify_batch(device=-1) over these GPUs ([] restores the single default device)."""
+    devs = list(devices)
+    arr = (ctypes.c_int * max(1, len(devs)))(*devs)
+    if lib().bcc_set_devices(arr, len(devs)) != 0:
+        raise ValueError(f"bad device list {devs}")
+
+
+def get_devices():
+    arr = (ctypes.c_int * 64)()
+    n = lib().bcc_get_devices(arr, 64)
+    return list(arr)[:n]
+
+
 def height_to_flags(height):
     """Soft-fork activation heights (src/lib.rs:45-65)."""
     flag = VERIFY_NONE
@@ -385,7 +409,8 @@ def _blob(parts):
 def pubkey_verify_batch(tuples, device=0):
     """[CPubKey(pub).Verify(hash32, der_sig) for (pub, hash32, der_sig) in tuples] as a bytes of
     0/1 (depend/bitcoin/src/pubkey.cpp:191-207): length filter + lax DER on the host, the
-    secp256k1 work on the GPU (include/bcc_amd.h bcc_pubkey_verify_batch)."""
+    secp256k1 work on the GPU (include/bcc_amd.h bcc_pubkey_verify_batch).  device=-1 shards the
+    tuples over the set_devices() GPUs."""
     n = len(tuples)
     if n == 0:
         return b""
@@ -411,16 +436,19 @@ class TupleSet:
                   "pub_04_bad_y", "pub_04", "pub_hybrid_ok", "pub_hybrid_bad", "pub_bad_header",
                   "wrong_key")
 
-    def __init__(self, n, kind="c4", seed=None, device=0, vectors=()):
+    def __init__(self, n, kind="c4", seed=None, device=0, vectors=(), first=0, total=None):
+        """Rows [first, first + n) of the global set of `total` rows (default: n) from `seed`."""
         L = blib()
+        total = first + n if total is None else total
         if kind == "c4":
-            self.h = L.bcc_tupleset_c4(n, 0x5EED0004 if seed is None else seed, device)
+            self.h = L.bcc_tupleset_c4_range(n, 0x5EED0004 if seed is None else seed, first,
+                                             total, device)
         elif kind == "c5":
             v = list(vectors)
-            self.h = L.bcc_tupleset_c5(n, 0x5EED0005 if seed is None else seed,
-                                       b"".join(x[0] for x in v), b"".join(x[1] for x in v),
-                                       b"".join(x[2] for x in v), bytes(int(x[3]) for x in v),
-                                       len(v), device)
+            self.h = L.bcc_tupleset_c5_range(n, 0x5EED0005 if seed is None else seed, first,
+                                             b"".join(x[0] for x in v), b"".join(x[1] for x in v),
+                                             b"".join(x[2] for x in v), bytes(int(x[3]) for x in v),
+                                             len(v), device)
         else:
             raise ValueError(kind)
         if not self.h:

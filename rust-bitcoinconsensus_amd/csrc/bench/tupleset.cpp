@@ -223,27 +223,36 @@ struct bcc_tupleset {
 extern "C" {
 
 bcc_tupleset* bcc_tupleset_c4(size_t n, uint64_t seed, int device) {
+    return bcc_tupleset_c4_range(n, seed, 0, n, device);
+}
+
+bcc_tupleset* bcc_tupleset_c4_range(size_t n, uint64_t seed, size_t first, size_t total,
+                                    int device) {
+    if (total < first + n || n == 0) return nullptr;
     auto* ts = new bcc_tupleset();
     ts->device = device;
     ts->kind = 4;
     ts->n = n;
-    std::vector<uint8_t> d(32 * n), m(32 * n), k(32 * n), px(32 * n), py(32 * n), ok(n),
-        r(32 * n), s(32 * n);
+    // keys for the n tuples plus the next global index (the wrong-key class takes key gi + 1)
+    std::vector<uint8_t> d(32 * (n + 1)), m(32 * n), k(32 * n), px(32 * (n + 1)), py(32 * (n + 1)),
+        ok(n + 1), r(32 * n), s(32 * n);
     ts->cls.resize(n);
+    tagged("mi355x-c4", seed, (first + n) % total, &d[32 * n], true);
     pfor(n, 1024, [&](size_t lo, size_t hi) {
-        for (size_t i = lo; i < hi; i++) {
-            tagged("mi355x-c4", seed, i, &d[32 * i], true);
-            tagged("mi355x-c4-msg", seed, i, &m[32 * i], false);
+        for (size_t li = lo; li < hi; li++) {
+            const size_t i = li, gi = first + li;  // local row, index in the global set
+            tagged("mi355x-c4", seed, gi, &d[32 * i], true);
+            tagged("mi355x-c4-msg", seed, gi, &m[32 * i], false);
             uint8_t nb[32 + 32 + 15];
             memcpy(nb, "mi355x-c4-nonce", 15);
             memcpy(nb + 15, &d[32 * i], 32);
             memcpy(nb + 47, &m[32 * i], 32);
             derive_scalar(nb, sizeof nb, &k[32 * i]);
-            uint64_t u = splitmix64(seed * 0x9E37 + i);
+            uint64_t u = splitmix64(seed * 0x9E37 + gi);
             ts->cls[i] = (u % 100) < 90 ? C4_VALID : (uint8_t)(1 + (u >> 8) % (C4_NCLASS - 1));
         }
     });
-    if (mi_gen_pubkeys(d.data(), n, px.data(), py.data(), ok.data(), device) != 0 ||
+    if (mi_gen_pubkeys(d.data(), n + 1, px.data(), py.data(), ok.data(), device) != 0 ||
         mi_gen_sign(d.data(), m.data(), k.data(), n, r.data(), s.data(), ok.data(), device) != 0) {
         delete ts;
         return nullptr;
@@ -263,7 +272,8 @@ bcc_tupleset* bcc_tupleset_c4(size_t n, uint64_t seed, int device) {
             std::vector<uint8_t> sig;
             for (size_t i = lo; i < hi; i++) {
                 const uint8_t c = ts->cls[i];
-                uint64_t u = splitmix64(seed ^ (i * 0xD1B54A32D192ED03ULL));
+                const size_t gi = first + i;
+                uint64_t u = splitmix64(seed ^ (gi * 0xD1B54A32D192ED03ULL));
                 uint8_t R[32], S[32], X[32], Y[32];
                 memcpy(R, &r[32 * i], 32);
                 memcpy(S, &s[32 * i], 32);
@@ -285,7 +295,7 @@ bcc_tupleset* bcc_tupleset_c4(size_t n, uint64_t seed, int device) {
                     case C4_R_ZEROPAD: rzeros = 1 + (int)(u % 3); break;
                     case C4_PUB_NO_SQRT: {
                         uint8_t cand[32];
-                        tagged("mi355x-c4-nosqrt", seed, i, cand, false);
+                        tagged("mi355x-c4-nosqrt", seed, gi, cand, false);
                         cand[0] &= 0x7f;  // < p
                         for (;;) {
                             Fe x = fe_from_be(cand);
@@ -306,12 +316,11 @@ bcc_tupleset* bcc_tupleset_c4(size_t n, uint64_t seed, int device) {
                     case C4_PUB_HYBRID_OK: full = true; hdr = 0x06 | (Y[31] & 1); break;
                     case C4_PUB_HYBRID_BAD: full = true; hdr = 0x06 | ((Y[31] & 1) ^ 1); break;
                     case C4_PUB_BAD_HEADER: hdr = 0x05; break;
-                    case C4_WRONG_KEY: {
-                        size_t j = (i + 1) % n;
-                        memcpy(X, &px[32 * j], 32);
-                        memcpy(Y, &py[32 * j], 32);
+                    case C4_WRONG_KEY: {  // the key of global tuple gi + 1 (row i + 1 here)
+                        memcpy(X, &px[32 * (i + 1)], 32);
+                        memcpy(Y, &py[32 * (i + 1)], 32);
                         hdr = 0x02 | (Y[31] & 1);
-                        if (j == i) X[31] ^= 1;
+                        if ((gi + 1) % total == gi) X[31] ^= 1;
                         break;
                     }
                     default: break;
@@ -353,6 +362,14 @@ bcc_tupleset* bcc_tupleset_c4(size_t n, uint64_t seed, int device) {
 bcc_tupleset* bcc_tupleset_c5(size_t n, uint64_t seed, const uint8_t* vec_sig64,
                               const uint8_t* vec_msg32, const uint8_t* vec_xonly32,
                               const uint8_t* vec_expect, size_t nvec, int device) {
+    return bcc_tupleset_c5_range(n, seed, 0, vec_sig64, vec_msg32, vec_xonly32, vec_expect, nvec,
+                                 device);
+}
+
+bcc_tupleset* bcc_tupleset_c5_range(size_t n, uint64_t seed, size_t first,
+                                    const uint8_t* vec_sig64, const uint8_t* vec_msg32,
+                                    const uint8_t* vec_xonly32, const uint8_t* vec_expect,
+                                    size_t nvec, int device) {
     auto* ts = new bcc_tupleset();
     ts->device = device;
     ts->kind = 5;
@@ -365,8 +382,8 @@ bcc_tupleset* bcc_tupleset_c5(size_t n, uint64_t seed, const uint8_t* vec_sig64,
     ts->expect.assign(n, 1);
     pfor(n, 1024, [&](size_t lo, size_t hi) {
         for (size_t i = lo; i < hi; i++) {
-            tagged("mi355x-c5", seed, i, &d[32 * i], true);
-            tagged("mi355x-c5-msg", seed, i, &ts->msg[32 * i], false);
+            tagged("mi355x-c5", seed, first + i, &d[32 * i], true);
+            tagged("mi355x-c5-msg", seed, first + i, &ts->msg[32 * i], false);
             uint8_t nb[32 + 32 + 15];
             memcpy(nb, "mi355x-c5-nonce", 15);
             memcpy(nb + 15, &d[32 * i], 32);
@@ -382,7 +399,7 @@ bcc_tupleset* bcc_tupleset_c5(size_t n, uint64_t seed, const uint8_t* vec_sig64,
     // the caller's vectors tiled at a fixed stride: row i with i % 1024 == 1 + j is vector j
     if (nvec && vec_sig64 && vec_msg32 && vec_xonly32 && vec_expect)
         for (size_t i = 0; i < n; i++) {
-            size_t j = i % 1024;
+            size_t j = (first + i) % 1024;
             if (j == 0 || j > nvec) continue;
             j -= 1;
             memcpy(&ts->sig64[64 * i], vec_sig64 + 64 * j, 64);

@@ -173,6 +173,10 @@ int finish(bcc_workload* w) {
 extern "C" {
 
 bcc_workload* bcc_workload_p2wpkh(size_t n, uint64_t seed, int device) {
+    return bcc_workload_p2wpkh_range(n, seed, 0, device);
+}
+
+bcc_workload* bcc_workload_p2wpkh_range(size_t n, uint64_t seed, size_t first, int device) {
     auto* w = new bcc_workload();
     w->device = device;
     w->n = n;
@@ -185,7 +189,7 @@ bcc_workload* bcc_workload_p2wpkh(size_t n, uint64_t seed, int device) {
         memcpy(buf, "mi355x-c2", 9);
         for (size_t i = lo; i < hi; i++) {
             for (int b = 0; b < 8; b++) buf[9 + b] = (uint8_t)(seed >> (8 * b));
-            for (int b = 0; b < 8; b++) buf[17 + b] = (uint8_t)((uint64_t)i >> (8 * b));
+            for (int b = 0; b < 8; b++) buf[17 + b] = (uint8_t)((uint64_t)(first + i) >> (8 * b));
             derive_scalar(buf, sizeof buf, &d[32 * i]);
         }
     });
@@ -210,18 +214,19 @@ bcc_workload* bcc_workload_p2wpkh(size_t n, uint64_t seed, int device) {
             spk[0] = 0x00;
             spk[1] = 0x14;
             memcpy(spk + 2, h160, 20);
-            uint64_t rnd = splitmix64(seed ^ (0xA5A5A5A5ULL * (i + 1)));
+            const uint64_t gi = first + i;  // index in the global (all-rank) set
+            uint64_t rnd = splitmix64(seed ^ (0xA5A5A5A5ULL * (gi + 1)));
             int64_t amount = 546 + (int64_t)(rnd % (uint64_t)(2100000000000000LL - 546 + 1));
             w->amount[i] = amount;
             // outpoint
             uint8_t outpoint[36], tmp[16];
-            for (int b = 0; b < 8; b++) tmp[b] = (uint8_t)((uint64_t)i >> (8 * b));
+            for (int b = 0; b < 8; b++) tmp[b] = (uint8_t)(gi >> (8 * b));
             for (int b = 0; b < 8; b++) tmp[8 + b] = (uint8_t)(seed >> (8 * b));
             sha256(tmp, 16, outpoint);
             memset(outpoint + 32, 0, 4);
             // output: P2WPKH to HASH160(le64(i) || "out")
             uint8_t otmp[11], oh[20];
-            for (int b = 0; b < 8; b++) otmp[b] = (uint8_t)((uint64_t)i >> (8 * b));
+            for (int b = 0; b < 8; b++) otmp[b] = (uint8_t)(gi >> (8 * b));
             memcpy(otmp + 8, "out", 3);
             hash160(otmp, 11, oh);
             std::vector<uint8_t> txout;

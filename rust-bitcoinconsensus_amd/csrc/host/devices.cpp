@@ -1,0 +1,164 @@
+// Node sharding: per-GPU persistent worker threads.
+//
+// The reference has no multi-GPU code; its batching precedent is Core's CCheckQueue
+// (depend/bitcoin/src/checkqueue.h:30-170), a pool of host workers draining one queue of script
+// checks.  Here every configured GPU gets one worker thread that owns that device's HIP stream,
+// device arena, pinned staging buffer and kernel scratch (the thread-local DeviceBatch /
+// ThreadCtx caches); a batch's device round is cut into contiguous, equally weighted groups of
+// whole transactions, one per GPU, which run concurrently, and the verdicts land in the caller's
+// array at each group's row offset (the host-side gather).  No collective sits on this path.
+#include "devices.h"
+
+#include <condition_variable>
+#include <cstdlib>
+#include <cstring>
+#include <deque>
+#include <future>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+
+#include "bcc_amd.h"
+
+namespace bcc {
+namespace host {
+
+int current_device();  // engine.cpp: bcc_set_device / BCC_DEVICE
+
+namespace {
+
+std::mutex g_devs_mu;
+std::vector<int> g_devs;  // explicit list (bcc_set_devices); empty: environment / single device
+bool g_devs_env_read = false;
+
+class Worker {
+public:
+    Worker() : th_([this] { loop(); }) {}
+    ~Worker() {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        th_.join();
+    }
+    std::future<int> submit(std::function<int()> f) {
+        auto task = std::make_shared<std::packaged_task<int()>>(std::move(f));
+        std::future<int> fut = task->get_future();
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            q_.push_back([task] { (*task)(); });
+        }
+        cv_.notify_one();
+        return fut;
+    }
+
+private:
+    void loop() {
+        for (;;) {
+            std::function<void()> job;
+            {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [this] { return stop_ || !q_.empty(); });
+                if (stop_ && q_.empty()) return;
+                job = std::move(q_.front());
+                q_.pop_front();
+            }
+            job();
+        }
+    }
+    std::mutex mu_;
+    std::condition_variable cv_;
+    std::deque<std::function<void()>> q_;
+    bool stop_ = false;
+    std::thread th_;
+};
+
+std::mutex g_workers_mu;
+std::map<int, std::unique_ptr<Worker>>& workers() {
+    static auto* w = new std::map<int, std::unique_ptr<Worker>>();  // lives for the process
+    return *w;
+}
+
+Worker& worker(int dev) {
+    std::lock_guard<std::mutex> lk(g_workers_mu);
+    auto& w = workers()[dev];
+    if (!w) w.reset(new Worker());
+    return *w;
+}
+
+}  // namespace
+
+std::vector<int> device_list() {
+    std::lock_guard<std::mutex> lk(g_devs_mu);
+    if (g_devs.empty() && !g_devs_env_read) {
+        g_devs_env_read = true;
+        if (const char* e = getenv("BCC_DEVICES")) {
+            std::string s(e);
+            size_t p = 0;
+            while (p < s.size()) {
+                size_t q = s.find(',', p);
+                if (q == std::string::npos) q = s.size();
+                if (q > p) g_devs.push_back(atoi(s.substr(p, q - p).c_str()));
+                p = q + 1;
+            }
+        }
+    }
+    if (!g_devs.empty()) return g_devs;
+    return {current_device()};
+}
+
+int run_on_devices(const std::vector<int>& devs, const std::vector<std::function<int()>>& jobs) {
+    if (jobs.size() == 1) return jobs[0]();
+    std::vector<std::future<int>> f;
+    f.reserve(jobs.size());
+    for (size_t d = 0; d < jobs.size(); d++) f.push_back(worker(devs[d]).submit(jobs[d]));
+    int rc = 0;
+    for (auto& x : f) {
+        int r = x.get();
+        if (r && !rc) rc = r;
+    }
+    return rc;
+}
+
+std::vector<size_t> split_balanced(const std::vector<size_t>& w, size_t k) {
+    size_t total = 0;
+    for (size_t x : w) total += x;
+    std::vector<size_t> b(k + 1, w.size());
+    b[0] = 0;
+    size_t acc = 0, i = 0;
+    for (size_t g = 1; g < k; g++) {
+        const size_t want = total * g / k;
+        while (i < w.size() && acc + w[i] / 2 < want) acc += w[i++];
+        b[g] = i;
+    }
+    return b;
+}
+
+}  // namespace host
+}  // namespace bcc
+
+using namespace bcc::host;
+
+extern "C" {
+
+int bcc_set_devices(const int* devices, int n) {
+    std::lock_guard<std::mutex> lk(g_devs_mu);
+    g_devs.clear();
+    g_devs_env_read = true;  // an explicit call overrides BCC_DEVICES
+    for (int i = 0; i < n; i++) {
+        if (devices[i] < 0) return -1;
+        g_devs.push_back(devices[i]);
+    }
+    return 0;
+}
+
+int bcc_get_devices(int* out, int cap) {
+    const std::vector<int> d = device_list();
+    for (int i = 0; i < (int)d.size() && i < cap; i++) out[i] = d[i];
+    return (int)d.size();
+}
+
+}  // extern "C"

@@ -1,0 +1,25 @@
+// Node sharding: the set of GPUs the library spreads a batch over, and one
+// persistent host worker thread per GPU.
+#pragma once
+#include <functional>
+#include <vector>
+
+namespace bcc {
+namespace host {
+
+// The configured devices: bcc_set_devices(), else BCC_DEVICES="0,1,..", else the single device
+// of bcc_set_device() / BCC_DEVICE (default 0).
+std::vector<int> device_list();
+
+// Runs jobs[d]() for every d concurrently, job d on the persistent worker thread of devs[d], so
+// that each device keeps its thread-local device batch, stream and kernel scratch from call to
+// call.  A single job runs inline on the calling thread (the single-device engine is per calling
+// thread, reentrant).  Returns the first nonzero job result, else 0.
+int run_on_devices(const std::vector<int>& devs, const std::vector<std::function<int()>>& jobs);
+
+// Contiguous split of `weights` (in order) into k groups of about equal total weight; returns the
+// k + 1 group boundaries (indices into weights).
+std::vector<size_t> split_balanced(const std::vector<size_t>& weights, size_t k);
+
+}  // namespace host
+}  // namespace bcc

@@ -23,6 +23,7 @@
 #include "../pipeline.h"
 #include "bcc_amd.h"
 #include "bitcoinconsensus.h"
+#include "devices.h"
 #include "engine.h"
 #include "hashes.h"
 #include "script.h"
@@ -32,9 +33,9 @@ namespace bcc {
 namespace host {
 
 namespace {
-
 int g_device = -1;
 std::mutex g_device_mu;
+}  // namespace
 
 int current_device() {
     std::lock_guard<std::mutex> lk(g_device_mu);
@@ -44,6 +45,8 @@ int current_device() {
     }
     return g_device;
 }
+
+namespace {
 
 thread_local bcc_batch_stats t_stats;
 
@@ -402,17 +405,19 @@ int device_round(int dev, const SighashJobs* const* pj, const TupleRows* const* 
     return gpu_verify_parts(dev, pj, pr, P, verdict, stage_s);
 }
 
-// The round's shards as device batches whose blobs stay under ROUND_BLOB_LIMIT (the device job
-// records use 32-bit byte offsets): consecutive shards are grouped greedily; a single shard above
-// the limit is an error (reported, never silently truncated).  A failed group is retried once on
-// a fresh device batch (gpu_verify_parts drops the failed one).  Returns 0 or the error.
-int run_device_round(int dev, const std::vector<Round>& rds, unsigned T,
-                     const std::vector<size_t>& row0, uint8_t* verdict, double* stage_total) {
-    unsigned g0 = 0;
-    while (g0 < T) {
+// Shards [t0, t1) of the round on device `dev`, as device batches whose blobs stay under
+// ROUND_BLOB_LIMIT (the device job records use 32-bit byte offsets): consecutive shards are
+// grouped greedily; a single shard above the limit is an error (reported, never silently
+// truncated).  A failed batch is retried once on a fresh device batch (gpu_verify_parts drops the
+// failed one); *retries counts those.  Returns 0 or the error.
+int run_device_group(int dev, const std::vector<Round>& rds, unsigned t0, unsigned t1,
+                     const std::vector<size_t>& row0, uint8_t* verdict, double* stage_total,
+                     size_t* retries) {
+    unsigned g0 = t0;
+    while (g0 < t1) {
         size_t sz[4] = {0, 0, 0, 0};
         unsigned g1 = g0;
-        for (; g1 < T; g1++) {
+        for (; g1 < t1; g1++) {
             const SighashJobs& j = rds[g1].jobs;
             const size_t add[4] = {j.aux.size(), j.pre.size(), j.tpl.size(), j.code.size()};
             bool fits = true;
@@ -434,11 +439,13 @@ int run_device_round(int dev, const std::vector<Round>& rds, unsigned T,
         double st = 0;
         int e = device_round(dev, pj.data(), pr.data(), pj.size(), verdict + row0[g0], &st);
         if (e != 0) {
-            fprintf(stderr, "[bcc] verify_batch: device round failed (hip error %d), retrying\n", e);
-            t_stats.device_retries++;
+            fprintf(stderr, "[bcc] verify_batch: device %d round failed (hip error %d), retrying\n",
+                    dev, e);
+            (*retries)++;
             e = device_round(dev, pj.data(), pr.data(), pj.size(), verdict + row0[g0], &st);
             if (e != 0) {
-                fprintf(stderr, "[bcc] verify_batch: device round failed again (hip error %d)\n", e);
+                fprintf(stderr, "[bcc] verify_batch: device %d round failed again (hip error %d)\n",
+                        dev, e);
                 return e;
             }
         }
@@ -446,6 +453,38 @@ int run_device_round(int dev, const std::vector<Round>& rds, unsigned T,
         g0 = g1;
     }
     return 0;
+}
+
+// One device round of the batch: the shards' deferred checks are cut into contiguous groups of
+// whole shards with about equal tuple counts, one per configured GPU (shard by
+// transaction, so each tx's BIP143 aux hashes stay on one device); the groups run concurrently on
+// the GPUs' worker threads and write their verdicts at their row offsets.
+int run_device_round(const std::vector<Round>& rds, unsigned T, const std::vector<size_t>& row0,
+                     uint8_t* verdict, double* stage_total, size_t* devices_used) {
+    const std::vector<int> devs = device_list();
+    std::vector<size_t> w(T);
+    for (unsigned t = 0; t < T; t++) w[t] = rds[t].pending.size();
+    const size_t D = std::min<size_t>(devs.size(), T);
+    const std::vector<size_t> cut = split_balanced(w, D);
+    std::vector<double> st(D, 0);
+    std::vector<size_t> rt(D, 0);
+    std::vector<std::function<int()>> jobs;
+    std::vector<int> jd;
+    for (size_t d = 0; d < D; d++) {
+        if (cut[d] == cut[d + 1]) continue;
+        jd.push_back(devs[d]);
+        jobs.push_back([&, d] {
+            return run_device_group(devs[d], rds, (unsigned)cut[d], (unsigned)cut[d + 1], row0,
+                                    verdict, &st[d], &rt[d]);
+        });
+    }
+    const int e = jobs.empty() ? 0 : run_on_devices(jd, jobs);
+    for (size_t d = 0; d < D; d++) {
+        *stage_total += st[d];
+        t_stats.device_retries += rt[d];
+    }
+    *devices_used = std::max(*devices_used, jobs.size());
+    return e;
 }
 
 // Runs the batch; fills ret/err per item.  Returns -1 if the device pipeline failed twice in a
@@ -471,7 +510,6 @@ long run_batch(const bcc_batch_item* items, size_t n, unsigned flags, int* ret_o
     auto since = [](clk::time_point a) { return std::chrono::duration<double>(clk::now() - a).count(); };
     t_stats.prepare_seconds = since(t0);
     auto& st = b.st;
-    const int dev = current_device();
     const auto shards = make_shards(b, T);
     std::vector<std::vector<uint32_t>> run_list(T), next_list(T);
     for (unsigned t = 0; t < T; t++)
@@ -511,7 +549,7 @@ long run_batch(const bcc_batch_item* items, size_t n, unsigned flags, int* ret_o
         auto g0 = clk::now();
         verdict.assign(npend, 0);
         double stage_s = 0;
-        int e = run_device_round(dev, rds, T, row0, verdict.data(), &stage_s);
+        int e = run_device_round(rds, T, row0, verdict.data(), &stage_s, &t_stats.devices);
         t_stats.stage_seconds += stage_s;
         gpu_s += std::chrono::duration<double>(clk::now() - g0).count();
         if (e != 0) {

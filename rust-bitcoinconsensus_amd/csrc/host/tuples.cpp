@@ -11,6 +11,7 @@
 #include <vector>
 
 #include "bcc_amd.h"
+#include "devices.h"
 #include "sighash.h"
 
 namespace bcc {
@@ -74,8 +75,19 @@ extern "C" int bcc_pubkey_verify_batch(const uint8_t* pub_blob, const uint64_t* 
                                        int device) {
     if (n == 0) return 0;
     if (!pub_off || !sig_off || !msg32 || !verdict) return -1;
-    bcc::TupleRows rows;
-    bcc::host::parse_rows(pub_blob, pub_off, msg32, sig_blob, sig_off, n, rows);
-    bcc::SighashJobs none;
-    return bcc::gpu_verify_batch(device, none, rows, verdict);
+    std::vector<int> devs = device < 0 ? bcc::host::device_list() : std::vector<int>{device};
+    const size_t D = std::min<size_t>(devs.size(), (n + 4095) / 4096);
+    std::vector<std::function<int()>> jobs;
+    for (size_t d = 0; d < D; d++) {
+        const size_t lo = n * d / D, hi = n * (d + 1) / D;
+        jobs.push_back([=] {  // contiguous equal range on devs[d] (offsets stay absolute)
+            bcc::TupleRows rows;
+            bcc::host::parse_rows(pub_blob, pub_off + lo, msg32 + 32 * lo, sig_blob, sig_off + lo,
+                                  hi - lo, rows);
+            bcc::SighashJobs none;
+            return bcc::gpu_verify_batch(devs[d], none, rows, verdict + lo);
+        });
+    }
+    devs.resize(D);
+    return bcc::host::run_on_devices(devs, jobs);
 }

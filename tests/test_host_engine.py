@@ -28,23 +28,8 @@ class Item(ctypes.Structure):
 
 @pytest.fixture(scope="module")
 def eng():
-    srcs = [os.path.join(HERE, "native", "engine_host_stub.cpp")]
-    hostdir = os.path.join(ROOT, "rust-bitcoinconsensus_amd", "csrc", "host")
-    srcs += [os.path.join(hostdir, f) for f in sorted(os.listdir(hostdir))
-             if f.endswith(".cpp") and f not in ("workload.cpp", "tupleset.cpp")]  # GPU generators
-    deps = srcs + [os.path.join(hostdir, f) for f in os.listdir(hostdir) if f.endswith(".h")]
-    deps += [os.path.join(ROOT, "oracle", "bcc_oracle.c"),
-             os.path.join(ROOT, "rust-bitcoinconsensus_amd", "csrc", "pipeline.h")]
-    if not os.path.exists(SO) or any(os.path.getmtime(d) > os.path.getmtime(SO) for d in deps):
-        os.makedirs(os.path.dirname(SO), exist_ok=True)
-        subprocess.check_call(["g++", "-O2", "-std=c++17", "-shared", "-fPIC",
-                               "-I" + os.path.join(ROOT, "include"),
-                               "-I" + os.path.join(ROOT, "rust-bitcoinconsensus_amd", "csrc"),
-                               "-o", SO] + srcs + ["-x", "c", os.path.join(ROOT, "oracle", "bcc_oracle.c")])
-    L = ctypes.CDLL(SO)
-    L.bitcoinconsensus_verify_batch.restype = ctypes.c_long
-    L.bcc_debug_fail_device_rounds.argtypes = [ctypes.c_int]
-    return L
+    import engine_stub
+    return engine_stub.load()
 
 
 def call(L, spk, amount, tx, nin, flags):
@@ -125,9 +110,6 @@ def test_pubkey_verify_batch_front_end(eng):
     msg = b"".join(t["hash"] for t in ts)
     out = ctypes.create_string_buffer(len(ts))
     u64p = ctypes.POINTER(ctypes.c_uint64)
-    eng.bcc_pubkey_verify_batch.argtypes = [ctypes.c_char_p, u64p, ctypes.c_char_p,
-                                            ctypes.c_char_p, u64p, ctypes.c_char_p,
-                                            ctypes.c_size_t, ctypes.c_int]
     assert eng.bcc_pubkey_verify_batch(pb, po, msg, sb, so, out, len(ts), 0) == 0
     bad = [(t["cls"], i) for i, t in enumerate(ts) if out.raw[i] != t["verdict"]]
     assert not bad, bad[:20]
@@ -154,7 +136,8 @@ class Stats(ctypes.Structure):
                                                 "aux_messages", "host_rejected")] + [
         (k, ctypes.c_double) for k in ("host_seconds", "gpu_seconds", "prepare_seconds",
                                        "interpret_seconds", "merge_seconds", "stage_seconds",
-                                       "total_seconds")] + [("device_retries", ctypes.c_size_t)]
+                                       "total_seconds")] + [("device_retries", ctypes.c_size_t),
+                                                             ("devices", ctypes.c_size_t)]
 
 
 def test_device_failure_retried_once(eng):
@@ -227,3 +210,42 @@ def test_witness_without_p2sh_pinned(eng):
         # with WITNESS_UNEXPECTED (the reference would assert here only on success)
         if v["name"].startswith("p2sh"):
             assert got[0] == 0, v["name"]
+
+
+def test_multi_device_verify_batch_identical(eng):
+    """Node sharding (§8e): verify_batch over 3 'devices' (the stub's pipeline ignores the id, but
+    the grouping, the per-device worker threads and the verdict gather are the product's) equals
+    the single-device results on every script case; the rounds really were split."""
+    import engine_stub
+    allc = cases()
+    by_flags = {}
+    for c in allc:
+        by_flags.setdefault(c["flags"], []).append(c)
+    cs = max(by_flags.values(), key=len)
+    vs = [dict(spk=c["spk"], tx=c["tx"], amount=c["amount"], nin=c["nin"], flags=c["flags"]) for c in cs]
+    rc1, single = _batch(eng, vs)
+    try:
+        engine_stub.set_devices(eng, [0, 1, 2])
+        rc3, multi = _batch(eng, vs)
+        st = Stats()
+        eng.bcc_last_batch_stats(ctypes.byref(st))
+    finally:
+        engine_stub.set_devices(eng, [])
+    assert multi == single and rc3 == rc1
+    assert multi == [(c["ret"], c["err"]) for c in cs]
+    assert st.devices == 3
+
+
+def test_pubkey_verify_batch_sharded(eng):
+    """bcc_pubkey_verify_batch(device = -1) over 3 devices: contiguous ranges, same verdicts."""
+    import engine_stub
+    from fixtures import ecdsa_tuples
+    ts = ecdsa_tuples() * 6
+    one = engine_stub.pubkey_verify(eng, ts, 0)
+    try:
+        engine_stub.set_devices(eng, [0, 1, 2])
+        many = engine_stub.pubkey_verify(eng, ts, -1)
+    finally:
+        engine_stub.set_devices(eng, [])
+    assert many == one
+    assert list(one) == [t["verdict"] for t in ts]

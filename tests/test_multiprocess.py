@@ -42,6 +42,50 @@ def test_aggregate_world2_gloo():
     assert res == [(0, 2.0, 201), (1, 2.0, 201)]
 
 
+def _shard_worker(rank, world, port, q):
+    """One rank of a sharded C4-style run: verdicts for its contiguous range of ONE global tuple
+    set (the product's host front end + the oracle-stubbed device pipeline), then bench.py's
+    bitmap all-gather."""
+    import torch.distributed as dist
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "tests")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import bench
+    import engine_stub
+    from fixtures import ecdsa_tuples
+    ts = ecdsa_tuples() * 3
+    n = len(ts)
+    lo, hi = n * rank // world, n * (rank + 1) // world
+    L = engine_stub.load()
+    local = engine_stub.pubkey_verify(L, ts[lo:hi])
+    full = bench.gather_verdicts(list(local), world, device="cpu")
+    q.put((rank, bytes(full.tolist())))
+    dist.destroy_process_group()
+
+
+def test_sharded_tuple_set_gather_world2_gloo():
+    """§8e: two ranks each verify their half of one tuple set; the gathered validity bitmap equals
+    the single-process verdicts (and the reference's labels)."""
+    sys.path[:0] = [os.path.join(ROOT, "tests")]
+    import engine_stub
+    from fixtures import ecdsa_tuples
+    engine_stub.load()  # build once, before the ranks start
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_shard_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    for p in ps:
+        p.join(300)
+        assert p.exitcode == 0
+    res = dict(q.get() for _ in range(2))
+    ts = ecdsa_tuples() * 3
+    single = engine_stub.pubkey_verify(engine_stub.load(), ts)
+    assert res[0] == res[1] == single
+    assert list(single) == [t["verdict"] for t in ts]
+
+
 def test_single_rank_passthrough():
     sys.path.insert(0, ROOT)
     import bench

@@ -56,7 +56,7 @@ BCC_HD void mad_acc(u64& acc, u32 a, u32 b) {
 }
 
 // 48 p with every limb raised to >= 2^29 + 2^27 by borrowing from the next one (computed by
-// tools/derive_fe29_constants.py): a - b + K48 never underflows a limb for normalised b.
+// tools/fe9/derive_constants.py): a - b + K48 never underflows a limb for normalised b.
 #define BCC_K48_LIMBS {0x3fff48d0u, 0x3ffffe7eu, 0x3ffffffeu, 0x3ffffffeu, 0x3ffffffeu, \
                        0x3ffffffeu, 0x3ffffffeu, 0x3ffffffeu, 0x2ffffffeu}
 // p in radix 2^29 (canonical digits)
