@@ -163,7 +163,8 @@ class BatchStats(ctypes.Structure):
                 ("host_seconds", ctypes.c_double), ("gpu_seconds", ctypes.c_double),
                 ("prepare_seconds", ctypes.c_double), ("interpret_seconds", ctypes.c_double),
                 ("merge_seconds", ctypes.c_double), ("stage_seconds", ctypes.c_double),
-                ("total_seconds", ctypes.c_double)]
+                ("total_seconds", ctypes.c_double), ("device_retries", ctypes.c_size_t),
+                ("devices", ctypes.c_size_t)]
 
 
 def _bind_consensus(L):

@@ -81,3 +81,18 @@ def test_python_mirror_api_surface():
     assert B.height_to_flags(481824) == B.VERIFY_ALL
     for name in ("verify", "verify_with_flags", "verify_batch", "version", "height_to_flags"):
         assert callable(getattr(B, name))
+
+
+def test_python_structs_match_c_layout(tmp_path):
+    """The ctypes mirrors of the ABI's structs have the C sizes (a short mirror would let the
+    library write past the Python buffer)."""
+    import bitcoinconsensus_amd as B
+    src = tmp_path / "sz.c"
+    src.write_text('#include <stdio.h>\n#include "bcc_bench.h"\nint main(void) { printf("%zu %zu %zu\\n",'
+                   ' sizeof(bcc_batch_stats), sizeof(bcc_batch_item), sizeof(bcc_tupleset_host));'
+                   ' return 0; }\n')
+    exe = tmp_path / "sz"
+    subprocess.check_call(["gcc", "-I" + os.path.join(ROOT, "include"), str(src), "-o", str(exe)])
+    got = [int(x) for x in subprocess.check_output([str(exe)]).split()]
+    assert got == [ctypes.sizeof(B.BatchStats), ctypes.sizeof(B.BatchItem),
+                   ctypes.sizeof(B.TuplesetHost)]
