@@ -82,6 +82,14 @@ bcc_workload* bcc_workload_from_items(const bcc_batch_item* items, size_t n, uns
                                       int device);
 /* copy back the verdicts of the staged tuple rows (one byte per tuple, bcc_workload_shape) */
 int bcc_workload_verdicts(bcc_workload* w, uint8_t* out);
+/* Mutated copies of a workload's items for agreement runs (see workload.cpp): kinds[i] = 0 for an
+ * untouched item, else 1 + the mutation (bit flip anywhere in the tx / in its back half, amount
+ * +-1, spent-script bit flip, truncated tx, nIn out of range).  Valid while the set lives. */
+typedef struct bcc_itemset bcc_itemset;
+bcc_itemset* bcc_workload_mutate(const bcc_workload* w, double rate, uint64_t seed,
+                                 uint8_t* kinds);
+const bcc_batch_item* bcc_itemset_items(const bcc_itemset* m, size_t* n);
+void bcc_itemset_free(bcc_itemset* m);
 /* item index of every staged tuple row (uint32 per tuple) */
 int bcc_workload_tuple_items(const bcc_workload* w, uint32_t* out);
 /* the sighash (msg32) rows of the last run, 32 bytes per tuple (synchronous) */

@@ -248,6 +248,28 @@ double ref_bulk_verify_script(int nthreads, long n, const unsigned char* spk_blo
     });
 }
 
+// The same over an array of the engine's batch items (struct bcc_batch_item of the engine's
+// include/bitcoinconsensus.h, restated here field by field): the bulk checker of agreement runs.
+struct ref_batch_item {
+    const unsigned char* spk;
+    unsigned int spk_len;
+    int64_t amount;
+    const unsigned char* tx;
+    unsigned int tx_len;
+    unsigned int n_in;
+};
+
+double ref_bulk_verify_items(int nthreads, long n, const ref_batch_item* items, unsigned int flags,
+                             int* ret, int* err) {
+    return run_pool(nthreads, n, [=](long i) {
+        bitcoinconsensus_error e = bitcoinconsensus_ERR_OK;
+        const ref_batch_item& it = items[i];
+        ret[i] = bitcoinconsensus_verify_script_with_amount(it.spk, it.spk_len, it.amount, it.tx,
+                                                            it.tx_len, it.n_in, flags, &e);
+        err[i] = (int)e;
+    });
+}
+
 // Tuple-level baseline: CPubKey::Verify over (pub, hash, sig) tuples. pub in 65-B slots with
 // lengths, sig in 80-B slots with lengths.
 double ref_bench_pubkey_verify(int nthreads, long n, const unsigned char* pub65, const int* publen,

@@ -360,6 +360,65 @@ const bcc_batch_item* bcc_workload_items(const bcc_workload* w, size_t* n) {
     return w ? w->items.data() : nullptr;
 }
 
+// Mutated copies of a workload's items (agreement runs): item i is mutated with probability
+// `rate` (splitmix of seed and i), kinds[i] = 0 (untouched) or 1 + the mutation: 1 flip one bit
+// of the tx (any byte), 2 flip one bit in the back half of the tx (witness / signatures / the
+// later inputs), 3 amount +-1, 4 flip one bit of the spent script, 5 drop the tx's last byte,
+// 6 nIn = number of inputs.  A mutated item gets its own copy of the tx; the others keep sharing
+// their tx buffer with their neighbours (the engine parses a shared buffer once).
+struct bcc_itemset {
+    std::vector<std::vector<uint8_t>> bufs;
+    std::vector<bcc_batch_item> items;
+};
+
+bcc_itemset* bcc_workload_mutate(const bcc_workload* w, double rate, uint64_t seed,
+                                 uint8_t* kinds) {
+    if (!w) return nullptr;
+    auto* m = new bcc_itemset();
+    m->items = w->items;
+    const uint64_t thr = (uint64_t)(rate * 18446744073709551615.0);
+    for (size_t i = 0; i < w->n; i++) {
+        uint64_t u = splitmix64(seed ^ (0x5851F42D4C957F2DULL * (i + 1)));
+        kinds[i] = 0;
+        if (u > thr) continue;
+        bcc_batch_item& it = m->items[i];
+        const uint64_t v = splitmix64(u);
+        const int kind = 1 + (int)(v % 6);
+        kinds[i] = (uint8_t)kind;
+        std::vector<uint8_t> tx(it.tx_to, it.tx_to + it.tx_to_len);
+        std::vector<uint8_t> spk(it.script_pubkey, it.script_pubkey + it.script_pubkey_len);
+        const uint64_t r = v >> 8;
+        switch (kind) {
+            case 1: if (!tx.empty()) tx[r % tx.size()] ^= (uint8_t)(1u << ((r >> 32) % 8)); break;
+            case 2: if (tx.size() > 1) tx[tx.size() / 2 + r % (tx.size() - tx.size() / 2)] ^= (uint8_t)(1u << ((r >> 32) % 8)); break;
+            case 3: it.amount += (r & 1) ? 1 : -1; break;
+            case 4: if (!spk.empty()) spk[r % spk.size()] ^= (uint8_t)(1u << ((r >> 32) % 8)); break;
+            case 5: if (!tx.empty()) tx.pop_back(); break;
+            case 6: {
+                bcc::host::Tx t;
+                if (bcc::host::parse_tx(it.tx_to, it.tx_to_len, t)) it.n_in = (unsigned)t.vin.size();
+                break;
+            }
+        }
+        m->bufs.push_back(std::move(tx));
+        const std::vector<uint8_t>& tb = m->bufs.back();
+        it.tx_to = tb.empty() ? nullptr : tb.data();
+        it.tx_to_len = (unsigned)tb.size();
+        m->bufs.push_back(std::move(spk));
+        const std::vector<uint8_t>& sb = m->bufs.back();
+        it.script_pubkey = sb.empty() ? nullptr : sb.data();
+        it.script_pubkey_len = (unsigned)sb.size();
+    }
+    return m;
+}
+
+const bcc_batch_item* bcc_itemset_items(const bcc_itemset* m, size_t* n) {
+    if (n) *n = m ? m->items.size() : 0;
+    return m ? m->items.data() : nullptr;
+}
+
+void bcc_itemset_free(bcc_itemset* m) { delete m; }
+
 int bcc_workload_tuple_items(const bcc_workload* w, uint32_t* out) {
     if (!w) return -1;
     if (!w->tuple_item.empty()) memcpy(out, w->tuple_item.data(), 4 * w->tuple_item.size());

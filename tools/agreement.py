@@ -1,6 +1,15 @@
 """Verdict agreement at scale (north star: 100 % agreement on >= 10M mixed valid / invalid inputs).
 
-    python tools/agreement.py [--c4 10000000] [--c5 4000000] [--out profiles/r01_agreement.json]
+    python tools/agreement.py [--c4 10000000] [--c5 4000000] [--scripts 10000000]
+                              [--out profiles/r01_agreement.json]
+
+--scripts: SCRIPT-level agreement through the drop-in batch ABI.  Chunks alternate C2 (1M P2WPKH
+spends, slices of one global set) and C3 (block413567-shaped transactions, P2PKH / P2WPKH / P2SH
+2-of-3); ~12 % of the items of every chunk are mutated (bcc_workload_mutate: bit flips anywhere in
+the tx or in its back half, amount +-1, spent-script bit flips, truncated txs, nIn out of range).
+Every item goes through bitcoinconsensus_verify_batch (host interpreter + GPU rounds) and through
+the REFERENCE's bitcoinconsensus_verify_script_with_amount (oracle/_ref, 16 host threads); (ret,
+err) must agree on every item.  Most chunks use VERIFY_ALL, two use P2SH|DERSIG and NONE.
 
 C4: the adversarial ECDSA tuple set (90 % valid + 18 classes, include/bcc_amd.h bcc_tupleset_c4)
 verified on the GPU, then every tuple re-verified by the REFERENCE (oracle/_ref: CPubKey::Verify of
@@ -55,10 +64,81 @@ def check(kind, n, R, threads):
     return out
 
 
+def check_scripts(total, R, threads):
+    import ctypes
+    L, BL = B.lib(), B.blib()
+    BL.bcc_workload_mutate.argtypes = [ctypes.c_void_p, ctypes.c_double, ctypes.c_uint64,
+                                       ctypes.c_void_p]
+    BL.bcc_workload_mutate.restype = ctypes.c_void_p
+    BL.bcc_itemset_items.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_size_t)]
+    BL.bcc_itemset_items.restype = ctypes.c_void_p
+    BL.bcc_itemset_free.argtypes = [ctypes.c_void_p]
+    L.bitcoinconsensus_verify_batch.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint,
+                                                ctypes.c_void_p, ctypes.c_void_p]
+    R.L.ref_bulk_verify_items.argtypes = [ctypes.c_int, ctypes.c_long, ctypes.c_void_p,
+                                          ctypes.c_uint, ctypes.c_void_p, ctypes.c_void_p]
+    R.L.ref_bulk_verify_items.restype = ctypes.c_double
+    shape = [tuple(t) for t in json.load(open(os.path.join(ROOT, "tests", "golden",
+                                                           "block413567_shape.json")))["txs"]]
+    kinds_names = ["untouched", "tx_bitflip", "tx_back_bitflip", "amount", "spk_bitflip",
+                   "truncated", "nin_range"]
+    done, chunk, out = 0, 0, dict(items=0, mismatches=0, valid=0, by_kind={}, by_chunk=[])
+    t0 = time.time()
+    while done < total:
+        flags = [B.VERIFY_ALL, B.VERIFY_P2SH | B.VERIFY_DERSIG, B.VERIFY_NONE][
+            0 if chunk < 8 else (chunk - 7) % 3]
+        if chunk % 2 == 0:
+            n = min(1_000_000, total - done)
+            wl = B.Workload(n, seed=0x5EED0001, first=done)
+            kind = "c2"
+        else:
+            ntx = 60 * len(shape)  # ~190k inputs
+            wl = B.Workload(kind="block", shape=(shape * 60)[:ntx], seed=0x5EED0003 + chunk)
+            kind = "c3"
+        n = wl.n
+        kinds = np.zeros(n, np.uint8)
+        ms = BL.bcc_workload_mutate(wl.h, 0.12, 0xA9EE + chunk, kinds.ctypes.data)
+        cnt = ctypes.c_size_t()
+        items = BL.bcc_itemset_items(ms, ctypes.byref(cnt))
+        ret = np.zeros(n, np.int32)
+        err = np.zeros(n, np.int32)
+        g0 = time.time()
+        rc = L.bitcoinconsensus_verify_batch(items, n, flags, ret.ctypes.data, err.ctypes.data)
+        g1 = time.time()
+        rret = np.zeros(n, np.int32)
+        rerr = np.zeros(n, np.int32)
+        rs = R.L.ref_bulk_verify_items(threads, n, items, flags, rret.ctypes.data,
+                                       rerr.ctypes.data)
+        bad = np.nonzero((ret != rret) | (err != rerr))[0]
+        for k in range(len(kinds_names)):
+            m = kinds == k
+            e = out["by_kind"].setdefault(kinds_names[k], dict(n=0, ref_valid=0, mismatches=0))
+            e["n"] += int(m.sum())
+            e["ref_valid"] += int(rret[m].sum())
+            e["mismatches"] += int(((ret != rret) | (err != rerr))[m].sum())
+        rec = dict(chunk=chunk, workload=kind, flags=flags, items=n, rc=int(rc),
+                   gpu_valid=int(ret.sum()), ref_valid=int(rret.sum()), mismatches=int(len(bad)),
+                   first_mismatches=[int(i) for i in bad[:10]],
+                   verify_batch_s=round(g1 - g0, 2), reference_s=round(rs, 2),
+                   elapsed_s=round(time.time() - t0, 1))
+        print(json.dumps(rec), flush=True)
+        out["by_chunk"].append(rec)
+        out["items"] += n
+        out["mismatches"] += int(len(bad))
+        out["valid"] += int(rret.sum())
+        BL.bcc_itemset_free(ms)
+        wl.free()
+        done += n
+        chunk += 1
+    out.update(config="scripts", reference_threads=threads, mutated_rate=0.12)
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--c4", type=int, default=10_000_000)
     ap.add_argument("--c5", type=int, default=4_000_000)
+    ap.add_argument("--scripts", type=int, default=0)
     ap.add_argument("--threads", type=int, default=16)
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "agreement.json"))
     a = ap.parse_args()
@@ -68,6 +148,8 @@ def main():
         res.append(check("c4", a.c4, R, a.threads))
     if a.c5:
         res.append(check("c5", a.c5, R, a.threads))
+    if a.scripts:
+        res.append(check_scripts(a.scripts, R, a.threads))
     json.dump(res, open(a.out, "w"), indent=1)
     assert all(r["mismatches"] == 0 for r in res), "GPU / reference verdicts differ"
 
