@@ -45,6 +45,49 @@ int mi_schnorr_verify_device(const uint8_t* d_sig64, const uint8_t* d_msg32,
                              const uint8_t* d_xonly32, uint8_t* d_verdict, size_t n,
                              void* stream);
 
+/* ---- BIP341 / BIP342 (Taproot) signature checks ------------------------------------------------
+ * Replaces GenericTransactionSignatureChecker::CheckSchnorrSignature per check
+ * (depend/bitcoin/src/script/interpreter.cpp:1678-1704): SignatureHashSchnorr (:1491-1574) over
+ * the tx's PrecomputedTransactionData initialised with its spent outputs (:1422-1472), then
+ * XOnlyPubKey::VerifySchnorr (pubkey.cpp:176-182).  The signature hash (TapSighash tagged
+ * SHA-256 and the tx's single-SHA-256 aux hashes) and the BIP340 verification run on the GPU.
+ * The fields mirror the checker's inputs: the spending tx, the outputs it spends (one per input,
+ * a serialized std::vector<CTxOut> as handed to PrecomputedTransactionData::Init), the input
+ * index, the signature (64 bytes, or 65 with the hash_type), the 32-byte x-only key, the
+ * sigversion and ScriptExecutionData's annex / tapleaf hash / OP_CODESEPARATOR position.
+ * Adjacent items with the same tx and spent_outputs pointers share the per-tx hashes. */
+#define BCC_SIGVERSION_TAPROOT 0   /* key path spend (SigVersion::TAPROOT) */
+#define BCC_SIGVERSION_TAPSCRIPT 1 /* BIP342 script path (SigVersion::TAPSCRIPT) */
+typedef struct bcc_taproot_check {
+    const unsigned char* tx;            /* serialized spending tx, exactly tx_len bytes */
+    unsigned int tx_len;
+    const unsigned char* spent_outputs; /* serialized std::vector<CTxOut>, one per input */
+    unsigned int spent_outputs_len;
+    unsigned int n_in;
+    const unsigned char* sig;           /* 64 or 65 bytes (anything else: SCHNORR_SIG_SIZE) */
+    unsigned int sig_len;
+    const unsigned char* pubkey32;      /* x-only key bytes */
+    int sigversion;                     /* BCC_SIGVERSION_* */
+    const unsigned char* annex;         /* the annex witness element incl. 0x50, NULL: none */
+    unsigned int annex_len;
+    const unsigned char* tapleaf_hash32; /* TAPSCRIPT only (execdata.m_tapleaf_hash) */
+    uint32_t codeseparator_pos;         /* TAPSCRIPT only (0xFFFFFFFF: none executed) */
+} bcc_taproot_check;
+/* script_error.h:73-75 values written to serror_out */
+#define BCC_SCRIPT_ERR_SCHNORR_SIG_SIZE 44
+#define BCC_SCRIPT_ERR_SCHNORR_SIG_HASHTYPE 45
+#define BCC_SCRIPT_ERR_SCHNORR_SIG 46
+/* ret_out[i] = 1 (valid) or 0 (serror_out[i] = one of the three codes above), or -1 where the
+ * reference checker cannot be built and asserts instead: the tx does not deserialize to exactly
+ * tx_len bytes, the spent outputs do not parse or their count differs from the tx's inputs,
+ * n_in >= inputs, or no witness-bearing input spends a 34-byte OP_1 script (the tx data would not
+ * be BIP341-ready); serror_out[i] = 1 (SCRIPT_ERR_UNKNOWN_ERROR) then.  sighash_out (optional,
+ * 32 bytes per item): the signature hash where one was computed, else zeros.  Synchronous on
+ * `device`, or for device = -1 spread over the bcc_set_devices() GPUs.  Returns 0, or -1 on bad
+ * arguments or a device failure (then no output is meaningful). */
+int bcc_taproot_verify_batch(const bcc_taproot_check* items, size_t n, int* ret_out,
+                             int* serror_out, unsigned char* sighash_out, int device);
+
 /* ---- tuple level with the CPubKey front end ---------------------------------------------------
  * verdict[i] = CPubKey(pub_i).Verify(msg_i, sig_i) (depend/bitcoin/src/pubkey.cpp:191-207) for n
  * tuples: pub_i = pub_blob[pub_off[i] .. pub_off[i+1]) (any length; the CPubKey length filter,

@@ -570,6 +570,7 @@ typedef struct {
     const uint8_t* script;
     size_t scriptlen;
     uint32_t sequence;
+    int has_witness;        /* scriptWitness non-empty */
 } txin_t;
 typedef struct {
     const uint8_t* ser; /* serialized CTxOut: value(8) || compactsize || script */
@@ -578,7 +579,7 @@ typedef struct {
 typedef struct {
     int32_t version;
     uint32_t locktime;
-    size_t nin, nout;
+    size_t nin, nout, ser_size;   /* ser_size: bytes consumed */
     txin_t* vin;
     txout_t* vout;
 } tx_t;
@@ -663,6 +664,7 @@ static int tx_parse(const uint8_t* p, size_t n, tx_t* tx) {
         for (size_t i = 0; i < tx->nin; i++) {
             uint64_t k = rd_cs(&r);
             if (k) any = 1;
+            tx->vin[i].has_witness = k != 0;
             for (uint64_t j = 0; j < k && !r.bad; j++) {
                 uint64_t l = rd_cs(&r);
                 rd_take(&r, (size_t)l);
@@ -673,6 +675,7 @@ static int tx_parse(const uint8_t* p, size_t n, tx_t* tx) {
     }
     if (flags) return 0;
     tx->locktime = (uint32_t)rd_le(&r, 4);
+    tx->ser_size = r.pos;
     return !r.bad;
 }
 
@@ -806,5 +809,166 @@ int bcco_sighash(const uint8_t* txb, size_t txlen, unsigned nIn, const uint8_t* 
     }
     free(b.p);
     tx_free(&tx);
+    return 1;
+}
+
+/* ========================================================================================== */
+/* BIP341 / BIP342 signature hash + CheckSchnorrSignature                                     */
+/* ========================================================================================== */
+/* std::vector<CTxOut> (serialize.h:318-347 vector rule): compactsize count, then per output
+ * value(8) || compactsize || script.  Fills out[] (the serialized CTxOut of each entry). */
+static int spent_parse(const uint8_t* p, size_t n, txout_t** out, size_t* cnt) {
+    rd_t r = {p, n, 0, 0};
+    uint64_t k = rd_cs(&r);
+    if (r.bad || k > n) return 0;
+    *cnt = (size_t)k;
+    *out = (txout_t*)calloc(k ? k : 1, sizeof(txout_t));
+    for (size_t i = 0; i < k; i++) {
+        size_t start = r.pos;
+        rd_take(&r, 8);
+        uint64_t sl = rd_cs(&r);
+        rd_take(&r, (size_t)sl);
+        if (r.bad) return 0;
+        (*out)[i].ser = p + start;
+        (*out)[i].serlen = r.pos - start;
+    }
+    return r.pos == n;
+}
+
+/* SHA256(SHA256(tag) || SHA256(tag) || msg) (hash.cpp TaggedHash + CHashWriter::GetSHA256) */
+static void tagged_sha256(const char* tag, const uint8_t* m, size_t n, uint8_t out[32]) {
+    uint8_t th[32];
+    bcco_sha256((const uint8_t*)tag, strlen(tag), th);
+    sha256_ctx c;
+    sha256_init(&c);
+    sha256_write(&c, th, 32);
+    sha256_write(&c, th, 32);
+    sha256_write(&c, m, n);
+    sha256_final(&c, out);
+}
+
+/* SignatureHashSchnorr (interpreter.cpp:1491-1574) with PrecomputedTransactionData::Init's
+ * single-SHA256 tx hashes (:1366-1417, :1455-1471) and the annex hash of
+ * VerifyWitnessProgram (:1889-1893: SHA256 of the annex serialized with its compactsize). */
+int bcco_sighash_schnorr(const uint8_t* txb, size_t txlen, const uint8_t* spent, size_t spentlen,
+                         unsigned nIn, int hash_type, int sigversion, const uint8_t* annex,
+                         size_t annexlen, const uint8_t tapleaf32[32], uint32_t codesep_pos,
+                         uint8_t out[32]) {
+    tx_t tx;
+    txout_t* so = NULL;
+    size_t nso = 0;
+    int rc = -1;
+    if (!tx_parse(txb, txlen, &tx) || tx.ser_size != txlen) { tx_free(&tx); return -1; }
+    if (!spent_parse(spent, spentlen, &so, &nso) || nso != tx.nin || nIn >= tx.nin) goto done;
+    {
+        /* m_bip341_taproot_ready (Init :1436-1452): some witness-bearing input spends a 34-byte
+         * scriptPubKey starting with OP_1; SignatureHashSchnorr asserts it (:1512) */
+        int ready = 0;
+        for (size_t i = 0; i < tx.nin; i++) {
+            const uint8_t* spk = so[i].ser + 8;
+            size_t spkl = so[i].serlen - 8;
+            if (tx.vin[i].has_witness && spkl == 35 && spk[0] == 34 && spk[1] == 0x51) ready = 1;
+        }
+        if (!ready) goto done;
+    }
+    rc = 0;
+    {
+        const int output_type = hash_type == 0 ? 1 : (hash_type & 3);
+        const int input_type = hash_type & 0x80;
+        if (!(hash_type <= 0x03 || (hash_type >= 0x81 && hash_type <= 0x83))) goto done;
+        if (output_type == 3 && nIn >= tx.nout) goto done;
+        buf_t b = {0};
+        bput_le(&b, 0, 1);                          /* epoch */
+        bput_le(&b, (uint64_t)hash_type, 1);
+        bput_le(&b, (uint32_t)tx.version, 4);
+        bput_le(&b, tx.locktime, 4);
+        if (!input_type) {
+            uint8_t h[32];
+            buf_t t = {0};
+            for (size_t i = 0; i < tx.nin; i++) bput(&t, tx.vin[i].prevout, 36);
+            bcco_sha256(t.p, t.n, h); bput(&b, h, 32); t.n = 0;
+            for (size_t i = 0; i < nso; i++) bput(&t, so[i].ser, 8);
+            bcco_sha256(t.p, t.n, h); bput(&b, h, 32); t.n = 0;
+            for (size_t i = 0; i < nso; i++) bput(&t, so[i].ser + 8, so[i].serlen - 8);
+            bcco_sha256(t.p, t.n, h); bput(&b, h, 32); t.n = 0;
+            for (size_t i = 0; i < tx.nin; i++) bput_le(&t, tx.vin[i].sequence, 4);
+            bcco_sha256(t.p, t.n, h); bput(&b, h, 32);
+            free(t.p);
+        }
+        if (output_type == 1) {
+            uint8_t h[32];
+            buf_t t = {0};
+            for (size_t i = 0; i < tx.nout; i++) bput(&t, tx.vout[i].ser, tx.vout[i].serlen);
+            bcco_sha256(t.p, t.n, h);
+            bput(&b, h, 32);
+            free(t.p);
+        }
+        const int ext_flag = sigversion == 1 ? 1 : 0;
+        bput_le(&b, (uint64_t)((ext_flag << 1) + (annex ? 1 : 0)), 1);   /* spend_type */
+        if (input_type) {
+            bput(&b, tx.vin[nIn].prevout, 36);
+            bput(&b, so[nIn].ser, so[nIn].serlen);
+            bput_le(&b, tx.vin[nIn].sequence, 4);
+        } else {
+            bput_le(&b, nIn, 4);
+        }
+        if (annex) {
+            uint8_t h[32];
+            buf_t t = {0};
+            bput_cs(&t, annexlen);
+            bput(&t, annex, annexlen);
+            bcco_sha256(t.p, t.n, h);
+            bput(&b, h, 32);
+            free(t.p);
+        }
+        if (output_type == 3) {
+            uint8_t h[32];
+            bcco_sha256(tx.vout[nIn].ser, tx.vout[nIn].serlen, h);
+            bput(&b, h, 32);
+        }
+        if (sigversion == 1) {
+            bput(&b, tapleaf32, 32);
+            bput_le(&b, 0, 1);                      /* key_version */
+            bput_le(&b, codesep_pos, 4);
+        }
+        tagged_sha256("TapSighash", b.p, b.n, out);
+        free(b.p);
+        rc = 1;
+    }
+done:
+    free(so);
+    tx_free(&tx);
+    return rc;
+}
+
+/* GenericTransactionSignatureChecker::CheckSchnorrSignature (interpreter.cpp:1678-1704):
+ * returns 1 (valid) or 0 with *serror = SCHNORR_SIG_SIZE / SCHNORR_SIG_HASHTYPE / SCHNORR_SIG
+ * (script_error.h:73-75 values), or -1 if the tx / spent outputs do not parse or nIn is out of
+ * range (the reference asserts there).  sighash32 (optional) receives the signature hash. */
+int bcco_taproot_check(const uint8_t* txb, size_t txlen, const uint8_t* spent, size_t spentlen,
+                       unsigned nIn, const uint8_t* sig, size_t siglen, const uint8_t pk32[32],
+                       int sigversion, const uint8_t* annex, size_t annexlen,
+                       const uint8_t tapleaf32[32], uint32_t codesep_pos, int* serror,
+                       uint8_t* sighash32) {
+    enum { ERR_SIZE = 44, ERR_HASHTYPE = 45, ERR_SIG = 46 };
+    uint8_t h[32];
+    *serror = 0;
+    /* the checker only exists for a parsed tx with its spent outputs (PrecomputedTransactionData
+     * asserts their count): inputs that do not meet that are refused before any check */
+    if (bcco_sighash_schnorr(txb, txlen, spent, spentlen, nIn, 0, sigversion, annex, annexlen,
+                             tapleaf32, codesep_pos, h) < 0)
+        return -1;
+    if (siglen != 64 && siglen != 65) { *serror = ERR_SIZE; return 0; }
+    int hash_type = 0;
+    if (siglen == 65) {
+        hash_type = sig[64];
+        if (hash_type == 0) { *serror = ERR_HASHTYPE; return 0; }
+    }
+    int rc = bcco_sighash_schnorr(txb, txlen, spent, spentlen, nIn, hash_type, sigversion, annex,
+                                  annexlen, tapleaf32, codesep_pos, h);
+    if (rc < 0) return -1;
+    if (rc == 0) { *serror = ERR_HASHTYPE; return 0; }
+    if (sighash32) memcpy(sighash32, h, 32);
+    if (!bcco_schnorr_verify(sig, h, pk32)) { *serror = ERR_SIG; return 0; }
     return 1;
 }

@@ -56,6 +56,28 @@ int bcco_ecmult_gen(const uint8_t k32[32], uint8_t x[32], uint8_t y[32]);
 int bcco_sighash(const uint8_t* tx, size_t txlen, unsigned nIn, const uint8_t* script,
                  size_t scriptlen, int hashtype, int64_t amount, int sigversion, uint8_t out32[32]);
 
+/* BIP341 / BIP342 SignatureHashSchnorr (interpreter.cpp:1491-1574) over a serialized tx and its
+ * spent outputs (a serialized std::vector<CTxOut>, one per input: PrecomputedTransactionData::Init
+ * :1422-1472).  sigversion 0 = TAPROOT (key path), 1 = TAPSCRIPT (tapleaf32 + codesep_pos used).
+ * annex = the annex witness element incl. its 0x50 byte, or NULL when absent.  Returns 1 with the
+ * hash, 0 where the reference returns false (bad hash_type, SINGLE without a matching output),
+ * -1 if the tx (all tx_len bytes, the bitcoinconsensus.cpp:91-92 size rule) or the spent outputs
+ * do not parse, their counts differ, nIn is out of range or the tx data would not be BIP341-ready
+ * (no witness-bearing input spends a 34-byte OP_1 script, interpreter.cpp:1436-1452). */
+int bcco_sighash_schnorr(const uint8_t* tx, size_t txlen, const uint8_t* spent, size_t spentlen,
+                         unsigned nIn, int hash_type, int sigversion, const uint8_t* annex,
+                         size_t annexlen, const uint8_t tapleaf32[32], uint32_t codesep_pos,
+                         uint8_t out32[32]);
+
+/* GenericTransactionSignatureChecker::CheckSchnorrSignature (interpreter.cpp:1678-1704): 1 valid;
+ * 0 invalid with *serror = 44 SCHNORR_SIG_SIZE / 45 SCHNORR_SIG_HASHTYPE / 46 SCHNORR_SIG
+ * (script_error.h:73-75); -1 for inputs bcco_sighash_schnorr refuses. */
+int bcco_taproot_check(const uint8_t* tx, size_t txlen, const uint8_t* spent, size_t spentlen,
+                       unsigned nIn, const uint8_t* sig, size_t siglen, const uint8_t pk32[32],
+                       int sigversion, const uint8_t* annex, size_t annexlen,
+                       const uint8_t tapleaf32[32], uint32_t codesep_pos, int* serror,
+                       uint8_t* sighash32);
+
 #ifdef __cplusplus
 }
 #endif

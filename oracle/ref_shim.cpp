@@ -12,6 +12,10 @@
 //                            (GenericTransactionSignatureChecker::VerifyECDSASignature,
 //                             depend/bitcoin/src/script/interpreter.cpp:1644-1676)
 //   * ref_schnorr_verify  -> secp256k1_schnorrsig_verify            secp256k1/src/modules/schnorrsig/main_impl.h:190-237
+//   * ref_taproot_check   -> GenericTransactionSignatureChecker::CheckSchnorrSignature with the
+//                            tx's PrecomputedTransactionData initialised with its spent outputs
+//                            (interpreter.cpp:1422-1472, 1491-1574, 1678-1704); the signature hash
+//                            is captured at VerifySchnorrSignature
 //   * ref_sign / ref_pubkey_create / ref_schnorr_sign: fixture generation only
 //   * ref_bench_* / ref_bulk_* -> dynamically chunked std::thread pool over the reference entry
 //                            points (cpu_baseline timing, bulk agreement checks)
@@ -20,6 +24,7 @@
 #include <script/bitcoinconsensus.h>
 #include <script/interpreter.h>
 #include <primitives/transaction.h>
+#include <hash.h>
 #include <pubkey.h>
 #include <version.h>
 #include <secp256k1.h>
@@ -84,6 +89,23 @@ protected:
         log.push_back(Capture{std::vector<unsigned char>(pubkey.begin(), pubkey.end()), vchSig,
                               sighash, ok});
         return ok;
+    }
+};
+
+class SchnorrCapturingChecker : public TransactionSignatureChecker {
+public:
+    mutable uint256 sighash;
+    mutable bool called = false;
+    SchnorrCapturingChecker(const CTransaction* tx, unsigned int nIn, const CAmount& amount,
+                            const PrecomputedTransactionData& txdata)
+        : TransactionSignatureChecker(tx, nIn, amount, txdata) {}
+
+protected:
+    bool VerifySchnorrSignature(Span<const unsigned char> sig, const XOnlyPubKey& pubkey,
+                                const uint256& h) const override {
+        sighash = h;
+        called = true;
+        return TransactionSignatureChecker::VerifySchnorrSignature(sig, pubkey, h);
     }
 };
 
@@ -190,6 +212,60 @@ int ref_schnorr_verify(const unsigned char* sig64, const unsigned char* msg32,
     secp256k1_xonly_pubkey pk;
     if (!secp256k1_xonly_pubkey_parse(sign_ctx(), &pk, xonly32)) return 0;
     return secp256k1_schnorrsig_verify(sign_ctx(), sig64, msg32, &pk);
+}
+
+// CheckSchnorrSignature (interpreter.cpp:1678-1704) for input nIn of tx, whose spent outputs are
+// the serialized std::vector<CTxOut> `spent` (PrecomputedTransactionData::Init).  sigversion 0 =
+// TAPROOT, 1 = TAPSCRIPT.  annex (incl. its 0x50 byte) or NULL; its hash is formed as
+// VerifyWitnessProgram does (:1889-1893).  Returns 1 / 0 (with *serror), or -1 if the tx / spent
+// outputs do not deserialize, their counts differ or nIn is out of range (the reference asserts).
+// *hashed = 1 when the signature hash was computed (then written to sighash32).
+int ref_taproot_check(const unsigned char* txb, size_t txlen, const unsigned char* spent,
+                      size_t spentlen, unsigned int nIn, const unsigned char* sig, size_t siglen,
+                      const unsigned char* pk32, int sigversion, const unsigned char* annex,
+                      size_t annexlen, const unsigned char* tapleaf32, uint32_t codesep_pos,
+                      int* serror, unsigned char* sighash32, int* hashed) {
+    try {
+        ByteReader ss(txb, txlen);
+        CTransaction tx(deserialize, ss);
+        std::vector<CTxOut> outs;
+        ByteReader so(spent, spentlen);
+        so >> outs;
+        unsigned char extra;
+        bool trailing = true;
+        try { so.read((char*)&extra, 1); } catch (const std::exception&) { trailing = false; }
+        if (trailing || outs.size() != tx.vin.size() || nIn >= tx.vin.size()) return -1;
+        // the tx must be exactly tx_len bytes (bitcoinconsensus.cpp:91-92's size rule)
+        if (GetSerializeSize(tx, PROTOCOL_VERSION) != txlen) return -1;
+        PrecomputedTransactionData txdata;
+        txdata.Init(tx, std::move(outs));
+        if (!txdata.m_bip341_taproot_ready) return -1;  // SignatureHashSchnorr would assert
+        ScriptExecutionData ed;
+        ed.m_annex_init = true;
+        ed.m_annex_present = annex != nullptr;
+        if (annex) {
+            std::vector<unsigned char> a(annex, annex + annexlen);
+            ed.m_annex_hash = (CHashWriter(SER_GETHASH, 0) << a).GetSHA256();
+        }
+        if (sigversion == 1) {
+            ed.m_tapleaf_hash_init = true;
+            ed.m_tapleaf_hash = uint256(std::vector<unsigned char>(tapleaf32, tapleaf32 + 32));
+            ed.m_codeseparator_pos_init = true;
+            ed.m_codeseparator_pos = codesep_pos;
+        }
+        SchnorrCapturingChecker chk(&tx, nIn, 0, txdata);
+        ScriptError serr = SCRIPT_ERR_OK;
+        bool ok = chk.CheckSchnorrSignature(Span<const unsigned char>(sig, siglen),
+                                            Span<const unsigned char>(pk32, 32),
+                                            sigversion == 1 ? SigVersion::TAPSCRIPT : SigVersion::TAPROOT,
+                                            ed, &serr);
+        *serror = (int)serr;
+        *hashed = chk.called ? 1 : 0;
+        if (chk.called) memcpy(sighash32, chk.sighash.begin(), 32);
+        return ok ? 1 : 0;
+    } catch (const std::exception&) {
+        return -1;
+    }
 }
 
 // ---- fixture generation helpers (NOT used by any parity check as a verdict source) ----

@@ -71,6 +71,9 @@ def lib():
         L.mi_schnorr_verify_device.argtypes = [vp] * 4 + [sz, vp]
         u64p = ctypes.POINTER(ctypes.c_uint64)
         L.bcc_pubkey_verify_batch.argtypes = [u8p, u64p, u8p, u8p, u64p, u8p, sz, ctypes.c_int]
+        L.bcc_taproot_verify_batch.argtypes = [ctypes.POINTER(TaprootCheck), sz,
+                                               ctypes.POINTER(ctypes.c_int),
+                                               ctypes.POINTER(ctypes.c_int), vp, ctypes.c_int]
         _bind_consensus(L)
         L.bcc_source_hash.restype = ctypes.c_char_p
         _lib = L
@@ -424,6 +427,63 @@ def pubkey_verify_batch(tuples, device=0):
     if rc != 0:
         raise RuntimeError(f"bcc_pubkey_verify_batch failed: {rc}")
     return out.raw[:n]
+
+
+SIGVERSION_TAPROOT = 0
+SIGVERSION_TAPSCRIPT = 1
+SCRIPT_ERR_SCHNORR_SIG_SIZE = 44
+SCRIPT_ERR_SCHNORR_SIG_HASHTYPE = 45
+SCRIPT_ERR_SCHNORR_SIG = 46
+
+
+class TaprootCheck(ctypes.Structure):
+    """include/bcc_amd.h bcc_taproot_check."""
+    _fields_ = [("tx", ctypes.c_char_p), ("tx_len", ctypes.c_uint),
+                ("spent_outputs", ctypes.c_char_p), ("spent_outputs_len", ctypes.c_uint),
+                ("n_in", ctypes.c_uint), ("sig", ctypes.c_char_p), ("sig_len", ctypes.c_uint),
+                ("pubkey32", ctypes.c_char_p), ("sigversion", ctypes.c_int),
+                ("annex", ctypes.c_char_p), ("annex_len", ctypes.c_uint),
+                ("tapleaf_hash32", ctypes.c_char_p), ("codeseparator_pos", ctypes.c_uint32)]
+
+
+def taproot_verify_batch(checks, device=0, sighashes=False, library=None):
+    """GenericTransactionSignatureChecker::CheckSchnorrSignature for each check
+    (depend/bitcoin/src/script/interpreter.cpp:1678-1704; include/bcc_amd.h
+    bcc_taproot_verify_batch).  A check is a dict with keys tx, spent (serialized
+    std::vector<CTxOut>), nin, sig, pk, sigversion and optionally annex (None: absent), tapleaf,
+    codesep.  Returns [(ret, serror)] (ret -1: inputs the reference checker cannot be built for),
+    plus the 32-byte sighashes when sighashes=True.  Adjacent checks of one tx should pass the
+    same tx / spent bytes objects: they then share the per-tx hashes.  `library`: another build
+    of the same C ABI (tests: the host code over the oracle stub)."""
+    n = len(checks)
+    arr = (TaprootCheck * max(n, 1))()
+    keep = []
+    for i, c in enumerate(checks):
+        tx, spent, sig, pk = bytes(c["tx"]), bytes(c["spent"]), bytes(c["sig"]), bytes(c["pk"])
+        annex = c.get("annex")
+        annex = None if annex is None else bytes(annex)
+        leaf = bytes(c.get("tapleaf") or bytes(32))
+        if i and checks[i - 1]["tx"] is c["tx"]:
+            tx = keep[-1][0]
+        if i and checks[i - 1]["spent"] is c["spent"]:
+            spent = keep[-1][1]
+        keep.append((tx, spent, sig, pk, annex, leaf))
+        assert len(pk) == 32 and len(leaf) == 32
+        arr[i] = TaprootCheck(tx, len(tx), spent, len(spent), c["nin"], sig, len(sig), pk,
+                              c.get("sigversion", SIGVERSION_TAPROOT),
+                              annex, 0 if annex is None else len(annex), leaf,
+                              c.get("codesep", 0xFFFFFFFF))
+    ret = (ctypes.c_int * max(n, 1))()
+    err = (ctypes.c_int * max(n, 1))()
+    hs = ctypes.create_string_buffer(32 * max(n, 1)) if sighashes else None
+    L = library if library is not None else lib()
+    rc = L.bcc_taproot_verify_batch(arr, n, ret, err, hs, device)
+    if rc != 0:
+        raise RuntimeError(f"bcc_taproot_verify_batch failed: {rc}")
+    out = [(ret[i], err[i]) for i in range(n)]
+    if sighashes:
+        return out, [hs.raw[32 * i: 32 * i + 32] for i in range(n)]
+    return out
 
 
 class TupleSet:

@@ -128,6 +128,12 @@ bool parse_tx(const uint8_t* data, size_t len, Tx& tx) {
     return true;
 }
 
+bool parse_txouts(const uint8_t* data, size_t len, std::vector<TxOut>& outs) {
+    Reader r{data, len};
+    outs.clear();
+    return read_vout(r, outs) && r.pos == len;
+}
+
 void put_compact_size(std::vector<uint8_t>& out, uint64_t v) {
     if (v < 253) {
         out.push_back((uint8_t)v);

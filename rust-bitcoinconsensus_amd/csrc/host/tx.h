@@ -48,6 +48,10 @@ struct Tx {
 // Returns false where the reference's deserializer throws (std::ios_base::failure).
 bool parse_tx(const uint8_t* data, size_t len, Tx& tx);
 
+// A serialized std::vector<CTxOut> occupying exactly len bytes (the spent outputs handed to
+// PrecomputedTransactionData::Init, interpreter.cpp:1422-1472).  False where it would not parse.
+bool parse_txouts(const uint8_t* data, size_t len, std::vector<TxOut>& outs);
+
 // CompactSize writer (serialize.h WriteCompactSize)
 void put_compact_size(std::vector<uint8_t>& out, uint64_t v);
 

@@ -19,13 +19,16 @@ struct PatchRec {
 };
 
 // SHA-256 padding appended on the host so that the kernels only run whole 64-byte blocks.
+// `prefix` = bytes already absorbed into the starting midstate (a tagged hash's 64-byte tag
+// block): they count in the length field but are not part of m.
 inline size_t sha_padded_len(size_t n) { return ((n + 8) / 64 + 1) * 64; }
-inline void sha_append_padded(std::vector<uint8_t>& buf, const uint8_t* m, size_t n) {
+inline void sha_append_padded(std::vector<uint8_t>& buf, const uint8_t* m, size_t n,
+                              size_t prefix = 0) {
     size_t L = sha_padded_len(n), base = buf.size();
     buf.resize(base + L, 0);
     if (n) memcpy(&buf[base], m, n);
     buf[base + n] = 0x80;
-    uint64_t bits = (uint64_t)n * 8;
+    uint64_t bits = (uint64_t)(n + prefix) * 8;
     for (int i = 0; i < 8; i++) buf[base + L - 1 - i] = (uint8_t)(bits >> (8 * i));
 }
 
@@ -106,6 +109,41 @@ struct TupleRows {
     }
     void clear() { tag.clear(); x.clear(); y.clear(); r.clear(); s.clear(); msg.clear(); }
 };
+
+// BIP341 / BIP342 signature checks (host/taproot.cpp): single-SHA256 aux messages (a tx's
+// sha_prevouts / sha_amounts / sha_scriptpubkeys / sha_sequences / sha_outputs, a check's
+// sha_annex / sha_single_output), SigMsg messages hashed as TapSighash tagged hashes (the
+// 64-byte tag block is the kernel's starting midstate) with the aux digests patched in, and the
+// BIP340 rows (sig64, x-only key) their digests feed.
+struct TaprootJobs {
+    std::vector<uint8_t> aux, msg;                   // padded messages, back to back
+    std::vector<uint32_t> aux_off, aux_nblk;         // in 64-byte blocks
+    std::vector<uint32_t> msg_off, msg_nblk, msg_row;
+    std::vector<PatchRec> patches;                   // aux digest -> msg blob byte offset
+    std::vector<uint8_t> sig64, pk32;                // BIP340 rows
+    size_t rows() const { return pk32.size() / 32; }
+    uint32_t add_aux(const uint8_t* m, size_t n) {
+        aux_off.push_back((uint32_t)(aux.size() / 64));
+        sha_append_padded(aux, m, n);
+        aux_nblk.push_back((uint32_t)(sha_padded_len(n) / 64));
+        return (uint32_t)aux_off.size() - 1;
+    }
+    uint32_t add_msg(const uint8_t* m, size_t n, uint32_t row) {
+        msg_off.push_back((uint32_t)(msg.size() / 64));
+        sha_append_padded(msg, m, n, 64);
+        msg_nblk.push_back((uint32_t)(sha_padded_len(n) / 64));
+        msg_row.push_back(row);
+        return (uint32_t)msg_off.size() - 1;
+    }
+};
+
+// SHA256(tag) || SHA256(tag) compressed from the IV: the starting midstate of the TapSighash
+// tagged hash (host/taproot.cpp computes it once).
+void tapsighash_midstate(uint32_t out[8]);
+
+// Stage + run + fetch on `device` (synchronous): BIP341 sighashes (msg32_out, optional, 32 bytes
+// per row) and BIP340 verdicts (1 valid).
+int gpu_taproot_verify(int device, const TaprootJobs& jobs, uint8_t* verdict, uint8_t* msg32_out);
 
 // Device scratch of the signature kernels: s^-1 rows (ECDSA) and, for one chunk of lanes, the
 // Q tables + ladder states.  Every synchronous entry point owns one per (thread, device), so

@@ -14,21 +14,36 @@
 #include "gpu_common.h"
 #include "pipeline.h"
 #include "sha256_device.h"
+#include "host/hashes.h"
 
 namespace bcc {
 
 __device__ __forceinline__ uint32_t bswap_u32(uint32_t x) { return __builtin_bswap32(x); }
 
+// A starting SHA-256 state passed by value (kernel argument: lands in SGPRs).
+struct ShaMid {
+    uint32_t s[8];
+};
+
 // Each lane streams its own message 64 bytes at a time (four 16-byte loads; messages are
-// 64-byte aligned so every load is a full aligned 16-byte access).
-__device__ __forceinline__ void sha256d_msg_lane(const uint8_t* __restrict__ buf,
-                                                 const uint32_t* __restrict__ off_blk,
-                                                 const uint32_t* __restrict__ nblk, uint32_t m,
-                                                 uint8_t* __restrict__ out,
-                                                 const uint32_t* __restrict__ out_row) {
+// 64-byte aligned so every load is a full aligned 16-byte access).  kDouble: SHA-256d (the
+// legacy / BIP143 sighashes and aux hashes); otherwise single SHA-256 (BIP341's tx hashes and
+// TapSighash).  kMid: start from `mid` (a tagged hash's absorbed tag block) instead of the IV.
+template <bool kDouble, bool kMid>
+__device__ __forceinline__ void sha256_msg_lane(const uint8_t* __restrict__ buf,
+                                                const uint32_t* __restrict__ off_blk,
+                                                const uint32_t* __restrict__ nblk, uint32_t m,
+                                                uint8_t* __restrict__ out,
+                                                const uint32_t* __restrict__ out_row,
+                                                const ShaMid& mid) {
     const uint4* p = reinterpret_cast<const uint4*>(buf + (size_t)off_blk[m] * 64);
     uint32_t st[8];
-    sha256_init_state(st);
+    if (kMid) {
+#pragma unroll
+        for (int k = 0; k < 8; k++) st[k] = mid.s[k];
+    } else {
+        sha256_init_state(st);
+    }
     const uint32_t nb = nblk[m];
     uint4 nxt[4];  // the next block, fetched while the current one is compressed
 #pragma unroll
@@ -49,11 +64,24 @@ __device__ __forceinline__ void sha256d_msg_lane(const uint8_t* __restrict__ buf
         sha256_compress(st, w);
     }
     uint32_t d[8];
-    sha256_of_digest(d, st);
+    if (kDouble) {
+        sha256_of_digest(d, st);
+    } else {
+#pragma unroll
+        for (int k = 0; k < 8; k++) d[k] = st[k];
+    }
     uint32_t row = out_row ? out_row[m] : m;
     uint4* o = reinterpret_cast<uint4*>(out + (size_t)row * 32);
     o[0] = make_uint4(bswap_u32(d[0]), bswap_u32(d[1]), bswap_u32(d[2]), bswap_u32(d[3]));
     o[1] = make_uint4(bswap_u32(d[4]), bswap_u32(d[5]), bswap_u32(d[6]), bswap_u32(d[7]));
+}
+
+__device__ __forceinline__ void sha256d_msg_lane(const uint8_t* __restrict__ buf,
+                                                 const uint32_t* __restrict__ off_blk,
+                                                 const uint32_t* __restrict__ nblk, uint32_t m,
+                                                 uint8_t* __restrict__ out,
+                                                 const uint32_t* __restrict__ out_row) {
+    sha256_msg_lane<true, false>(buf, off_blk, nblk, m, out, out_row, ShaMid{});
 }
 
 __global__ __launch_bounds__(256) void sha256d_msgs_kernel(const uint8_t* __restrict__ buf,
@@ -63,6 +91,30 @@ __global__ __launch_bounds__(256) void sha256d_msgs_kernel(const uint8_t* __rest
                                                            const uint32_t* __restrict__ out_row) {
     uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
     if (m < nmsg) sha256d_msg_lane(buf, off_blk, nblk, m, out, out_row);
+}
+
+// BIP341 (Taproot) stage: KT1 single SHA-256 of the aux messages (a tx's sha_prevouts /
+// sha_amounts / sha_scriptpubkeys / sha_sequences / sha_outputs, a check's sha_annex /
+// sha_single_output: interpreter.cpp:1366-1417, 1551-1561, 1889-1893) ...
+__global__ __launch_bounds__(64) void sha256_aux_kernel(const uint8_t* __restrict__ buf,
+                                                        const uint32_t* __restrict__ off_blk,
+                                                        const uint32_t* __restrict__ nblk,
+                                                        uint32_t n, uint8_t* __restrict__ out) {
+    uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
+    if (m < n) sha256_msg_lane<false, false>(buf, off_blk, nblk, m, out, nullptr, ShaMid{});
+}
+
+// ... and KT3 the SigMsg of each check (aux digests patched in by K2) hashed as the TapSighash
+// tagged hash (interpreter.cpp:1486, 1514-1572): the two 32-byte tag digests are one block,
+// absorbed on the host into `mid`; the digest lands in the check's BIP340 msg row.
+__global__ __launch_bounds__(256) void tapsighash_kernel(const uint8_t* __restrict__ buf,
+                                                         const uint32_t* __restrict__ off_blk,
+                                                         const uint32_t* __restrict__ nblk,
+                                                         uint32_t n, uint8_t* __restrict__ out,
+                                                         const uint32_t* __restrict__ out_row,
+                                                         ShaMid mid) {
+    uint32_t m = blockIdx.x * blockDim.x + threadIdx.x;
+    if (m < n) sha256_msg_lane<false, true>(buf, off_blk, nblk, m, out, out_row, mid);
 }
 
 // K3': legacy SIGHASH_ALL preimages assembled from the tx template while hashing (TplJob).
@@ -451,6 +503,142 @@ int gpu_verify_parts(int device, const SighashJobs* const* jobs, const TupleRows
     if (!e) e = b.fetch_verdicts(verdict);
     if (e) cache[device].reset();  // a retry starts from a fresh batch (streams, arena, scratch)
     return e;
+}
+
+// ------------------------------------------------------------------------------------------
+// BIP341 / BIP342 batch (host/taproot.cpp builds the jobs).
+void tapsighash_midstate(uint32_t out[8]) {
+    uint8_t th[32];
+    host::sha256(reinterpret_cast<const uint8_t*>("TapSighash"), 10, th);
+    uint32_t w[16];
+    for (int k = 0; k < 16; k++) {
+        const uint8_t* b = th + 4 * (k & 7);
+        w[k] = (uint32_t)b[0] << 24 | (uint32_t)b[1] << 16 | (uint32_t)b[2] << 8 | b[3];
+    }
+    sha256_init_state(out);
+    sha256_compress(out, w);
+}
+
+namespace {
+
+// Per (thread, device) state of gpu_taproot_verify: stream, kernel scratch, device arena and its
+// pinned host image, grown on demand and reused by later calls.
+struct TaprootCtx {
+    int dev = -1;
+    hipStream_t stream = nullptr;
+    SigScratch sc;
+    void* arena = nullptr;
+    size_t cap = 0;
+    void* image = nullptr;
+    size_t image_cap = 0;
+    ~TaprootCtx() {
+        if (dev >= 0) (void)hipSetDevice(dev);
+        if (stream) (void)hipStreamDestroy(stream);
+        if (arena) (void)hipFree(arena);
+        if (image) (void)hipHostFree(image);
+    }
+};
+
+}  // namespace
+
+int gpu_taproot_verify(int device, const TaprootJobs& J, uint8_t* verdict, uint8_t* msg32_out) {
+    const size_t n = J.rows();
+    if (n == 0) return 0;
+    if (device < 0 || device >= 64) return (int)hipErrorInvalidDevice;
+    if (J.aux.size() >= ((size_t)1 << 32) || J.msg.size() >= ((size_t)1 << 32)) {
+        fprintf(stderr, "[bcc] gpu_taproot_verify: a message blob exceeds 4 GiB; split the batch\n");
+        return (int)hipErrorInvalidValue;
+    }
+    thread_local std::unique_ptr<TaprootCtx> ctxs[64];
+    if (!ctxs[device]) {
+        auto c = std::make_unique<TaprootCtx>();
+        c->dev = device;
+        BCC_HIP_TRY(hipSetDevice(device));
+        BCC_HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+        ctxs[device] = std::move(c);
+    }
+    TaprootCtx& c = *ctxs[device];
+    BCC_HIP_TRY(hipSetDevice(device));
+    const size_t naux = J.aux_off.size(), nmsg = J.msg_off.size(), npat = J.patches.size();
+    // layout: sig64 | pk32 | msg32 | verdict | aux | msg | aux_off | aux_nblk | msg_off |
+    //         msg_nblk | msg_row | patches | aux digests (not uploaded)
+    size_t sizes[] = {64 * n,       32 * n,       32 * n,       n,
+                      J.aux.size(), J.msg.size(), 4 * naux,     4 * naux,
+                      4 * nmsg,     4 * nmsg,     4 * nmsg,     sizeof(PatchRec) * npat,
+                      32 * naux};
+    const int NB = sizeof(sizes) / sizeof(sizes[0]);
+    size_t off[NB], total = 0;
+    for (int i = 0; i < NB; i++) {
+        off[i] = total;
+        total += align256(sizes[i]);
+    }
+    const size_t upload = off[NB - 1];
+    if (total > c.cap) {
+        if (c.arena) BCC_HIP_TRY(hipFree(c.arena));
+        c.arena = nullptr;
+        c.cap = 0;
+        BCC_HIP_TRY(hipMalloc(&c.arena, total));
+        c.cap = total;
+    }
+    if (upload > c.image_cap) {
+        if (c.image) BCC_HIP_TRY(hipHostFree(c.image));
+        c.image = nullptr;
+        c.image_cap = 0;
+        BCC_HIP_TRY(hipHostMalloc(&c.image, upload, hipHostMallocDefault));
+        c.image_cap = upload;
+    }
+    uint8_t* h = (uint8_t*)c.image;
+    auto cp = [&](int b, const void* src, size_t len) {
+        if (len) memcpy(h + off[b], src, len);
+    };
+    cp(0, J.sig64.data(), 64 * n);
+    cp(1, J.pk32.data(), 32 * n);
+    memset(h + off[2], 0, 32 * n);
+    cp(4, J.aux.data(), J.aux.size());
+    cp(5, J.msg.data(), J.msg.size());
+    cp(6, J.aux_off.data(), 4 * naux);
+    cp(7, J.aux_nblk.data(), 4 * naux);
+    cp(8, J.msg_off.data(), 4 * nmsg);
+    cp(9, J.msg_nblk.data(), 4 * nmsg);
+    cp(10, J.msg_row.data(), 4 * nmsg);
+    cp(11, J.patches.data(), sizeof(PatchRec) * npat);
+    uint8_t* a = (uint8_t*)c.arena;
+    hipStream_t st = c.stream;
+    ShaMid mid;
+    tapsighash_midstate(mid.s);
+    BCC_HIP_TRY(hipMemcpyAsync(a, h, upload, hipMemcpyHostToDevice, st));
+    if (naux) {
+        hipLaunchKernelGGL(sha256_aux_kernel, dim3((unsigned)((naux + 63) / 64)), dim3(64), 0, st,
+                           a + off[4], (const uint32_t*)(a + off[6]), (const uint32_t*)(a + off[7]),
+                           (uint32_t)naux, a + off[12]);
+        BCC_HIP_TRY(hipGetLastError());
+    }
+    if (npat) {
+        hipLaunchKernelGGL(patch_digests_kernel, dim3((unsigned)((npat + 255) / 256)), dim3(256), 0,
+                           st, a + off[5], (const PatchRec*)(a + off[11]), a + off[12],
+                           (uint32_t)npat);
+        BCC_HIP_TRY(hipGetLastError());
+    }
+    if (nmsg) {
+        hipLaunchKernelGGL(tapsighash_kernel, dim3((unsigned)((nmsg + 255) / 256)), dim3(256), 0, st,
+                           a + off[5], (const uint32_t*)(a + off[8]), (const uint32_t*)(a + off[9]),
+                           (uint32_t)nmsg, a + off[2], (const uint32_t*)(a + off[10]), mid);
+        BCC_HIP_TRY(hipGetLastError());
+    }
+    if (int e = schnorr_launch(c.sc, a + off[0], a + off[2], a + off[1], a + off[3], n, st)) {
+        ctxs[device].reset();
+        return e;
+    }
+    int rc = 0;
+    if ((rc = (int)hipMemcpyAsync(verdict, a + off[3], n, hipMemcpyDeviceToHost, st)) ||
+        (msg32_out &&
+         (rc = (int)hipMemcpyAsync(msg32_out, a + off[2], 32 * n, hipMemcpyDeviceToHost, st))) ||
+        (rc = (int)hipStreamSynchronize(st))) {
+        fprintf(stderr, "[bcc] gpu_taproot_verify failed: %d\n", rc);
+        ctxs[device].reset();  // a retry starts from a fresh stream / arena / scratch
+        return rc;
+    }
+    return 0;
 }
 
 }  // namespace bcc

@@ -36,6 +36,11 @@ def load():
     u64p = ctypes.POINTER(ctypes.c_uint64)
     L.bcc_pubkey_verify_batch.argtypes = [ctypes.c_char_p, u64p, ctypes.c_char_p, ctypes.c_char_p,
                                           u64p, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int]
+    import bitcoinconsensus_amd as B
+    L.bcc_taproot_verify_batch.argtypes = [ctypes.POINTER(B.TaprootCheck), ctypes.c_size_t,
+                                           ctypes.POINTER(ctypes.c_int),
+                                           ctypes.POINTER(ctypes.c_int), ctypes.c_void_p,
+                                           ctypes.c_int]
     return L
 
 

@@ -70,4 +70,32 @@ int gpu_verify_batch(int, const SighashJobs& j, const TupleRows& rows, uint8_t* 
     return 0;
 }
 
+// BIP341 jobs (host/taproot.cpp): aux messages single SHA-256, patch, TapSighash over the
+// tag prefix + the message (the length field of a message counts the 64-byte tag block), BIP340.
+int gpu_taproot_verify(int, const TaprootJobs& j, uint8_t* verdict, uint8_t* msg32_out) {
+    std::vector<uint8_t> auxd(32 * j.aux_off.size());
+    for (size_t a = 0; a < j.aux_off.size(); a++) {
+        const uint8_t* m = &j.aux[(size_t)j.aux_off[a] * 64];
+        bcco_sha256(m, unpadded_len(m, (size_t)j.aux_nblk[a] * 64), &auxd[32 * a]);
+    }
+    std::vector<uint8_t> msgs = j.msg;
+    for (const auto& p : j.patches) memcpy(&msgs[p.pre_byte], &auxd[32 * p.aux], 32);
+    uint8_t tag[32];
+    bcco_sha256(reinterpret_cast<const uint8_t*>("TapSighash"), 10, tag);
+    const size_t n = j.rows();
+    std::vector<uint8_t> h(32 * n, 0);
+    for (size_t k = 0; k < j.msg_off.size(); k++) {
+        const uint8_t* m = &msgs[(size_t)j.msg_off[k] * 64];
+        size_t L = unpadded_len(m, (size_t)j.msg_nblk[k] * 64) - 64;
+        std::vector<uint8_t> full(tag, tag + 32);
+        full.insert(full.end(), tag, tag + 32);
+        full.insert(full.end(), m, m + L);
+        bcco_sha256(full.data(), full.size(), &h[32 * j.msg_row[k]]);
+    }
+    for (size_t i = 0; i < n; i++)
+        verdict[i] = (uint8_t)bcco_schnorr_verify(&j.sig64[64 * i], &h[32 * i], &j.pk32[32 * i]);
+    if (msg32_out) memcpy(msg32_out, h.data(), 32 * n);
+    return 0;
+}
+
 }  // namespace bcc

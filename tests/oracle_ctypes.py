@@ -40,6 +40,12 @@ class Oracle:
         L.bcco_ecmult_gen.argtypes = [c_u8p, c_u8p, c_u8p]
         L.bcco_sighash.argtypes = [c_u8p, c_sz, ctypes.c_uint, c_u8p, c_sz, ctypes.c_int,
                                    ctypes.c_int64, ctypes.c_int, c_u8p]
+        L.bcco_sighash_schnorr.argtypes = [c_u8p, c_sz, c_u8p, c_sz, ctypes.c_uint, ctypes.c_int,
+                                           ctypes.c_int, c_u8p, c_sz, c_u8p, ctypes.c_uint32,
+                                           c_u8p]
+        L.bcco_taproot_check.argtypes = [c_u8p, c_sz, c_u8p, c_sz, ctypes.c_uint, c_u8p, c_sz,
+                                         c_u8p, ctypes.c_int, c_u8p, c_sz, c_u8p, ctypes.c_uint32,
+                                         ctypes.POINTER(ctypes.c_int), c_u8p]
 
     def sha256(self, b):
         o = ctypes.create_string_buffer(32)
@@ -84,6 +90,24 @@ class Oracle:
                                  sigversion, o)
         return o.raw if ok else None
 
+    def sighash_schnorr(self, tx, spent, nin, hash_type, sigversion, annex=None,
+                        tapleaf=bytes(32), codesep=0xFFFFFFFF):
+        """(rc, sighash): rc 1 ok, 0 reference returns false, -1 refused inputs."""
+        o = ctypes.create_string_buffer(32)
+        rc = self.L.bcco_sighash_schnorr(tx, len(tx), spent, len(spent), nin, hash_type,
+                                         sigversion, annex, len(annex or b""), tapleaf, codesep, o)
+        return rc, o.raw
+
+    def taproot_check(self, tx, spent, nin, sig, pk, sigversion, annex=None, tapleaf=bytes(32),
+                      codesep=0xFFFFFFFF):
+        """(ret, serror) of CheckSchnorrSignature; ret -1 for refused inputs."""
+        e = ctypes.c_int(0)
+        h = ctypes.create_string_buffer(32)
+        r = self.L.bcco_taproot_check(tx, len(tx), spent, len(spent), nin, sig, len(sig), pk,
+                                      sigversion, annex, len(annex or b""), tapleaf, codesep,
+                                      ctypes.byref(e), h)
+        return r, e.value
+
 
 class Reference:
     """The reference (Bitcoin Core v0.21 libbitcoinconsensus + libsecp256k1), see ref_shim.cpp."""
@@ -117,6 +141,9 @@ class Reference:
         L.ref_bulk_verify_script.argtypes = [ctypes.c_int, ctypes.c_long] + [vp] * 6 + [
             ctypes.c_uint, vp, vp]
         L.ref_bulk_verify_script.restype = ctypes.c_double
+        L.ref_taproot_check.argtypes = [c_u8p, c_sz, c_u8p, c_sz, ctypes.c_uint, c_u8p, c_sz,
+                                        c_u8p, ctypes.c_int, c_u8p, c_sz, c_u8p, ctypes.c_uint32,
+                                        i32p, c_u8p, i32p]
 
     def verify_script_with_amount(self, spk, amount, tx, nin, flags):
         e = ctypes.c_int(0)
@@ -180,6 +207,18 @@ class Reference:
         p = lambda a: a.ctypes.data  # noqa: E731
         t = self.L.ref_bench_schnorr_verify(threads, n, p(sig64), p(msg32), p(xonly32), p(out))
         return out[:n], t
+
+    def taproot_check(self, tx, spent, nin, sig, pk, sigversion, annex=None, tapleaf=bytes(32),
+                      codesep=0xFFFFFFFF):
+        """CheckSchnorrSignature (interpreter.cpp:1678-1704) -> (ret, serror, sighash or None);
+        ret -1 where the reference would assert (unparsable tx / spent outputs, counts)."""
+        e = ctypes.c_int(0)
+        hashed = ctypes.c_int(0)
+        h = ctypes.create_string_buffer(32)
+        r = self.L.ref_taproot_check(tx, len(tx), spent, len(spent), nin, sig, len(sig), pk,
+                                     sigversion, annex, len(annex or b""), tapleaf, codesep,
+                                     ctypes.byref(e), h, ctypes.byref(hashed))
+        return r, e.value, (h.raw if hashed.value else None)
 
     def pubkey_create(self, sk, compressed=True):
         out = ctypes.create_string_buffer(65)

@@ -88,11 +88,14 @@ def test_python_structs_match_c_layout(tmp_path):
     library write past the Python buffer)."""
     import bitcoinconsensus_amd as B
     src = tmp_path / "sz.c"
-    src.write_text('#include <stdio.h>\n#include "bcc_bench.h"\nint main(void) { printf("%zu %zu %zu\\n",'
-                   ' sizeof(bcc_batch_stats), sizeof(bcc_batch_item), sizeof(bcc_tupleset_host));'
+    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "bcc_bench.h"\n'
+                   'int main(void) { printf("%zu %zu %zu %zu %zu\\n",'
+                   ' sizeof(bcc_batch_stats), sizeof(bcc_batch_item), sizeof(bcc_tupleset_host),'
+                   ' sizeof(bcc_taproot_check), offsetof(bcc_taproot_check, codeseparator_pos));'
                    ' return 0; }\n')
     exe = tmp_path / "sz"
     subprocess.check_call(["gcc", "-I" + os.path.join(ROOT, "include"), str(src), "-o", str(exe)])
     got = [int(x) for x in subprocess.check_output([str(exe)]).split()]
     assert got == [ctypes.sizeof(B.BatchStats), ctypes.sizeof(B.BatchItem),
-                   ctypes.sizeof(B.TuplesetHost)]
+                   ctypes.sizeof(B.TuplesetHost), ctypes.sizeof(B.TaprootCheck),
+                   B.TaprootCheck.codeseparator_pos.offset]

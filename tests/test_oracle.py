@@ -3,7 +3,7 @@ import random
 
 import pytest
 
-from fixtures import ecdsa_tuples, load_json, schnorr_tuples
+from fixtures import ecdsa_tuples, load_json, schnorr_tuples, taproot_checks
 from oracle_ctypes import Oracle, Reference, reference_available
 
 O = Oracle()
@@ -35,6 +35,27 @@ def test_oracle_schnorr_tuples_match_reference_verdicts():
     assert sum(t["verdict"] for t in ts) >= 400 and len({t["cls"] for t in ts}) >= 14
     bad = [(t["cls"], i) for i, t in enumerate(ts)
            if O.schnorr_verify(t["sig"], t["msg"], t["pub"]) != t["verdict"]]
+    assert not bad, bad[:10]
+
+
+def test_oracle_taproot_checks_match_reference():
+    """BIP341 SignatureHashSchnorr + CheckSchnorrSignature restatement vs the reference's
+    (ret, serror, sighash) on every committed case (make_taproot_fixtures.py)."""
+    cases = taproot_checks()
+    assert len(cases) > 2000 and sum(c["ret"] == 1 for c in cases) > 250
+    bad = []
+    for i, c in enumerate(cases):
+        ret, serr = O.taproot_check(c["tx"], c["spent"], c["nin"], c["sig"], c["pk"],
+                                    c["sigversion"], c["annex"], c["tapleaf"], c["codesep"])
+        want_err = c["serror"] if c["ret"] == 0 else 0
+        if ret != c["ret"] or (ret == 0 and serr != want_err):
+            bad.append((i, c["cls"], ret, serr, c["ret"], c["serror"]))
+        if c["sighash"] is not None:
+            ht = c["sig"][64] if len(c["sig"]) == 65 else 0
+            rc, h = O.sighash_schnorr(c["tx"], c["spent"], c["nin"], ht, c["sigversion"],
+                                      c["annex"], c["tapleaf"], c["codesep"])
+            if rc != 1 or h != c["sighash"]:
+                bad.append((i, c["cls"], "sighash"))
     assert not bad, bad[:10]
 
 
