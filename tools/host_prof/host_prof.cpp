@@ -9,6 +9,7 @@
 #include <vector>
 
 #include "../../include/bitcoinconsensus.h"
+#include "../../include/bcc_amd.h"
 #include "../../rust-bitcoinconsensus_amd/csrc/host/hashes.h"
 #include "../../rust-bitcoinconsensus_amd/csrc/pipeline.h"
 
@@ -77,7 +78,13 @@ int main(int argc, char** argv) {
         auto t0 = std::chrono::steady_clock::now();
         long v = bitcoinconsensus_verify_batch(items.data(), n, 0xE15, ret.data(), err.data());
         double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-        printf("n %zu valid %ld  %.1f ms  %.2f M items/s\n", n, v, 1e3 * s, n / s / 1e6);
+        bcc_batch_stats st;
+        bcc_last_batch_stats(&st);
+        printf("n %zu valid %ld  %.1f ms  %.2f M items/s | prepare %.1f interpret %.1f merge %.1f "
+               "stage %.1f gpu %.1f host %.1f total %.1f ms\n", n, v, 1e3 * s, n / s / 1e6,
+               1e3 * st.prepare_seconds, 1e3 * st.interpret_seconds, 1e3 * st.merge_seconds,
+               1e3 * st.stage_seconds, 1e3 * st.gpu_seconds, 1e3 * st.host_seconds,
+               1e3 * st.total_seconds);
     }
     return 0;
 }
