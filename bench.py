@@ -239,8 +239,10 @@ class C2:
 
     def extra(self, sighash_ms):
         sh = self.shape
-        b = 64 * (sh["sighash_blocks"] + sh["aux_blocks"]) + 32 * (sh["preimages"] + sh["aux_messages"])
-        out = {"sighash_stage": dict(kernels="sha256d aux + patch + sha256d preimage",
+        b = sh["sighash_bytes"]
+        out = {"sighash_stage": dict(kernels="sha256d aux/legacy templates + BIP143 from raw tx bytes "
+                                             "(K_wtx parse + per-tx hashes, K_win preimage) + patch + "
+                                             "sha256d preimages",
                                      avg_ms=sighash_ms, algorithmic_bytes=b,
                                      achieved_GBps=b / (sighash_ms * 1e-3) / 1e9, peak_GBps=8000.0)}
         if type(self) is C2:

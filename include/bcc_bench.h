@@ -95,6 +95,8 @@ int bcc_workload_tuple_items(const bcc_workload* w, uint32_t* out);
 /* the sighash (msg32) rows of the last run, 32 bytes per tuple (synchronous) */
 int bcc_workload_msgs(bcc_workload* w, uint8_t* out);
 /* algorithmic work of one run: bytes hashed + written by the sighash stage, tuples verified */
+/* algorithmic bytes of one sighash-stage run over the staged batch (DeviceBatch::sighash_bytes) */
+size_t bcc_workload_sighash_bytes(const bcc_workload* w);
 void bcc_workload_shape(const bcc_workload* w, size_t* tuples, size_t* sighash_blocks,
                         size_t* aux_blocks, size_t* preimages, size_t* aux_messages);
 /* export item i as (spk, amount, tx) for CPU-baseline / parity checks: returns tx length and

@@ -130,6 +130,8 @@ def blib():
         L.bcc_workload_msgs.argtypes = [vp, u8p]
         szp = ctypes.POINTER(sz)
         L.bcc_workload_shape.argtypes = [vp, szp, szp, szp, szp, szp]
+        L.bcc_workload_sighash_bytes.argtypes = [vp]
+        L.bcc_workload_sighash_bytes.restype = sz
         L.bcc_workload_item.argtypes = [vp, sz, u8p, szp, ctypes.POINTER(ctypes.c_int64), u8p, sz]
         L.bcc_workload_item.restype = sz
         L.mi_gen_pubkeys.argtypes = [u8p, sz, u8p, u8p, u8p, ctypes.c_int]
@@ -264,8 +266,10 @@ class Workload:
     def shape(self):
         v = [ctypes.c_size_t() for _ in range(5)]
         blib().bcc_workload_shape(self.h, *[ctypes.byref(x) for x in v])
-        return dict(zip(("tuples", "sighash_blocks", "aux_blocks", "preimages", "aux_messages"),
-                        (x.value for x in v)))
+        d = dict(zip(("tuples", "sighash_blocks", "aux_blocks", "preimages", "aux_messages"),
+                     (x.value for x in v)))
+        d["sighash_bytes"] = blib().bcc_workload_sighash_bytes(self.h)
+        return d
 
     def item(self, i):
         """(spent script, amount, tx bytes, input index) of item i."""

@@ -344,6 +344,8 @@ void bcc_workload_shape(const bcc_workload* w, size_t* tuples, size_t* sighash_b
     if (aux_messages) *aux_messages = w->batch->n_aux();
 }
 
+size_t bcc_workload_sighash_bytes(const bcc_workload* w) { return w ? w->batch->sighash_bytes() : 0; }
+
 size_t bcc_workload_item(const bcc_workload* w, size_t i, uint8_t* spk, size_t* spk_len,
                          int64_t* amount, uint8_t* tx, size_t cap) {
     if (!w || i >= w->n) return 0;

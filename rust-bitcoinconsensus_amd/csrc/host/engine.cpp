@@ -67,6 +67,7 @@ struct TxEntry {
     int32_t aux[3] = {-1, -1, -1};  // aux message index per AuxKind in the current round
     int64_t tpl = -1;               // legacy template offset in the current round (-1: none)
     uint32_t tpl_len = 0;
+    int32_t wtx = -1;               // WtxRec index in the current round (-1: none)
 };
 
 struct Item {
@@ -215,7 +216,27 @@ public:
             if (build_legacy_preimage(tx, nin, code, hashtype, scratch))
                 jobs.add_pre(scratch.data(), scratch.size(), row);
             // else: SIGHASH_SINGLE bug, msg stays ONE
-        } else {
+        } else if ((hashtype & 0x1f) != 3) {
+            // BIP143 assembled on the device from the raw tx bytes (pipeline.h WinJob): the
+            // host appends the tx once per round and a record per check
+            if (it.tx->wtx < 0) {
+                it.tx->wtx = (int32_t)jobs.add_wtx(it.in->tx_to, it.in->tx_to_len, tx.vin.size());
+                touched.push_back(it.tx);
+            }
+            scratch.clear();
+            put_compact_size(scratch, code.size());
+            scratch.insert(scratch.end(), code.begin(), code.end());
+            WinJob wj{};
+            wj.tx = (uint32_t)it.tx->wtx;
+            wj.nin = nin;
+            wj.code_off = jobs.add_code(scratch.data(), scratch.size());
+            wj.code_len = (uint32_t)scratch.size();
+            wj.hashtype = (uint32_t)hashtype;
+            wj.row = row;
+            wj.amount_lo = (uint32_t)(uint64_t)it.in->amount;
+            wj.amount_hi = (uint32_t)((uint64_t)it.in->amount >> 32);
+            jobs.wjobs.push_back(wj);
+        } else {  // SIGHASH_SINGLE: host preimage, single-output aux message
             Bip143Job& job = bip143;
             build_bip143_preimage(tx, nin, code, hashtype, it.in->amount, job);
             uint32_t pre = jobs.add_pre(job.preimage.data(), job.preimage.size(), row);
@@ -250,6 +271,7 @@ public:
         for (auto* t : touched) {
             t->aux[0] = t->aux[1] = t->aux[2] = -1;
             t->tpl = -1;
+            t->wtx = -1;
         }
         touched.clear();
     }
@@ -325,6 +347,7 @@ void prepare(BatchState& b, const bcc_batch_item* items, size_t n, unsigned flag
             TxEntry& e = b.txs[k];
             e.aux[0] = e.aux[1] = e.aux[2] = -1;
             e.tpl = -1;
+            e.wtx = -1;
             e.ok = flags_ok && in->tx_to != nullptr && parse_tx(in->tx_to, in->tx_to_len, e.tx);
             const size_t end = k + 1 < E ? b.tx_first[k + 1] : n;
             for (size_t i = b.tx_first[k]; i < end; i++) {
@@ -415,15 +438,16 @@ int run_device_group(int dev, const std::vector<Round>& rds, unsigned t0, unsign
                      size_t* retries) {
     unsigned g0 = t0;
     while (g0 < t1) {
-        size_t sz[4] = {0, 0, 0, 0};
+        size_t sz[5] = {0, 0, 0, 0, 0};
         unsigned g1 = g0;
         for (; g1 < t1; g1++) {
             const SighashJobs& j = rds[g1].jobs;
-            const size_t add[4] = {j.aux.size(), j.pre.size(), j.tpl.size(), j.code.size()};
+            const size_t add[5] = {j.aux.size(), j.pre.size(), j.tpl.size(), j.code.size(),
+                                   j.txraw.size()};
             bool fits = true;
-            for (int k = 0; k < 4; k++) fits &= sz[k] + add[k] <= ROUND_BLOB_LIMIT;
+            for (int k = 0; k < 5; k++) fits &= sz[k] + add[k] <= ROUND_BLOB_LIMIT;
             if (!fits) break;
-            for (int k = 0; k < 4; k++) sz[k] += add[k];
+            for (int k = 0; k < 5; k++) sz[k] += add[k];
         }
         if (g1 == g0) {
             fprintf(stderr, "[bcc] verify_batch: one shard's sighash jobs exceed %zu bytes\n",
@@ -541,8 +565,9 @@ long run_batch(const bcc_batch_item* items, size_t n, unsigned flags, int* ret_o
         row0[T] = npend;
         if (!any || npend == 0) break;
         for (unsigned t = 0; t < T; t++) {
-            t_stats.preimages += rds[t].jobs.pre_off.size() + rds[t].jobs.tjobs.size();
-            t_stats.aux_messages += rds[t].jobs.aux_off.size();
+            t_stats.preimages += rds[t].jobs.pre_off.size() + rds[t].jobs.tjobs.size() +
+                                 rds[t].jobs.wjobs.size();
+            t_stats.aux_messages += rds[t].jobs.aux_off.size() + 3 * rds[t].jobs.wtx.size();
         }
         t_stats.rounds++;
         t_stats.tuples += npend;
@@ -666,6 +691,21 @@ void append_round(SighashJobs& dst, TupleRows& drows, const SighashJobs& src,
         t.code_off += code0;
         t.row += row0;
         dst.tjobs.push_back(t);
+    }
+    const uint32_t raw0 = (uint32_t)dst.txraw.size(), wtx0 = (uint32_t)dst.wtx.size();
+    const uint32_t win0 = dst.win_entries;
+    cat(dst.txraw, src.txraw);
+    for (WtxRec r : src.wtx) {
+        r.tx_off += raw0;
+        r.in_base += win0;
+        dst.wtx.push_back(r);
+    }
+    dst.win_entries += src.win_entries;
+    for (WinJob w : src.wjobs) {
+        w.tx += wtx0;
+        w.code_off += code0;
+        w.row += row0;
+        dst.wjobs.push_back(w);
     }
 }
 

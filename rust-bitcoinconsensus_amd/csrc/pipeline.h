@@ -49,6 +49,30 @@ struct TplJob {
     uint32_t nblk;      // padded message length in 64-byte blocks
 };
 
+// BIP143 jobs built on the device from the raw transaction bytes: per tx a
+// WtxRec (K_wtx parses the wire format, primitives/transaction.h:188-224 / serialize.h:318-347,
+// records every input's outpoint / nSequence offsets and hashes hashPrevouts / hashSequence /
+// hashOutputs, interpreter.cpp:1366-1397), per check a WinJob (K_win assembles the BIP143
+// preimage, interpreter.cpp:1581-1625, from the tx bytes, those hashes and its own fields and
+// hashes it into the tuple's msg row).  The host only appends the tx bytes once per round and a
+// 40-byte record per check; no preimage or aux message exists on the host.
+struct WtxRec {
+    uint32_t tx_off;   // byte offset of the raw tx in the txraw blob (4-aligned)
+    uint32_t tx_len;
+    uint32_t in_base;  // first entry of this tx's inputs in the device input table
+    uint32_t n_in;     // vin.size() as the host parsed it (table capacity)
+};
+struct WinJob {
+    uint32_t tx;        // WtxRec index
+    uint32_t nin;
+    uint32_t code_off;  // compactsize || scriptCode in the code blob (4-aligned)
+    uint32_t code_len;
+    uint32_t hashtype;  // not SIGHASH_SINGLE (those keep the host preimage path)
+    uint32_t row;       // tuple row whose msg receives the sighash
+    uint32_t amount_lo, amount_hi;
+    uint32_t pad[2];
+};
+
 struct SighashJobs {
     std::vector<uint8_t> aux, pre;                  // padded messages, back to back
     std::vector<uint32_t> aux_off, aux_nblk;        // offsets / lengths in 64-byte blocks
@@ -57,6 +81,22 @@ struct SighashJobs {
     std::vector<uint8_t> tpl, code;                 // templates / code segments (4-aligned,
                                                     // templates followed by 8 zero bytes)
     std::vector<TplJob> tjobs;
+    std::vector<uint8_t> txraw;                     // raw txs of the WinJobs (4-aligned)
+    std::vector<WtxRec> wtx;
+    std::vector<WinJob> wjobs;
+    uint32_t win_entries = 0;                       // sum of WtxRec::n_in
+    uint32_t add_wtx(const uint8_t* tx, size_t n, size_t n_in) {
+        WtxRec r;
+        r.tx_off = (uint32_t)txraw.size();
+        r.tx_len = (uint32_t)n;
+        r.in_base = win_entries;
+        r.n_in = (uint32_t)n_in;
+        txraw.insert(txraw.end(), tx, tx + n);
+        txraw.resize(r.tx_off + ((n + 3) & ~(size_t)3), 0);
+        win_entries += (uint32_t)n_in;
+        wtx.push_back(r);
+        return (uint32_t)wtx.size() - 1;
+    }
     uint32_t add_tpl(const uint8_t* m, size_t n) {
         uint32_t off = (uint32_t)tpl.size();
         tpl.insert(tpl.end(), m, m + n);
@@ -89,6 +129,7 @@ struct SighashJobs {
         aux.clear(); pre.clear(); aux_off.clear(); aux_nblk.clear();
         pre_off.clear(); pre_nblk.clear(); pre_row.clear(); patches.clear();
         tpl.clear(); code.clear(); tjobs.clear();
+        txraw.clear(); wtx.clear(); wjobs.clear(); win_entries = 0;
     }
 };
 
@@ -193,7 +234,12 @@ public:
     int fetch_verdicts(uint8_t* out);            // synchronous D2H (waits for the last run)
     int fetch_msgs(uint8_t* out);                // synchronous D2H (tests)
     size_t n_tuples() const { return n_rows_; }
-    size_t n_pre() const { return n_pre_ + n_tjob_; }     // sighash messages (both kinds)
+    size_t n_pre() const { return n_pre_ + n_tjob_ + n_wjob_; }  // sighash messages (all kinds)
+    size_t n_wtx() const { return n_wtx_; }
+    // Algorithmic bytes of one run of the sighash stage: padded messages + digests of the host-built
+    // jobs, and raw tx bytes + job records + scriptCode fields + per-tx hashes + sighashes of the
+    // device-built BIP143 jobs.
+    size_t sighash_bytes() const { return sighash_bytes_; }
     size_t n_aux() const { return n_aux_; }
     size_t pre_blocks() const { return pre_blocks_ + tjob_blocks_; }
     size_t aux_blocks() const { return aux_blocks_; }
@@ -205,12 +251,16 @@ public:
 private:
     int sync();
     void* pick(void* stream);
+    int launch_wtx(void* stream);
+    int launch_sighash(struct ihipStream_t* st, void* ev_wtx);
     int dev_;
     void* own_stream_ = nullptr;   // hipStream_t, created on first use
     void* last_stream_ = nullptr;  // stream of the last run
     void* side_stream_ = nullptr;  // K_inv beside the sighash kernels (run())
+    void* wtx_stream_ = nullptr;   // K_wtx beside both (run())
     void* ev_fork_ = nullptr;      // hipEvent_t: run() start on the main stream
     void* ev_join_ = nullptr;      // hipEvent_t: K_inv done on the side stream
+    void* ev_wtx_ = nullptr;       // hipEvent_t: K_wtx done on the side stream
     SigScratch scratch_;
     void* arena_ = nullptr;
     size_t cap_ = 0;
@@ -224,6 +274,11 @@ private:
     size_t n_tjob_ = 0, tjob_blocks_ = 0;
     uint8_t *d_tpl_ = nullptr, *d_code_ = nullptr;
     TplJob* d_tjob_ = nullptr;
+    size_t n_wtx_ = 0, n_wjob_ = 0, n_win_ = 0, sighash_bytes_ = 0;
+    uint8_t *d_txraw_ = nullptr, *d_txd_ = nullptr, *d_zeros_ = nullptr;
+    WtxRec* d_wtx_ = nullptr;
+    WinJob* d_wjob_ = nullptr;
+    uint32_t* d_intab_ = nullptr;
 };
 
 // One-shot helper: stage + run + fetch on `device` (synchronous).

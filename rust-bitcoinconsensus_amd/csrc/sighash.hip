@@ -209,6 +209,371 @@ __global__ __launch_bounds__(64) void sha256d_aux_tpl_kernel(
 }
 
 
+// ------------------------------------------------------------------------------------------
+// §8f rank 4: BIP143 sighashes from the raw transaction bytes (pipeline.h WtxRec / WinJob).
+// Every lane streams bytes into a SHA-256 whose 64-byte block buffer and state live in the lane's
+// own LDS slot (96 bytes, + 4 so that lane slots start on different banks), so byte positions can
+// be dynamic without scratch memory; the compression reads the block back as 16 words.
+constexpr int XS_SLOT = 100;   // bytes per lane: block[64] | state[32] | pad
+constexpr int XS_WG = 64;      // lanes per workgroup of the extraction kernels
+
+__device__ __noinline__ void xs_compress(uint8_t* slot) {
+    const uint32_t* b = reinterpret_cast<const uint32_t*>(slot);
+    uint32_t* st = reinterpret_cast<uint32_t*>(slot + 64);
+    uint32_t w[16], s8[8];
+#pragma unroll
+    for (int k = 0; k < 16; k++) w[k] = bswap_u32(b[k]);
+#pragma unroll
+    for (int k = 0; k < 8; k++) s8[k] = st[k];
+    sha256_compress(s8, w);
+#pragma unroll
+    for (int k = 0; k < 8; k++) st[k] = s8[k];
+}
+
+struct XSha {
+    uint8_t* slot;
+    uint32_t fill;   // bytes in the block buffer
+    uint32_t total;  // message bytes so far
+};
+
+__device__ __forceinline__ void xs_init(XSha& h, uint8_t* slot) {
+    h.slot = slot;
+    h.fill = 0;
+    h.total = 0;
+    uint32_t* st = reinterpret_cast<uint32_t*>(slot + 64);
+    uint32_t iv[8];
+    sha256_init_state(iv);
+#pragma unroll
+    for (int k = 0; k < 8; k++) st[k] = iv[k];
+}
+
+// n message bytes from global memory.  Per step: the (up to 17) aligned dwords covering the next
+// min(n, 64 - fill) source bytes are loaded together (one memory latency per block, not per
+// byte), realigned with funnel shifts, and written into the block buffer: as dwords when the fill
+// position is 4-aligned, else byte by byte.  Bytes written past the step's end are scratch that a
+// later step or the padding overwrites (the slot has 4 spare bytes after the block).
+__device__ __forceinline__ void xs_put(XSha& h, const uint8_t* __restrict__ src, uint32_t n) {
+    h.total += n;
+    while (n) {
+        const uint32_t take = min(n, 64u - h.fill);
+        const uintptr_t a = reinterpret_cast<uintptr_t>(src);
+        const uint32_t* w = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3);
+        const uint32_t sh = (uint32_t)(a & 3), nd = (sh + take + 3) >> 2;
+        uint32_t v[17];
+#pragma unroll
+        for (int k = 0; k < 17; k++) v[k] = (uint32_t)k < nd ? w[k] : 0u;
+        uint32_t r[16];
+#pragma unroll
+        for (int k = 0; k < 16; k++) r[k] = __builtin_amdgcn_alignbyte(v[k + 1], v[k], sh);
+        uint8_t* dst = h.slot + h.fill;
+        if ((h.fill & 3) == 0) {
+            uint32_t* d4 = reinterpret_cast<uint32_t*>(dst);
+#pragma unroll
+            for (int k = 0; k < 16; k++)
+                if ((uint32_t)(4 * k) < take) d4[k] = r[k];
+        } else {
+#pragma unroll
+            for (int i = 0; i < 64; i++)
+                if ((uint32_t)i < take) dst[i] = (uint8_t)(r[i >> 2] >> (8 * (i & 3)));
+        }
+        h.fill += take;
+        src += take;
+        n -= take;
+        if (h.fill == 64) {
+            xs_compress(h.slot);
+            h.fill = 0;
+        }
+    }
+}
+
+// SHA-256 padding + final compression(s), then the second SHA-256 of SHA-256d: big-endian
+// digest bytes to out (4-aligned).
+__device__ __forceinline__ void xs_final_d(XSha& h, uint8_t* __restrict__ out) {
+    const uint64_t bits = (uint64_t)h.total * 8;
+    h.slot[h.fill++] = 0x80;
+    if (h.fill > 56) {
+        while (h.fill < 64) h.slot[h.fill++] = 0;
+        xs_compress(h.slot);
+        h.fill = 0;
+    }
+    while (h.fill < 56) h.slot[h.fill++] = 0;
+#pragma unroll
+    for (int k = 0; k < 8; k++) h.slot[56 + k] = (uint8_t)(bits >> (8 * (7 - k)));
+    xs_compress(h.slot);
+    const uint32_t* st = reinterpret_cast<const uint32_t*>(h.slot + 64);
+    uint32_t d[8], e[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) d[k] = st[k];
+    sha256_of_digest(e, d);
+    uint4* o = reinterpret_cast<uint4*>(out);
+    o[0] = make_uint4(bswap_u32(e[0]), bswap_u32(e[1]), bswap_u32(e[2]), bswap_u32(e[3]));
+    o[1] = make_uint4(bswap_u32(e[4]), bswap_u32(e[5]), bswap_u32(e[6]), bswap_u32(e[7]));
+}
+
+// The wire bytes of one tx seen through a 128-byte window in the lane's LDS slot: a refill
+// loads the 32 dwords of the window together (one memory latency per window, so the parse walk
+// over a many-input tx does not pay one latency per field).
+constexpr int XW_BYTES = 128;
+struct XWin {
+    uint8_t* w;           // LDS window
+    const uint32_t* t4;   // the tx bytes as dwords (4-aligned, zero-padded to a dword)
+    uint32_t base;        // tx offset of w[0] (4-aligned)
+    uint32_t nd;          // dwords in the padded tx
+};
+
+// (plain arguments: a noinline callee taking the struct by reference would put it on the stack)
+__device__ __noinline__ void xw_refill(uint8_t* w, const uint32_t* __restrict__ t4, uint32_t nd,
+                                       uint32_t base) {
+    const uint32_t d0 = base >> 2;
+    uint32_t v[XW_BYTES / 4];
+#pragma unroll
+    for (int k = 0; k < XW_BYTES / 4; k++) v[k] = d0 + k < nd ? t4[d0 + k] : 0u;
+    uint32_t* w4 = reinterpret_cast<uint32_t*>(w);
+#pragma unroll
+    for (int k = 0; k < XW_BYTES / 4; k++) w4[k] = v[k];
+}
+
+__device__ __forceinline__ uint32_t xw_byte(XWin& x, uint32_t pos) {
+    if (pos - x.base >= (uint32_t)XW_BYTES) {
+        x.base = pos & ~3u;
+        xw_refill(x.w, x.t4, x.nd, x.base);
+    }
+    return x.w[pos - x.base];
+}
+
+// ReadCompactSize (serialize.h:318-347) from the wire bytes; the host has already checked that
+// the tx deserializes (canonical sizes), so no range checks beyond the buffer bound.
+__device__ __forceinline__ uint32_t wire_cs(XWin& x, uint32_t& pos) {
+    const uint32_t c = xw_byte(x, pos++);
+    if (c < 253) return c;
+    uint32_t v = xw_byte(x, pos) | xw_byte(x, pos + 1) << 8;
+    if (c == 253) {
+        pos += 2;
+        return v;
+    }
+    v |= xw_byte(x, pos + 2) << 16 | xw_byte(x, pos + 3) << 24;
+    pos += c == 254 ? 4 : 8;  // sizes above MAX_SIZE (0x02000000) never parse on the host
+    return v;
+}
+
+// Big-endian message word at byte offset `off` of a 4-aligned, zero-padded byte array (any
+// alignment of off: two aligned dword loads and a funnel shift).
+__device__ __forceinline__ uint32_t be_word_at(const uint32_t* __restrict__ t4, uint32_t off) {
+    const uint32_t q = off >> 2;
+    return bswap_u32(__builtin_amdgcn_alignbyte(t4[q + 1], t4[q], off & 3));
+}
+
+// SHA-256d of a padded message of L bytes whose data words come from word(m) (big-endian; only
+// the first L - 4m bytes of the last partial word are used).  All 16 words of a block are formed
+// (their loads issued together) before the block is compressed.  Digest bytes to out (16-aligned).
+template <class W>
+__device__ __forceinline__ void sha256d_words(W word, uint32_t L, uint8_t* __restrict__ out) {
+    uint32_t st[8];
+    sha256_init_state(st);
+    const uint32_t nb = (L + 8) / 64 + 1, full = L >> 2, rem = L & 3;
+    for (uint32_t b = 0; b < nb; b++) {
+        uint32_t w[16];
+#pragma unroll
+        for (int q = 0; q < 16; q++) {
+            const uint32_t m = 16 * b + q;
+            uint32_t v;
+            if (m < full) {
+                v = word(m);
+            } else if (m == full) {  // last data bytes (rem of them) then 0x80
+                const uint32_t d = rem ? word(m) : 0u;
+                const uint32_t keep = rem ? 0xFFFFFFFFu << (32 - 8 * rem) : 0u;
+                v = (d & keep) | (0x80u << (24 - 8 * rem));
+            } else {
+                v = 0u;
+            }
+            if (b + 1 == nb && q == 14) v = (uint32_t)((uint64_t)L >> 29);
+            if (b + 1 == nb && q == 15) v = L << 3;
+            w[q] = v;
+        }
+        sha256_compress(st, w);
+    }
+    uint32_t d[8];
+    sha256_of_digest(d, st);
+    uint4* o = reinterpret_cast<uint4*>(out);
+    o[0] = make_uint4(bswap_u32(d[0]), bswap_u32(d[1]), bswap_u32(d[2]), bswap_u32(d[3]));
+    o[1] = make_uint4(bswap_u32(d[4]), bswap_u32(d[5]), bswap_u32(d[6]), bswap_u32(d[7]));
+}
+
+// One input of the vin list: returns its outpoint offset, leaves *seq at its nSequence offset
+// and pos after it.
+__device__ __forceinline__ uint32_t wire_input(XWin& x, uint32_t& pos, uint32_t* seq) {
+    const uint32_t po = pos;
+    pos += 36;
+    pos += wire_cs(x, pos);
+    *seq = pos;
+    pos += 4;
+    return po;
+}
+
+// K_wtx: three lanes per tx, one per BIP143 per-tx hash (PrecomputedTransactionData,
+// interpreter.cpp:1366-1397, 1422-1472), so that a many-input tx's three SHA-256 chains run side
+// by side.  Lanes [0, n) hash the prevouts, [n, 2n) the sequences, [2n, 3n) the outputs (waves
+// stay role-uniform).  Every lane deserializes the wire format itself (UnserializeTransaction,
+// primitives/transaction.h:188-224: version, segwit marker / flag, vin, vout) through its LDS
+// window, just ahead of the words it hashes; message words are gathered straight from the tx
+// bytes (two aligned dword loads + a funnel shift per word, a block's words issued together):
+//   txd[0:32]  hashPrevouts  = SHA256d(outpoint_0 || ... )   (36 bytes = 9 words per input; the
+//                                                              prevout lane also writes the
+//                                                              input table K_win reads)
+//   txd[32:64] hashSequence  = SHA256d(nSequence_0 || ... )  (one word per input)
+//   txd[64:96] hashOutputs   = SHA256d(the serialized outputs: one contiguous range of the tx)
+__global__ __launch_bounds__(XS_WG) void bip143_tx_kernel(const uint8_t* __restrict__ txraw,
+                                                          const WtxRec* __restrict__ recs,
+                                                          uint32_t n, uint32_t* __restrict__ intab,
+                                                          uint8_t* __restrict__ txd) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[XS_WG * (XW_BYTES + 4)];
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= 3 * n) return;
+    const uint32_t role = g / n, i = g - role * n;
+    const WtxRec r = recs[i];
+    const uint8_t* t = txraw + r.tx_off;
+    const uint32_t* t4 = reinterpret_cast<const uint32_t*>(t);
+    XWin x;
+    x.w = lds + threadIdx.x * (XW_BYTES + 4);
+    x.t4 = t4;
+    x.nd = (r.tx_len + 3) >> 2;
+    x.base = 0;
+    xw_refill(x.w, x.t4, x.nd, 0);
+    uint32_t pos = 4;
+    uint32_t nin = wire_cs(x, pos);
+    if (nin == 0 && xw_byte(x, pos++) != 0) nin = wire_cs(x, pos);  // marker 0x00, flag (BIP144)
+    nin = min(nin, r.n_in);
+    uint8_t* d = txd + 96 * (size_t)i;
+    uint32_t st[8];
+    sha256_init_state(st);
+    if (role == 0) {
+        // hashPrevouts: word m is word m % 9 of input m / 9's outpoint; the (at most three)
+        // inputs a block touches are parsed into registers just before it
+        uint32_t* tab = intab + 2 * (size_t)r.in_base;
+        const uint32_t L = 36 * nin, nb = (L + 8) / 64 + 1;
+        uint32_t kf = 0, np = 0, p0 = 0, p1 = 0, p2 = 0, sq;
+        auto next = [&]() -> uint32_t {
+            if (np >= nin) return 0u;
+            const uint32_t po = wire_input(x, pos, &sq);
+            tab[2 * np] = po;
+            tab[2 * np + 1] = sq;
+            np++;
+            return po;
+        };
+        p0 = next();
+        p1 = next();
+        p2 = next();
+        for (uint32_t b = 0; b < nb; b++) {
+            const uint32_t k0 = (16 * b) / 9;
+            while (kf < k0) {
+                p0 = p1;
+                p1 = p2;
+                p2 = next();
+                kf++;
+            }
+            uint32_t w[16];
+#pragma unroll
+            for (int q = 0; q < 16; q++) {
+                const uint32_t m = 16 * b + q, k = m / 9;
+                uint32_t v = 0u;
+                if (m < L / 4) {
+                    const uint32_t kk = k - kf;
+                    const uint32_t po = kk == 0 ? p0 : kk == 1 ? p1 : p2;
+                    v = be_word_at(t4, po + 4 * (m - 9 * k));
+                } else if (m == L / 4) {
+                    v = 0x80000000u;
+                }
+                if (b + 1 == nb && q == 14) v = L >> 29;
+                if (b + 1 == nb && q == 15) v = L << 3;
+                w[q] = v;
+            }
+            sha256_compress(st, w);
+        }
+        while (np < nin) next();  // (L = 0 edge: no block needed the inputs)
+    } else if (role == 1) {
+        // hashSequence: word m is input m's nSequence, parsed inline
+        const uint32_t L = 4 * nin, nb = (L + 8) / 64 + 1;
+        uint32_t np = 0;
+        for (uint32_t b = 0; b < nb; b++) {
+            uint32_t w[16];
+#pragma unroll
+            for (int q = 0; q < 16; q++) {
+                const uint32_t m = 16 * b + q;
+                uint32_t v = 0u;
+                if (m < nin) {
+                    uint32_t sq;
+                    wire_input(x, pos, &sq);
+                    np++;
+                    v = be_word_at(t4, sq);
+                } else if (m == nin) {
+                    v = 0x80000000u;
+                }
+                if (b + 1 == nb && q == 14) v = L >> 29;
+                if (b + 1 == nb && q == 15) v = L << 3;
+                w[q] = v;
+            }
+            sha256_compress(st, w);
+        }
+    } else {
+        // hashOutputs: skip the inputs, find the serialized outputs' range, hash it
+        for (uint32_t k = 0; k < nin; k++) {
+            uint32_t sq;
+            wire_input(x, pos, &sq);
+        }
+        const uint32_t nout = wire_cs(x, pos), o0 = pos;
+        for (uint32_t k = 0; k < nout && pos < r.tx_len; k++) {
+            pos += 8;
+            pos += wire_cs(x, pos);
+        }
+        const uint32_t o1 = min(pos, r.tx_len);
+        sha256d_words([&](uint32_t m) { return be_word_at(t4, o0 + 4 * m); }, o1 - o0, d + 64);
+        return;
+    }
+    uint32_t dd[8];
+    sha256_of_digest(dd, st);
+    uint4* o = reinterpret_cast<uint4*>(d + 32 * role);
+    o[0] = make_uint4(bswap_u32(dd[0]), bswap_u32(dd[1]), bswap_u32(dd[2]), bswap_u32(dd[3]));
+    o[1] = make_uint4(bswap_u32(dd[4]), bswap_u32(dd[5]), bswap_u32(dd[6]), bswap_u32(dd[7]));
+}
+
+// K_win: one lane per BIP143 check (not SIGHASH_SINGLE).  SignatureHash WITNESS_V0
+// (interpreter.cpp:1581-1625): version || hashPrevouts || hashSequence || outpoint ||
+// scriptCode || amount || nSequence || hashOutputs || locktime || hashtype, with the hashes
+// zeroed per ANYONECANPAY / NONE, streamed from the tx bytes, the K_wtx digests and the job
+// record, SHA-256d into the tuple's msg row.
+__global__ __launch_bounds__(XS_WG) void bip143_in_kernel(const uint8_t* __restrict__ txraw,
+                                                          const WtxRec* __restrict__ recs,
+                                                          const WinJob* __restrict__ jobs,
+                                                          uint32_t n, const uint32_t* __restrict__ intab,
+                                                          const uint8_t* __restrict__ txd,
+                                                          const uint8_t* __restrict__ code,
+                                                          const uint8_t* __restrict__ zeros,
+                                                          uint8_t* __restrict__ msg) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[XS_WG * XS_SLOT];
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const WinJob* jp = jobs + i;
+    const WinJob j = *jp;
+    const WtxRec r = recs[j.tx];
+    const uint8_t* t = txraw + r.tx_off;
+    const uint8_t* d = txd + 96 * (size_t)j.tx;
+    const uint32_t* tab = intab + 2 * ((size_t)r.in_base + j.nin);
+    const bool acp = (j.hashtype & 0x80) != 0, none = (j.hashtype & 0x1f) == 2;
+    XSha h;
+    xs_init(h, lds + threadIdx.x * XS_SLOT);
+    xs_put(h, t, 4);
+    xs_put(h, acp ? zeros : d, 32);
+    xs_put(h, acp || none ? zeros : d + 32, 32);
+    xs_put(h, t + tab[0], 36);
+    xs_put(h, code + j.code_off, j.code_len);
+    xs_put(h, reinterpret_cast<const uint8_t*>(&jp->amount_lo), 8);
+    xs_put(h, t + tab[1], 4);
+    xs_put(h, none ? zeros : d + 64, 32);
+    xs_put(h, t + r.tx_len - 4, 4);
+    xs_put(h, reinterpret_cast<const uint8_t*>(&jp->hashtype), 4);
+    xs_final_d(h, msg + 32 * (size_t)j.row);
+}
+
 __global__ __launch_bounds__(256) void patch_digests_kernel(uint8_t* __restrict__ pre,
                                                             const PatchRec* __restrict__ patches,
                                                             const uint8_t* __restrict__ auxd,
@@ -246,8 +611,10 @@ DeviceBatch::~DeviceBatch() {
     (void)hipSetDevice(dev_);
     if (own_stream_) (void)hipStreamDestroy((hipStream_t)own_stream_);
     if (side_stream_) (void)hipStreamDestroy((hipStream_t)side_stream_);
+    if (wtx_stream_) (void)hipStreamDestroy((hipStream_t)wtx_stream_);
     if (ev_fork_) (void)hipEventDestroy((hipEvent_t)ev_fork_);
     if (ev_join_) (void)hipEventDestroy((hipEvent_t)ev_join_);
+    if (ev_wtx_) (void)hipEventDestroy((hipEvent_t)ev_wtx_);
     if (arena_) (void)hipFree(arena_);
     if (host_image_) (void)hipHostFree(host_image_);
 }
@@ -286,7 +653,8 @@ int DeviceBatch::stage(const SighashJobs& j, const TupleRows& rows) {
 int DeviceBatch::stage_parts(const SighashJobs* const* J, const TupleRows* const* Rw, size_t P) {
     if (int e = sync()) return e;  // the previous run may still read the arena / the image
     std::vector<size_t> row0(P + 1, 0), auxb0(P + 1, 0), preb0(P + 1, 0), auxi0(P + 1, 0),
-        prei0(P + 1, 0), pat0(P + 1, 0), tpl0(P + 1, 0), code0(P + 1, 0), tj0(P + 1, 0);
+        prei0(P + 1, 0), pat0(P + 1, 0), tpl0(P + 1, 0), code0(P + 1, 0), tj0(P + 1, 0),
+        raw0(P + 1, 0), wtx0(P + 1, 0), wj0(P + 1, 0), win0(P + 1, 0);
     size_t tjblk = 0;
     for (size_t p = 0; p < P; p++) {
         row0[p + 1] = row0[p] + Rw[p]->size();
@@ -298,12 +666,16 @@ int DeviceBatch::stage_parts(const SighashJobs* const* J, const TupleRows* const
         tpl0[p + 1] = tpl0[p] + J[p]->tpl.size();
         code0[p + 1] = code0[p] + J[p]->code.size();
         tj0[p + 1] = tj0[p] + J[p]->tjobs.size();
+        raw0[p + 1] = raw0[p] + J[p]->txraw.size();
+        wtx0[p + 1] = wtx0[p] + J[p]->wtx.size();
+        wj0[p + 1] = wj0[p] + J[p]->wjobs.size();
+        win0[p + 1] = win0[p] + J[p]->win_entries;
         for (const auto& t : J[p]->tjobs) tjblk += t.nblk;
     }
-    if (auxb0[P] >= ((size_t)1 << 32) || preb0[P] >= ((size_t)1 << 32) ||
-        tpl0[P] >= ((size_t)1 << 32) || code0[P] >= ((size_t)1 << 32) ||
-        row0[P] >= ((size_t)1 << 32)) {
-        // the job records (PatchRec, TplJob, offsets) are 32-bit: refuse, never wrap
+    const size_t LIM = (size_t)1 << 32;
+    if (auxb0[P] >= LIM || preb0[P] >= LIM || tpl0[P] >= LIM || code0[P] >= LIM ||
+        raw0[P] >= LIM || row0[P] >= LIM || win0[P] >= LIM / 2) {
+        // the job records (PatchRec, TplJob, WtxRec, WinJob, offsets) are 32-bit: refuse, never wrap
         fprintf(stderr, "[bcc] DeviceBatch::stage_parts: a job blob exceeds 4 GiB; split the round\n");
         return (int)hipErrorInvalidValue;
     }
@@ -315,18 +687,34 @@ int DeviceBatch::stage_parts(const SighashJobs* const* J, const TupleRows* const
     aux_blocks_ = auxb0[P] / 64;
     n_tjob_ = tj0[P];
     tjob_blocks_ = tjblk;
+    n_wtx_ = wtx0[P];
+    n_wjob_ = wj0[P];
+    n_win_ = win0[P];
+    sighash_bytes_ = 64 * (pre_blocks_ + aux_blocks_ + tjob_blocks_) + 32 * (n_pre_ + n_aux_ + n_tjob_);
+    for (size_t p = 0; p < P; p++) {
+        for (const WtxRec& r : J[p]->wtx) sighash_bytes_ += r.tx_len + 96;
+        for (const WinJob& w : J[p]->wjobs) sighash_bytes_ += w.code_len + sizeof(WinJob) + 32;
+    }
     const size_t R = n_rows_;
-    size_t sizes[] = {R,         32 * R,           32 * R,         32 * R,        32 * R,
-                      32 * R,    R,                auxb0[P],       preb0[P],      32 * n_aux_,
-                      4 * n_aux_, 4 * n_aux_,      4 * n_pre_,     4 * n_pre_,    4 * n_pre_,
-                      sizeof(PatchRec) * n_patch_, tpl0[P],        code0[P],
-                      sizeof(TplJob) * n_tjob_};
-    const int NB = sizeof(sizes) / sizeof(sizes[0]);
+    // regions filled from the host image first (one copy), device-written ones after them
+    enum { TAG, X, Y, RR, S, M, AUX, PRE, AUX_OFF, AUX_NBLK, PRE_OFF, PRE_NBLK, PRE_ROW, PATCH,
+           TPL, CODE, TJOB, TXRAW, WTX, WJOB, ZEROS, UPLOADED, V = UPLOADED, AUXD, INTAB, TXD, NB };
+    size_t sizes[NB] = {};
+    sizes[TAG] = R; sizes[X] = sizes[Y] = sizes[RR] = sizes[S] = sizes[M] = 32 * R;
+    sizes[AUX] = auxb0[P]; sizes[PRE] = preb0[P];
+    sizes[AUX_OFF] = sizes[AUX_NBLK] = 4 * n_aux_;
+    sizes[PRE_OFF] = sizes[PRE_NBLK] = sizes[PRE_ROW] = 4 * n_pre_;
+    sizes[PATCH] = sizeof(PatchRec) * n_patch_;
+    sizes[TPL] = tpl0[P]; sizes[CODE] = code0[P]; sizes[TJOB] = sizeof(TplJob) * n_tjob_;
+    sizes[TXRAW] = raw0[P]; sizes[WTX] = sizeof(WtxRec) * n_wtx_; sizes[WJOB] = sizeof(WinJob) * n_wjob_;
+    sizes[ZEROS] = 64;
+    sizes[V] = R; sizes[AUXD] = 32 * n_aux_; sizes[INTAB] = 8 * n_win_; sizes[TXD] = 96 * n_wtx_;
     size_t off[NB], total = 0;
     for (int i = 0; i < NB; i++) {
         off[i] = total;
         total += align256(sizes[i]);
     }
+    const size_t upload = off[UPLOADED];
     if (total > cap_) {
         if (arena_) BCC_HIP_TRY(hipFree(arena_));
         arena_ = nullptr;
@@ -334,21 +722,25 @@ int DeviceBatch::stage_parts(const SighashJobs* const* J, const TupleRows* const
         BCC_HIP_TRY(hipMalloc(&arena_, total));
         cap_ = total;
     }
-    if (total > host_cap_) {
+    if (upload > host_cap_) {
         if (host_image_) BCC_HIP_TRY(hipHostFree(host_image_));
         host_image_ = nullptr;
         host_cap_ = 0;
-        BCC_HIP_TRY(hipHostMalloc(&host_image_, total, hipHostMallocDefault));
-        host_cap_ = total;
+        BCC_HIP_TRY(hipHostMalloc(&host_image_, upload, hipHostMallocDefault));
+        host_cap_ = upload;
     }
     uint8_t* a = (uint8_t*)arena_;
-    d_tag = a + off[0]; d_x = a + off[1]; d_y = a + off[2]; d_r = a + off[3]; d_s = a + off[4];
-    d_m = a + off[5]; d_v = a + off[6]; d_aux_ = a + off[7]; d_pre_ = a + off[8]; d_auxd_ = a + off[9];
-    d_aux_off_ = (uint32_t*)(a + off[10]); d_aux_nblk_ = (uint32_t*)(a + off[11]);
-    d_pre_off_ = (uint32_t*)(a + off[12]); d_pre_nblk_ = (uint32_t*)(a + off[13]);
-    d_pre_row_ = (uint32_t*)(a + off[14]); d_patch_ = (PatchRec*)(a + off[15]);
-    d_tpl_ = a + off[16]; d_code_ = a + off[17]; d_tjob_ = (TplJob*)(a + off[18]);
+    d_tag = a + off[TAG]; d_x = a + off[X]; d_y = a + off[Y]; d_r = a + off[RR]; d_s = a + off[S];
+    d_m = a + off[M]; d_v = a + off[V]; d_aux_ = a + off[AUX]; d_pre_ = a + off[PRE];
+    d_auxd_ = a + off[AUXD];
+    d_aux_off_ = (uint32_t*)(a + off[AUX_OFF]); d_aux_nblk_ = (uint32_t*)(a + off[AUX_NBLK]);
+    d_pre_off_ = (uint32_t*)(a + off[PRE_OFF]); d_pre_nblk_ = (uint32_t*)(a + off[PRE_NBLK]);
+    d_pre_row_ = (uint32_t*)(a + off[PRE_ROW]); d_patch_ = (PatchRec*)(a + off[PATCH]);
+    d_tpl_ = a + off[TPL]; d_code_ = a + off[CODE]; d_tjob_ = (TplJob*)(a + off[TJOB]);
+    d_txraw_ = a + off[TXRAW]; d_wtx_ = (WtxRec*)(a + off[WTX]); d_wjob_ = (WinJob*)(a + off[WJOB]);
+    d_zeros_ = a + off[ZEROS]; d_intab_ = (uint32_t*)(a + off[INTAB]); d_txd_ = a + off[TXD];
     uint8_t* h = (uint8_t*)host_image_;
+    memset(h + off[ZEROS], 0, 64);
     auto fill = [&](size_t p) {
         const SighashJobs& j = *J[p];
         const TupleRows& rw = *Rw[p];
@@ -356,31 +748,31 @@ int DeviceBatch::stage_parts(const SighashJobs* const* J, const TupleRows* const
         auto cp = [&](int b, size_t at, const void* src, size_t len) {
             if (len) memcpy(h + off[b] + at, src, len);
         };
-        cp(0, r0, rw.tag.data(), nr);
-        cp(1, 32 * r0, rw.x.data(), 32 * nr);
-        cp(2, 32 * r0, rw.y.data(), 32 * nr);
-        cp(3, 32 * r0, rw.r.data(), 32 * nr);
-        cp(4, 32 * r0, rw.s.data(), 32 * nr);
-        cp(5, 32 * r0, rw.msg.data(), 32 * nr);
-        cp(7, auxb0[p], j.aux.data(), j.aux.size());
-        cp(8, preb0[p], j.pre.data(), j.pre.size());
+        cp(TAG, r0, rw.tag.data(), nr);
+        cp(X, 32 * r0, rw.x.data(), 32 * nr);
+        cp(Y, 32 * r0, rw.y.data(), 32 * nr);
+        cp(RR, 32 * r0, rw.r.data(), 32 * nr);
+        cp(S, 32 * r0, rw.s.data(), 32 * nr);
+        cp(M, 32 * r0, rw.msg.data(), 32 * nr);
+        cp(AUX, auxb0[p], j.aux.data(), j.aux.size());
+        cp(PRE, preb0[p], j.pre.data(), j.pre.size());
         const uint32_t ablk = (uint32_t)(auxb0[p] / 64), pblk = (uint32_t)(preb0[p] / 64);
-        uint32_t* ao = (uint32_t*)(h + off[10]) + auxi0[p];
+        uint32_t* ao = (uint32_t*)(h + off[AUX_OFF]) + auxi0[p];
         for (size_t k = 0; k < j.aux_off.size(); k++) ao[k] = j.aux_off[k] + ablk;
-        cp(11, 4 * auxi0[p], j.aux_nblk.data(), 4 * j.aux_nblk.size());
-        uint32_t* po = (uint32_t*)(h + off[12]) + prei0[p];
-        uint32_t* pr = (uint32_t*)(h + off[14]) + prei0[p];
+        cp(AUX_NBLK, 4 * auxi0[p], j.aux_nblk.data(), 4 * j.aux_nblk.size());
+        uint32_t* po = (uint32_t*)(h + off[PRE_OFF]) + prei0[p];
+        uint32_t* pr = (uint32_t*)(h + off[PRE_ROW]) + prei0[p];
         for (size_t k = 0; k < j.pre_off.size(); k++) {
             po[k] = j.pre_off[k] + pblk;
             pr[k] = j.pre_row[k] + (uint32_t)r0;
         }
-        cp(13, 4 * prei0[p], j.pre_nblk.data(), 4 * j.pre_nblk.size());
-        PatchRec* pt = (PatchRec*)(h + off[15]) + pat0[p];
+        cp(PRE_NBLK, 4 * prei0[p], j.pre_nblk.data(), 4 * j.pre_nblk.size());
+        PatchRec* pt = (PatchRec*)(h + off[PATCH]) + pat0[p];
         for (size_t k = 0; k < j.patches.size(); k++)
             pt[k] = PatchRec{j.patches[k].pre_byte + pblk * 64, j.patches[k].aux + (uint32_t)auxi0[p]};
-        cp(16, tpl0[p], j.tpl.data(), j.tpl.size());
-        cp(17, code0[p], j.code.data(), j.code.size());
-        TplJob* tj = (TplJob*)(h + off[18]) + tj0[p];
+        cp(TPL, tpl0[p], j.tpl.data(), j.tpl.size());
+        cp(CODE, code0[p], j.code.data(), j.code.size());
+        TplJob* tj = (TplJob*)(h + off[TJOB]) + tj0[p];
         for (size_t k = 0; k < j.tjobs.size(); k++) {
             TplJob t = j.tjobs[k];
             t.tpl_off += (uint32_t)tpl0[p];
@@ -388,8 +780,24 @@ int DeviceBatch::stage_parts(const SighashJobs* const* J, const TupleRows* const
             t.row += (uint32_t)r0;
             tj[k] = t;
         }
+        cp(TXRAW, raw0[p], j.txraw.data(), j.txraw.size());
+        WtxRec* wr = (WtxRec*)(h + off[WTX]) + wtx0[p];
+        for (size_t k = 0; k < j.wtx.size(); k++) {
+            WtxRec t = j.wtx[k];
+            t.tx_off += (uint32_t)raw0[p];
+            t.in_base += (uint32_t)win0[p];
+            wr[k] = t;
+        }
+        WinJob* wj = (WinJob*)(h + off[WJOB]) + wj0[p];
+        for (size_t k = 0; k < j.wjobs.size(); k++) {
+            WinJob t = j.wjobs[k];
+            t.tx += (uint32_t)wtx0[p];
+            t.code_off += (uint32_t)code0[p];
+            t.row += (uint32_t)r0;
+            wj[k] = t;
+        }
     };
-    if (P == 1 || total < ((size_t)1 << 20)) {
+    if (P == 1 || upload < ((size_t)1 << 20)) {
         for (size_t p = 0; p < P; p++) fill(p);
     } else {
         std::vector<std::thread> th;
@@ -398,19 +806,39 @@ int DeviceBatch::stage_parts(const SighashJobs* const* J, const TupleRows* const
         for (auto& x : th) x.join();
     }
     BCC_HIP_TRY(hipSetDevice(dev_));
-    BCC_HIP_TRY(hipMemcpy(arena_, host_image_, total, hipMemcpyHostToDevice));
+    BCC_HIP_TRY(hipMemcpy(arena_, host_image_, upload, hipMemcpyHostToDevice));
     return 0;
 }
 
-int DeviceBatch::run_sighash(void* stream) {
-    BCC_HIP_TRY(hipSetDevice(dev_));
-    hipStream_t st = (hipStream_t)pick(stream);
-    if (!st) return (int)hipErrorOutOfMemory;
+int DeviceBatch::launch_wtx(void* stream) {
+    if (n_wtx_) {  // K_wtx: device-side deserialization + BIP143 per-tx hashes
+        hipLaunchKernelGGL(bip143_tx_kernel, dim3((unsigned)((3 * n_wtx_ + XS_WG - 1) / XS_WG)),
+                           dim3(XS_WG), 0, (hipStream_t)stream, d_txraw_, d_wtx_, (uint32_t)n_wtx_,
+                           d_intab_, d_txd_);
+        BCC_HIP_TRY(hipGetLastError());
+    }
+    return 0;
+}
+
+// The sighash kernels on `st`; K_wtx too unless run() already launched it on the side stream
+// (then K_win waits for `ev_wtx`).
+int DeviceBatch::launch_sighash(hipStream_t st, void* ev_wtx) {
     if (n_aux_ + n_tjob_) {  // K1 + K3' in one launch
         const size_t lanes = n_aux_ + n_tjob_;
         hipLaunchKernelGGL(sha256d_aux_tpl_kernel, dim3((unsigned)((lanes + 63) / 64)), dim3(64), 0, st,
                            d_aux_, d_aux_off_, d_aux_nblk_, (uint32_t)n_aux_, d_auxd_, d_tpl_, d_code_,
                            d_tjob_, (uint32_t)n_tjob_, d_m);
+        BCC_HIP_TRY(hipGetLastError());
+    }
+    if (ev_wtx) {
+        if (n_wtx_) BCC_HIP_TRY(hipStreamWaitEvent(st, (hipEvent_t)ev_wtx, 0));
+    } else if (int e = launch_wtx(st)) {
+        return e;
+    }
+    if (n_wjob_) {  // K_win: BIP143 preimages assembled from the raw tx bytes and hashed
+        hipLaunchKernelGGL(bip143_in_kernel, dim3((unsigned)((n_wjob_ + XS_WG - 1) / XS_WG)),
+                           dim3(XS_WG), 0, st, d_txraw_, d_wtx_, d_wjob_, (uint32_t)n_wjob_,
+                           d_intab_, d_txd_, d_code_, d_zeros_, d_m);
         BCC_HIP_TRY(hipGetLastError());
     }
     if (n_patch_) {
@@ -427,6 +855,13 @@ int DeviceBatch::run_sighash(void* stream) {
     return 0;
 }
 
+int DeviceBatch::run_sighash(void* stream) {
+    BCC_HIP_TRY(hipSetDevice(dev_));
+    hipStream_t st = (hipStream_t)pick(stream);
+    if (!st) return (int)hipErrorOutOfMemory;
+    return launch_sighash(st, nullptr);
+}
+
 int DeviceBatch::run_ecdsa(void* stream) {
     BCC_HIP_TRY(hipSetDevice(dev_));
     void* st = pick(stream);
@@ -440,26 +875,37 @@ int DeviceBatch::run(void* stream) {
     BCC_HIP_TRY(hipSetDevice(dev_));
     hipStream_t st = (hipStream_t)pick(stream);
     if (!st) return (int)hipErrorOutOfMemory;
-    if (n_rows_ == 0 || n_aux_ + n_tjob_ + n_pre_ == 0) {
+    if (n_rows_ == 0 || n_aux_ + n_tjob_ + n_pre_ + n_wjob_ == 0) {
         if (int e = run_sighash(st)) return e;
         return run_ecdsa(st);
     }
     if (!side_stream_) {
-        hipStream_t s = nullptr;
-        hipEvent_t a = nullptr, b = nullptr;
+        hipStream_t s = nullptr, s2 = nullptr;
+        hipEvent_t a = nullptr, b = nullptr, c = nullptr;
         BCC_HIP_TRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+        BCC_HIP_TRY(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
         BCC_HIP_TRY(hipEventCreateWithFlags(&a, hipEventDisableTiming));
         BCC_HIP_TRY(hipEventCreateWithFlags(&b, hipEventDisableTiming));
+        BCC_HIP_TRY(hipEventCreateWithFlags(&c, hipEventDisableTiming));
         side_stream_ = s;
+        wtx_stream_ = s2;
         ev_fork_ = a;
         ev_join_ = b;
+        ev_wtx_ = c;
     }
-    hipStream_t side = (hipStream_t)side_stream_;
+    hipStream_t side = (hipStream_t)side_stream_, ws = (hipStream_t)wtx_stream_;
     BCC_HIP_TRY(hipEventRecord((hipEvent_t)ev_fork_, st));
     BCC_HIP_TRY(hipStreamWaitEvent(side, (hipEvent_t)ev_fork_, 0));
+    // K_wtx on a stream of its own (a many-input tx's serial hash chains overlap K1 + K3' on the
+    // main stream and K_inv + K_key on the side stream)
+    if (n_wtx_) {
+        BCC_HIP_TRY(hipStreamWaitEvent(ws, (hipEvent_t)ev_fork_, 0));
+        if (int e = launch_wtx(ws)) return e;
+        BCC_HIP_TRY(hipEventRecord((hipEvent_t)ev_wtx_, ws));
+    }
     if (int e = ecdsa_launch_pre(scratch_, d_tag, d_x, d_y, d_s, n_rows_, side)) return e;
     BCC_HIP_TRY(hipEventRecord((hipEvent_t)ev_join_, side));
-    if (int e = run_sighash(st)) return e;
+    if (int e = launch_sighash(st, ev_wtx_)) return e;
     BCC_HIP_TRY(hipStreamWaitEvent(st, (hipEvent_t)ev_join_, 0));
     return ecdsa_launch_after_pre(scratch_, d_x, d_r, d_s, d_m, d_v, n_rows_, st);
 }

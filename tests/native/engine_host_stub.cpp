@@ -53,6 +53,14 @@ int gpu_verify_batch(int, const SighashJobs& j, const TupleRows& rows, uint8_t* 
         for (int b = 0; b < 4; b++) m.push_back((uint8_t)(t.hashtype >> (8 * b)));
         bcco_sha256d(m.data(), m.size(), &msg[32 * t.row]);
     }
+    for (const WinJob& w : j.wjobs) {  // BIP143 from the raw tx: the oracle's own sighash
+        const WtxRec& r = j.wtx[w.tx];
+        const uint8_t* c = &j.code[w.code_off];
+        size_t hdr = c[0] < 253 ? 1 : c[0] == 253 ? 3 : 5;
+        const int64_t amount = (int64_t)((uint64_t)w.amount_hi << 32 | w.amount_lo);
+        bcco_sighash(&j.txraw[r.tx_off], r.tx_len, w.nin, c + hdr, w.code_len - hdr,
+                     (int)w.hashtype, amount, 1, &msg[32 * w.row]);
+    }
     for (size_t i = 0; i < rows.size(); i++) {
         uint8_t pub[65];
         pub[0] = rows.tag[i];
