@@ -213,6 +213,88 @@ __device__ __forceinline__ void fe_reduce512_asm(uint32_t (&r)[8], const uint32_
     }
 }
 
+// r = t mod p (weak, r < 2^256), in carry chains of inline asm (no 64-bit adds, no zero-extension
+// moves).  With 2^256 == 2^32 + 977 (mod p) and p_i = t[8+i] * 977 (64-bit, v_mad_u64_u32):
+//   x = sum_i t[i] 2^32i + sum_i t[8+i] 2^32(i+1) + sum_i lo(p_i) 2^32i + sum_i hi(p_i) 2^32(i+1)
+// as three carry chains over ten limbs (A: t_lo + lo(p) on VCC, B: + t_hi << 32, C: + hi(p) << 32,
+// on SGPR pairs, skewed so that neighbouring instructions are independent), then top = x8 + x9 2^32
+// (< 2^34) folded once more as top * 977 + top << 32 (chains D, E); that cannot wrap past 2^256
+// more than once, and the rare wrap adds 2^32 + 977 (a wave-uniform branch).
+// gfx950 resolves VCC / SGPR carry dependencies between back-to-back VALU instructions in
+// hardware (tools/hazard/carry_hazard.hip: 3 x 4M biased chains per form, 0 mismatches), so the
+// chains carry no s_nop pads.
+__device__ __forceinline__ void fe_reduce512_chain(uint32_t (&r)[8], const uint32_t (&t)[16]) {
+    // one statement per limb; the three carries travel between statements in SGPR pairs, and
+    // each product p_i = t[8+i] * 977 is formed just ahead of its limb (few live registers)
+    uint32_t x[10];
+    uint64_t ca, cb, cc;
+    uint64_t p = (uint64_t)t[8] * 977u, q;
+    x[0] = t[0];
+    asm("v_add_co_u32_e64 %0, %1, %0, %2" : "+v"(x[0]), "=s"(ca) : "v"((uint32_t)p));
+    q = (uint64_t)t[9] * 977u;
+    x[1] = t[1];
+    asm("v_addc_co_u32_e64 %0, %1, %0, %4, %1\n\t"
+        "v_add_co_u32_e64 %0, %2, %0, %5\n\t"
+        "v_add_co_u32_e64 %0, %3, %0, %6"
+        : "+v"(x[1]), "+s"(ca), "=s"(cb), "=s"(cc)
+        : "v"((uint32_t)q), "v"(t[8]), "v"((uint32_t)(p >> 32)));
+#pragma unroll
+    for (int i = 2; i < 8; i++) {
+        p = q;
+        q = (uint64_t)t[8 + i] * 977u;
+        x[i] = t[i];
+        asm("v_addc_co_u32_e64 %0, %1, %0, %4, %1\n\t"
+            "v_addc_co_u32_e64 %0, %2, %0, %5, %2\n\t"
+            "v_addc_co_u32_e64 %0, %3, %0, %6, %3"
+            : "+v"(x[i]), "+s"(ca), "+s"(cb), "+s"(cc)
+            : "v"((uint32_t)q), "v"(t[7 + i]), "v"((uint32_t)(p >> 32)));
+    }
+    asm("v_addc_co_u32_e64 %0, %2, 0, 0, %2\n\t"
+        "v_addc_co_u32_e64 %0, %3, %0, %5, %3\n\t"
+        "v_addc_co_u32_e64 %0, %4, %0, %6, %4\n\t"
+        "v_addc_co_u32_e64 %1, %3, 0, 0, %3\n\t"
+        "v_addc_co_u32_e64 %1, %4, %1, 0, %4"
+        : "=&v"(x[8]), "=&v"(x[9]), "+s"(ca), "+s"(cb), "+s"(cc)
+        : "v"(t[15]), "v"((uint32_t)(q >> 32)));
+    const uint32_t x0 = x[0], x1 = x[1], x2 = x[2], x3 = x[3], x4 = x[4], x5 = x[5], x6 = x[6],
+                   x7 = x[7], x8 = x[8], x9 = x[9];
+    // fold top = x8 + x9 * 2^32 (< 2^34): + top * 977 (f) at limb 0, + top at limb 1
+    const uint64_t f = (uint64_t)x8 * 977u;
+    const uint32_t flo = (uint32_t)f, fhi = (uint32_t)(f >> 32) + x9 * 977u;
+    uint32_t w;
+    uint64_t ce;
+    asm("v_add_co_u32_e64 %[r0], vcc, %[x0], %[flo]\n\t"
+        "v_addc_co_u32_e64 %[r1], vcc, %[x1], %[fhi], vcc\n\t"
+        "v_addc_co_u32_e64 %[r2], vcc, %[x2], %[x9], vcc\n\t"
+        "v_add_co_u32_e64 %[r1], %[ce], %[r1], %[x8]\n\t"
+        "v_addc_co_u32_e64 %[r3], vcc, %[x3], 0, vcc\n\t"
+        "v_addc_co_u32_e64 %[r2], %[ce], %[r2], 0, %[ce]\n\t"
+        "v_addc_co_u32_e64 %[r4], vcc, %[x4], 0, vcc\n\t"
+        "v_addc_co_u32_e64 %[r3], %[ce], %[r3], 0, %[ce]\n\t"
+        "v_addc_co_u32_e64 %[r5], vcc, %[x5], 0, vcc\n\t"
+        "v_addc_co_u32_e64 %[r4], %[ce], %[r4], 0, %[ce]\n\t"
+        "v_addc_co_u32_e64 %[r6], vcc, %[x6], 0, vcc\n\t"
+        "v_addc_co_u32_e64 %[r5], %[ce], %[r5], 0, %[ce]\n\t"
+        "v_addc_co_u32_e64 %[r7], vcc, %[x7], 0, vcc\n\t"
+        "v_addc_co_u32_e64 %[r6], %[ce], %[r6], 0, %[ce]\n\t"
+        "v_addc_co_u32_e64 %[w], vcc, 0, 0, vcc\n\t"
+        "v_addc_co_u32_e64 %[r7], %[ce], %[r7], 0, %[ce]\n\t"
+        "v_addc_co_u32_e64 %[w], %[ce], %[w], 0, %[ce]"
+        : [r0] "=&v"(r[0]), [r1] "=&v"(r[1]), [r2] "=&v"(r[2]), [r3] "=&v"(r[3]),
+          [r4] "=&v"(r[4]), [r5] "=&v"(r[5]), [r6] "=&v"(r[6]), [r7] "=&v"(r[7]), [w] "=&v"(w),
+          [ce] "=&s"(ce)
+        : [x0] "v"(x0), [x1] "v"(x1), [x2] "v"(x2), [x3] "v"(x3), [x4] "v"(x4), [x5] "v"(x5),
+          [x6] "v"(x6), [x7] "v"(x7), [x8] "v"(x8), [x9] "v"(x9), [flo] "v"(flo), [fhi] "v"(fhi)
+        : "vcc");
+    if (w) {  // wrapped past 2^256 (rare): add 2^32 + 977 once more; cannot carry again
+        uint32_t c3;
+        r[0] = addc(r[0], 977u, 0, c3);
+        r[1] = addc(r[1], 1u, c3, c3);
+#pragma unroll
+        for (int i = 2; i < 8; i++) r[i] = addc(r[i], 0, c3, c3);
+    }
+}
+
 #endif
 
 }  // namespace bcc

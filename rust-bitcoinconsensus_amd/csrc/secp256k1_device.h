@@ -180,11 +180,23 @@ BCC_HD void fe_reduce512(fe& r, const u32 (&t)[16]) {
 
 // Device builds use the inline-asm carry-chain product / reduction (fe_asm.h); host builds
 // (tests/native) use the portable formulation above.  Both compute the same weak residue class.
+// Device reduction: the C formulation (fe_reduce512_asm, default) or the carry-chain asm
+// (fe_asm.h fe_reduce512_chain: ~30 % fewer instructions per reduction, but 4-6 % SLOWER in the
+// ladder, its VALU -> SGPR carry round trips being longer than the moves it saves; interleaved A/B
+// in profiles/r02/ab_field_reduction_sqrtail.txt).  A compile-time switch for A/B builds.
+#ifndef BCC_RED_CHAIN
+#define BCC_RED_CHAIN 0
+#endif
+
 BCC_HD void fe_mul(fe& r, const fe& a, const fe& b) {
     u32 t[16];
 #if defined(__HIP_DEVICE_COMPILE__)
     mul_256x256_col(t, a.v, b.v);
+#if BCC_RED_CHAIN
+    fe_reduce512_chain(r.v, t);
+#else
     fe_reduce512_asm(r.v, t);
+#endif
 #else
     mul_256x256(t, a.v, b.v);
     fe_reduce512(r, t);
@@ -195,7 +207,11 @@ BCC_HD void fe_sqr(fe& r, const fe& a) {
     u32 t[16];
 #if defined(__HIP_DEVICE_COMPILE__)
     sqr_256_col(t, a.v);
+#if BCC_RED_CHAIN
+    fe_reduce512_chain(r.v, t);
+#else
     fe_reduce512_asm(r.v, t);
+#endif
 #else
     sqr_256(t, a.v);
     fe_reduce512(r, t);
