@@ -122,6 +122,13 @@ int bcc_get_devices(int* out, int cap);
  * Bounds the per-caller device scratch (900 B per lane); results do not depend on it. */
 int bcc_set_chunk_lanes(size_t lanes);
 
+/* bitcoinconsensus_verify_batch pipelines a batch of at least two chunks: it is cut into chunks of
+ * about `items` inputs (whole transactions), and each chunk's device round runs on a worker thread
+ * while the host deserializes and interprets the next chunk.  0 disables it (the default, or the
+ * BCC_PIPELINE_CHUNK environment variable; measured slower end to end on one MI355X box, see
+ * DESIGN.md).  Results never depend on it. */
+int bcc_set_pipeline_chunk(size_t items);
+
 /* bitcoinconsensus_verify_batch keeps its host-side state (items, parsed transactions, job
  * buffers) with the calling thread for reuse by its next call; batches above 4M items release it
  * on return.  This releases the calling thread's state now. */

@@ -123,6 +123,10 @@ int run_on_devices(const std::vector<int>& devs, const std::vector<std::function
     return rc;
 }
 
+std::future<int> run_async(std::function<int()> job) {
+    return worker(-1).submit(std::move(job));  // key -1: the pipeline worker (no device of its own)
+}
+
 std::vector<size_t> split_balanced(const std::vector<size_t>& w, size_t k) {
     size_t total = 0;
     for (size_t x : w) total += x;

@@ -2,6 +2,7 @@
 // persistent host worker thread per GPU.
 #pragma once
 #include <functional>
+#include <future>
 #include <vector>
 
 namespace bcc {
@@ -16,6 +17,11 @@ std::vector<int> device_list();
 // call.  A single job runs inline on the calling thread (the single-device engine is per calling
 // thread, reentrant).  Returns the first nonzero job result, else 0.
 int run_on_devices(const std::vector<int>& devs, const std::vector<std::function<int()>>& jobs);
+
+// Runs job() on the persistent pipeline worker thread (bitcoinconsensus_verify_batch overlaps a
+// chunk's device rounds with the next chunk's host pass there; the worker's thread-local device
+// batch is the pipeline's arena).
+std::future<int> run_async(std::function<int()> job);
 
 // Contiguous split of `weights` (in order) into k groups of about equal total weight; returns the
 // k + 1 group boundaries (indices into weights).

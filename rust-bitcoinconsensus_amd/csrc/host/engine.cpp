@@ -14,6 +14,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <future>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -416,10 +417,6 @@ std::vector<std::vector<uint32_t>> make_shards(const BatchState& b, unsigned T) 
     return sh;
 }
 
-// Host state of bitcoinconsensus_verify_batch, per calling thread, reused across its calls.
-thread_local BatchState tl_state;
-thread_local std::vector<Round> tl_rounds;
-
 // One device round over the parts [p0, p1): fault injection first, then the device pipeline.
 int device_round(int dev, const SighashJobs* const* pj, const TupleRows* const* pr, size_t P,
                  uint8_t* verdict, double* stage_s) {
@@ -484,7 +481,8 @@ int run_device_group(int dev, const std::vector<Round>& rds, unsigned t0, unsign
 // transaction, so each tx's BIP143 aux hashes stay on one device); the groups run concurrently on
 // the GPUs' worker threads and write their verdicts at their row offsets.
 int run_device_round(const std::vector<Round>& rds, unsigned T, const std::vector<size_t>& row0,
-                     uint8_t* verdict, double* stage_total, size_t* devices_used) {
+                     uint8_t* verdict, double* stage_total, size_t* devices_used,
+                     size_t* retries) {
     const std::vector<int> devs = device_list();
     std::vector<size_t> w(T);
     for (unsigned t = 0; t < T; t++) w[t] = rds[t].pending.size();
@@ -505,82 +503,151 @@ int run_device_round(const std::vector<Round>& rds, unsigned T, const std::vecto
     const int e = jobs.empty() ? 0 : run_on_devices(jd, jobs);
     for (size_t d = 0; d < D; d++) {
         *stage_total += st[d];
-        t_stats.device_retries += rt[d];
+        *retries += rt[d];
     }
     *devices_used = std::max(*devices_used, jobs.size());
     return e;
 }
 
-// Runs the batch; fills ret/err per item.  Returns -1 if the device pipeline failed twice in a
-// row for some round: the items that round left unfinished get ret 0 and BCC_ERR_DEVICE_FAILURE
-// (never a consensus verdict); all other items carry their final results.
-// Host work (deserialization, interpreter passes, preimage building) runs on up to
-// host_threads() threads over whole-transaction shards; each round's deferred checks of all
-// shards go to the GPU together.  Only the items that need another run take part in a round.
-long run_batch(const bcc_batch_item* items, size_t n, unsigned flags, int* ret_out,
-               bitcoinconsensus_error* err_out) {
-    using clk = std::chrono::steady_clock;
-    t_stats = bcc_batch_stats{};
-    t_stats.items = n;
-    double host_s = 0, gpu_s = 0;
-    auto t0 = clk::now();
-    const unsigned T = n >= 256 ? std::min<unsigned>(host_threads(), (unsigned)(n / 64)) : 1u;
-    // per calling thread, reused across calls (capacity kept: no per-call allocation storm)
-    // (plain references: a lambda run on a worker thread must not name the thread_locals, which
-    // would resolve to that worker's own instances)
-    BatchState& b = tl_state;
-    std::vector<Round>& rds = tl_rounds;
-    prepare(b, items, n, flags, T);
-    auto since = [](clk::time_point a) { return std::chrono::duration<double>(clk::now() - a).count(); };
-    t_stats.prepare_seconds = since(t0);
-    auto& st = b.st;
-    const auto shards = make_shards(b, T);
-    std::vector<std::vector<uint32_t>> run_list(T), next_list(T);
-    for (unsigned t = 0; t < T; t++)
-        for (uint32_t i : shards[t])
-            if (st[i].active) run_list[t].push_back(i);
-    if (rds.size() < T) rds.resize(T);
-    for (unsigned t = 0; t < T; t++) {
-        rds[t].keys.clear();
-        rds[t].touched.clear();  // pointers into the previous call's tx entries: never followed
-    }
-    std::vector<size_t> row0(T + 1, 0);
+// One chunk of a batch: its host state, its rounds and its device round in flight.  Chunks of one
+// call are independent (every item's verdict depends on its own tx only).
+struct ChunkRun {
+    BatchState b;
+    std::vector<Round> rds;
+    std::vector<std::vector<uint32_t>> shards, run_list, next_list;
+    std::vector<size_t> row0;
     std::vector<uint8_t> verdict;
+    unsigned T = 1;
+    size_t n = 0, npend = 0;
+    bool pending_round = false;  // a device round for the current run lists is due
+    std::future<int> fut;        // the device round in flight (pipelined)
+    int sync_rc = 0;             // result of a synchronous device round
+    double stage_s = 0;
+    size_t devices_used = 0, retries = 0;
+};
+
+// Host state of bitcoinconsensus_verify_batch, per calling thread, reused across its calls: two
+// chunk slots (one on the host, one on the device when pipelined).
+thread_local ChunkRun tl_chunk[2];
+
+using clk = std::chrono::steady_clock;
+inline double since(clk::time_point a) { return std::chrono::duration<double>(clk::now() - a).count(); }
+
+// One interpreter pass over the chunk's run lists; sets up the device round it needs (if any).
+void chunk_interpret(ChunkRun& c) {
+    std::vector<char> ran(c.T, 0);
+    auto i0 = clk::now();
+    run_threads(c.T, [&](unsigned t) {
+        c.rds[t].reset();
+        ran[t] = interpret_shard(c.b, c.run_list[t], c.rds[t]);
+    });
+    t_stats.interpret_seconds += since(i0);
+    size_t npend = 0;
+    bool any = false;
+    for (unsigned t = 0; t < c.T; t++) {
+        c.row0[t] = npend;
+        npend += c.rds[t].pending.size();
+        any |= ran[t] != 0;
+    }
+    c.row0[c.T] = npend;
+    c.npend = npend;
+    c.pending_round = any && npend != 0;
+    if (!c.pending_round) return;
+    for (unsigned t = 0; t < c.T; t++) {
+        t_stats.preimages += c.rds[t].jobs.pre_off.size() + c.rds[t].jobs.tjobs.size() +
+                             c.rds[t].jobs.wjobs.size();
+        t_stats.aux_messages += c.rds[t].jobs.aux_off.size() + 3 * c.rds[t].jobs.wtx.size();
+    }
+    t_stats.rounds++;
+    t_stats.tuples += npend;
+    c.verdict.assign(npend, 0);
+}
+
+// prepare + shards + the first interpreter pass of items [0, n) of `items`.
+void chunk_start(ChunkRun& c, const bcc_batch_item* items, size_t n, unsigned flags) {
+    auto t0 = clk::now();
+    c.n = n;
+    c.T = n >= 256 ? std::min<unsigned>(host_threads(), (unsigned)(n / 64)) : 1u;
+    const unsigned T = c.T;
+    prepare(c.b, items, n, flags, T);
+    t_stats.prepare_seconds += since(t0);
+    c.shards = make_shards(c.b, T);
+    c.run_list.assign(T, {});
+    c.next_list.assign(T, {});
+    for (unsigned t = 0; t < T; t++)
+        for (uint32_t i : c.shards[t])
+            if (c.b.st[i].active) c.run_list[t].push_back(i);
+    if (c.rds.size() < T) c.rds.resize(T);
+    for (unsigned t = 0; t < T; t++) {
+        c.rds[t].keys.clear();
+        c.rds[t].touched.clear();  // pointers into a previous call's tx entries: never followed
+        c.rds[t].host_rejected = 0;
+    }
+    c.row0.assign(T + 1, 0);
+    c.stage_s = 0;
+    c.devices_used = 0;
+    c.retries = 0;
+    chunk_interpret(c);
+}
+
+// The chunk's pending device round (its arguments stay valid until the chunk's next pass).
+int chunk_device_round(ChunkRun& c) {
+    return run_device_round(c.rds, c.T, c.row0, c.verdict.data(), &c.stage_s, &c.devices_used,
+                            &c.retries);
+}
+
+// Stitches a device round's verdicts into the items; the items whose speculation failed get
+// another interpreter pass (their run lists).
+void chunk_stitch(ChunkRun& c) {
+    auto& st = c.b.st;
+    run_threads(c.T, [&](unsigned t) {
+        const Round& rd = c.rds[t];
+        const uint8_t* v = c.verdict.data() + c.row0[t];
+        for (size_t k = 0; k < rd.pending.size(); k++)
+            st[rd.pending[k].item].cache[rd.pending[k].slot].v = v[k] ? 1 : 0;
+        c.next_list[t].clear();
+        for (uint32_t i : c.run_list[t]) {
+            Item& it = st[i];
+            if (it.pending.empty()) continue;
+            bool all_true = true;
+            for (uint32_t k : it.pending) all_true &= v[k] != 0;
+            if (!all_true) {  // speculation was wrong somewhere: re-run
+                it.active = true;
+                c.next_list[t].push_back(i);
+            }
+        }
+        c.run_list[t].swap(c.next_list[t]);
+    });
+}
+
+// Completes the chunk: waits for (or runs) its device rounds, re-runs items until every run is
+// final, writes ret / err.  `async`: device rounds go to the pipeline worker.  Returns the valid
+// count, or -1 if a device round failed twice (those items get BCC_ERR_DEVICE_FAILURE).
+long chunk_finish(ChunkRun& c, int* ret_out, bitcoinconsensus_error* err_out, bool async,
+                  double* gpu_s) {
+    auto& st = c.b.st;
     long status = 0;
-    for (size_t round = 0;; round++) {
-        std::vector<char> ran(T, 0);
-        auto i0 = clk::now();
-        run_threads(T, [&](unsigned t) {
-            rds[t].reset();
-            ran[t] = interpret_shard(b, run_list[t], rds[t]);
-        });
-        t_stats.interpret_seconds += since(i0);
-        size_t npend = 0;
-        bool any = false;
-        for (unsigned t = 0; t < T; t++) {
-            row0[t] = npend;
-            npend += rds[t].pending.size();
-            any |= ran[t] != 0;
-        }
-        row0[T] = npend;
-        if (!any || npend == 0) break;
-        for (unsigned t = 0; t < T; t++) {
-            t_stats.preimages += rds[t].jobs.pre_off.size() + rds[t].jobs.tjobs.size() +
-                                 rds[t].jobs.wjobs.size();
-            t_stats.aux_messages += rds[t].jobs.aux_off.size() + 3 * rds[t].jobs.wtx.size();
-        }
-        t_stats.rounds++;
-        t_stats.tuples += npend;
+    while (c.pending_round) {
         auto g0 = clk::now();
-        verdict.assign(npend, 0);
-        double stage_s = 0;
-        int e = run_device_round(rds, T, row0, verdict.data(), &stage_s, &t_stats.devices);
-        t_stats.stage_seconds += stage_s;
-        gpu_s += std::chrono::duration<double>(clk::now() - g0).count();
+        int e;
+        if (c.fut.valid()) {
+            e = c.fut.get();
+        } else if (async) {
+            e = run_async([&c] { return chunk_device_round(c); }).get();
+        } else {
+            e = chunk_device_round(c);
+        }
+        *gpu_s += since(g0);
+        t_stats.stage_seconds += c.stage_s;
+        t_stats.device_retries += c.retries;
+        t_stats.devices = std::max(t_stats.devices, c.devices_used);
+        c.stage_s = 0;
+        c.retries = 0;
+        c.pending_round = false;
         if (e != 0) {
             status = -1;
-            for (unsigned t = 0; t < T; t++)
-                for (uint32_t i : run_list[t]) {
+            for (unsigned t = 0; t < c.T; t++)
+                for (uint32_t i : c.run_list[t]) {
                     Item& it = st[i];
                     if (it.pending.empty()) continue;  // this run consulted no deferred check
                     it.result = false;
@@ -589,52 +656,102 @@ long run_batch(const bcc_batch_item* items, size_t n, unsigned flags, int* ret_o
                 }
             break;
         }
-        run_threads(T, [&](unsigned t) {
-            const Round& rd = rds[t];
-            const uint8_t* v = verdict.data() + row0[t];
-            for (size_t k = 0; k < rd.pending.size(); k++)
-                st[rd.pending[k].item].cache[rd.pending[k].slot].v = v[k] ? 1 : 0;
-            next_list[t].clear();
-            for (uint32_t i : run_list[t]) {
-                Item& it = st[i];
-                if (it.pending.empty()) continue;
-                bool all_true = true;
-                for (uint32_t k : it.pending) all_true &= v[k] != 0;
-                if (!all_true) {  // speculation was wrong somewhere: re-run
-                    it.active = true;
-                    next_list[t].push_back(i);
-                }
-            }
-            run_list[t].swap(next_list[t]);
-        });
+        chunk_stitch(c);
+        chunk_interpret(c);
     }
-    for (unsigned t = 0; t < T; t++) t_stats.host_rejected += rds[t].host_rejected;
+    for (unsigned t = 0; t < c.T; t++) t_stats.host_rejected += c.rds[t].host_rejected;
     long valid = 0;
-    for (size_t i = 0; i < n; i++) {
+    for (size_t i = 0; i < c.n; i++) {
         Item& it = st[i];
         int ret = (it.err == bitcoinconsensus_ERR_OK && it.result) ? 1 : 0;
         ret_out[i] = ret;
         if (err_out) err_out[i] = it.err;
         valid += ret;
     }
-    // The state stays with the calling thread for its next call, except after a very large batch:
-    // then it is released, in parallel (freeing from one thread costs more than the
-    // interpreter pass itself).
-    if (n > ((size_t)1 << 22)) {
-        run_threads(T, [&](unsigned t) {
-            for (uint32_t i : shards[t]) {
-                decltype(st[i].cache)().swap(st[i].cache);
-                std::vector<uint32_t>().swap(st[i].pending);
+    return status < 0 ? -1 : valid;
+}
+
+// The state stays with the calling thread for its next call, except after a very large chunk:
+// then it is released, in parallel (freeing from one thread costs more than the interpreter pass
+// itself).
+void chunk_release_if_large(ChunkRun& c) {
+    if (c.n <= ((size_t)1 << 22)) return;
+    auto& st = c.b.st;
+    run_threads(c.T, [&](unsigned t) {
+        for (uint32_t i : c.shards[t]) {
+            decltype(st[i].cache)().swap(st[i].cache);
+            std::vector<uint32_t>().swap(st[i].pending);
+        }
+        c.rds[t] = Round();
+        const size_t E = c.b.txs.size();
+        for (size_t k = share_lo(E, t, c.T); k < share_lo(E, t + 1, c.T); k++) c.b.txs[k].tx = Tx();
+    });
+    c.b = BatchState();
+    c.rds = std::vector<Round>();
+}
+
+// Items per pipelined chunk (bcc_set_pipeline_chunk, BCC_PIPELINE_CHUNK; 0 disables pipelining).
+// Off by default: measured on the GPU box, the overlap hides the chunk's device round but the
+// next chunk's deserialization pass runs 6-7x slower beside it (prepare 13-16 -> 95-106 ms for
+// 1M inputs in 262k chunks; profiles/r02/e2e_pipeline_ab.txt), a net loss.
+std::atomic<size_t> g_pipeline_chunk{[] {
+    const char* e = getenv("BCC_PIPELINE_CHUNK");
+    return e ? (size_t)atoll(e) : (size_t)0;
+}()};
+size_t pipeline_chunk() { return g_pipeline_chunk.load(std::memory_order_relaxed); }
+
+// Runs the batch; fills ret/err per item.  Returns -1 if the device pipeline failed twice in a
+// row for some round: the items that round left unfinished get ret 0 and BCC_ERR_DEVICE_FAILURE
+// (never a consensus verdict); all other items carry their final results.
+// Host work (deserialization, interpreter passes, job building) runs on up to host_threads()
+// threads over whole-transaction shards; each round's deferred checks of all shards go to the GPU
+// together.  A batch of at least two pipeline chunks is cut into chunks of whole transactions
+// whose first device round runs on the pipeline worker while the host works on the next chunk
+// (double-buffered: two chunk slots, the worker's own device batch).
+long run_batch(const bcc_batch_item* items, size_t n, unsigned flags, int* ret_out,
+               bitcoinconsensus_error* err_out) {
+    t_stats = bcc_batch_stats{};
+    t_stats.items = n;
+    double gpu_s = 0;
+    auto t0 = clk::now();
+    const size_t chunk = pipeline_chunk();
+    long status = 0, valid = 0;
+    auto account = [&](long r) {
+        if (r < 0) status = -1;
+        else valid += r;
+    };
+    if (chunk == 0 || n < 2 * chunk) {
+        ChunkRun& c = tl_chunk[0];
+        chunk_start(c, items, n, flags);
+        account(chunk_finish(c, ret_out, err_out, false, &gpu_s));
+        chunk_release_if_large(c);
+    } else {
+        // chunk boundaries between transactions (adjacent items of one tx stay together)
+        std::vector<size_t> cut{0};
+        while (cut.back() < n) {
+            size_t e = std::min(n, cut.back() + chunk);
+            while (e < n && items[e].tx_to == items[e - 1].tx_to) e++;
+            cut.push_back(e);
+        }
+        ChunkRun* prev = nullptr;
+        size_t prev_lo = 0;
+        for (size_t k = 0; k + 1 < cut.size(); k++) {
+            ChunkRun& c = tl_chunk[k & 1];
+            chunk_start(c, items + cut[k], cut[k + 1] - cut[k], flags);
+            if (prev) {
+                account(chunk_finish(*prev, ret_out + prev_lo, err_out ? err_out + prev_lo : nullptr,
+                                     true, &gpu_s));
             }
-            rds[t] = Round();
-            const size_t E = b.txs.size();
-            for (size_t k = share_lo(E, t, T); k < share_lo(E, t + 1, T); k++) b.txs[k].tx = Tx();
-        });
-        b = BatchState();
-        rds = std::vector<Round>();
+            if (c.pending_round) c.fut = run_async([&c] { return chunk_device_round(c); });
+            prev = &c;
+            prev_lo = cut[k];
+        }
+        account(chunk_finish(*prev, ret_out + prev_lo, err_out ? err_out + prev_lo : nullptr, true,
+                             &gpu_s));
+        chunk_release_if_large(tl_chunk[0]);
+        chunk_release_if_large(tl_chunk[1]);
     }
-    host_s = std::chrono::duration<double>(clk::now() - t0).count() - gpu_s;
-    t_stats.host_seconds = host_s;
+    t_stats.host_seconds = since(t0) - gpu_s;
     t_stats.gpu_seconds = gpu_s;
     return status < 0 ? -1 : valid;
 }
@@ -776,9 +893,13 @@ long bitcoinconsensus_verify_batch(const bcc_batch_item* items, size_t n, unsign
 
 void bcc_debug_fail_device_rounds(int rounds) { g_fail_rounds.store(rounds > 0 ? rounds : 0); }
 
+int bcc_set_pipeline_chunk(size_t items) {
+    g_pipeline_chunk.store(items, std::memory_order_relaxed);
+    return 0;
+}
+
 void bcc_release_thread_state(void) {
-    tl_state = BatchState();
-    tl_rounds = std::vector<Round>();
+    for (auto& c : tl_chunk) c = ChunkRun();
 }
 
 int bcc_set_device(int device) {

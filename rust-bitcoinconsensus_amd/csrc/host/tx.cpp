@@ -57,11 +57,12 @@ struct Reader {
     }
 };
 
-bool read_vin(Reader& r, std::vector<TxIn>& vin) {
-    uint64_t k = r.compact();
+// The vin list after its compact-size count k has been read.
+bool read_vin_items(Reader& r, std::vector<TxIn>& vin, uint64_t k) {
     if (r.bad || k > r.n - r.pos) return false;  // every element needs >= 1 byte: EOF anyway
-    vin.resize((size_t)k);
+    vin.resize((size_t)k);  // existing elements (and their witness capacity) are reused
     for (auto& in : vin) {
+        in.witness.clear();
         in.prevout = r.take(36);
         in.script_sig = r.bytes();
         in.sequence = (uint32_t)r.le(4);
@@ -69,6 +70,8 @@ bool read_vin(Reader& r, std::vector<TxIn>& vin) {
     }
     return true;
 }
+
+bool read_vin(Reader& r, std::vector<TxIn>& vin) { return read_vin_items(r, vin, r.compact()); }
 
 bool read_vout(Reader& r, std::vector<TxOut>& vout) {
     uint64_t k = r.compact();
@@ -89,23 +92,28 @@ bool read_vout(Reader& r, std::vector<TxOut>& vout) {
 
 bool parse_tx(const uint8_t* data, size_t len, Tx& tx) {
     Reader r{data, len};
-    tx.vin.clear();   // keep capacity: callers reuse Tx objects across batches
-    tx.vout.clear();
+    // no clear(): vin / vout are resized in place, so a reused Tx keeps its elements and their
+    // witness vectors' capacity (no per-input allocation when callers reuse Tx objects)
     tx.version = 0;
     tx.locktime = 0;
     tx.ser_size = 0;
     tx.version = (int32_t)(uint32_t)r.le(4);
     if (r.bad) return false;
     uint8_t flags = 0;
-    if (!read_vin(r, tx.vin)) return false;
-    if (tx.vin.empty()) {           // dummy (segwit marker) or an empty vin
+    const uint64_t k = r.compact();
+    if (r.bad) return false;
+    if (k == 0) {  // dummy (segwit marker) or an empty vin; vin is not shrunk before we know
         flags = (uint8_t)r.le(1);
         if (r.bad) return false;
         if (flags != 0) {
             if (!read_vin(r, tx.vin)) return false;
             if (!read_vout(r, tx.vout)) return false;
+        } else {
+            tx.vin.clear();
+            tx.vout.clear();
         }
     } else {
+        if (!read_vin_items(r, tx.vin, k)) return false;
         if (!read_vout(r, tx.vout)) return false;
     }
     if (flags & 1) {

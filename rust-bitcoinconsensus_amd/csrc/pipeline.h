@@ -266,6 +266,8 @@ private:
     size_t cap_ = 0;
     void* host_image_ = nullptr;  // pinned host image of the arena (staging)
     size_t host_cap_ = 0;
+    void* vbuf_ = nullptr;        // pinned verdict buffer (fetch_verdicts)
+    size_t vcap_ = 0;
     size_t n_rows_ = 0, n_pre_ = 0, n_aux_ = 0, n_patch_ = 0, pre_blocks_ = 0, aux_blocks_ = 0;
     uint8_t *d_aux_ = nullptr, *d_pre_ = nullptr, *d_auxd_ = nullptr;
     uint32_t *d_aux_off_ = nullptr, *d_aux_nblk_ = nullptr, *d_pre_off_ = nullptr,

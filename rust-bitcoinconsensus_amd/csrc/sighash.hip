@@ -493,7 +493,6 @@ __global__ __launch_bounds__(XS_WG) void bip143_tx_kernel(const uint8_t* __restr
     } else if (role == 1) {
         // hashSequence: word m is input m's nSequence, parsed inline
         const uint32_t L = 4 * nin, nb = (L + 8) / 64 + 1;
-        uint32_t np = 0;
         for (uint32_t b = 0; b < nb; b++) {
             uint32_t w[16];
 #pragma unroll
@@ -503,7 +502,6 @@ __global__ __launch_bounds__(XS_WG) void bip143_tx_kernel(const uint8_t* __restr
                 if (m < nin) {
                     uint32_t sq;
                     wire_input(x, pos, &sq);
-                    np++;
                     v = be_word_at(t4, sq);
                 } else if (m == nin) {
                     v = 0x80000000u;
@@ -617,6 +615,7 @@ DeviceBatch::~DeviceBatch() {
     if (ev_wtx_) (void)hipEventDestroy((hipEvent_t)ev_wtx_);
     if (arena_) (void)hipFree(arena_);
     if (host_image_) (void)hipHostFree(host_image_);
+    if (vbuf_) (void)hipHostFree(vbuf_);
 }
 
 void* DeviceBatch::pick(void* stream) {
@@ -910,9 +909,22 @@ int DeviceBatch::run(void* stream) {
     return ecdsa_launch_after_pre(scratch_, d_x, d_r, d_s, d_m, d_v, n_rows_, st);
 }
 
+// Verdicts come back through a pinned buffer of the batch (an asynchronous copy on the run's stream,
+// then one host memcpy): a pageable D2H copy would pin the caller's pages on every call.
 int DeviceBatch::fetch_verdicts(uint8_t* out) {
-    if (int e = sync()) return e;
-    if (n_rows_) BCC_HIP_TRY(hipMemcpy(out, d_v, n_rows_, hipMemcpyDeviceToHost));
+    if (!n_rows_) return sync();
+    if (n_rows_ > vcap_) {
+        if (vbuf_) BCC_HIP_TRY(hipHostFree(vbuf_));
+        vbuf_ = nullptr;
+        vcap_ = 0;
+        BCC_HIP_TRY(hipHostMalloc(&vbuf_, n_rows_, hipHostMallocDefault));
+        vcap_ = n_rows_;
+    }
+    BCC_HIP_TRY(hipSetDevice(dev_));
+    hipStream_t st = (hipStream_t)pick(last_stream_);
+    BCC_HIP_TRY(hipMemcpyAsync(vbuf_, d_v, n_rows_, hipMemcpyDeviceToHost, st));
+    BCC_HIP_TRY(hipStreamSynchronize(st));
+    memcpy(out, vbuf_, n_rows_);
     return 0;
 }
 

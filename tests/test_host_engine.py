@@ -13,6 +13,8 @@ import subprocess
 
 import pytest
 
+import engine_stub
+
 from fixtures import load_json
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -91,6 +93,24 @@ def test_script_cases_as_batches(eng):
         got = list(zip(ret, err))
         assert got == exp
         assert nvalid == sum(r for r, _ in exp)
+
+
+def test_script_cases_pipelined(eng):
+    """The same batches cut into pipeline chunks of 97 items (chunk device rounds on the worker
+    thread overlapping the next chunk's host pass), alone and over three devices: identical to the
+    single calls; an injected device failure in a pipelined chunk is retried."""
+    eng.bcc_set_pipeline_chunk.argtypes = [ctypes.c_size_t]
+    try:
+        eng.bcc_set_pipeline_chunk(97)
+        test_script_cases_as_batches(eng)
+        engine_stub.set_devices(eng, [0, 1, 2])
+        test_script_cases_as_batches(eng)
+        engine_stub.set_devices(eng, [])
+        eng.bcc_debug_fail_device_rounds(1)
+        test_script_cases_as_batches(eng)
+    finally:
+        engine_stub.set_devices(eng, [])
+        eng.bcc_set_pipeline_chunk(0)
 
 
 def test_pubkey_verify_batch_front_end(eng):
