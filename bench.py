@@ -1,6 +1,6 @@
 """bench.py — ECDSA verifies/s of the MI355X signature hot path (BASELINE.json metric).
 
-    python bench.py [--gpus N --steps K --warmup W --config c2|c3|c4|c5 --n UNITS_PER_GPU]
+    python bench.py [--gpus N --steps K --warmup W --config c2|c3|c4|c5|c5t --n UNITS_PER_GPU]
     (N > 1: python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1
              --master-port P bench.py --gpus N ...)
 
@@ -49,8 +49,9 @@ UBENCH_OPS = {0: "v_mad_u64_u32", 1: "v_mul_lo_u32", 2: "v_mul_hi_u32", 3: "v_ad
               15: "v_cndmask_b32", 16: "mad_u64_u32+addc pair", 17: "mul_lo+mul_hi pair",
               18: "mad_u64_u32+add_u32 pair"}
 METRIC = "ECDSA verifies/sec (node) at 1/2/4/8 MI355X; % of int-ALU roofline"
-DEFAULT_N = {"c2": 1_000_000, "c3": 4000, "c4": 8_000_000, "c5": 16_000_000}
-SEEDS = {"c2": 0x5EED0001, "c3": 0x5EED0003, "c4": 0x5EED0004, "c5": 0x5EED0005}
+DEFAULT_N = {"c2": 1_000_000, "c3": 4000, "c4": 8_000_000, "c5": 16_000_000, "c5t": 1_000_000}
+SEEDS = {"c2": 0x5EED0001, "c3": 0x5EED0003, "c4": 0x5EED0004, "c5": 0x5EED0005,
+         "c5t": 0x5EED0006}
 CPU_PASSES = 3                    # timed passes of the CPU baseline (median), after 1 warm-up
 
 
@@ -442,12 +443,185 @@ class TupleJob:
         return f"synthetic (deterministic {self.kind.upper()} tuples, GPU-generated keys/signatures)"
 
 
+class C5T:
+    """BIP341 key-path Taproot spends through bcc_taproot_verify_batch:
+    GenericTransactionSignatureChecker::CheckSchnorrSignature per check (interpreter.cpp:1678-1704),
+    i.e. SignatureHashSchnorr over the tx + its spent outputs and the BIP340 verification, end to
+    end from host buffers (host SigMsg building, H2D, GPU aux / TapSighash / Schnorr kernels)."""
+    unit = "checks/s"
+    data = ("synthetic (1-in/1-out key-path Taproot spends, GPU-generated keys and BIP340 "
+            "signatures over the engine's own BIP341 sighashes, 5% of signatures corrupted)")
+
+    def __init__(self, B, n, seed, dev, first=0, total=None):
+        import ctypes
+        import hashlib
+        import numpy as np
+        self.B, self.n, self.units, self.dev = B, n, n, dev
+        self.mads = MADS_PER_SCHNORR
+        self.kernel = "taproot end to end (host SigMsg + GPU tapsighash + schnorr prep/ladder/parity)"
+        rng = np.random.default_rng(seed + first)
+        d = rng.integers(0, 256, size=(n, 32), dtype=np.uint8)
+        d[:, 0] &= 0x7F  # < n, != 0 (w.p. 1 - 2^-120)
+        d[:, 31] |= 1
+        BL = B.blib()
+        u8 = lambda a: a.ctypes.data_as(ctypes.c_char_p)  # noqa: E731
+        sig = np.zeros((n, 64), np.uint8)
+        xo = np.zeros((n, 32), np.uint8)
+        ok = np.zeros(n, np.uint8)
+        k = rng.integers(0, 256, size=(n, 32), dtype=np.uint8)
+        k[:, 0] &= 0x7F
+        k[:, 31] |= 1
+        m = np.zeros((n, 32), np.uint8)
+        assert BL.mi_gen_schnorr_sign(u8(d), u8(m), u8(k), n, u8(sig), u8(xo), u8(ok), dev) == 0
+        # tx: v2 | marker/flag | 1 input | 1 P2TR output | witness [sig64] | locktime (162 bytes)
+        L = 162
+        tx = np.zeros((n, L), np.uint8)
+        tx[:, 0] = 2
+        tx[:, 5] = 1
+        tx[:, 6] = 1
+        tx[:, 7:39] = rng.integers(0, 256, size=(n, 32), dtype=np.uint8)   # prevout txid
+        tx[:, 39] = rng.integers(0, 4, size=n, dtype=np.uint8)             # vout
+        tx[:, 44:48] = 0xFF                                                 # nSequence
+        tx[:, 48] = 1
+        tx[:, 49:57] = rng.integers(0, 256, size=(n, 8), dtype=np.uint8)
+        tx[:, 56] &= 0x03
+        tx[:, 57] = 34
+        tx[:, 58] = 0x51
+        tx[:, 59] = 0x20
+        tx[:, 60:92] = rng.integers(0, 256, size=(n, 32), dtype=np.uint8)
+        tx[:, 92] = 1
+        tx[:, 93] = 64
+        tx[:, 94:158] = 0x5A
+        spent = np.zeros((n, 44), np.uint8)
+        spent[:, 0] = 1
+        spent[:, 1:9] = rng.integers(0, 256, size=(n, 8), dtype=np.uint8)
+        spent[:, 8] &= 0x03
+        spent[:, 9] = 34
+        spent[:, 10] = 0x51
+        spent[:, 11] = 0x20
+        spent[:, 12:44] = xo
+        self.tx, self.spent, self.xo = tx, spent, xo
+        self.sig = np.zeros((n, 64), np.uint8)
+        self.leaf = np.zeros(32, np.uint8)
+        T = B.TaprootCheck
+        arr = (T * n)()
+        base_tx, base_sp = tx.ctypes.data, spent.ctypes.data
+        base_sig, base_pk = self.sig.ctypes.data, xo.ctypes.data
+        vp = ctypes.c_void_p
+        # fill the struct array through a numpy view (n ctypes assignments would take seconds)
+        view = np.ctypeslib.as_array(ctypes.cast(arr, ctypes.POINTER(ctypes.c_uint8)),
+                                     shape=(n * ctypes.sizeof(T),)).view(np.uint8)
+        rec = np.zeros(1, dtype=np.dtype({"names": [f for f, _ in T._fields_],
+                                          "formats": ["u8", "u4", "u8", "u4", "u4", "u8", "u4",
+                                                      "u8", "i4", "u8", "u4", "u8", "u4"],
+                                          "offsets": [getattr(T, f).offset for f, _ in T._fields_],
+                                          "itemsize": ctypes.sizeof(T)}))
+        recs = view.view(rec.dtype)
+        idx = np.arange(n, dtype=np.uint64)
+        recs["tx"] = base_tx + idx * L
+        recs["tx_len"] = L
+        recs["spent_outputs"] = base_sp + idx * 44
+        recs["spent_outputs_len"] = 44
+        recs["n_in"] = 0
+        recs["sig"] = base_sig + idx * 64
+        recs["sig_len"] = 64
+        recs["pubkey32"] = base_pk + idx * 32
+        recs["sigversion"] = 0
+        recs["annex"] = 0
+        recs["annex_len"] = 0
+        recs["tapleaf_hash32"] = self.leaf.ctypes.data
+        recs["codeseparator_pos"] = 0xFFFFFFFF
+        self.arr = arr
+        self.ret = np.zeros(n, np.int32)
+        self.err = np.zeros(n, np.int32)
+        Lb = B.lib()
+        self.L = Lb
+        hs = np.zeros((n, 32), np.uint8)
+        assert Lb.bcc_taproot_verify_batch(arr, n, self._p(self.ret), self._p(self.err),
+                                           hs.ctypes.data, dev) == 0
+        assert BL.mi_gen_schnorr_sign(u8(d), u8(hs), u8(k), n, u8(self.sig), u8(xo), u8(ok),
+                                      dev) == 0
+        bad = rng.random(n) < 0.05
+        self.sig[bad, rng.integers(0, 64)] ^= 0x10
+        self.expect = int((~bad).sum())
+        self.hs = hs
+        del hashlib
+
+    @staticmethod
+    def _p(a):
+        import ctypes
+        return a.ctypes.data_as(ctypes.POINTER(ctypes.c_int))
+
+    def step(self, sp):
+        rc = self.L.bcc_taproot_verify_batch(self.arr, self.n, self._p(self.ret),
+                                             self._p(self.err), None, self.dev)
+        assert rc == 0
+
+    def valid(self):
+        self.step(None)
+        return int((self.ret == 1).sum())
+
+    def item_verdicts(self):
+        return bytes((self.ret == 1).astype("uint8"))
+
+    def kernel_times(self, stream, reps):
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            self.step(None)
+        return 0.0, (time.perf_counter() - t0) / reps * 1e3
+
+    shape = property(lambda self: {"tuples": self.n})
+
+    def extra(self, sighash_ms):
+        return {"expected_valid": self.expect,
+                "note": "value = checks/s of bcc_taproot_verify_batch end to end from host buffers; "
+                        "roofline = the BIP340 work unit over that end-to-end time (a lower bound "
+                        "for the kernels)"}
+
+    def cpu(self, sample):
+        import ctypes
+        import numpy as np
+        R = _reference()
+        if R is None:
+            return None
+        sample = min(sample, self.n)
+        R.L.ref_bulk_taproot.argtypes = [ctypes.c_int, ctypes.c_long, ctypes.c_void_p,
+                                         ctypes.c_void_p, ctypes.c_void_p]
+        R.L.ref_bulk_taproot.restype = ctypes.c_double
+        hw = host_cpu_info()
+        threads = hw["threads_used"]
+        ret = np.zeros(sample, np.int32)
+        err = np.zeros(sample, np.int32)
+        base = ctypes.addressof(self.arr)
+        rate, passes = median_rate(lambda: R.L.ref_bulk_taproot(
+            threads, sample, base, ret.ctypes.data, err.ctypes.data), sample)
+        n1 = max(1, sample // 16)
+        rate1, _ = median_rate(lambda: R.L.ref_bulk_taproot(
+            1, n1, base, ret.ctypes.data, err.ctypes.data), n1, passes=1)
+        R.L.ref_bulk_taproot(threads, sample, base, ret.ctypes.data, err.ctypes.data)
+        mism = int(((ret == 1) != (self.ret[:sample] == 1)).sum() +
+                   ((ret == 0) & (err != self.err[:sample])).sum())
+        return dict(value=rate, unit="checks/s", cores=threads, kind="reference",
+                    sample=f"first {sample} C5T checks, CheckSchnorrSignature (reference "
+                           f"interpreter.cpp:1678-1704 via oracle/_ref), dynamically chunked "
+                           f"std::thread pool x{threads}, median of {CPU_PASSES} passes after 1 "
+                           f"warm-up; reference accepted {int((ret == 1).sum())}/{sample}; "
+                           f"GPU (ret, serror) mismatches on the sample: {mism}",
+                    passes=passes, single_core_value=rate1, host=hw, gpu_verdict_mismatches=mism)
+
+    def config(self, world):
+        return {"workload": "C5T: BIP341 key-path Taproot spends, SignatureHashSchnorr + BIP340 "
+                            "through bcc_taproot_verify_batch end to end (SURVEY 8f rank 3)",
+                "checks_per_gpu": self.n, "global_checks": self.n * world,
+                "parallelism": f"shard x{world} (independent checks, no collective)"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--config", choices=("c2", "c3", "c4", "c5"), default="c2")
+    ap.add_argument("--config", choices=("c2", "c3", "c4", "c5", "c5t"), default="c2")
     ap.add_argument("--n", type=int, default=None,
                     help="units per GPU: inputs (c2), transactions (c3), tuples (c4, c5)")
     ap.add_argument("--seed", type=int, default=None)
@@ -479,6 +653,8 @@ def main():
     first, total = rank * n, world * n
     if args.config in ("c2", "c3"):
         job = (C2 if args.config == "c2" else C3)(B, n, seed, dev, first=first, total=total)
+    elif args.config == "c5t":
+        job = C5T(B, n, seed, dev, first=first, total=total)
     else:
         job = TupleJob(B, n, seed, dev, args.config, first=first, total=total)
     log(f"[rank {rank}] staged {args.config} x{n} in {time.time() - t0:.1f}s")
@@ -514,7 +690,7 @@ def main():
 
     # per-kernel timing with HIP events on the launch stream (outside the timed region)
     sighash_ms, sig_ms = job.kernel_times(stream, max(3, args.steps))
-    sig_units = job.shape["tuples"] if args.config in ("c2", "c3") else job.units
+    sig_units = job.shape["tuples"] if args.config in ("c2", "c3", "c5t") else job.units
 
     total = job.units * world * args.steps
     value = total / elapsed
@@ -537,7 +713,8 @@ def main():
                                     verifies_per_s=sig_units / (sig_ms * 1e-3)))
         cpu = None
         if world == 1 and not args.no_cpu:
-            default_sample = {"c2": 200_000, "c3": 100_000, "c4": 400_000, "c5": 400_000}
+            default_sample = {"c2": 200_000, "c3": 100_000, "c4": 400_000, "c5": 400_000,
+                              "c5t": 200_000}
             cpu = job.cpu(args.cpu_sample or default_sample[args.config])
         out = {
             "metric": METRIC, "value": value, "unit": job.unit, "n_gpus": world,

@@ -346,6 +346,37 @@ double ref_bulk_verify_items(int nthreads, long n, const ref_batch_item* items, 
     });
 }
 
+// The engine's bcc_taproot_check items (include/bcc_amd.h), restated field by field: the bulk
+// checker / CPU baseline of the Taproot bench (CheckSchnorrSignature per item).
+struct ref_taproot_item {
+    const unsigned char* tx;
+    unsigned int tx_len;
+    const unsigned char* spent;
+    unsigned int spent_len;
+    unsigned int n_in;
+    const unsigned char* sig;
+    unsigned int sig_len;
+    const unsigned char* pk32;
+    int sigversion;
+    const unsigned char* annex;
+    unsigned int annex_len;
+    const unsigned char* tapleaf32;
+    uint32_t codesep_pos;
+};
+
+double ref_bulk_taproot(int nthreads, long n, const ref_taproot_item* items, int* ret, int* serr) {
+    static const unsigned char zero32[32] = {0};
+    return run_pool(nthreads, n, [=](long i) {
+        const ref_taproot_item& it = items[i];
+        unsigned char h[32];
+        int hashed = 0;
+        ret[i] = ref_taproot_check(it.tx, it.tx_len, it.spent, it.spent_len, it.n_in, it.sig,
+                                   it.sig_len, it.pk32, it.sigversion, it.annex, it.annex_len,
+                                   it.tapleaf32 ? it.tapleaf32 : zero32, it.codesep_pos, &serr[i],
+                                   h, &hashed);
+    });
+}
+
 // Tuple-level baseline: CPubKey::Verify over (pub, hash, sig) tuples. pub in 65-B slots with
 // lengths, sig in 80-B slots with lengths.
 double ref_bench_pubkey_verify(int nthreads, long n, const unsigned char* pub65, const int* publen,

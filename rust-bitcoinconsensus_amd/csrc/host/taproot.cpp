@@ -103,6 +103,18 @@ uint32_t tx_aux(TxState& s, TaprootJobs& J, int kind, std::vector<uint8_t>& scra
 void build_part(const bcc_taproot_check* items, size_t lo, size_t hi, int* ret, int* serr,
                 Part& P) {
     TaprootJobs& J = P.jobs;
+    const size_t cnt = hi - lo;  // capacity for the common shape (a key path spend of its own tx)
+    J.aux.reserve(cnt * 5 * 64);
+    J.aux_off.reserve(cnt * 5);
+    J.aux_nblk.reserve(cnt * 5);
+    J.msg.reserve(cnt * 192);
+    J.msg_off.reserve(cnt);
+    J.msg_nblk.reserve(cnt);
+    J.msg_row.reserve(cnt);
+    J.patches.reserve(cnt * 5);
+    J.sig64.reserve(cnt * 64);
+    J.pk32.reserve(cnt * 32);
+    P.item_of_row.reserve(cnt);
     TxState s;
     std::vector<uint8_t> m, scratch;
     m.reserve(512);
@@ -198,33 +210,6 @@ void build_part(const bcc_taproot_check* items, size_t lo, size_t hi, int* ret, 
     }
 }
 
-// Concatenation of the parts (message / aux / row indices fixed up per part).
-void merge_parts(std::vector<Part>& parts, TaprootJobs& J, std::vector<uint32_t>& item_of_row) {
-    if (parts.size() == 1) {
-        J = std::move(parts[0].jobs);
-        item_of_row = std::move(parts[0].item_of_row);
-        return;
-    }
-    for (Part& p : parts) {
-        const TaprootJobs& q = p.jobs;
-        const uint32_t ablk = (uint32_t)(J.aux.size() / 64), mblk = (uint32_t)(J.msg.size() / 64);
-        const uint32_t aux0 = (uint32_t)J.aux_off.size(), row0 = (uint32_t)J.rows();
-        J.aux.insert(J.aux.end(), q.aux.begin(), q.aux.end());
-        J.msg.insert(J.msg.end(), q.msg.begin(), q.msg.end());
-        for (uint32_t v : q.aux_off) J.aux_off.push_back(v + ablk);
-        J.aux_nblk.insert(J.aux_nblk.end(), q.aux_nblk.begin(), q.aux_nblk.end());
-        for (uint32_t v : q.msg_off) J.msg_off.push_back(v + mblk);
-        J.msg_nblk.insert(J.msg_nblk.end(), q.msg_nblk.begin(), q.msg_nblk.end());
-        for (uint32_t v : q.msg_row) J.msg_row.push_back(v + row0);
-        for (const PatchRec& r : q.patches)
-            J.patches.push_back(PatchRec{r.pre_byte + mblk * 64, r.aux + aux0});
-        J.sig64.insert(J.sig64.end(), q.sig64.begin(), q.sig64.end());
-        J.pk32.insert(J.pk32.end(), q.pk32.begin(), q.pk32.end());
-        item_of_row.insert(item_of_row.end(), p.item_of_row.begin(), p.item_of_row.end());
-        p = Part();
-    }
-}
-
 // Items [lo, hi) on `device`: host parts in parallel, one GPU round, verdicts scattered back.
 // A round whose message blobs would not fit the kernels' 32-bit offsets is split in two.
 int run_range(const bcc_taproot_check* items, size_t lo, size_t hi, int* ret, int* serr,
@@ -257,15 +242,19 @@ int run_range(const bcc_taproot_check* items, size_t lo, size_t hi, int* ret, in
         if (int e = run_range(items, lo, mid, ret, serr, sighash_out, device)) return e;
         return run_range(items, mid, hi, ret, serr, sighash_out, device);
     }
-    TaprootJobs J;
+    std::vector<const TaprootJobs*> pj;
     std::vector<uint32_t> item_of_row;
-    merge_parts(parts, J, item_of_row);
-    const size_t n = J.rows();
+    for (const Part& q : parts) {
+        pj.push_back(&q.jobs);
+        item_of_row.insert(item_of_row.end(), q.item_of_row.begin(), q.item_of_row.end());
+    }
+    const size_t n = item_of_row.size();
     if (sighash_out)
         for (size_t i = lo; i < hi; i++) memset(sighash_out + 32 * i, 0, 32);
     if (n == 0) return 0;
     std::vector<uint8_t> verdict(n), msg(sighash_out ? 32 * n : 0);
-    if (int e = gpu_taproot_verify(device, J, verdict.data(), sighash_out ? msg.data() : nullptr))
+    if (int e = gpu_taproot_verify_parts(device, pj.data(), pj.size(), verdict.data(),
+                                         sighash_out ? msg.data() : nullptr))
         return e;
     for (size_t r = 0; r < n; r++) {
         const uint32_t i = item_of_row[r];

@@ -185,6 +185,9 @@ void tapsighash_midstate(uint32_t out[8]);
 // Stage + run + fetch on `device` (synchronous): BIP341 sighashes (msg32_out, optional, 32 bytes
 // per row) and BIP340 verdicts (1 valid).
 int gpu_taproot_verify(int device, const TaprootJobs& jobs, uint8_t* verdict, uint8_t* msg32_out);
+// The same over the concatenation of P parts (rows in part order).
+int gpu_taproot_verify_parts(int device, const TaprootJobs* const* parts, size_t P,
+                             uint8_t* verdict, uint8_t* msg32_out);
 
 // Device scratch of the signature kernels: s^-1 rows (ECDSA) and, for one chunk of lanes, the
 // Q tables + ladder states.  Every synchronous entry point owns one per (thread, device), so

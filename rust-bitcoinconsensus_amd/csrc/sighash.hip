@@ -1000,10 +1000,28 @@ struct TaprootCtx {
 }  // namespace
 
 int gpu_taproot_verify(int device, const TaprootJobs& J, uint8_t* verdict, uint8_t* msg32_out) {
-    const size_t n = J.rows();
+    const TaprootJobs* p = &J;
+    return gpu_taproot_verify_parts(device, &p, 1, verdict, msg32_out);
+}
+
+// The parts (one per host thread) are concatenated straight into the pinned image, each part by
+// its own thread with its index fix-ups (no merged host copy), then go to HBM in one DMA copy.
+int gpu_taproot_verify_parts(int device, const TaprootJobs* const* Jp, size_t P, uint8_t* verdict,
+                             uint8_t* msg32_out) {
+    std::vector<size_t> row0(P + 1, 0), aux0(P + 1, 0), msg0(P + 1, 0), auxi0(P + 1, 0),
+        msgi0(P + 1, 0), pat0(P + 1, 0);
+    for (size_t q = 0; q < P; q++) {
+        row0[q + 1] = row0[q] + Jp[q]->rows();
+        aux0[q + 1] = aux0[q] + Jp[q]->aux.size();
+        msg0[q + 1] = msg0[q] + Jp[q]->msg.size();
+        auxi0[q + 1] = auxi0[q] + Jp[q]->aux_off.size();
+        msgi0[q + 1] = msgi0[q] + Jp[q]->msg_off.size();
+        pat0[q + 1] = pat0[q] + Jp[q]->patches.size();
+    }
+    const size_t n = row0[P];
     if (n == 0) return 0;
     if (device < 0 || device >= 64) return (int)hipErrorInvalidDevice;
-    if (J.aux.size() >= ((size_t)1 << 32) || J.msg.size() >= ((size_t)1 << 32)) {
+    if (aux0[P] >= ((size_t)1 << 32) || msg0[P] >= ((size_t)1 << 32)) {
         fprintf(stderr, "[bcc] gpu_taproot_verify: a message blob exceeds 4 GiB; split the batch\n");
         return (int)hipErrorInvalidValue;
     }
@@ -1017,12 +1035,11 @@ int gpu_taproot_verify(int device, const TaprootJobs& J, uint8_t* verdict, uint8
     }
     TaprootCtx& c = *ctxs[device];
     BCC_HIP_TRY(hipSetDevice(device));
-    const size_t naux = J.aux_off.size(), nmsg = J.msg_off.size(), npat = J.patches.size();
+    const size_t naux = auxi0[P], nmsg = msgi0[P], npat = pat0[P];
     // layout: sig64 | pk32 | msg32 | verdict | aux | msg | aux_off | aux_nblk | msg_off |
     //         msg_nblk | msg_row | patches | aux digests (not uploaded)
-    size_t sizes[] = {64 * n,       32 * n,       32 * n,       n,
-                      J.aux.size(), J.msg.size(), 4 * naux,     4 * naux,
-                      4 * nmsg,     4 * nmsg,     4 * nmsg,     sizeof(PatchRec) * npat,
+    size_t sizes[] = {64 * n,  32 * n,   32 * n,   n,        aux0[P],  msg0[P], 4 * naux,
+                      4 * naux, 4 * nmsg, 4 * nmsg, 4 * nmsg, sizeof(PatchRec) * npat,
                       32 * naux};
     const int NB = sizeof(sizes) / sizeof(sizes[0]);
     size_t off[NB], total = 0;
@@ -1046,20 +1063,40 @@ int gpu_taproot_verify(int device, const TaprootJobs& J, uint8_t* verdict, uint8
         c.image_cap = upload;
     }
     uint8_t* h = (uint8_t*)c.image;
-    auto cp = [&](int b, const void* src, size_t len) {
-        if (len) memcpy(h + off[b], src, len);
-    };
-    cp(0, J.sig64.data(), 64 * n);
-    cp(1, J.pk32.data(), 32 * n);
     memset(h + off[2], 0, 32 * n);
-    cp(4, J.aux.data(), J.aux.size());
-    cp(5, J.msg.data(), J.msg.size());
-    cp(6, J.aux_off.data(), 4 * naux);
-    cp(7, J.aux_nblk.data(), 4 * naux);
-    cp(8, J.msg_off.data(), 4 * nmsg);
-    cp(9, J.msg_nblk.data(), 4 * nmsg);
-    cp(10, J.msg_row.data(), 4 * nmsg);
-    cp(11, J.patches.data(), sizeof(PatchRec) * npat);
+    auto fill = [&](size_t q) {
+        const TaprootJobs& J = *Jp[q];
+        const size_t r0 = row0[q], nr = J.rows();
+        auto cp = [&](int b, size_t at, const void* src, size_t len) {
+            if (len) memcpy(h + off[b] + at, src, len);
+        };
+        cp(0, 64 * r0, J.sig64.data(), 64 * nr);
+        cp(1, 32 * r0, J.pk32.data(), 32 * nr);
+        cp(4, aux0[q], J.aux.data(), J.aux.size());
+        cp(5, msg0[q], J.msg.data(), J.msg.size());
+        const uint32_t ablk = (uint32_t)(aux0[q] / 64), mblk = (uint32_t)(msg0[q] / 64);
+        uint32_t* ao = (uint32_t*)(h + off[6]) + auxi0[q];
+        for (size_t k = 0; k < J.aux_off.size(); k++) ao[k] = J.aux_off[k] + ablk;
+        cp(7, 4 * auxi0[q], J.aux_nblk.data(), 4 * J.aux_nblk.size());
+        uint32_t* mo = (uint32_t*)(h + off[8]) + msgi0[q];
+        uint32_t* mr = (uint32_t*)(h + off[10]) + msgi0[q];
+        for (size_t k = 0; k < J.msg_off.size(); k++) {
+            mo[k] = J.msg_off[k] + mblk;
+            mr[k] = J.msg_row[k] + (uint32_t)r0;
+        }
+        cp(9, 4 * msgi0[q], J.msg_nblk.data(), 4 * J.msg_nblk.size());
+        PatchRec* pt = (PatchRec*)(h + off[11]) + pat0[q];
+        for (size_t k = 0; k < J.patches.size(); k++)
+            pt[k] = PatchRec{J.patches[k].pre_byte + mblk * 64, J.patches[k].aux + (uint32_t)auxi0[q]};
+    };
+    if (P == 1) {
+        fill(0);
+    } else {
+        std::vector<std::thread> th;
+        for (size_t q = 1; q < P; q++) th.emplace_back(fill, q);
+        fill(0);
+        for (auto& x : th) x.join();
+    }
     uint8_t* a = (uint8_t*)c.arena;
     hipStream_t st = c.stream;
     ShaMid mid;

@@ -80,6 +80,17 @@ int gpu_verify_batch(int, const SighashJobs& j, const TupleRows& rows, uint8_t* 
 
 // BIP341 jobs (host/taproot.cpp): aux messages single SHA-256, patch, TapSighash over the
 // tag prefix + the message (the length field of a message counts the 64-byte tag block), BIP340.
+int gpu_taproot_verify(int, const TaprootJobs& j, uint8_t* verdict, uint8_t* msg32_out);
+int gpu_taproot_verify_parts(int dev, const TaprootJobs* const* parts, size_t P, uint8_t* verdict,
+                             uint8_t* msg32_out) {
+    size_t r0 = 0;
+    for (size_t q = 0; q < P; q++) {
+        gpu_taproot_verify(dev, *parts[q], verdict + r0, msg32_out ? msg32_out + 32 * r0 : nullptr);
+        r0 += parts[q]->rows();
+    }
+    return 0;
+}
+
 int gpu_taproot_verify(int, const TaprootJobs& j, uint8_t* verdict, uint8_t* msg32_out) {
     std::vector<uint8_t> auxd(32 * j.aux_off.size());
     for (size_t a = 0; a < j.aux_off.size(); a++) {
