@@ -52,6 +52,10 @@ METRIC = "ECDSA verifies/sec (node) at 1/2/4/8 MI355X; % of int-ALU roofline"
 DEFAULT_N = {"c2": 1_000_000, "c3": 4000, "c4": 8_000_000, "c5": 16_000_000, "c5t": 1_000_000}
 SEEDS = {"c2": 0x5EED0001, "c3": 0x5EED0003, "c4": 0x5EED0004, "c5": 0x5EED0005,
          "c5t": 0x5EED0006}
+# the ECDSA stage's kernels: the square-root-free path (default) or the round-1 path
+ECDSA_KERNELS = ("ecdsa (batch_sinv + ecdsa_key + ecdsa_prep + ecdsa_ladder)"
+                 if os.environ.get("BCC_ECDSA_PATH") == "legacy" else
+                 "ecdsa (batch_sinv + ecdsa_tprep + ecdsa_tladder + ecdsa_tfin; no key square root)")
 CPU_PASSES = 3                    # timed passes of the CPU baseline (median), after 1 warm-up
 
 
@@ -284,7 +288,7 @@ class C2:
 
     data = "synthetic (deterministic P2WPKH spends, GPU-generated keys/signatures)"
     mads = MADS_PER_VERIFY
-    kernel = "ecdsa (batch_sinv + ecdsa_key + ecdsa_prep + ecdsa_ladder)"
+    kernel = ECDSA_KERNELS
 
 
 class C3(C2):
@@ -360,7 +364,7 @@ class TupleJob:
         self.units = self.n = n
         self.unit = "verifies/s"
         self.mads = MADS_PER_VERIFY if kind == "c4" else MADS_PER_SCHNORR
-        self.kernel = ("ecdsa (batch_sinv + ecdsa_key + ecdsa_prep + ecdsa_ladder)" if kind == "c4"
+        self.kernel = (ECDSA_KERNELS if kind == "c4"
                        else "schnorr (prep + ladder + y-parity batch inversion)")
 
     def step(self, sp):
@@ -703,7 +707,7 @@ def main():
         if traffic is None and os.path.exists(tf):
             tj = json.load(open(tf))
             t = tj.get(f"{args.config}@{sig_units}") or tj.get(args.config)
-            if t and t.get("units") == sig_units:
+            if t and t.get("units") == sig_units and t.get("kernel") == job.kernel:
                 traffic, tsrc = t["traffic_bytes"], t["source"]
         roof = dict(bound="int-alu", kernel=job.kernel,
                     achieved=achieved / 1e12, peak=peak / 1e12, unit="T(v_mad_u64_u32)/s",

@@ -24,8 +24,10 @@
 #include <atomic>
 #include <cstdlib>
 #include <memory>
+#include <string>
 
 #include "ecdsa_lane.h"
+#include "ecdsa_twist.h"
 #include "gpu_common.h"
 #include "pipeline.h"
 
@@ -426,11 +428,253 @@ __global__ __launch_bounds__(256) void schnorr_parity_kernel(u32* __restrict__ q
 }
 
 // ------------------------------------------------------------------------------------------
+// ECDSA, square-root-free path (ecdsa_twist.h): K_tprep -> K_tladder -> K_tfin.  The key is never
+// decompressed (no K_key); A = u1 G comes from the comb tables in HBM, B = u2 Q_w from the
+// lane's Q table; K_tfin inverts every lane's beta by Montgomery's trick and decides.
+// Per-lane state words (wave blocks, TSTATE_WORDS per lane):
+// ------------------------------------------------------------------------------------------
+enum : int {
+    T_K = 0,       // 16 scalar words: k1, k2, u1
+    T_FLAGS = 16,
+    T_SIGMA = 17,  // 8
+    T_R = 25,      // 8
+    T_V = 33,      // 8: x^3 + 7
+    T_Y = 41,      // 8: y of an uncompressed key
+    T_STAT = 49,   // TW_REJECT / TW_NORMAL / TW_EXCEPT (written by the ladder)
+    T_AL = 50,     // 8: alpha
+    T_BE = 58,     // 8: beta
+    T_KK = 66,     // 8: K = Z3^2
+    T_PRE = 74,    // 8: K_tfin's prefix product
+    TSTATE_WORDS = 82,
+};
+
+__device__ __forceinline__ void tw_store(u32* w, int at, const u32 (&v)[8]) {
+#pragma unroll
+    for (int j = 0; j < 8; j++) w[(at + j) * LANE_STRIDE] = v[j];
+}
+__device__ __forceinline__ void tw_load(u32 (&v)[8], const u32* w, int at) {
+#pragma unroll
+    for (int j = 0; j < 8; j++) v[j] = w[(at + j) * LANE_STRIDE];
+}
+
+// The ladder's view of the twist state: flags and sigma in registers, the scalar words, r, v
+// and y loaded at their use (address hidden from LICM as in LadderStateView).
+struct TwistStateView {
+    const u32* p;
+    u32 flags;
+    fe sigma;
+    __device__ __forceinline__ u32 kword(int s, int w) const {
+        const u32* q = p;
+        asm volatile("" : "+v"(q));
+        const __attribute__((address_space(1))) u32* g = (const __attribute__((address_space(1))) u32*)q;
+        return g[(size_t)(T_K + s * 4 + w) * LANE_STRIDE];
+    }
+    __device__ __forceinline__ void get_r(sc& o) const { tw_load(o.v, p, T_R); }
+    __device__ __forceinline__ void get_v(fe& o) const { tw_load(o.v, p, T_V); }
+    __device__ __forceinline__ void get_y(fe& o) const { tw_load(o.v, p, T_Y); }
+};
+
+// comb tables in HBM: entry (win, i) = 16 words x || y, read as four 16-byte loads
+struct GCombGlobal {
+    const u32* base;
+    __device__ void get(int win, int i, fe& x, fe& y) const {
+        const uint4* q = reinterpret_cast<const uint4*>(base + ((size_t)win * CTAB + i) * 16);
+        const uint4 a = q[0], b = q[1], c = q[2], d = q[3];
+        x.v[0] = a.x; x.v[1] = a.y; x.v[2] = a.z; x.v[3] = a.w;
+        x.v[4] = b.x; x.v[5] = b.y; x.v[6] = b.z; x.v[7] = b.w;
+        y.v[0] = c.x; y.v[1] = c.y; y.v[2] = c.z; y.v[3] = c.w;
+        y.v[4] = d.x; y.v[5] = d.y; y.v[6] = d.z; y.v[7] = d.w;
+    }
+};
+
+// a lane's parked Jacobian point in its own (dead after the Q loop) table words: 24 words + inf
+__device__ __forceinline__ void park_gej(u32* q, const gej& a, bool inf) {
+    uint4* p = reinterpret_cast<uint4*>(q);
+    p[0] = make_uint4(a.x.v[0], a.x.v[1], a.x.v[2], a.x.v[3]);
+    p[1] = make_uint4(a.x.v[4], a.x.v[5], a.x.v[6], a.x.v[7]);
+    p[2] = make_uint4(a.y.v[0], a.y.v[1], a.y.v[2], a.y.v[3]);
+    p[3] = make_uint4(a.y.v[4], a.y.v[5], a.y.v[6], a.y.v[7]);
+    p[4] = make_uint4(a.z.v[0], a.z.v[1], a.z.v[2], a.z.v[3]);
+    p[5] = make_uint4(a.z.v[4], a.z.v[5], a.z.v[6], a.z.v[7]);
+    p[6] = make_uint4(inf ? 1u : 0u, 0u, 0u, 0u);
+}
+__device__ __forceinline__ bool unpark_gej(const u32* q, gej& a) {
+    asm volatile("" : "+v"(q));  // a real reload: the point must not stay live in registers
+    const uint4* p = reinterpret_cast<const uint4*>(q);
+    uint4 u;
+    u = p[0]; a.x.v[0] = u.x; a.x.v[1] = u.y; a.x.v[2] = u.z; a.x.v[3] = u.w;
+    u = p[1]; a.x.v[4] = u.x; a.x.v[5] = u.y; a.x.v[6] = u.z; a.x.v[7] = u.w;
+    u = p[2]; a.y.v[0] = u.x; a.y.v[1] = u.y; a.y.v[2] = u.z; a.y.v[3] = u.w;
+    u = p[3]; a.y.v[4] = u.x; a.y.v[5] = u.y; a.y.v[6] = u.z; a.y.v[7] = u.w;
+    u = p[4]; a.z.v[0] = u.x; a.z.v[1] = u.y; a.z.v[2] = u.z; a.z.v[3] = u.w;
+    u = p[5]; a.z.v[4] = u.x; a.z.v[5] = u.y; a.z.v[6] = u.z; a.z.v[7] = u.w;
+    return p[6].x != 0;
+}
+constexpr int PARK_B = 0, PARK_A = 32;  // word offsets in the lane's table
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void ecdsa_tprep_kernel(
+    const uint8_t* __restrict__ tag, const uint8_t* __restrict__ px,
+    const uint8_t* __restrict__ py, const uint8_t* __restrict__ pr, const uint8_t* __restrict__ ps,
+    const uint8_t* __restrict__ pm, const u32* __restrict__ psinv, size_t base, size_t cnt,
+    u32* __restrict__ qtab, u32* __restrict__ state) {
+    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= cnt) return;
+    const size_t i = base + t;
+    fe x, y;
+    sc r, s, m, si;
+    load_be32(x, px + 32 * i);
+    load_be32(y, py + 32 * i);
+    load_be32(r, pr + 32 * i);
+    load_be32(s, ps + 32 * i);
+    load_be32(m, pm + 32 * i);
+    load_limbs(si, psinv + 8 * i);
+    QTableGlobal qt{lane_table(qtab, t)};
+    TwistState st;
+    twist_prep_lane(tag[i], x, y, r, s, m, &si, qt, st);
+    u32* w = lane_words(state, t, TSTATE_WORDS);
+#pragma unroll
+    for (int a = 0; a < 4; a++)
+#pragma unroll
+        for (int b = 0; b < 4; b++) w[(T_K + a * 4 + b) * LANE_STRIDE] = st.k[a][b];
+    w[T_FLAGS * LANE_STRIDE] = st.flags;
+    tw_store(w, T_SIGMA, st.sigma.v);
+    tw_store(w, T_R, st.r.v);
+    tw_store(w, T_V, st.v.v);
+    tw_store(w, T_Y, st.ychk.v);
+}
+
+// Ladder workgroups of 256 lanes: no LDS (the comb tables are read from HBM / L2), so the only
+// occupancy limit is the register file (4 waves per SIMD at <= 128 VGPRs).
+#ifndef BCC_TLADDER_WG
+#define BCC_TLADDER_WG 256
+#endif
+constexpr int TLADDER_WG = BCC_TLADDER_WG;
+
+__global__ __launch_bounds__(TLADDER_WG) __attribute__((amdgpu_waves_per_eu(BCC_LADDER_WAVES, BCC_LADDER_WAVES))) void ecdsa_tladder_kernel(
+    u32* __restrict__ state, u32* __restrict__ qtab, const u32* __restrict__ gcomb, size_t cnt) {
+    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= cnt) return;
+    u32* w = lane_words(state, t, TSTATE_WORDS);
+    TwistStateView st;
+    st.p = w;
+    st.flags = w[T_FLAGS * LANE_STRIDE];
+    if (!(st.flags & LS_VALID)) {
+        w[T_STAT * LANE_STRIDE] = TW_REJECT;
+        return;
+    }
+    tw_load(st.sigma.v, w, T_SIGMA);
+    u32* lt = lane_table(qtab, t);
+    QTableGlobal qt{lt};
+    GCombGlobal gc{gcomb};
+    u32 stat = TW_NORMAL;
+    {
+        gej B;
+        const bool binf = twist_accumulate_q(st, qt, B);
+        park_gej(lt + PARK_B, B, binf);
+    }
+    gej A, B;
+    const bool ainf = twist_accumulate_g(st, gc, A);
+    const bool binf = unpark_gej(lt + PARK_B, B);
+    fe v, al, be, K;
+    sc r;
+    st.get_v(v);
+    st.get_r(r);  // loaded here, used last by twist_combine
+    if (binf || ainf || !twist_combine(A, B, st.sigma, v, r, al, be, K)) {
+        park_gej(lt + PARK_A, A, ainf);
+        stat = TW_EXCEPT;
+    } else {
+        tw_store(w, T_AL, al.v);
+        tw_store(w, T_BE, be.v);
+        tw_store(w, T_KK, K.v);
+    }
+    w[T_STAT * LANE_STRIDE] = stat;
+}
+
+// beta^-1 for every normal lane of a chunk by Montgomery's trick over the strided sub-chunk
+// {t, t+T, ...} (3 mults per lane + one Fermat inversion per thread), then the verdicts; the
+// exceptional lanes (adversarial only) run the exact fallback here, divergently.
+__global__ __launch_bounds__(256) void ecdsa_tfin_kernel(u32* __restrict__ state,
+                                                         const u32* __restrict__ qtab,
+                                                         uint8_t* __restrict__ verdict,
+                                                         size_t base, size_t cnt, size_t T) {
+    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= cnt || t >= T) return;
+    fe acc = fe_one();
+    size_t last = t;
+    for (size_t i = t; i < cnt; i += T) {
+        u32* w = lane_words(state, i, TSTATE_WORDS);
+        tw_store(w, T_PRE, acc.v);  // product of the betas before i
+        if (w[T_STAT * LANE_STRIDE] == TW_NORMAL) {
+            fe b;
+            tw_load(b.v, w, T_BE);
+            fe_mul(acc, acc, b);
+        }
+        last = i;
+    }
+    fe inv;
+    fe_inv(inv, acc);
+    for (size_t i = last + T; i > t;) {
+        i -= T;
+        const u32* w = lane_words(state, i, TSTATE_WORDS);
+        const u32 stat = w[T_STAT * LANE_STRIDE];
+        int ok = 0;
+        if (stat != TW_REJECT) {
+            const u32 flags = w[T_FLAGS * LANE_STRIDE];
+            fe v, y;
+            sc r;
+            tw_load(v.v, w, T_V);
+            tw_load(y.v, w, T_Y);
+            tw_load(r.v, w, T_R);
+            if (stat == TW_NORMAL) {
+                fe pre, b, binv, al, K;
+                tw_load(pre.v, w, T_PRE);
+                tw_load(b.v, w, T_BE);
+                fe_mul(binv, inv, pre);  // beta_i^-1
+                fe_mul(inv, inv, b);     // (beta_t ... beta_{i-1})^-1
+                tw_load(al.v, w, T_AL);
+                tw_load(K.v, w, T_KK);
+                ok = twist_final(al, K, binv, v, y, flags, r);
+            } else {
+                const u32* lt = lane_table(const_cast<u32*>(qtab), i);
+                gej A, B;
+                fe sigma;
+                const bool ainf = unpark_gej(lt + PARK_A, A);
+                const bool binf = unpark_gej(lt + PARK_B, B);
+                tw_load(sigma.v, w, T_SIGMA);
+                ok = twist_exceptional(A, ainf, B, binf, sigma, v, y, flags, r);
+            }
+        }
+        verdict[base + i] = (uint8_t)ok;
+    }
+}
+
+// ------------------------------------------------------------------------------------------
 // G tables (one read-only copy per device) and caller-owned scratch
 // ------------------------------------------------------------------------------------------
 static std::mutex g_gtab_mu;
 static fe* g_gtab[64];
+static u32* g_gcomb[64];
 static int g_cus[64];
+
+static const std::vector<fe>& host_gcomb() {
+    static std::vector<fe> t;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        t.resize((size_t)CWIN * CTAB * 2);
+        build_g_comb(t.data());
+    });
+    return t;
+}
+
+// ECDSA path: the square-root-free twist path (default) or the round-1 path with K_key
+// (BCC_ECDSA_PATH=legacy), for A/B runs on one build.
+static bool ecdsa_twist() {
+    static const bool on = [] {
+        const char* e = getenv("BCC_ECDSA_PATH");
+        return !(e && std::string(e) == "legacy");
+    }();
+    return on;
+}
 
 static const std::vector<fe>& host_gtab() {
     static std::vector<fe> t;
@@ -468,6 +712,11 @@ static int device_tables(int* dev, fe** gtab, int* cus) {
         BCC_HIP_TRY(hipMalloc(&d, h.size() * sizeof(fe)));
         BCC_HIP_TRY(hipMemcpy(d, h.data(), h.size() * sizeof(fe), hipMemcpyHostToDevice));
         BCC_HIP_TRY(hipDeviceGetAttribute(&g_cus[*dev], hipDeviceAttributeMultiprocessorCount, *dev));
+        const auto& hc = host_gcomb();
+        fe* dc = nullptr;
+        BCC_HIP_TRY(hipMalloc(&dc, hc.size() * sizeof(fe)));
+        BCC_HIP_TRY(hipMemcpy(dc, hc.data(), hc.size() * sizeof(fe), hipMemcpyHostToDevice));
+        g_gcomb[*dev] = reinterpret_cast<u32*>(dc);
         g_gtab[*dev] = d;
     }
     *gtab = g_gtab[*dev];
@@ -496,7 +745,7 @@ static int ensure_scratch(SigScratch& sc, int dev, size_t n, bool with_sinv, siz
         if (sc.chunk) BCC_HIP_TRY(hipFree(sc.chunk));
         sc.chunk = nullptr;
         sc.chunk_cap = 0;
-        BCC_HIP_TRY(hipMalloc(&sc.chunk, want * (QTABLE_WORDS + STATE_WORDS) * sizeof(u32)));
+        BCC_HIP_TRY(hipMalloc(&sc.chunk, want * (QTABLE_WORDS + TSTATE_WORDS) * sizeof(u32)));
         sc.chunk_cap = want;
     }
     if (with_sinv && n > sc.sinv_cap) {
@@ -526,6 +775,7 @@ int ecdsa_launch_pre(SigScratch& sc, const uint8_t* d_tag, const uint8_t* d_x,
     hipLaunchKernelGGL(batch_sinv_kernel, dim3((unsigned)((T + 255) / 256)), dim3(256), 0,
                        (hipStream_t)stream, d_s, sinv, n, T);
     BCC_HIP_TRY(hipGetLastError());
+    if (ecdsa_twist()) return 0;  // no key decompression on the twist path
     hipLaunchKernelGGL(ecdsa_key_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
                        (hipStream_t)stream, d_tag, d_x, d_y, n, sinv + 8 * sc.sinv_cap,
                        sinv + 16 * sc.sinv_cap);
@@ -537,12 +787,12 @@ int ecdsa_launch(SigScratch& sc, const uint8_t* d_tag, const uint8_t* d_x, const
                  const uint8_t* d_r, const uint8_t* d_s, const uint8_t* d_m, uint8_t* d_verdict,
                  size_t n, void* stream) {
     if (int e = ecdsa_launch_pre(sc, d_tag, d_x, d_y, d_s, n, stream)) return e;
-    return ecdsa_launch_after_pre(sc, d_x, d_r, d_s, d_m, d_verdict, n, stream);
+    return ecdsa_launch_after_pre(sc, d_tag, d_x, d_y, d_r, d_s, d_m, d_verdict, n, stream);
 }
 
-int ecdsa_launch_after_pre(SigScratch& sc, const uint8_t* d_x, const uint8_t* d_r,
-                           const uint8_t* d_s, const uint8_t* d_m, uint8_t* d_verdict, size_t n,
-                           void* stream) {
+int ecdsa_launch_after_pre(SigScratch& sc, const uint8_t* d_tag, const uint8_t* d_x,
+                           const uint8_t* d_y, const uint8_t* d_r, const uint8_t* d_s,
+                           const uint8_t* d_m, uint8_t* d_verdict, size_t n, void* stream) {
     if (n == 0) return 0;
     int dev = 0, cus = 0;
     fe* gtab = nullptr;
@@ -551,6 +801,27 @@ int ecdsa_launch_after_pre(SigScratch& sc, const uint8_t* d_x, const uint8_t* d_
     if (int e = ensure_scratch(sc, dev, n, true, &C)) return e;  // sized by ecdsa_launch_pre
     hipStream_t sm = (hipStream_t)stream;
     u32* sinv = (u32*)sc.sinv;
+    if (ecdsa_twist()) {
+        u32* qtab = (u32*)sc.chunk;
+        u32* state = qtab + C * QTABLE_WORDS;
+        const u32* gcomb = g_gcomb[dev];
+        for (size_t base = 0; base < n; base += C) {
+            const size_t cnt = std::min(C, n - base);
+            hipLaunchKernelGGL(ecdsa_tprep_kernel, dim3((unsigned)((cnt + 255) / 256)), dim3(256),
+                               0, sm, d_tag, d_x, d_y, d_r, d_s, d_m, sinv, base, cnt, qtab, state);
+            BCC_HIP_TRY(hipGetLastError());
+            hipLaunchKernelGGL(ecdsa_tladder_kernel,
+                               dim3((unsigned)((cnt + TLADDER_WG - 1) / TLADDER_WG)),
+                               dim3(TLADDER_WG), 0, sm, state, qtab, gcomb, cnt);
+            BCC_HIP_TRY(hipGetLastError());
+            // the batched beta inversion: sub-chunks of <= 16 lanes, at least one wave per SIMD
+            const size_t T = std::max<size_t>((cnt + 15) / 16, std::min<size_t>(cnt, (size_t)cus * 256));
+            hipLaunchKernelGGL(ecdsa_tfin_kernel, dim3((unsigned)((T + 255) / 256)), dim3(256), 0,
+                               sm, state, qtab, d_verdict, base, cnt, T);
+            BCC_HIP_TRY(hipGetLastError());
+        }
+        return 0;
+    }
     const u32* keyy = sinv + 8 * sc.sinv_cap;
     const u32* kok = sinv + 16 * sc.sinv_cap;
     u32* qtab = (u32*)sc.chunk;

@@ -215,9 +215,9 @@ int ecdsa_launch(SigScratch& sc, const uint8_t* d_tag, const uint8_t* d_x, const
 // after them (must be ordered after both, and after the sighash kernels that write m).
 int ecdsa_launch_pre(SigScratch& sc, const uint8_t* d_tag, const uint8_t* d_x,
                      const uint8_t* d_y, const uint8_t* d_s, size_t n, void* stream);
-int ecdsa_launch_after_pre(SigScratch& sc, const uint8_t* d_x, const uint8_t* d_r,
-                           const uint8_t* d_s, const uint8_t* d_m, uint8_t* d_verdict, size_t n,
-                           void* stream);
+int ecdsa_launch_after_pre(SigScratch& sc, const uint8_t* d_tag, const uint8_t* d_x,
+                           const uint8_t* d_y, const uint8_t* d_r, const uint8_t* d_s,
+                           const uint8_t* d_m, uint8_t* d_verdict, size_t n, void* stream);
 int schnorr_launch(SigScratch& sc, const uint8_t* d_sig64, const uint8_t* d_msg32,
                    const uint8_t* d_xonly32, uint8_t* d_verdict, size_t n, void* stream);
 

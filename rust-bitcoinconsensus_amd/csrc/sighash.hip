@@ -906,7 +906,7 @@ int DeviceBatch::run(void* stream) {
     BCC_HIP_TRY(hipEventRecord((hipEvent_t)ev_join_, side));
     if (int e = launch_sighash(st, ev_wtx_)) return e;
     BCC_HIP_TRY(hipStreamWaitEvent(st, (hipEvent_t)ev_join_, 0));
-    return ecdsa_launch_after_pre(scratch_, d_x, d_r, d_s, d_m, d_v, n_rows_, st);
+    return ecdsa_launch_after_pre(scratch_, d_tag, d_x, d_y, d_r, d_s, d_m, d_v, n_rows_, st);
 }
 
 // Verdicts come back through a pinned buffer of the batch (an asynchronous copy on the run's stream,

@@ -2,6 +2,7 @@
 // (rust-bitcoinconsensus_amd/csrc/ecdsa_lane.h) on the CPU, so the exact arithmetic the HIP kernel
 // executes can be checked against the oracle without a GPU. Never linked into the product.
 #include "../../rust-bitcoinconsensus_amd/csrc/ecdsa_lane.h"
+#include "../../rust-bitcoinconsensus_amd/csrc/ecdsa_twist.h"
 
 #include <cstring>
 #include <vector>
@@ -34,6 +35,34 @@ extern "C" int lane_verify(unsigned tag, const unsigned char* x32, const unsigne
     QTableArray qt;
     GTableArray gt{gtab().data()};
     return ecdsa_verify_lane(tag, px, py, r, s, m, qt, gt);
+}
+
+static std::vector<fe>& gcomb() {
+    static std::vector<fe> t;
+    if (t.empty()) {
+        t.resize((size_t)CWIN * CTAB * 2);
+        build_g_comb(t.data());
+    }
+    return t;
+}
+
+// the square-root-free ECDSA path (ecdsa_twist.h), same arguments as lane_verify
+extern "C" int lane_verify_twist(unsigned tag, const unsigned char* x32, const unsigned char* y32,
+                                 const unsigned char* r32, const unsigned char* s32,
+                                 const unsigned char* m32) {
+    fe px, py, t;
+    sc r, s, m;
+    fe_from_be_bytes(px, x32);
+    fe_from_be_bytes(py, y32);
+    fe_from_be_bytes(t, r32);
+    memcpy(r.v, t.v, 32);
+    fe_from_be_bytes(t, s32);
+    memcpy(s.v, t.v, 32);
+    fe_from_be_bytes(t, m32);
+    memcpy(m.v, t.v, 32);
+    QTableArray qt;
+    GCombArray gc{gcomb().data()};
+    return ecdsa_verify_twist_lane(tag, px, py, r, s, m, qt, gc);
 }
 
 // BIP340: sig64 = r.x || s, msg32, x-only key (secp256k1_schnorrsig_verify argument order)

@@ -21,7 +21,8 @@ SO = os.path.join(HERE, "native", "_build", "lane_host.so")
 def lane():
     src = os.path.join(HERE, "native", "lane_host.cpp")
     deps = [src] + [os.path.join(HERE, "..", "rust-bitcoinconsensus_amd", "csrc", f)
-                    for f in ("ecdsa_lane.h", "secp256k1_device.h", "sha256_device.h")]
+                    for f in ("ecdsa_lane.h", "ecdsa_twist.h", "secp256k1_device.h",
+                              "sha256_device.h")]
     if not os.path.exists(SO) or any(os.path.getmtime(d) > os.path.getmtime(SO) for d in deps):
         os.makedirs(os.path.dirname(SO), exist_ok=True)
         subprocess.check_call(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-o", SO, src])
@@ -64,3 +65,76 @@ def test_lane_code_matches_reference_fixtures(lane):
         if got != t["verdict"]:
             bad.append((t["cls"], got, t["verdict"]))
     assert not bad, bad[:10]
+
+
+def test_lane_twist_matches_reference_fixtures(lane):
+    """The square-root-free path (csrc/ecdsa_twist.h) on every fixture tuple: compressed keys
+    never decompressed, the key's y recovered as -alpha / beta; exceptional classes (R at
+    infinity, x(A) == x(B), u1 == 0) take the exact fallback."""
+    O = Oracle()
+    bad = []
+    classes = {}
+    for t in ecdsa_tuples():
+        tag, x, y = pub_to_tuple(t["pub"])
+        ok, r, s = O.der_parse_lax(t["sig"])
+        if not ok:
+            r = s = bytes(32)
+        got = lane.lane_verify_twist(tag, x, y, r, s, t["hash"])
+        classes[t["cls"]] = classes.get(t["cls"], 0) + 1
+        if got != t["verdict"]:
+            bad.append((t["cls"], got, t["verdict"]))
+    assert not bad, bad[:10]
+    assert len(classes) > 10
+
+
+def _der(r, s):
+    def enc(v):
+        b = v.to_bytes(32, "big").lstrip(b"\0") or b"\0"
+        if b[0] & 0x80:
+            b = b"\0" + b
+        return b"\x02" + bytes([len(b)]) + b
+    body = enc(r) + enc(s)
+    return b"\x30" + bytes([len(body)]) + body
+
+
+def test_lane_twist_random_vs_oracle(lane):
+    """Random signed tuples with mutations (flipped key parity, random x -- about half of them
+    non-residues --, hybrid / uncompressed encodings, negated y, message and s flips) through
+    the square-root-free lane code against the oracle's CPubKey::Verify."""
+    O = Oracle()
+    rng = random.Random(11)
+    P = 2**256 - 2**32 - 977
+    bad, seen = [], set()
+    for i in range(240):
+        d = rng.randrange(1, N)
+        msg = rng.randbytes(32)
+        qx, qy = (int.from_bytes(b, "big") for b in O.ecmult_gen(d.to_bytes(32, "big")))
+        k = rng.randrange(1, N)
+        rx = int.from_bytes(O.ecmult_gen(k.to_bytes(32, "big"))[0], "big")
+        r = rx % N
+        s = pow(k, N - 2, N) * (int.from_bytes(msg, "big") % N + r * d) % N
+        mode = i % 8
+        comp = mode in (0, 1, 2, 3)
+        if mode == 1:
+            qy = P - qy                      # flipped parity: the signature is for -Q
+        elif mode == 2:
+            qx = rng.randrange(P)            # random x: non-residue about half the time
+        elif mode == 3 or mode == 6:
+            msg = bytes([msg[0] ^ 1]) + msg[1:]
+        elif mode == 4:
+            s = N - s                        # high s: normalised, still valid
+        elif mode == 5:
+            qy = P - qy                      # uncompressed, wrong y sign
+        if comp:
+            pub = bytes([2 + (qy & 1)]) + qx.to_bytes(32, "big")
+        else:
+            tag = rng.choice([4, 6 + (qy & 1)])
+            pub = bytes([tag]) + qx.to_bytes(32, "big") + qy.to_bytes(32, "big")
+        exp = O.pubkey_verify(pub, msg, _der(r, s))
+        tag, x, y = pub_to_tuple(pub)
+        got = lane.lane_verify_twist(tag, x, y, r.to_bytes(32, "big"), s.to_bytes(32, "big"), msg)
+        seen.add((mode, exp))
+        if got != exp:
+            bad.append((i, mode, got, exp))
+    assert not bad, bad[:10]
+    assert {(0, 1), (1, 0), (2, 0), (4, 1), (5, 0), (7, 1)} <= seen
