@@ -53,9 +53,13 @@ DEFAULT_N = {"c2": 1_000_000, "c3": 4000, "c4": 8_000_000, "c5": 16_000_000, "c5
 SEEDS = {"c2": 0x5EED0001, "c3": 0x5EED0003, "c4": 0x5EED0004, "c5": 0x5EED0005,
          "c5t": 0x5EED0006}
 # the ECDSA stage's kernels: the square-root-free path (default) or the round-1 path
-ECDSA_KERNELS = ("ecdsa (batch_sinv + ecdsa_key + ecdsa_prep + ecdsa_ladder)"
-                 if os.environ.get("BCC_ECDSA_PATH") == "legacy" else
-                 "ecdsa (batch_sinv + ecdsa_tprep + ecdsa_tladder + ecdsa_tfin; no key square root)")
+_LEGACY = os.environ.get("BCC_ECDSA_PATH") == "legacy"
+ECDSA_KERNELS = ("ecdsa (batch_sinv + ecdsa_key + ecdsa_prep + ecdsa_ladder)" if _LEGACY else
+                 "ecdsa (batch_sinv + ecdsa_tprep + twist_ladder<ecdsa> + twist_fin<ecdsa>; "
+                 "no key square root)")
+SCHNORR_KERNELS = ("schnorr (prep + ladder + y-parity batch inversion)" if _LEGACY else
+                   "schnorr (schnorr_tprep + twist_ladder<bip340> + twist_fin<bip340>; "
+                   "no lift_x square root)")
 CPU_PASSES = 3                    # timed passes of the CPU baseline (median), after 1 warm-up
 
 
@@ -365,7 +369,7 @@ class TupleJob:
         self.unit = "verifies/s"
         self.mads = MADS_PER_VERIFY if kind == "c4" else MADS_PER_SCHNORR
         self.kernel = (ECDSA_KERNELS if kind == "c4"
-                       else "schnorr (prep + ladder + y-parity batch inversion)")
+                       else SCHNORR_KERNELS)
 
     def step(self, sp):
         self.ts.run(sp)

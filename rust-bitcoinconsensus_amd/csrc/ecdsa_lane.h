@@ -18,14 +18,18 @@
 namespace bcc {
 
 // window widths
-constexpr int WQ = 4;                         // Q / lambda*Q digits: table of 8 odd multiples
+#ifndef BCC_WQ_BITS
+#define BCC_WQ_BITS 4
+#endif
+constexpr int WQ = BCC_WQ_BITS;               // Q / lambda*Q digits: table of 2^(WQ-1) odd multiples
 #ifndef BCC_WG_BITS
 #define BCC_WG_BITS 10
 #endif
 constexpr int WG = BCC_WG_BITS;               // G / 2^128*G digits: tables of 2^(WG-1) odd multiples
-constexpr int QTAB = 1 << (WQ - 1);           // 8
+constexpr int QTAB = 1 << (WQ - 1);           // 8 for WQ = 4
 constexpr int GTAB = 1 << (WG - 1);
-constexpr int TOPQ = 124;                     // WQ * 31: top digit position for 128-bit scalars
+constexpr int TOPQ = (127 / WQ) * WQ;         // top digit position for 128-bit scalars (124)
+static_assert(TOPQ + WQ >= 128, "top Q digit must cover bit 127");
 constexpr int TOPG = (127 / WG) * WG;         // top G digit position: 120 for WG = 8, 10, 12
 static_assert(TOPG + WG >= 128 && TOPG <= TOPQ, "top G digit must cover bit 127 inside the ladder");
 
@@ -195,6 +199,85 @@ BCC_HD void build_q_table(const fe& qx, const fe& qy, QT& qt, fe& sigma) {
         if (i > 0) fe_mul(f, f, h);
     }
     fe_mul(sigma, d.z, cur.z);                   // total scale Zd * Z_last
+}
+
+// The same table by co-Z arithmetic (Meloni's ZADDU; DBLU for the first doubling): every
+// T_i = T_{i-1} + 2Q is one co-Z addition that also re-expresses 2Q with T_i's Z (4M + 2S instead
+// of a mixed addition's 8M + 3S); the Z ratios h_i = X_{2Q} - X_{T_{i-1}} feed the same backward
+// rescale to the common Z as build_q_table.  Same output (entries up to the curve scale sigma).
+template <class QT>
+BCC_HD void build_q_table_coz(const fe& qx, const fe& qy, QT& qt, fe& sigma) {
+    fe dx, dy, tx, ty;
+    {  // DBLU: D = 2Q with Z = 2y, T_0 = Q with the same Z
+        fe b, e, l, sx, m, t;
+        fe_sqr(b, qx);             // x^2
+        fe_sqr(e, qy);             // y^2
+        fe_sqr(l, e);              // y^4
+        fe_add(t, qx, e);
+        fe_sqr(t, t);
+        fe_sub(t, t, b);
+        fe_sub(t, t, l);
+        fe_shl<1>(sx, t);          // S = 4 x y^2 (= x (2y)^2)
+        fe_shl<1>(m, b);
+        fe_add(m, m, b);           // M = 3 x^2
+        fe_sqr(t, m);
+        fe_shl<1>(dx, sx);
+        fe_sub(dx, t, dx);         // X(2Q) = M^2 - 2S
+        fe_sub(t, sx, dx);
+        fe_mul(t, m, t);
+        fe_shl<3>(ty, l);          // 8 y^4 (= y (2y)^3)
+        fe_sub(dy, t, ty);         // Y(2Q) = M (S - X) - 8 y^4
+        tx = sx;
+    }
+    qt.put(0, 0, tx);
+    qt.put(0, 2, ty);
+    for (int i = 1; i < QTAB; i++) {  // ZADDU(D, T_{i-1}) -> T_i = D + T_{i-1}, D co-Z with T_i
+        fe h, c, w1, w2, d, a1, t, ry;
+        fe_sub(h, dx, tx);         // Z_i = Z_{i-1} h
+        fe_sqr(c, h);
+        fe_mul(w1, dx, c);
+        fe_mul(w2, tx, c);
+        fe_sub(ry, dy, ty);
+        fe_sqr(d, ry);
+        fe_sub(t, w1, w2);
+        fe_mul(a1, dy, t);
+        fe_sub(t, d, w1);
+        fe_sub(tx, t, w2);         // X3 = (Yd - Yt)^2 - W1 - W2
+        fe_sub(t, w1, tx);
+        fe_mul(t, ry, t);
+        fe_sub(ty, t, a1);         // Y3 = (Yd - Yt)(W1 - X3) - A1
+        dx = w1;                   // D re-expressed with Z_i
+        dy = a1;
+        qt.put(i, 0, tx);
+        qt.put(i, 2, ty);
+        qt.put(i, 1, h);           // slot 1 holds h_i until the rescale pass
+    }
+    fe f = fe_one(), f2, f3, beta;
+    {
+        const u32 bl[8] = BCC_BETA_LIMBS;
+        fe_set(beta, bl);
+    }
+    for (int i = QTAB - 1; i >= 0; i--) {  // entry i times f_i = prod_{j>i} h_j = Z_last / Z_i
+        fe ex, ey, h;
+        qt.get(i, 0, ex);
+        qt.get(i, 2, ey);
+        if (i > 0) qt.get(i, 1, h);
+        if (i < QTAB - 1) {
+            fe_sqr(f2, f);
+            fe_mul(f3, f2, f);
+            fe_mul(ex, ex, f2);
+            fe_mul(ey, ey, f3);
+        }
+        fe bx;
+        fe_mul(bx, ex, beta);
+        qt.put(i, 0, ex);
+        qt.put(i, 1, bx);
+        qt.put(i, 2, ey);
+        if (i > 0) fe_mul(f, f, h);
+    }
+    fe y2;
+    fe_shl<1>(y2, qy);
+    fe_mul(sigma, f, y2);          // Z_last = 2y prod h_i
 }
 
 // x^3 + 7

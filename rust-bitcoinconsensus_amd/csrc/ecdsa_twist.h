@@ -30,11 +30,14 @@
 namespace bcc {
 
 #ifndef BCC_COMB_BITS
-#define BCC_COMB_BITS 10
+#define BCC_COMB_BITS 12  // 22 windows x 2048 points = 2.75 MiB of tables (L2-resident per XCD)
+#endif
+#ifndef BCC_QTAB_COZ
+#define BCC_QTAB_COZ 1  // the Q_w table by co-Z additions (build_q_table_coz)
 #endif
 constexpr int WC = BCC_COMB_BITS;                 // comb window: 2^(WC-1) odd multiples per window
 constexpr int CTAB = 1 << (WC - 1);
-constexpr int CTOP = (256 + WC - 1) / WC - 1;     // top window index (25 for WC = 10)
+constexpr int CTOP = (256 + WC - 1) / WC - 1;     // top window index (21 for WC = 12)
 constexpr int CWIN = CTOP + 1;                    // windows
 static_assert(WC * CTOP + 1 + (WC - 1) >= 256, "top comb digit must cover bit 255");
 
@@ -167,7 +170,11 @@ BCC_HD bool twist_prep_lane(u32 tag, const fe& px, const fe& py, const sc& r_in,
     fe qx, qy;
     fe_mul(qx, px, v);
     fe_sqr(qy, v);
+#if BCC_QTAB_COZ
+    build_q_table_coz(qx, qy, qt, st.sigma);
+#else
     build_q_table(qx, qy, qt, st.sigma);
+#endif
     return true;
 }
 
@@ -410,6 +417,195 @@ BCC_HD int ecdsa_verify_twist_lane(u32 tag, const fe& px, const fe& py, const sc
     fe binv;
     fe_inv(binv, be);
     return twist_final(al, K, binv, st.v, st.ychk, st.flags, st.r);
+}
+
+// ------------------------------------------------------------------------------------------
+// BIP340 on the same path (secp256k1_schnorrsig_verify, modules/schnorrsig/main_impl.h:190-237):
+// the x-only key's even-y lift (extrakeys/main_impl.h:21-39) is never computed either.
+// R = s G - e P = A + B with A = s G (comb) and B = (-e) P_w (Q ladder on E_w).  Besides
+// x(R) == r (alpha + w beta == 0, as for ECDSA) the reference needs y(R) even.  With the same
+// quantities, Y3 = c0 + w c1 and Z3 = w Z1 Zb H, so
+//   y(R) = (c0 w + v c1) / Dd,   Dd = v^2 D^3,  D = Z1 Zb H,
+//   M = U1 H^2 - X3r,  X3r = S2^2 + v s1^2 - H^3 - 2 U1 H^2,
+//   c0 = S2 (M - 2 v s1^2),  c1 = s1 (2 S2^2 - M - H^3),
+// and w = gamma once gamma has passed.  beta and Dd are inverted together (one batched inversion
+// of beta Dd per tuple).
+// ------------------------------------------------------------------------------------------
+
+// Prep: rx < p (main_impl.h:207), s < n (:211-214), x < p (extrakeys), the challenge e, u1 = s
+// for the comb and u2 = -e for the Q ladder, the Q_w table.  The key parity to match is even.
+template <class QT>
+BCC_HD bool schnorr_twist_prep(const fe& px, const fe& rx, const sc& s_in, const sc& m, QT& qt,
+                               TwistState& st) {
+    const u32 N[8] = BCC_N_LIMBS;
+    st.flags = 0;
+    if (!fe_lt_p(rx)) return false;
+    if (!u256_lt(s_in.v, N)) return false;
+    if (!fe_lt_p(px)) return false;
+    fe v;
+    curve_rhs(v, px);
+    sc e, u2, u1 = s_in, k1, k2;
+    schnorr_challenge(e, rx, px, m);
+    sc_neg(u2, e);
+    u32 flags = LS_VALID | LS_COMP;  // even y: LS_PAR clear
+    sc_split_lambda(k1, k2, u2);
+    if ((k1.v[4] | k1.v[5] | k1.v[6] | k1.v[7]) != 0) {
+        sc_neg(k1, k1);
+        flags |= LS_NEG0;
+    }
+    if ((k2.v[4] | k2.v[5] | k2.v[6] | k2.v[7]) != 0) {
+        sc_neg(k2, k2);
+        flags |= LS_NEG1;
+    }
+    if (sc_is_zero(u1)) {
+        flags |= LS_U1ZERO;
+        u1.v[0] = 1u;
+    } else if ((u1.v[0] & 1u) == 0) {
+        sc_neg(u1, u1);
+        flags |= LS_NEGU1;
+    }
+    for (int i = 0; i < 4; i++) {
+        st.k[0][i] = k1.v[i];
+        st.k[1][i] = k2.v[i];
+        st.k[2][i] = u1.v[i];
+        st.k[3][i] = u1.v[4 + i];
+    }
+    for (int q = 0; q < 2; q++) {
+        if ((st.k[q][0] & 1u) == 0) flags |= LS_CORR0 << q;
+        st.k[q][0] |= 1u;
+    }
+    st.flags = flags;
+    for (int i = 0; i < 8; i++) st.r.v[i] = rx.v[i];
+    st.v = v;
+    st.ychk = fe_zero();
+    fe qx, qy;
+    fe_mul(qx, px, v);
+    fe_sqr(qy, v);
+#if BCC_QTAB_COZ
+    build_q_table_coz(qx, qy, qt, st.sigma);
+#else
+    build_q_table(qx, qy, qt, st.sigma);
+#endif
+    return true;
+}
+
+// alpha, beta as twist_combine, plus Dd, c0, c1 for the y-parity of R.  False for the exceptional
+// configurations (x(A) == x(B), beta == 0; Dd == 0 follows from H == 0).
+BCC_HD bool schnorr_twist_combine(const gej& A, const gej& B, const fe& sigma, const fe& v,
+                                  const fe& rx, fe& al, fe& be, fe& dd, fe& c0, fe& c1) {
+    fe zb, zb2, z12, u1, u2, s1, s2, h, hh, t, x3r, m;
+    fe_mul(zb, B.z, sigma);
+    fe_sqr(zb2, zb);
+    fe_sqr(z12, A.z);
+    fe_mul(u2, B.x, z12);          // U2 = X2 Z1^2
+    fe_mul(t, z12, A.z);
+    fe_mul(s2, B.y, t);            // S2 = Y2 Z1^3
+    fe_mul(t, A.y, zb2);
+    fe_mul(t, t, zb);
+    fe_mul(s1, t, v);              // s1 = Y1 Zb^3 v
+    fe_mul(t, A.x, zb2);
+    fe_mul(u1, t, v);              // U1 = X1 Zb^2 v
+    fe_sub(h, u2, u1);
+    if (fe_is_zero(h)) return false;
+    fe_mul(be, s2, s1);
+    fe_shl<1>(be, be);             // beta = 2 S2 s1
+    if (fe_is_zero(be)) return false;
+    fe_mul(t, A.z, zb);
+    fe_mul(t, t, h);               // D = Z1 Zb H
+    fe_sqr(dd, t);
+    fe_mul(dd, dd, t);
+    fe_sqr(t, v);
+    fe_mul(dd, dd, t);             // Dd = v^2 D^3
+    fe_sqr(hh, h);
+    fe_mul(t, z12, zb2);
+    fe_mul(t, t, v);
+    fe K;
+    fe_mul(K, t, hh);              // K = Z3^2
+    fe h3, s22, vs12, u1h2;
+    fe_mul(h3, hh, h);
+    fe_mul(u1h2, u1, hh);
+    fe_sqr(s22, s2);
+    fe_sqr(t, s1);
+    fe_mul(vs12, t, v);
+    fe_add(x3r, s22, vs12);
+    fe_sub(x3r, x3r, h3);
+    fe_sub(x3r, x3r, u1h2);
+    fe_sub(x3r, x3r, u1h2);        // X3r = S2^2 + v s1^2 - H^3 - 2 U1 H^2
+    fe_mul(al, rx, K);
+    fe_sub(al, al, x3r);           // alpha = r K - X3r
+    fe_sub(m, u1h2, x3r);          // M = U1 H^2 - X3r
+    fe_sub(t, m, vs12);
+    fe_sub(t, t, vs12);
+    fe_mul(c0, s2, t);             // c0 = S2 (M - 2 v s1^2)
+    fe_shl<1>(t, s22);
+    fe_sub(t, t, m);
+    fe_sub(t, t, h3);
+    fe_mul(c1, s1, t);             // c1 = s1 (2 S2^2 - M - H^3)
+    return true;
+}
+
+// The verdict of a normal BIP340 lane from ic = (beta Dd)^-1.
+BCC_HD int schnorr_twist_final(const fe& al, const fe& be, const fe& dd, const fe& c0,
+                               const fe& c1, const fe& ic, const fe& v) {
+    fe binv, dinv, g, g2, y, t;
+    fe_mul(binv, dd, ic);
+    fe_mul(dinv, be, ic);
+    fe_mul(g, al, binv);
+    fe_neg(g, g);
+    fe_normalize(g);
+    fe_sqr(g2, g);
+    if (!fe_equal(g2, v)) return 0;          // x(R) != r, or x^3 + 7 not a square
+    if (g.v[0] & 1u) return 0;               // gamma is not the even-y lift: x(R) != r
+    fe_mul(y, c0, g);
+    fe_mul(t, v, c1);
+    fe_add(y, y, t);
+    fe_mul(y, y, dinv);
+    fe_normalize(y);
+    return (y.v[0] & 1u) == 0 ? 1 : 0;       // y(R) even (main_impl.h:234-236)
+}
+
+// Exact fallback for the exceptional BIP340 lanes: the even-y lift by the square root, the plain
+// Jacobian sum, x(R) == r and y(R) even with a per-lane inversion.
+BCC_HD int schnorr_twist_exceptional(const gej& A, bool ainf, const gej& B, bool binf,
+                                     const fe& sigma, const fe& v, const fe& rx) {
+    fe w;
+    if (!fe_sqrt(w, v)) return 0;
+    fe_normalize(w);
+    if (w.v[0] & 1u) fe_neg(w, w);
+    if (ainf && binf) return 0;
+    gej be = B, R;
+    bool rinf = false;
+    fe zb;
+    fe_mul(zb, B.z, sigma);
+    fe_mul(be.z, zb, w);
+    if (binf) R = A;
+    else if (ainf) R = be;
+    else gej_add_gej(R, rinf, A, be);
+    if (rinf) return 0;
+    fe z2, lhs, zi;
+    fe_sqr(z2, R.z);
+    fe_mul(lhs, rx, z2);
+    if (!fe_equal(lhs, R.x)) return 0;
+    fe_inv(zi, R.z);
+    return schnorr_y_even(R.y, zi) ? 1 : 0;
+}
+
+// Whole BIP340 verify on one lane (host tests).
+template <class QT, class GC>
+BCC_HD int schnorr_verify_twist_lane(const fe& px, const fe& rx, const sc& s, const sc& m,
+                                     QT& qt, const GC& gc) {
+    TwistState st;
+    if (!schnorr_twist_prep(px, rx, s, m, qt, st)) return 0;
+    gej A, B;
+    const bool binf = twist_accumulate_q(st, qt, B);
+    const bool ainf = twist_accumulate_g(st, gc, A);
+    fe al, be, dd, c0, c1;
+    if (binf || ainf || !schnorr_twist_combine(A, B, st.sigma, st.v, rx, al, be, dd, c0, c1))
+        return schnorr_twist_exceptional(A, ainf, B, binf, st.sigma, st.v, rx);
+    fe c, ic;
+    fe_mul(c, be, dd);
+    fe_inv(ic, c);
+    return schnorr_twist_final(al, be, dd, c0, c1, ic, st.v);
 }
 
 // Host build of the comb tables: per window the odd multiples of 2^(WC win) G in Jacobian

@@ -445,7 +445,9 @@ enum : int {
     T_BE = 58,     // 8: beta
     T_KK = 66,     // 8: K = Z3^2
     T_PRE = 74,    // 8: K_tfin's prefix product
-    TSTATE_WORDS = 82,
+    T_C0 = 82,     // 8: BIP340 only: c0, c1 of y(R) (T_KK then holds Dd)
+    T_C1 = 90,
+    TSTATE_WORDS = 98,
 };
 
 __device__ __forceinline__ void tw_store(u32* w, int at, const u32 (&v)[8]) {
@@ -543,6 +545,34 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
     tw_store(w, T_Y, st.ychk.v);
 }
 
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void schnorr_tprep_kernel(
+    const uint8_t* __restrict__ psig, const uint8_t* __restrict__ pm,
+    const uint8_t* __restrict__ ppk, size_t base, size_t cnt, u32* __restrict__ qtab,
+    u32* __restrict__ state) {
+    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= cnt) return;
+    const size_t i = base + t;
+    fe px, rx;
+    sc s, m;
+    load_be32(rx, psig + 64 * i);
+    load_be32(s, psig + 64 * i + 32);
+    load_be32(m, pm + 32 * i);
+    load_be32(px, ppk + 32 * i);
+    QTableGlobal qt{lane_table(qtab, t)};
+    TwistState st;
+    schnorr_twist_prep(px, rx, s, m, qt, st);
+    u32* w = lane_words(state, t, TSTATE_WORDS);
+#pragma unroll
+    for (int a = 0; a < 4; a++)
+#pragma unroll
+        for (int b = 0; b < 4; b++) w[(T_K + a * 4 + b) * LANE_STRIDE] = st.k[a][b];
+    w[T_FLAGS * LANE_STRIDE] = st.flags;
+    tw_store(w, T_SIGMA, st.sigma.v);
+    tw_store(w, T_R, st.r.v);
+    tw_store(w, T_V, st.v.v);
+    tw_store(w, T_Y, st.ychk.v);
+}
+
 // Ladder workgroups of 256 lanes: no LDS (the comb tables are read from HBM / L2), so the only
 // occupancy limit is the register file (4 waves per SIMD at <= 128 VGPRs).
 #ifndef BCC_TLADDER_WG
@@ -550,7 +580,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
 #endif
 constexpr int TLADDER_WG = BCC_TLADDER_WG;
 
-__global__ __launch_bounds__(TLADDER_WG) __attribute__((amdgpu_waves_per_eu(BCC_LADDER_WAVES, BCC_LADDER_WAVES))) void ecdsa_tladder_kernel(
+template <bool BIP340>
+__global__ __launch_bounds__(TLADDER_WG) __attribute__((amdgpu_waves_per_eu(BCC_LADDER_WAVES, BCC_LADDER_WAVES))) void twist_ladder_kernel(
     u32* __restrict__ state, u32* __restrict__ qtab, const u32* __restrict__ gcomb, size_t cnt) {
     const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= cnt) return;
@@ -578,14 +609,27 @@ __global__ __launch_bounds__(TLADDER_WG) __attribute__((amdgpu_waves_per_eu(BCC_
     fe v, al, be, K;
     sc r;
     st.get_v(v);
-    st.get_r(r);  // loaded here, used last by twist_combine
-    if (binf || ainf || !twist_combine(A, B, st.sigma, v, r, al, be, K)) {
+    st.get_r(r);  // loaded here, used last by the combine
+    bool ok;
+    if constexpr (BIP340) {
+        fe c0, c1, rx;
+#pragma unroll
+        for (int j = 0; j < 8; j++) rx.v[j] = r.v[j];
+        ok = !binf && !ainf && schnorr_twist_combine(A, B, st.sigma, v, rx, al, be, K, c0, c1);
+        if (ok) {
+            tw_store(w, T_C0, c0.v);
+            tw_store(w, T_C1, c1.v);
+        }
+    } else {
+        ok = !binf && !ainf && twist_combine(A, B, st.sigma, v, r, al, be, K);
+    }
+    if (!ok) {
         park_gej(lt + PARK_A, A, ainf);
         stat = TW_EXCEPT;
     } else {
         tw_store(w, T_AL, al.v);
         tw_store(w, T_BE, be.v);
-        tw_store(w, T_KK, K.v);
+        tw_store(w, T_KK, K.v);  // BIP340: Dd
     }
     w[T_STAT * LANE_STRIDE] = stat;
 }
@@ -593,10 +637,21 @@ __global__ __launch_bounds__(TLADDER_WG) __attribute__((amdgpu_waves_per_eu(BCC_
 // beta^-1 for every normal lane of a chunk by Montgomery's trick over the strided sub-chunk
 // {t, t+T, ...} (3 mults per lane + one Fermat inversion per thread), then the verdicts; the
 // exceptional lanes (adversarial only) run the exact fallback here, divergently.
-__global__ __launch_bounds__(256) void ecdsa_tfin_kernel(u32* __restrict__ state,
-                                                         const u32* __restrict__ qtab,
-                                                         uint8_t* __restrict__ verdict,
-                                                         size_t base, size_t cnt, size_t T) {
+template <bool BIP340>
+__device__ __forceinline__ void twist_fin_elem(const u32* w, fe& c) {  // the inverted element
+    tw_load(c.v, w, T_BE);
+    if constexpr (BIP340) {
+        fe dd;
+        tw_load(dd.v, w, T_KK);
+        fe_mul(c, c, dd);  // beta Dd
+    }
+}
+
+template <bool BIP340>
+__global__ __launch_bounds__(256) void twist_fin_kernel(u32* __restrict__ state,
+                                                        const u32* __restrict__ qtab,
+                                                        uint8_t* __restrict__ verdict,
+                                                        size_t base, size_t cnt, size_t T) {
     const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= cnt || t >= T) return;
     fe acc = fe_one();
@@ -606,7 +661,7 @@ __global__ __launch_bounds__(256) void ecdsa_tfin_kernel(u32* __restrict__ state
         tw_store(w, T_PRE, acc.v);  // product of the betas before i
         if (w[T_STAT * LANE_STRIDE] == TW_NORMAL) {
             fe b;
-            tw_load(b.v, w, T_BE);
+            twist_fin_elem<BIP340>(w, b);
             fe_mul(acc, acc, b);
         }
         last = i;
@@ -628,12 +683,20 @@ __global__ __launch_bounds__(256) void ecdsa_tfin_kernel(u32* __restrict__ state
             if (stat == TW_NORMAL) {
                 fe pre, b, binv, al, K;
                 tw_load(pre.v, w, T_PRE);
-                tw_load(b.v, w, T_BE);
-                fe_mul(binv, inv, pre);  // beta_i^-1
-                fe_mul(inv, inv, b);     // (beta_t ... beta_{i-1})^-1
+                twist_fin_elem<BIP340>(w, b);
+                fe_mul(binv, inv, pre);  // element_i^-1
+                fe_mul(inv, inv, b);     // (element_t ... element_{i-1})^-1
                 tw_load(al.v, w, T_AL);
                 tw_load(K.v, w, T_KK);
-                ok = twist_final(al, K, binv, v, y, flags, r);
+                if constexpr (BIP340) {
+                    fe be, c0, c1;
+                    tw_load(be.v, w, T_BE);
+                    tw_load(c0.v, w, T_C0);
+                    tw_load(c1.v, w, T_C1);
+                    ok = schnorr_twist_final(al, be, K, c0, c1, binv, v);
+                } else {
+                    ok = twist_final(al, K, binv, v, y, flags, r);
+                }
             } else {
                 const u32* lt = lane_table(const_cast<u32*>(qtab), i);
                 gej A, B;
@@ -641,7 +704,14 @@ __global__ __launch_bounds__(256) void ecdsa_tfin_kernel(u32* __restrict__ state
                 const bool ainf = unpark_gej(lt + PARK_A, A);
                 const bool binf = unpark_gej(lt + PARK_B, B);
                 tw_load(sigma.v, w, T_SIGMA);
-                ok = twist_exceptional(A, ainf, B, binf, sigma, v, y, flags, r);
+                if constexpr (BIP340) {
+                    fe rx;
+#pragma unroll
+                    for (int j = 0; j < 8; j++) rx.v[j] = r.v[j];
+                    ok = schnorr_twist_exceptional(A, ainf, B, binf, sigma, v, rx);
+                } else {
+                    ok = twist_exceptional(A, ainf, B, binf, sigma, v, y, flags, r);
+                }
             }
         }
         verdict[base + i] = (uint8_t)ok;
@@ -666,8 +736,8 @@ static const std::vector<fe>& host_gcomb() {
     return t;
 }
 
-// ECDSA path: the square-root-free twist path (default) or the round-1 path with K_key
-// (BCC_ECDSA_PATH=legacy), for A/B runs on one build.
+// Signature path: the square-root-free twist path (default; ECDSA and BIP340) or the round-1 path
+// with the key square root (BCC_ECDSA_PATH=legacy), for A/B runs on one build.
 static bool ecdsa_twist() {
     static const bool on = [] {
         const char* e = getenv("BCC_ECDSA_PATH");
@@ -792,7 +862,8 @@ int ecdsa_launch(SigScratch& sc, const uint8_t* d_tag, const uint8_t* d_x, const
 
 int ecdsa_launch_after_pre(SigScratch& sc, const uint8_t* d_tag, const uint8_t* d_x,
                            const uint8_t* d_y, const uint8_t* d_r, const uint8_t* d_s,
-                           const uint8_t* d_m, uint8_t* d_verdict, size_t n, void* stream) {
+                           const uint8_t* d_m, uint8_t* d_verdict, size_t n, void* stream,
+                           void* ev_rows_read) {
     if (n == 0) return 0;
     int dev = 0, cus = 0;
     fe* gtab = nullptr;
@@ -810,13 +881,15 @@ int ecdsa_launch_after_pre(SigScratch& sc, const uint8_t* d_tag, const uint8_t* 
             hipLaunchKernelGGL(ecdsa_tprep_kernel, dim3((unsigned)((cnt + 255) / 256)), dim3(256),
                                0, sm, d_tag, d_x, d_y, d_r, d_s, d_m, sinv, base, cnt, qtab, state);
             BCC_HIP_TRY(hipGetLastError());
-            hipLaunchKernelGGL(ecdsa_tladder_kernel,
+            if (ev_rows_read && base + cnt >= n)
+                BCC_HIP_TRY(hipEventRecord((hipEvent_t)ev_rows_read, sm));
+            hipLaunchKernelGGL(twist_ladder_kernel<false>,
                                dim3((unsigned)((cnt + TLADDER_WG - 1) / TLADDER_WG)),
                                dim3(TLADDER_WG), 0, sm, state, qtab, gcomb, cnt);
             BCC_HIP_TRY(hipGetLastError());
             // the batched beta inversion: sub-chunks of <= 16 lanes, at least one wave per SIMD
             const size_t T = std::max<size_t>((cnt + 15) / 16, std::min<size_t>(cnt, (size_t)cus * 256));
-            hipLaunchKernelGGL(ecdsa_tfin_kernel, dim3((unsigned)((T + 255) / 256)), dim3(256), 0,
+            hipLaunchKernelGGL(twist_fin_kernel<false>, dim3((unsigned)((T + 255) / 256)), dim3(256), 0,
                                sm, state, qtab, d_verdict, base, cnt, T);
             BCC_HIP_TRY(hipGetLastError());
         }
@@ -851,6 +924,24 @@ int schnorr_launch(SigScratch& sc, const uint8_t* d_sig64, const uint8_t* d_msg3
     hipStream_t sm = (hipStream_t)stream;
     u32* qtab = (u32*)sc.chunk;
     u32* state = qtab + C * QTABLE_WORDS;
+    if (ecdsa_twist()) {  // BIP340 on the square-root-free path
+        const u32* gcomb = g_gcomb[dev];
+        for (size_t base = 0; base < n; base += C) {
+            const size_t cnt = std::min(C, n - base);
+            hipLaunchKernelGGL(schnorr_tprep_kernel, dim3((unsigned)((cnt + 255) / 256)), dim3(256),
+                               0, sm, d_sig64, d_msg32, d_xonly32, base, cnt, qtab, state);
+            BCC_HIP_TRY(hipGetLastError());
+            hipLaunchKernelGGL(twist_ladder_kernel<true>,
+                               dim3((unsigned)((cnt + TLADDER_WG - 1) / TLADDER_WG)),
+                               dim3(TLADDER_WG), 0, sm, state, qtab, gcomb, cnt);
+            BCC_HIP_TRY(hipGetLastError());
+            const size_t T = std::max<size_t>((cnt + 15) / 16, std::min<size_t>(cnt, (size_t)cus * 256));
+            hipLaunchKernelGGL(twist_fin_kernel<true>, dim3((unsigned)((T + 255) / 256)), dim3(256), 0,
+                               sm, state, qtab, d_verdict, base, cnt, T);
+            BCC_HIP_TRY(hipGetLastError());
+        }
+        return 0;
+    }
     for (size_t base = 0; base < n; base += C) {
         size_t cnt = std::min(C, n - base);
         unsigned blocks = (unsigned)((cnt + 255) / 256);

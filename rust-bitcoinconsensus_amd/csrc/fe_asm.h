@@ -213,6 +213,50 @@ __device__ __forceinline__ void fe_reduce512_asm(uint32_t (&r)[8], const uint32_
     }
 }
 
+// r = t mod p (weak), third formulation: s = t_hi * 977 as a chain of v_mad_u64_u32 whose 64-bit
+// addend is the previous product's high word (p >> 32: one move into a zero-high pair, no 64-bit
+// add), then x = t_lo + s + (t_hi << 32) as two carry chains, then the top fold as in
+// fe_reduce512_asm.  Fewer moves and no v_lshl_add_u64 per limb.
+__device__ __forceinline__ void fe_reduce512_v3(uint32_t (&r)[8], const uint32_t (&t)[16]) {
+    uint32_t s[9];
+    uint64_t p = (uint64_t)t[8] * 977u;
+    s[0] = (uint32_t)p;
+#pragma unroll
+    for (int i = 1; i < 8; i++) {
+        p = (uint64_t)t[8 + i] * 977u + (p >> 32);
+        s[i] = (uint32_t)p;
+    }
+    s[8] = (uint32_t)(p >> 32);
+    uint32_t x[9], ca, cb;
+    x[0] = addc(t[0], s[0], 0, ca);
+    x[1] = addc(t[1], s[1], ca, ca);
+    x[1] = addc(x[1], t[8], 0, cb);
+#pragma unroll
+    for (int i = 2; i < 8; i++) {
+        x[i] = addc(t[i], s[i], ca, ca);
+        x[i] = addc(x[i], t[7 + i], cb, cb);
+    }
+    x[8] = addc(s[8], t[15], ca, ca);
+    x[8] = addc(x[8], 0, cb, cb);
+    const uint32_t x9 = ca + cb;  // top = x8 + x9 2^32 < 2^34
+    uint64_t f = (uint64_t)x[8] * 977u + x[0];
+    r[0] = (uint32_t)f;
+    uint32_t c2;
+    uint64_t f1 = (uint64_t)x[1] + x[8] + (f >> 32) + (uint64_t)x9 * 977u;  // < 2^34
+    r[1] = (uint32_t)f1;
+    uint32_t carry = (uint32_t)(f1 >> 32) + x9;  // into limb 2, small
+    r[2] = addc(x[2], carry, 0, c2);
+#pragma unroll
+    for (int i = 3; i < 8; i++) r[i] = addc(x[i], 0, c2, c2);
+    if (c2) {  // wrapped past 2^256 (rare): add 2^32 + 977 once more, cannot carry again
+        uint32_t c3;
+        r[0] = addc(r[0], 977u, 0, c3);
+        r[1] = addc(r[1], 1u, c3, c3);
+#pragma unroll
+        for (int i = 2; i < 8; i++) r[i] = addc(r[i], 0, c3, c3);
+    }
+}
+
 // r = t mod p (weak, r < 2^256), in carry chains of inline asm (no 64-bit adds, no zero-extension
 // moves).  With 2^256 == 2^32 + 977 (mod p) and p_i = t[8+i] * 977 (64-bit, v_mad_u64_u32):
 //   x = sum_i t[i] 2^32i + sum_i t[8+i] 2^32(i+1) + sum_i lo(p_i) 2^32i + sum_i hi(p_i) 2^32(i+1)

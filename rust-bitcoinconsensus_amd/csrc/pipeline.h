@@ -215,9 +215,13 @@ int ecdsa_launch(SigScratch& sc, const uint8_t* d_tag, const uint8_t* d_x, const
 // after them (must be ordered after both, and after the sighash kernels that write m).
 int ecdsa_launch_pre(SigScratch& sc, const uint8_t* d_tag, const uint8_t* d_x,
                      const uint8_t* d_y, const uint8_t* d_s, size_t n, void* stream);
+// ev_rows_read (optional hipEvent_t) is recorded on `stream` once the last kernel that reads the
+// s / m / key rows and the s^-1 rows has been launched (the prep kernel): later writers of those
+// rows (the next run's front kernels) need only wait for it, not for the ladder.
 int ecdsa_launch_after_pre(SigScratch& sc, const uint8_t* d_tag, const uint8_t* d_x,
                            const uint8_t* d_y, const uint8_t* d_r, const uint8_t* d_s,
-                           const uint8_t* d_m, uint8_t* d_verdict, size_t n, void* stream);
+                           const uint8_t* d_m, uint8_t* d_verdict, size_t n, void* stream,
+                           void* ev_rows_read = nullptr);
 int schnorr_launch(SigScratch& sc, const uint8_t* d_sig64, const uint8_t* d_msg32,
                    const uint8_t* d_xonly32, uint8_t* d_verdict, size_t n, void* stream);
 
@@ -264,6 +268,10 @@ private:
     void* ev_fork_ = nullptr;      // hipEvent_t: run() start on the main stream
     void* ev_join_ = nullptr;      // hipEvent_t: K_inv done on the side stream
     void* ev_wtx_ = nullptr;       // hipEvent_t: K_wtx done on the side stream
+    void* ev_rows_ = nullptr;      // hipEvent_t: the last run's prep kernel (rows read)
+    void* ev_front_ = nullptr;     // hipEvent_t: this run's sighash kernels done (overlap mode)
+    bool rows_pending_ = false;    // ev_rows_ recorded by an earlier run (on rows_stream_)
+    void* rows_stream_ = nullptr;
     SigScratch scratch_;
     void* arena_ = nullptr;
     size_t cap_ = 0;

@@ -187,6 +187,12 @@ BCC_HD void fe_reduce512(fe& r, const u32 (&t)[16]) {
 #ifndef BCC_RED_CHAIN
 #define BCC_RED_CHAIN 0
 #endif
+// fe_reduce512_v3 (default): the 977-products chained through their high words, two carry chains
+// for the rest: 4.4 % fewer VALU instructions in the ladder's doubling / addition and +2.4 % on
+// C2 (interleaved A/B, profiles/r02tw4/ab_summary.txt).
+#ifndef BCC_RED_V3
+#define BCC_RED_V3 1
+#endif
 
 BCC_HD void fe_mul(fe& r, const fe& a, const fe& b) {
     u32 t[16];
@@ -194,6 +200,8 @@ BCC_HD void fe_mul(fe& r, const fe& a, const fe& b) {
     mul_256x256_col(t, a.v, b.v);
 #if BCC_RED_CHAIN
     fe_reduce512_chain(r.v, t);
+#elif BCC_RED_V3
+    fe_reduce512_v3(r.v, t);
 #else
     fe_reduce512_asm(r.v, t);
 #endif
@@ -209,6 +217,8 @@ BCC_HD void fe_sqr(fe& r, const fe& a) {
     sqr_256_col(t, a.v);
 #if BCC_RED_CHAIN
     fe_reduce512_chain(r.v, t);
+#elif BCC_RED_V3
+    fe_reduce512_v3(r.v, t);
 #else
     fe_reduce512_asm(r.v, t);
 #endif
@@ -657,17 +667,43 @@ BCC_HD void sc_neg(sc& r, const sc& a) {
 
 BCC_HD bool sc_is_zero(const sc& a) { return u256_is_zero(a.v); }
 
-// r = a^(n-2) mod n, left-to-right square-and-multiply over the constant exponent.  The bit
-// test is wave-uniform, so there is no divergence and no runtime-indexed table (which would
-// live in scratch).  The batched path (ecdsa_verify.hip, batch_inverse kernel) amortises this.
+// r = a^(n-2) mod n by a left-to-right sliding window (w = 4) over the constant exponent: the odd
+// powers a, a^3, ..., a^15 in registers, then 58 steps "square sq times, multiply by a^(2 idx + 1)"
+// (252 squarings + 58 + 7 multiplications, against 254 + 191 for plain square-and-multiply).  The
+// step list is a constant table, so every branch is wave-uniform and the power table is indexed
+// by constants only (no scratch).  The batched path (batch_sinv_kernel) amortises this.
 BCC_HD void sc_inv(sc& r, const sc& a) {
     // n - 2 = FFFFFFFF FFFFFFFF FFFFFFFF FFFFFFFE BAAEDCE6 AF48A03B BFD25E8C D036413F
-    const u32 E[8] = {0xD036413Fu, 0xBFD25E8Cu, 0xAF48A03Bu, 0xBAAEDCE6u,
-                      0xFFFFFFFEu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
-    sc acc = a;  // bit 255 is set
-    for (int b = 254; b >= 0; b--) {
-        sc_sqr(acc, acc);
-        if ((E[b >> 5] >> (b & 31)) & 1u) sc_mul(acc, acc, a);
+    static constexpr uint8_t SQ[58] = {0, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4,
+                                       4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 3, 5, 3, 4, 4, 5, 2, 5, 6,
+                                       5, 4, 3, 6, 10, 4, 5, 4, 5, 6, 4, 5, 6, 10, 4, 9, 4, 1};
+    static constexpr uint8_t IX[58] = {7, 7, 7, 7, 7, 7, 7, 7, 7, 7, 7, 7, 7, 7, 7, 7, 7, 7, 7, 7,
+                                       7, 7, 7, 7, 7, 7, 7, 7, 7, 7, 7, 3, 5, 2, 2, 3, 6, 1, 3, 6,
+                                       5, 6, 0, 2, 3, 3, 7, 7, 4, 5, 6, 1, 6, 6, 4, 4, 7, 0};
+    sc p0 = a, p1, p2, p3, p4, p5, p6, p7, a2;
+    sc_sqr(a2, a);
+    sc_mul(p1, p0, a2);
+    sc_mul(p2, p1, a2);
+    sc_mul(p3, p2, a2);
+    sc_mul(p4, p3, a2);
+    sc_mul(p5, p4, a2);
+    sc_mul(p6, p5, a2);
+    sc_mul(p7, p6, a2);
+    sc acc = p7;  // step 0: a^15
+#pragma unroll 1
+    for (int k = 1; k < 58; k++) {
+#pragma unroll 1
+        for (int q = 0; q < SQ[k]; q++) sc_sqr(acc, acc);
+        switch (IX[k]) {
+        case 0: sc_mul(acc, acc, p0); break;
+        case 1: sc_mul(acc, acc, p1); break;
+        case 2: sc_mul(acc, acc, p2); break;
+        case 3: sc_mul(acc, acc, p3); break;
+        case 4: sc_mul(acc, acc, p4); break;
+        case 5: sc_mul(acc, acc, p5); break;
+        case 6: sc_mul(acc, acc, p6); break;
+        default: sc_mul(acc, acc, p7); break;
+        }
     }
     r = acc;
 }

@@ -65,6 +65,22 @@ extern "C" int lane_verify_twist(unsigned tag, const unsigned char* x32, const u
     return ecdsa_verify_twist_lane(tag, px, py, r, s, m, qt, gc);
 }
 
+// BIP340 on the square-root-free path (ecdsa_twist.h)
+extern "C" int lane_schnorr_verify_twist(const unsigned char* sig64, const unsigned char* msg32,
+                                         const unsigned char* xonly32) {
+    fe px, rx, t;
+    sc s, m;
+    fe_from_be_bytes(rx, sig64);
+    fe_from_be_bytes(t, sig64 + 32);
+    memcpy(s.v, t.v, 32);
+    fe_from_be_bytes(t, msg32);
+    memcpy(m.v, t.v, 32);
+    fe_from_be_bytes(px, xonly32);
+    QTableArray qt;
+    GCombArray gc{gcomb().data()};
+    return schnorr_verify_twist_lane(px, rx, s, m, qt, gc);
+}
+
 // BIP340: sig64 = r.x || s, msg32, x-only key (secp256k1_schnorrsig_verify argument order)
 extern "C" int lane_schnorr_verify(const unsigned char* sig64, const unsigned char* msg32,
                                    const unsigned char* xonly32) {

@@ -37,6 +37,16 @@ def test_lane_schnorr_matches_reference_fixtures(lane):
 
 
 @pytest.mark.skipif(not reference_available(), reason="oracle/_ref not built")
+def test_lane_schnorr_twist_matches_reference_fixtures(lane):
+    """BIP340 on the square-root-free path: the 15 BIP340 vectors and the reference-labelled
+    Schnorr tuples (bad keys, off-curve x, R at infinity, odd y(R), mutated s / e)."""
+    ts = bip340_vectors() + schnorr_tuples()
+    bad = [(t["cls"], t["verdict"]) for t in ts
+           if lane.lane_schnorr_verify_twist(t["sig"], t["msg"], t["pub"]) != t["verdict"]]
+    assert not bad, bad[:10]
+
+
+@pytest.mark.skipif(not reference_available(), reason="oracle/_ref not built")
 def test_lane_schnorr_signer_vs_reference(lane):
     """The generator's BIP340 signer (synthetic C5 inputs) produces signatures the reference
     accepts, for the x-only key the reference derives."""
@@ -138,3 +148,35 @@ def test_lane_twist_random_vs_oracle(lane):
             bad.append((i, mode, got, exp))
     assert not bad, bad[:10]
     assert {(0, 1), (1, 0), (2, 0), (4, 1), (5, 0), (7, 1)} <= seen
+
+
+def test_lane_schnorr_twist_random_vs_legacy_lane(lane):
+    """Random BIP340 signatures (the generator's signer) with mutations -- s, e (message), r,
+    the key's x (a non-residue about half the time) -- through the square-root-free lane code
+    against the round-1 lane code, which test_lane_schnorr_matches_reference_fixtures pins."""
+    rng = random.Random(23)
+    bad, seen = [], set()
+    for i in range(160):
+        d = rng.randrange(1, N).to_bytes(32, "big")
+        k = rng.randrange(1, N).to_bytes(32, "big")
+        msg = rng.randbytes(32)
+        sig, xo = ctypes.create_string_buffer(64), ctypes.create_string_buffer(32)
+        assert lane.lane_schnorr_sign(d, msg, k, sig, xo) == 1
+        sig, xo = bytearray(sig.raw), bytearray(xo.raw)
+        mode = i % 5
+        if mode == 1:
+            sig[40] ^= 4
+        elif mode == 2:
+            msg = bytes([msg[0] ^ 1]) + msg[1:]
+        elif mode == 3:
+            sig[5] ^= 1
+        elif mode == 4:
+            xo = bytearray(rng.randbytes(32))
+        sig, xo = bytes(sig), bytes(xo)
+        exp = lane.lane_schnorr_verify(sig, msg, xo)
+        got = lane.lane_schnorr_verify_twist(sig, msg, xo)
+        seen.add((mode, exp))
+        if got != exp:
+            bad.append((i, mode, got, exp))
+    assert not bad, bad[:10]
+    assert (0, 1) in seen and (1, 0) in seen
