@@ -81,6 +81,21 @@ __device__ __forceinline__ void sqr_256_asm(uint32_t (&t)[16], const uint32_t (&
     OPC " %[r6], vcc, 0, %[r6], vcc\n\t" OPC " %[r7], vcc, 0, %[r7], vcc\n"       \
     ".Ldone%=:"
 
+// The carry (borrow) of limb 7, in VCC, as t1 = c and t0 = 977 c: two selects (default), or
+// (BCC_ADD_NOCND) one add-with-carry of zeros plus a 24-bit multiply, no v_cndmask.
+#ifndef BCC_ADD_NOCND
+#define BCC_ADD_NOCND 0
+#endif
+#if BCC_ADD_NOCND
+#define BCC_CARRY_TO_T01                                                           \
+    "v_addc_co_u32_e64 %[t1], %[tmp], 0, 0, vcc\n\t"                               \
+    "v_mul_u32_u24_e32 %[t0], %[k977], %[t1]\n\t"
+#else
+#define BCC_CARRY_TO_T01                                                           \
+    "v_cndmask_b32_e64 %[t0], 0, %[k977], vcc\n\t"                                 \
+    "v_cndmask_b32_e64 %[t1], 0, 1, vcc\n\t"
+#endif
+
 #define BCC_R_OUT                                                                  \
     [r0] "=&v"(r[0]), [r1] "=&v"(r[1]), [r2] "=&v"(r[2]), [r3] "=&v"(r[3]),      \
     [r4] "=&v"(r[4]), [r5] "=&v"(r[5]), [r6] "=&v"(r[6]), [r7] "=&v"(r[7]),      \
@@ -100,8 +115,7 @@ __device__ __forceinline__ void fe_add_asm(uint32_t (&r)[8], const uint32_t (&a)
         "v_addc_co_u32_e32 %[r5], vcc, %[a5], %[b5], vcc\n\t"
         "v_addc_co_u32_e32 %[r6], vcc, %[a6], %[b6], vcc\n\t"
         "v_addc_co_u32_e32 %[r7], vcc, %[a7], %[b7], vcc\n\t"
-        "v_cndmask_b32_e64 %[t0], 0, %[k977], vcc\n\t"
-        "v_cndmask_b32_e64 %[t1], 0, 1, vcc\n\t"
+        BCC_CARRY_TO_T01
         "v_add_co_u32_e32 %[r0], vcc, %[r0], %[t0]\n\t"
         "v_addc_co_u32_e32 %[r1], vcc, %[r1], %[t1], vcc\n\t"
         BCC_FOLD_TAIL("v_add_co_u32_e32", "v_addc_co_u32_e32", "v_addc_co_u32_e32")
@@ -128,8 +142,7 @@ __device__ __forceinline__ void fe_sub_asm(uint32_t (&r)[8], const uint32_t (&a)
         "v_subb_co_u32_e32 %[r5], vcc, %[a5], %[b5], vcc\n\t"
         "v_subb_co_u32_e32 %[r6], vcc, %[a6], %[b6], vcc\n\t"
         "v_subb_co_u32_e32 %[r7], vcc, %[a7], %[b7], vcc\n\t"
-        "v_cndmask_b32_e64 %[t0], 0, %[k977], vcc\n\t"
-        "v_cndmask_b32_e64 %[t1], 0, 1, vcc\n\t"
+        BCC_CARRY_TO_T01
         "v_sub_co_u32_e32 %[r0], vcc, %[r0], %[t0]\n\t"
         "v_subb_co_u32_e32 %[r1], vcc, %[r1], %[t1], vcc\n\t"
         BCC_FOLD_TAIL("v_sub_co_u32_e32", "v_subb_co_u32_e32", "v_subbrev_co_u32_e32")
@@ -236,9 +249,11 @@ __device__ __forceinline__ void fe_reduce512_v3(uint32_t (&r)[8], const uint32_t
         x[i] = addc(t[i], s[i], ca, ca);
         x[i] = addc(x[i], t[7 + i], cb, cb);
     }
+    uint32_t dz;
     x[8] = addc(s[8], t[15], ca, ca);
+    uint32_t x9 = addc(0u, 0u, ca, dz);  // the carries as values by add-with-carry (no selects)
     x[8] = addc(x[8], 0, cb, cb);
-    const uint32_t x9 = ca + cb;  // top = x8 + x9 2^32 < 2^34
+    x9 = addc(x9, 0u, cb, dz);           // top = x8 + x9 2^32 < 2^34
     uint64_t f = (uint64_t)x[8] * 977u + x[0];
     r[0] = (uint32_t)f;
     uint32_t c2;

@@ -700,6 +700,15 @@ std::atomic<size_t> g_pipeline_chunk{[] {
 }()};
 size_t pipeline_chunk() { return g_pipeline_chunk.load(std::memory_order_relaxed); }
 
+// Staging threads of a pipelined device round (BCC_PIPELINE_STAGE_THREADS, default 4).
+unsigned pipeline_stage_threads() {
+    static const unsigned v = [] {
+        const char* e = getenv("BCC_PIPELINE_STAGE_THREADS");
+        return e ? (unsigned)atoi(e) : 4u;
+    }();
+    return v;
+}
+
 // Runs the batch; fills ret/err per item.  Returns -1 if the device pipeline failed twice in a
 // row for some round: the items that round left unfinished get ret 0 and BCC_ERR_DEVICE_FAILURE
 // (never a consensus verdict); all other items carry their final results.
@@ -742,7 +751,11 @@ long run_batch(const bcc_batch_item* items, size_t n, unsigned flags, int* ret_o
                 account(chunk_finish(*prev, ret_out + prev_lo, err_out ? err_out + prev_lo : nullptr,
                                      true, &gpu_s));
             }
-            if (c.pending_round) c.fut = run_async([&c] { return chunk_device_round(c); });
+            if (c.pending_round)
+                c.fut = run_async([&c] {
+                    set_stage_threads(pipeline_stage_threads());  // beside the host pass
+                    return chunk_device_round(c);
+                });
             prev = &c;
             prev_lo = cut[k];
         }

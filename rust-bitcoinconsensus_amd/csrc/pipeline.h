@@ -269,6 +269,8 @@ private:
     void* ev_join_ = nullptr;      // hipEvent_t: K_inv done on the side stream
     void* ev_wtx_ = nullptr;       // hipEvent_t: K_wtx done on the side stream
     void* ev_rows_ = nullptr;      // hipEvent_t: the last run's prep kernel (rows read)
+    void* ev_block_ = nullptr;     // hipEvent_t (blocking sync): host waits sleep, not spin
+    int wait(void* stream);
     void* ev_front_ = nullptr;     // hipEvent_t: this run's sighash kernels done (overlap mode)
     bool rows_pending_ = false;    // ev_rows_ recorded by an earlier run (on rows_stream_)
     void* rows_stream_ = nullptr;
@@ -293,6 +295,12 @@ private:
     WinJob* d_wjob_ = nullptr;
     uint32_t* d_intab_ = nullptr;
 };
+
+// Threads the calling thread's device batches use to fill their pinned staging image (0: one per
+// part, the default).  The batch engine lowers it on its pipeline worker, whose staging runs
+// beside the host pass: the GPU box's CPU share is a CFS quota, and threads beyond it are
+// throttled for the rest of the quota period.
+void set_stage_threads(unsigned n);
 
 // One-shot helper: stage + run + fetch on `device` (synchronous).
 // *stage_seconds (optional) receives the host -> HBM staging time.

@@ -614,6 +614,7 @@ DeviceBatch::~DeviceBatch() {
     if (ev_join_) (void)hipEventDestroy((hipEvent_t)ev_join_);
     if (ev_wtx_) (void)hipEventDestroy((hipEvent_t)ev_wtx_);
     if (ev_rows_) (void)hipEventDestroy((hipEvent_t)ev_rows_);
+    if (ev_block_) (void)hipEventDestroy((hipEvent_t)ev_block_);
     if (ev_front_) (void)hipEventDestroy((hipEvent_t)ev_front_);
     if (arena_) (void)hipFree(arena_);
     if (host_image_) (void)hipHostFree(host_image_);
@@ -633,11 +634,27 @@ void* DeviceBatch::pick(void* stream) {
     return stream;
 }
 
-int DeviceBatch::sync() {
-    BCC_HIP_TRY(hipSetDevice(dev_));
-    if (last_stream_) BCC_HIP_TRY(hipStreamSynchronize((hipStream_t)last_stream_));
+// Host waits on a blocking-sync event: the waiting thread sleeps instead of spinning on a core
+// (the host pass may be running beside it on the same CPU share).
+int DeviceBatch::wait(void* stream) {
+    if (!ev_block_) {
+        hipEvent_t e = nullptr;
+        BCC_HIP_TRY(hipEventCreateWithFlags(&e, hipEventBlockingSync | hipEventDisableTiming));
+        ev_block_ = e;
+    }
+    BCC_HIP_TRY(hipEventRecord((hipEvent_t)ev_block_, (hipStream_t)stream));
+    BCC_HIP_TRY(hipEventSynchronize((hipEvent_t)ev_block_));
     return 0;
 }
+
+int DeviceBatch::sync() {
+    BCC_HIP_TRY(hipSetDevice(dev_));
+    if (last_stream_) return wait(last_stream_);
+    return 0;
+}
+
+thread_local unsigned tl_stage_threads = 0;
+void set_stage_threads(unsigned n) { tl_stage_threads = n; }
 
 static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
@@ -799,12 +816,16 @@ int DeviceBatch::stage_parts(const SighashJobs* const* J, const TupleRows* const
             wj[k] = t;
         }
     };
-    if (P == 1 || upload < ((size_t)1 << 20)) {
+    const size_t nth = std::min<size_t>(P, tl_stage_threads ? tl_stage_threads : P);
+    if (nth <= 1 || upload < ((size_t)1 << 20)) {
         for (size_t p = 0; p < P; p++) fill(p);
     } else {
+        auto fill_some = [&](size_t t) {
+            for (size_t p = t; p < P; p += nth) fill(p);
+        };
         std::vector<std::thread> th;
-        for (size_t p = 1; p < P; p++) th.emplace_back(fill, p);
-        fill(0);
+        for (size_t t = 1; t < nth; t++) th.emplace_back(fill_some, t);
+        fill_some(0);
         for (auto& x : th) x.join();
     }
     BCC_HIP_TRY(hipSetDevice(dev_));
@@ -963,7 +984,7 @@ int DeviceBatch::fetch_verdicts(uint8_t* out) {
     BCC_HIP_TRY(hipSetDevice(dev_));
     hipStream_t st = (hipStream_t)pick(last_stream_);
     BCC_HIP_TRY(hipMemcpyAsync(vbuf_, d_v, n_rows_, hipMemcpyDeviceToHost, st));
-    BCC_HIP_TRY(hipStreamSynchronize(st));
+    if (int e = wait(st)) return e;
     memcpy(out, vbuf_, n_rows_);
     return 0;
 }

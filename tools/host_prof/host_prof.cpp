@@ -18,6 +18,7 @@ int gpu_verify_batch(int, const SighashJobs&, const TupleRows& rows, uint8_t* ve
     memset(verdict, 1, rows.size());
     return 0;
 }
+void set_stage_threads(unsigned) {}  // the device batch is stubbed out
 int gpu_verify_parts(int, const SighashJobs* const*, const TupleRows* const* rows, size_t parts,
                      uint8_t* verdict, double*) {
     size_t n = 0;
