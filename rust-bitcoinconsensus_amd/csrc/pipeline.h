@@ -265,6 +265,7 @@ private:
     void* last_stream_ = nullptr;  // stream of the last run
     void* side_stream_ = nullptr;  // K_inv beside the sighash kernels (run())
     void* wtx_stream_ = nullptr;   // K_wtx beside both (run())
+    void* sh_stream_ = nullptr;    // the other sighash kernels (run(), overlap mode)
     void* ev_fork_ = nullptr;      // hipEvent_t: run() start on the main stream
     void* ev_join_ = nullptr;      // hipEvent_t: K_inv done on the side stream
     void* ev_wtx_ = nullptr;       // hipEvent_t: K_wtx done on the side stream

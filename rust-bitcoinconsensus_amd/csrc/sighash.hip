@@ -609,6 +609,7 @@ DeviceBatch::~DeviceBatch() {
     (void)hipSetDevice(dev_);
     if (own_stream_) (void)hipStreamDestroy((hipStream_t)own_stream_);
     if (side_stream_) (void)hipStreamDestroy((hipStream_t)side_stream_);
+    if (sh_stream_) (void)hipStreamDestroy((hipStream_t)sh_stream_);
     if (wtx_stream_) (void)hipStreamDestroy((hipStream_t)wtx_stream_);
     if (ev_fork_) (void)hipEventDestroy((hipEvent_t)ev_fork_);
     if (ev_join_) (void)hipEventDestroy((hipEvent_t)ev_join_);
@@ -892,12 +893,14 @@ int DeviceBatch::run_ecdsa(void* stream) {
     return ecdsa_launch(scratch_, d_tag, d_x, d_y, d_r, d_s, d_m, d_v, n_rows_, st);
 }
 
-// Consecutive run()s of a batch overlap (default; BCC_OVERLAP_RUNS=0 turns it off): see
-// DeviceBatch::run.  Measured on C2 1M: 84.2-85.6 -> 86.2-86.5 M verifies/s (profiles/r02tw3).
+// Consecutive run()s of a resident batch may overlap (BCC_OVERLAP_RUNS=1): see DeviceBatch::run.
+// Off by default: +1.5 % on the staged C2 loop (84.2-85.6 -> 86.2-86.5 M verifies/s,
+// profiles/r02tw3) but -15 % on C3's verify_batch calls (1.78-1.80 -> 1.43-1.61 M inputs/s,
+// profiles/r02tw7): its fourth stream exceeds the box's 4 hardware queues per process.
 static bool overlap_runs() {
     static const bool on = [] {
         const char* e = getenv("BCC_OVERLAP_RUNS");
-        return !(e && atoi(e) == 0);
+        return e && atoi(e) != 0;
     }();
     return on;
 }
@@ -938,15 +941,28 @@ int DeviceBatch::run(void* stream) {
             ev_rows_ = a;
             ev_front_ = b;
         }
+        if (!sh_stream_) {
+            hipStream_t s3 = nullptr;
+            BCC_HIP_TRY(hipStreamCreateWithFlags(&s3, hipStreamNonBlocking));
+            sh_stream_ = s3;
+        }
+        hipStream_t ss = (hipStream_t)sh_stream_;
         BCC_HIP_TRY(hipEventRecord((hipEvent_t)ev_fork_, st));  // staging / earlier work on st
         hipEvent_t gate = rows_pending_ && rows_stream_ == st ? (hipEvent_t)ev_rows_
                                                               : (hipEvent_t)ev_fork_;
         BCC_HIP_TRY(hipStreamWaitEvent(side, gate, 0));
         BCC_HIP_TRY(hipStreamWaitEvent(ws, gate, 0));
+        BCC_HIP_TRY(hipStreamWaitEvent(ss, gate, 0));
         if (int e = ecdsa_launch_pre(scratch_, d_tag, d_x, d_y, d_s, n_rows_, side)) return e;
         BCC_HIP_TRY(hipEventRecord((hipEvent_t)ev_join_, side));
-        if (int e = launch_sighash(ws, nullptr)) return e;  // K_wtx in order on ws
-        BCC_HIP_TRY(hipEventRecord((hipEvent_t)ev_front_, ws));
+        // K_wtx on ws beside K1 + K3' on ss (a block's long legacy chains and its BIP143 per-tx
+        // chains overlap), K_win on ss after both
+        if (n_wtx_) {
+            if (int e = launch_wtx(ws)) return e;
+            BCC_HIP_TRY(hipEventRecord((hipEvent_t)ev_wtx_, ws));
+        }
+        if (int e = launch_sighash(ss, ev_wtx_)) return e;
+        BCC_HIP_TRY(hipEventRecord((hipEvent_t)ev_front_, ss));
         BCC_HIP_TRY(hipStreamWaitEvent(st, (hipEvent_t)ev_join_, 0));
         BCC_HIP_TRY(hipStreamWaitEvent(st, (hipEvent_t)ev_front_, 0));
         rows_pending_ = true;
