@@ -633,7 +633,7 @@ extern "C" bcc_workload* bcc_workload_block(const uint32_t* tx_nin, const uint32
                 }
                 if (p.type == IN_P2WPKH) {  // BIP143 (interpreter.cpp:1581-1625)
                     Bip143Job job;
-                    build_bip143_preimage(tx, i, code, 1, p.amount, job);
+                    build_bip143_preimage(tx, i, Bytes(code.begin(), code.end()), 1, p.amount, job);
                     for (int k = 0; k < 3; k++) {
                         if (!job.need[k]) continue;
                         build_aux_message(tx, (AuxKind)k, aux);
@@ -641,7 +641,7 @@ extern "C" bcc_workload* bcc_workload_block(const uint32_t* tx_nin, const uint32
                     }
                     sha256d(job.preimage.data(), job.preimage.size(), p.m);
                 } else {  // legacy (interpreter.cpp:1273-1364)
-                    if (!build_legacy_preimage(tx, i, code, 1, pre)) abort();
+                    if (!build_legacy_preimage(tx, i, Bytes(code.begin(), code.end()), 1, pre)) abort();
                     sha256d(pre.data(), pre.size(), p.m);
                 }
                 const int nsig = p.type == IN_MS ? 2 : 1;

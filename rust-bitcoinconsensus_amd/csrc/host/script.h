@@ -14,12 +14,14 @@
 #include <cstdint>
 #include <vector>
 
+#include "pool.h"
 #include "tx.h"
 
 namespace bcc {
 namespace host {
 
-typedef std::vector<uint8_t> Bytes;
+// interpreter byte vectors (stack elements, script codes) on the small-block pool (pool.h)
+typedef std::vector<uint8_t, PoolAlloc<uint8_t>> Bytes;
 
 enum SigVersion { SIGVERSION_BASE = 0, SIGVERSION_WITNESS_V0 = 1 };
 
