@@ -707,18 +707,28 @@ def main():
         rates = {UBENCH_OPS[op]: round(B.microbench(op, 2048) / 1e12, 2) for op in UBENCH_OPS}
         achieved = sig_units * job.mads / (sig_ms * 1e-3)
         traffic, tsrc = args.traffic, "--traffic" if args.traffic else None
+        mix = None
         tf = os.path.join(ROOT, "profiles", "traffic.json")
         if traffic is None and os.path.exists(tf):
             tj = json.load(open(tf))
             t = tj.get(f"{args.config}@{sig_units}") or tj.get(args.config)
             if t and t.get("units") == sig_units and t.get("kernel") == job.kernel:
                 traffic, tsrc = t["traffic_bytes"], t["source"]
+                mix = t.get("instruction_mix")
         roof = dict(bound="int-alu", kernel=job.kernel,
                     achieved=achieved / 1e12, peak=peak / 1e12, unit="T(v_mad_u64_u32)/s",
                     frac=achieved / peak, traffic=traffic, traffic_source=tsrc,
                     issue_rates_T_per_s=rates,
                     per_launch=dict(verifies=sig_units, mads=sig_units * job.mads, avg_ms=sig_ms,
                                     verifies_per_s=sig_units / (sig_ms * 1e-3)))
+        if mix:
+            # the instruction-mix ceiling: every VALU instruction of the stage issued at the rate the
+            # ladder sustains (the stage is VALU-issue-bound), from the committed SQ counter pass
+            ceil_vps = mix["ladder_issue_rate_T_per_s"] * 1e12 / mix["valu_lane_instructions_per_verify"]
+            roof["instruction_mix_ceiling"] = dict(
+                frac=ceil_vps * job.mads / peak, verifies_per_s=ceil_vps,
+                valu_lane_instructions_per_verify=mix["valu_lane_instructions_per_verify"],
+                issue_rate_T_per_s=mix["ladder_issue_rate_T_per_s"], source=mix["source"])
         cpu = None
         if world == 1 and not args.no_cpu:
             default_sample = {"c2": 200_000, "c3": 100_000, "c4": 400_000, "c5": 400_000,
