@@ -722,13 +722,16 @@ def main():
                     per_launch=dict(verifies=sig_units, mads=sig_units * job.mads, avg_ms=sig_ms,
                                     verifies_per_s=sig_units / (sig_ms * 1e-3)))
         if mix:
-            # the instruction-mix ceiling: every VALU instruction of the stage issued at the rate the
-            # ladder sustains (the stage is VALU-issue-bound), from the committed SQ counter pass
-            ceil_vps = mix["ladder_issue_rate_T_per_s"] * 1e12 / mix["valu_lane_instructions_per_verify"]
-            roof["instruction_mix_ceiling"] = dict(
-                frac=ceil_vps * job.mads / peak, verifies_per_s=ceil_vps,
+            # the instruction mix behind frac (committed SQ counter pass): the stage is VALU-issue-
+            # bound, so frac ~= (counted mads / issued VALU instructions) x (the mix's issue rate /
+            # the v_mad_u64_u32 peak); raising frac means issuing fewer non-mad instructions
+            share = job.mads / mix["valu_lane_instructions_per_verify"]
+            roof["instruction_mix"] = dict(
                 valu_lane_instructions_per_verify=mix["valu_lane_instructions_per_verify"],
-                issue_rate_T_per_s=mix["ladder_issue_rate_T_per_s"], source=mix["source"])
+                ladder_valu_per_verify=mix["ladder_valu_per_verify"],
+                counted_mad_share=share, issue_rate_T_per_s=mix["ladder_issue_rate_T_per_s"],
+                frac_estimate=share * mix["ladder_issue_rate_T_per_s"] * 1e12 / peak,
+                source=mix["source"])
         cpu = None
         if world == 1 and not args.no_cpu:
             default_sample = {"c2": 200_000, "c3": 100_000, "c4": 400_000, "c5": 400_000,
