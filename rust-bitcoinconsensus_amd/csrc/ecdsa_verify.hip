@@ -1,15 +1,21 @@
-// ECDSA verify on gfx950: stages (b) and (c) of the hot path.  One lane = one tuple; the
-// per-lane algorithm is ecdsa_lane.h.
+// ECDSA verify on gfx950: stages (b) and (c) of the hot path.  One lane = one tuple.
 //
+// Default, square-root-free path (ecdsa_twist.h):
 //   K_inv     batch_sinv_kernel     s^-1 mod n by Montgomery's trick over strided chunks of <= 16
-//                                   tuples (3 mults/tuple + one Fermat inversion per chunk)
-//   K_key     ecdsa_key_kernel      pubkey parse / decompression (square root), high occupancy
-//   K_prep    ecdsa_prep_kernel     scalar checks, u1/u2, GLV split, Q table
-//   K_ladder  ecdsa_ladder_kernel   Strauss ladder (shared doublings) + inversion-free x-check
-// K_inv and K_key need only the s and key rows: DeviceBatch::run launches them on a side stream
-// beside the sighash kernels.  K_prep and K_ladder are separate launches so that each gets its
-// own register allocation (ladder: 4 waves per SIMD).  Tuples are processed in chunks of up to
-// 4M lanes so the per-tuple scratch (Q table + ladder state, ~900 B) stays bounded.
+//                                   tuples (3 mults/tuple + one sliding-window Fermat inversion)
+//   K_tprep   ecdsa_tprep_kernel    key parse without a square root, v = x^3 + 7, Q_w = (x v, v^2),
+//                                   u1 u2, GLV split, co-Z Q_w table
+//   K_tladder twist_ladder_kernel   B = u2 Q_w (Strauss, shared doublings), A = u1 G (fixed-base
+//                                   comb from HBM tables), alpha / beta / K of the x-test
+//   K_tfin    twist_fin_kernel      batched beta^-1, "gamma = -alpha / beta is the key's y",
+//                                   exact fallback for the exceptional lanes
+// BIP340 runs the same three kernels (schnorr_tprep_kernel, twist_*_kernel<true>).
+// Round-1 path (BCC_ECDSA_PATH=legacy): K_inv, K_key (pubkey decompression), K_prep, K_ladder
+// (G tables in LDS), and for BIP340 schnorr_{prep,ladder,parity}_kernel.
+// K_inv needs only the s rows: DeviceBatch::run launches it on a side stream beside the sighash
+// kernels.  Prep and ladder are separate launches so that each gets its own register allocation
+// (ladder: 4 waves per SIMD).  Tuples are processed in chunks of up to 4M lanes so the per-tuple
+// scratch (Q table + ladder state, ~1.4 KB) stays bounded.
 //
 // HBM layout (all device-resident):
 //   tag[n]            u8   pubkey header byte (0 = rejected by the host length filter)

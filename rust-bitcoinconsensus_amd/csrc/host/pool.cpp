@@ -25,6 +25,7 @@ int size_class(size_t bytes) {
 
 std::mutex g_mu;
 Block* g_free[NCLASS] = {};  // the reservoir (guarded by g_mu)
+size_t g_chunks = 0;         // chunks carved so far (guarded by g_mu)
 
 struct Cache {
     Block* head[NCLASS] = {};
@@ -53,6 +54,7 @@ void refill(Cache& pc, int c) {
     // carve a new chunk into blocks of this class (never freed: bounded by the peak live count)
     char* m = static_cast<char*>(std::malloc(CHUNK_BYTES));
     if (!m) throw std::bad_alloc();
+    g_chunks++;
     const size_t sz = CLASS_BYTES[c];
     for (size_t off = 0; off + sz <= CHUNK_BYTES; off += sz) {
         Block* b = reinterpret_cast<Block*>(m + off);
@@ -62,6 +64,11 @@ void refill(Cache& pc, int c) {
 }
 
 }  // namespace
+
+size_t pool_chunks() {
+    std::lock_guard<std::mutex> lk(g_mu);
+    return g_chunks;
+}
 
 void* pool_alloc(size_t bytes) {
     const int c = size_class(bytes);

@@ -15,6 +15,7 @@ namespace host {
 
 void* pool_alloc(size_t bytes);
 void pool_free(void* p, size_t bytes);
+size_t pool_chunks();  // 64 KiB chunks carved so far (tests: the reservoir bounds the growth)
 
 template <class T>
 struct PoolAlloc {
