@@ -194,6 +194,7 @@ public:
         uint8_t ybuf[32] = {0};
         const uint8_t* y = pub.size() == 65 ? pub.data() + 33 : ybuf;  // y unused for 02/03
         uint32_t row = rows.add(pub[0], pub.data() + 1, y, r, s, one);
+        if (pub.size() == 65) rows.y_unused = false;
         if (sv == SIGVERSION_BASE && legacy_all_type(hashtype)) {
             // device-assembled from the tx template (pipeline.h TplJob)
             if (it.tx->tpl < 0) {
@@ -221,7 +222,18 @@ public:
             // BIP143 assembled on the device from the raw tx bytes (pipeline.h WinJob): the
             // host appends the tx once per round and a record per check
             if (it.tx->wtx < 0) {
-                it.tx->wtx = (int32_t)jobs.add_wtx(it.in->tx_to, it.in->tx_to_len, tx.vin.size());
+                const uint8_t* raw = it.in->tx_to;
+                const size_t len = it.in->tx_to_len;
+                if (tx.has_witness() && !tx.vout.empty() && len > 10) {
+                    // upload the tx without marker, flag and witnesses (BIP144 layout: the
+                    // inputs start at byte 6, the outputs end where the witnesses begin)
+                    const Span& last = tx.vout.back().ser;
+                    const size_t mid = (size_t)(last.p + last.n - (raw + 6));
+                    it.tx->wtx = (int32_t)jobs.add_wtx3(raw, 4, raw + 6, mid, raw + len - 4, 4,
+                                                        tx.vin.size());
+                } else {
+                    it.tx->wtx = (int32_t)jobs.add_wtx(raw, len, tx.vin.size());
+                }
                 touched.push_back(it.tx);
             }
             scratch.clear();
@@ -268,6 +280,8 @@ public:
     void reset() {
         jobs.clear();
         rows.clear();
+        rows.msg_one = true;   // every row enters with msg = ONE (defer)
+        rows.y_unused = true;  // until a 65-byte key is deferred
         pending.clear();
         for (auto* t : touched) {
             t->aux[0] = t->aux[1] = t->aux[2] = -1;

@@ -97,6 +97,24 @@ struct SighashJobs {
         wtx.push_back(r);
         return (uint32_t)wtx.size() - 1;
     }
+    // the same from three pieces: a segwit tx without its marker, flag and witnesses (version ||
+    // vin || vout || locktime: everything the BIP143 kernels read, at about half the bytes)
+    uint32_t add_wtx3(const uint8_t* a, size_t na, const uint8_t* b, size_t nb, const uint8_t* c,
+                      size_t nc, size_t n_in) {
+        WtxRec r;
+        const size_t n = na + nb + nc;
+        r.tx_off = (uint32_t)txraw.size();
+        r.tx_len = (uint32_t)n;
+        r.in_base = win_entries;
+        r.n_in = (uint32_t)n_in;
+        txraw.insert(txraw.end(), a, a + na);
+        txraw.insert(txraw.end(), b, b + nb);
+        txraw.insert(txraw.end(), c, c + nc);
+        txraw.resize(r.tx_off + ((n + 3) & ~(size_t)3), 0);
+        win_entries += (uint32_t)n_in;
+        wtx.push_back(r);
+        return (uint32_t)wtx.size() - 1;
+    }
     uint32_t add_tpl(const uint8_t* m, size_t n) {
         uint32_t off = (uint32_t)tpl.size();
         tpl.insert(tpl.end(), m, m + n);
@@ -137,6 +155,11 @@ struct SighashJobs {
 // are overwritten on the device by K3; constant ones (SIGHASH_SINGLE bug) are set by the host.
 struct TupleRows {
     std::vector<uint8_t> tag, x, y, r, s, msg;
+    // Producers that know may set these so that staging skips uploading rows (default: upload):
+    // msg_one = every msg row is uint256 ONE (the rows the GPU sighash kernels do not overwrite
+    // keep it; the device initialises the msg rows itself), y_unused = no 65-byte key (the y
+    // rows are never read).  clear() resets both.
+    bool msg_one = false, y_unused = false;
     size_t size() const { return tag.size(); }
     uint32_t add(uint8_t t, const uint8_t* x32, const uint8_t* y32, const uint8_t* r32,
                  const uint8_t* s32, const uint8_t* m32) {
@@ -148,7 +171,10 @@ struct TupleRows {
         msg.insert(msg.end(), m32, m32 + 32);
         return (uint32_t)tag.size() - 1;
     }
-    void clear() { tag.clear(); x.clear(); y.clear(); r.clear(); s.clear(); msg.clear(); }
+    void clear() {
+        tag.clear(); x.clear(); y.clear(); r.clear(); s.clear(); msg.clear();
+        msg_one = y_unused = false;
+    }
 };
 
 // BIP341 / BIP342 signature checks (host/taproot.cpp): single-SHA256 aux messages (a tx's

@@ -717,8 +717,15 @@ int DeviceBatch::stage_parts(const SighashJobs* const* J, const TupleRows* const
     }
     const size_t R = n_rows_;
     // regions filled from the host image first (one copy), device-written ones after them
-    enum { TAG, X, Y, RR, S, M, AUX, PRE, AUX_OFF, AUX_NBLK, PRE_OFF, PRE_NBLK, PRE_ROW, PATCH,
-           TPL, CODE, TJOB, TXRAW, WTX, WJOB, ZEROS, UPLOADED, V = UPLOADED, AUXD, INTAB, TXD, NB };
+    // Y and M go up only when some part needs them (TupleRows::y_unused / msg_one)
+    enum { TAG, X, RR, S, AUX, PRE, AUX_OFF, AUX_NBLK, PRE_OFF, PRE_NBLK, PRE_ROW, PATCH,
+           TPL, CODE, TJOB, TXRAW, WTX, WJOB, ZEROS, UPLOADED, Y = UPLOADED, M, V, AUXD, INTAB, TXD,
+           NB };
+    bool need_y = false, need_m = false;
+    for (size_t p = 0; p < P; p++) {
+        need_y |= !Rw[p]->y_unused && Rw[p]->size() != 0;
+        need_m |= !Rw[p]->msg_one && Rw[p]->size() != 0;
+    }
     size_t sizes[NB] = {};
     sizes[TAG] = R; sizes[X] = sizes[Y] = sizes[RR] = sizes[S] = sizes[M] = 32 * R;
     sizes[AUX] = auxb0[P]; sizes[PRE] = preb0[P];
@@ -734,7 +741,7 @@ int DeviceBatch::stage_parts(const SighashJobs* const* J, const TupleRows* const
         off[i] = total;
         total += align256(sizes[i]);
     }
-    const size_t upload = off[UPLOADED];
+    const size_t upload = off[UPLOADED], upload_ym = off[V];  // the image holds Y and M too
     if (total > cap_) {
         if (arena_) BCC_HIP_TRY(hipFree(arena_));
         arena_ = nullptr;
@@ -742,12 +749,12 @@ int DeviceBatch::stage_parts(const SighashJobs* const* J, const TupleRows* const
         BCC_HIP_TRY(hipMalloc(&arena_, total));
         cap_ = total;
     }
-    if (upload > host_cap_) {
+    if (upload_ym > host_cap_) {
         if (host_image_) BCC_HIP_TRY(hipHostFree(host_image_));
         host_image_ = nullptr;
         host_cap_ = 0;
-        BCC_HIP_TRY(hipHostMalloc(&host_image_, upload, hipHostMallocDefault));
-        host_cap_ = upload;
+        BCC_HIP_TRY(hipHostMalloc(&host_image_, upload_ym, hipHostMallocDefault));
+        host_cap_ = upload_ym;
     }
     uint8_t* a = (uint8_t*)arena_;
     d_tag = a + off[TAG]; d_x = a + off[X]; d_y = a + off[Y]; d_r = a + off[RR]; d_s = a + off[S];
@@ -770,10 +777,10 @@ int DeviceBatch::stage_parts(const SighashJobs* const* J, const TupleRows* const
         };
         cp(TAG, r0, rw.tag.data(), nr);
         cp(X, 32 * r0, rw.x.data(), 32 * nr);
-        cp(Y, 32 * r0, rw.y.data(), 32 * nr);
+        if (need_y) cp(Y, 32 * r0, rw.y.data(), 32 * nr);
         cp(RR, 32 * r0, rw.r.data(), 32 * nr);
         cp(S, 32 * r0, rw.s.data(), 32 * nr);
-        cp(M, 32 * r0, rw.msg.data(), 32 * nr);
+        if (need_m) cp(M, 32 * r0, rw.msg.data(), 32 * nr);
         cp(AUX, auxb0[p], j.aux.data(), j.aux.size());
         cp(PRE, preb0[p], j.pre.data(), j.pre.size());
         const uint32_t ablk = (uint32_t)(auxb0[p] / 64), pblk = (uint32_t)(preb0[p] / 64);
@@ -831,6 +838,13 @@ int DeviceBatch::stage_parts(const SighashJobs* const* J, const TupleRows* const
     }
     BCC_HIP_TRY(hipSetDevice(dev_));
     BCC_HIP_TRY(hipMemcpy(arena_, host_image_, upload, hipMemcpyHostToDevice));
+    if (need_y) BCC_HIP_TRY(hipMemcpy(a + off[Y], h + off[Y], 32 * R, hipMemcpyHostToDevice));
+    if (need_m) {
+        BCC_HIP_TRY(hipMemcpy(a + off[M], h + off[M], 32 * R, hipMemcpyHostToDevice));
+    } else if (R) {  // every row's msg is uint256 ONE (byte 0 = 1); the sighash kernels overwrite theirs
+        BCC_HIP_TRY(hipMemset(a + off[M], 0, 32 * R));
+        BCC_HIP_TRY(hipMemset2D(a + off[M], 32, 1, 1, R));
+    }
     return 0;
 }
 
