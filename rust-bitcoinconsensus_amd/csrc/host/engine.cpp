@@ -89,6 +89,11 @@ struct Item {
     };
     std::vector<Check> cache;
     std::vector<uint32_t> pending;  // deferred rows the last run consulted (answered "true")
+    // HASH160 of the P2WPKH witness key, computed ahead in a batch by prepare() (h160_src: the
+    // hashed bytes; null when none)
+    const uint8_t* h160_src = nullptr;
+    uint32_t h160_len = 0;
+    uint8_t h160[20];
 };
 
 struct Pending {
@@ -133,6 +138,10 @@ public:
     bool check_ecdsa(const Bytes& sig, const Bytes& pub, const Bytes& code, SigVersion sv) override;
     void hint_ecdsa(const Bytes& sig, const Bytes& pub, const Bytes& code, SigVersion sv) override;
     bool hint_all() const override { return it_.runs > 1; }  // a re-run: queue every pair
+    const uint8_t* cached_hash160(const uint8_t* p, size_t n) const override {
+        return it_.h160_src && n == it_.h160_len && memcmp(p, it_.h160_src, n) == 0 ? it_.h160
+                                                                                     : nullptr;
+    }
     bool check_locktime(int64_t n) override { return tx_check_locktime(it_.tx->tx, it_.in->n_in, n); }
     bool check_sequence(int64_t n) override { return tx_check_sequence(it_.tx->tx, it_.in->n_in, n); }
 
@@ -385,6 +394,36 @@ void prepare(BatchState& b, const bcc_batch_item* items, size_t n, unsigned flag
                 }
             }
         }
+        // HASH160 of every P2WPKH witness key of this thread's share, eight at a time (the
+        // interpreter's OP_HASH160 finds it by content, DeferringChecker::cached_hash160)
+        const size_t i0 = share_lo(E, t, T) < E ? b.tx_first[share_lo(E, t, T)] : n;
+        const size_t i1 = share_lo(E, t + 1, T) < E ? b.tx_first[share_lo(E, t + 1, T)] : n;
+        constexpr size_t BATCH = 64;
+        const uint8_t* hp[BATCH];
+        size_t hn[BATCH];
+        uint8_t* ho[BATCH];
+        size_t k = 0;
+        auto flush = [&] {
+            if (k) hash160_batch(hp, hn, ho, k);
+            k = 0;
+        };
+        for (size_t i = i0; i < i1; i++) {
+            Item& it = st[i];
+            it.h160_src = nullptr;
+            if (!it.active) continue;
+            const bcc_batch_item* in = it.in;
+            const uint8_t* spk = in->script_pubkey;
+            if (in->script_pubkey_len != 22 || spk[0] != 0x00 || spk[1] != 0x14) continue;
+            const auto& wit = it.tx->tx.vin[in->n_in].witness;
+            if (wit.size() != 2 || (wit[1].n != 33 && wit[1].n != 65)) continue;
+            it.h160_src = wit[1].p;
+            it.h160_len = (uint32_t)wit[1].n;
+            hp[k] = wit[1].p;
+            hn[k] = wit[1].n;
+            ho[k] = it.h160;
+            if (++k == BATCH) flush();
+        }
+        flush();
     });
 }
 

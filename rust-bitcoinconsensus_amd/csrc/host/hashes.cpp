@@ -270,6 +270,83 @@ void ripemd160(const uint8_t* p, size_t n, uint8_t out[20]) {
     }
 }
 
+// RIPEMD-160 of eight 32-byte messages at once (the second half of HASH160), one message per
+// 32-bit lane of AVX2 registers: the same 80 double-line steps as ripemd160_block, unrolled so
+// that selectors, word indices and rotations are constants.
+namespace {
+#define RV_ROL(x, n) _mm256_or_si256(_mm256_slli_epi32((x), (n)), _mm256_srli_epi32((x), 32 - (n)))
+__attribute__((target("avx2"))) inline __m256i rfv(int j, __m256i x, __m256i y, __m256i z) {
+    const __m256i ones = _mm256_set1_epi32(-1);
+    switch (j / 16) {
+        case 0: return _mm256_xor_si256(_mm256_xor_si256(x, y), z);
+        case 1: return _mm256_or_si256(_mm256_and_si256(x, y), _mm256_andnot_si256(x, z));
+        case 2: return _mm256_xor_si256(_mm256_or_si256(x, _mm256_xor_si256(y, ones)), z);
+        case 3: return _mm256_or_si256(_mm256_and_si256(x, z), _mm256_andnot_si256(z, y));
+        default: return _mm256_xor_si256(x, _mm256_or_si256(y, _mm256_xor_si256(z, ones)));
+    }
+}
+
+__attribute__((target("avx2"))) void ripemd160_32x8_avx2(const uint8_t* const in[8],
+                                                          uint8_t* const out[8]) {
+    __m256i X[16];
+    for (int w = 0; w < 8; w++)
+        X[w] = _mm256_setr_epi32((int)le32(in[0] + 4 * w), (int)le32(in[1] + 4 * w),
+                                 (int)le32(in[2] + 4 * w), (int)le32(in[3] + 4 * w),
+                                 (int)le32(in[4] + 4 * w), (int)le32(in[5] + 4 * w),
+                                 (int)le32(in[6] + 4 * w), (int)le32(in[7] + 4 * w));
+    X[8] = _mm256_set1_epi32(0x80);  // padding of a 32-byte message: 0x80, zeros, bit length 256
+    for (int w = 9; w < 16; w++) X[w] = _mm256_setzero_si256();
+    X[14] = _mm256_set1_epi32(256);
+    const uint32_t H[5] = {0x67452301, 0xEFCDAB89, 0x98BADCFE, 0x10325476, 0xC3D2E1F0};
+    __m256i al = _mm256_set1_epi32((int)H[0]), bl = _mm256_set1_epi32((int)H[1]),
+            cl = _mm256_set1_epi32((int)H[2]), dl = _mm256_set1_epi32((int)H[3]),
+            el = _mm256_set1_epi32((int)H[4]);
+    __m256i ar = al, br = bl, cr = cl, dr = dl, er = el;
+#pragma GCC unroll 80
+    for (int j = 0; j < 80; j++) {
+        __m256i t = _mm256_add_epi32(_mm256_add_epi32(al, rfv(j, bl, cl, dl)),
+                                     _mm256_add_epi32(X[RL[j]], _mm256_set1_epi32((int)KL[j / 16])));
+        t = _mm256_add_epi32(RV_ROL(t, SL[j]), el);
+        al = el; el = dl; dl = RV_ROL(cl, 10); cl = bl; bl = t;
+        t = _mm256_add_epi32(_mm256_add_epi32(ar, rfv(79 - j, br, cr, dr)),
+                             _mm256_add_epi32(X[RR[j]], _mm256_set1_epi32((int)KR[j / 16])));
+        t = _mm256_add_epi32(RV_ROL(t, SR[j]), er);
+        ar = er; er = dr; dr = RV_ROL(cr, 10); cr = br; br = t;
+    }
+    __m256i h[5];
+    h[0] = _mm256_add_epi32(_mm256_add_epi32(_mm256_set1_epi32((int)H[1]), cl), dr);
+    h[1] = _mm256_add_epi32(_mm256_add_epi32(_mm256_set1_epi32((int)H[2]), dl), er);
+    h[2] = _mm256_add_epi32(_mm256_add_epi32(_mm256_set1_epi32((int)H[3]), el), ar);
+    h[3] = _mm256_add_epi32(_mm256_add_epi32(_mm256_set1_epi32((int)H[4]), al), br);
+    h[4] = _mm256_add_epi32(_mm256_add_epi32(_mm256_set1_epi32((int)H[0]), bl), cr);
+    alignas(32) uint32_t v[5][8];
+    for (int k = 0; k < 5; k++) _mm256_store_si256(reinterpret_cast<__m256i*>(v[k]), h[k]);
+    for (int m = 0; m < 8; m++)
+        for (int k = 0; k < 5; k++)
+            for (int b = 0; b < 4; b++) out[m][4 * k + b] = (uint8_t)(v[k][m] >> (8 * b));
+}
+#undef RV_ROL
+
+bool have_avx2() {
+    static const bool v = __builtin_cpu_supports("avx2") && !getenv("BCC_NO_AVX2");
+    return v;
+}
+}  // namespace
+
+void hash160_batch(const uint8_t* const* p, const size_t* n, uint8_t* const* out, size_t count) {
+    size_t i = 0;
+    if (have_avx2()) {
+        uint8_t d[8][32];
+        const uint8_t* in[8];
+        for (int k = 0; k < 8; k++) in[k] = d[k];
+        for (; i + 8 <= count; i += 8) {
+            for (int k = 0; k < 8; k++) sha256(p[i + k], n[i + k], d[k]);
+            ripemd160_32x8_avx2(in, out + i);
+        }
+    }
+    for (; i < count; i++) hash160(p[i], n[i], out[i]);
+}
+
 void hash160(const uint8_t* p, size_t n, uint8_t out[20]) {
     uint8_t t[32];
     sha256(p, n, t);

@@ -24,6 +24,8 @@ void sha1(const uint8_t* p, size_t n, uint8_t out[20]);
 void ripemd160(const uint8_t* p, size_t n, uint8_t out[20]);
 bool sha256_uses_shani();                                                 // x86 SHA extensions in use
 void hash160(const uint8_t* p, size_t n, uint8_t out[20]);              // RIPEMD160(SHA256(x))
+// hash160 of count messages (eight at a time: RIPEMD-160 of the digests on AVX2 when present)
+void hash160_batch(const uint8_t* const* p, const size_t* n, uint8_t* const* out, size_t count);
 
 }  // namespace host
 }  // namespace bcc

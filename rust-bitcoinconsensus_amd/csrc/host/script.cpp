@@ -460,7 +460,11 @@ bool eval_script(std::vector<Bytes>& stack, const uint8_t* script, size_t script
                         if (opcode == OP_RIPEMD160) ripemd160(v.data(), v.size(), h.data());
                         else if (opcode == OP_SHA1) sha1(v.data(), v.size(), h.data());
                         else if (opcode == OP_SHA256) sha256(v.data(), v.size(), h.data());
-                        else if (opcode == OP_HASH160) hash160(v.data(), v.size(), h.data());
+                        else if (opcode == OP_HASH160) {
+                            const uint8_t* c = checker.cached_hash160(v.data(), v.size());
+                            if (c) memcpy(h.data(), c, 20);
+                            else hash160(v.data(), v.size(), h.data());
+                        }
                         else sha256d(v.data(), v.size(), h.data());
                         popstack(stack);
                         stack.push_back(std::move(h));

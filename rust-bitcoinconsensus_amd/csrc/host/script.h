@@ -88,6 +88,9 @@ public:
     // checker turns this on for items that already needed a re-run, so that the key advance of
     // an m-of-n with many keys costs at most one more device round.
     virtual bool hint_all() const { return false; }
+    // HASH160 of `p` if the checker already holds it (computed ahead in a batch for exactly these
+    // bytes), else nullptr; OP_HASH160 then uses it instead of hashing again.
+    virtual const uint8_t* cached_hash160(const uint8_t*, size_t) const { return nullptr; }
     virtual bool check_locktime(int64_t n) = 0;
     virtual bool check_sequence(int64_t n) = 0;
 };

@@ -8,4 +8,19 @@ void th_sha1(const unsigned char* p, unsigned long n, unsigned char* out) { bcc:
 void th_ripemd160(const unsigned char* p, unsigned long n, unsigned char* out) { bcc::host::ripemd160(p, n, out); }
 void th_hash160(const unsigned char* p, unsigned long n, unsigned char* out) { bcc::host::hash160(p, n, out); }
 int th_shani() { return bcc::host::sha256_uses_shani() ? 1 : 0; }
+// hash160_batch over count messages packed back to back (lengths in n), digests to out[20 * i]
+void th_hash160_batch(const unsigned char* blob, const unsigned long* n, unsigned long count,
+                      unsigned char* out) {
+    const unsigned char* ptr[64];
+    size_t len[64];
+    unsigned char* o[64];
+    size_t at = 0;
+    for (unsigned long i = 0; i < count && i < 64; i++) {
+        ptr[i] = blob + at;
+        len[i] = n[i];
+        o[i] = out + 20 * i;
+        at += n[i];
+    }
+    bcc::host::hash160_batch(ptr, len, o, count < 64 ? count : 64);
+}
 }

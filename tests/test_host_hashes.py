@@ -76,3 +76,23 @@ def test_host_sha256_portable_path(so):
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True)
     assert r.returncode == 0, r.stderr
     assert r.stdout.strip() == "0"
+
+
+def test_host_hash160_batch_matches_scalar(so):
+    """hash160_batch (eight RIPEMD-160s per AVX2 pass when the CPU has it, the scalar path for the
+    rest) against hash160 on the same messages: key-sized and odd-sized inputs, batch sizes that
+    leave remainders."""
+    import ctypes
+    import random
+    L = ctypes.CDLL(so)
+    rng = random.Random(160)
+    for count in (1, 7, 8, 9, 16, 23, 64):
+        msgs = [rng.randbytes(rng.choice([33, 65, 0, 1, 31, 32, 55, 56, 64, 100, 200]))
+                for _ in range(count)]
+        n = (ctypes.c_ulong * count)(*[len(m) for m in msgs])
+        out = ctypes.create_string_buffer(20 * count)
+        L.th_hash160_batch(b"".join(msgs), n, ctypes.c_ulong(count), out)
+        for i, m in enumerate(msgs):
+            exp = ctypes.create_string_buffer(20)
+            L.th_hash160(m, len(m), exp)
+            assert out.raw[20 * i: 20 * i + 20] == exp.raw, (count, i, len(m))
