@@ -144,7 +144,27 @@ void Sha256::finalize(uint8_t out[32]) {
     }
 }
 
-void sha256(const uint8_t* p, size_t n, uint8_t out[32]) { Sha256().write(p, n).finalize(out); }
+void sha256(const uint8_t* p, size_t n, uint8_t out[32]) {
+    if (n <= 55) {  // one padded block built in place (keys, digests): a single compression
+        alignas(16) uint8_t blk[64];
+        memcpy(blk, p, n);
+        blk[n] = 0x80;
+        memset(blk + n + 1, 0, 55 - n);
+        const uint64_t bits = (uint64_t)n * 8;
+        for (int i = 0; i < 8; i++) blk[56 + i] = (uint8_t)(bits >> (56 - 8 * i));
+        uint32_t st[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a,
+                          0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
+        sha256_block(st, blk);
+        for (int i = 0; i < 8; i++) {
+            out[4 * i] = (uint8_t)(st[i] >> 24);
+            out[4 * i + 1] = (uint8_t)(st[i] >> 16);
+            out[4 * i + 2] = (uint8_t)(st[i] >> 8);
+            out[4 * i + 3] = (uint8_t)st[i];
+        }
+        return;
+    }
+    Sha256().write(p, n).finalize(out);
+}
 
 void sha256d(const uint8_t* p, size_t n, uint8_t out[32]) {
     uint8_t t[32];
@@ -331,6 +351,7 @@ bool have_avx2() {
     static const bool v = __builtin_cpu_supports("avx2") && !getenv("BCC_NO_AVX2");
     return v;
 }
+
 }  // namespace
 
 void hash160_batch(const uint8_t* const* p, const size_t* n, uint8_t* const* out, size_t count) {
@@ -340,6 +361,8 @@ void hash160_batch(const uint8_t* const* p, const size_t* n, uint8_t* const* out
         const uint8_t* in[8];
         for (int k = 0; k < 8; k++) in[k] = d[k];
         for (; i + 8 <= count; i += 8) {
+            // SHA-256 per message with the SHA extensions (an 8-lane AVX2 SHA-256 measured no
+            // faster), then the eight RIPEMD-160s together
             for (int k = 0; k < 8; k++) sha256(p[i + k], n[i + k], d[k]);
             ripemd160_32x8_avx2(in, out + i);
         }
