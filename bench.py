@@ -627,8 +627,8 @@ class C5T:
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", choices=("c2", "c3", "c4", "c5", "c5t"), default="c2")
     ap.add_argument("--n", type=int, default=None,
                     help="units per GPU: inputs (c2), transactions (c3), tuples (c4, c5)")

@@ -95,14 +95,12 @@ struct GCombArray {
     }
 };
 
-// Prep: key parse without a square root, scalar checks, u1 / u2, GLV split of u2, the odd
-// fix-ups and the Q_w table.  Returns false (st.flags = 0) when the tuple is rejected outright:
-// the reference's pubkey parse failures (other than "x^3 + 7 is not a square", which the final
-// test catches) and its r / s range checks (ecdsa_impl.h:216-222).
+// Prep, key half: key parse without a square root and the Q_w table (nothing here depends on
+// the signature or the message, so K_tkey can run beside the sighash kernels).  Returns false
+// (st.flags = 0) on the reference's pubkey parse failures other than "x^3 + 7 is not a square",
+// which the final test catches; else st.flags = LS_VALID | LS_COMP / LS_PAR.
 template <class QT>
-BCC_HD bool twist_prep_lane(u32 tag, const fe& px, const fe& py, const sc& r_in, const sc& s_in,
-                            const sc& m_in, const sc* sinv_pre, QT& qt, TwistState& st) {
-    const u32 N[8] = BCC_N_LIMBS;
+BCC_HD bool twist_prep_key(u32 tag, const fe& px, const fe& py, QT& qt, TwistState& st) {
     st.flags = 0;
     const bool compressed = (tag == 2u || tag == 3u);
     const bool full = (tag == 4u || tag == 6u || tag == 7u);
@@ -122,6 +120,28 @@ BCC_HD bool twist_prep_lane(u32 tag, const fe& px, const fe& py, const sc& r_in,
         if (!fe_equal(t, v)) return false;
         st.ychk = py;
     }
+    st.v = v;
+    // Q_w = (x v, v^2): Q on E_w; the table lands on E_w scaled once more by st.sigma
+    fe qx, qy;
+    fe_mul(qx, px, v);
+    fe_sqr(qy, v);
+#if BCC_QTAB_COZ
+    build_q_table_coz(qx, qy, qt, st.sigma);
+#else
+    build_q_table(qx, qy, qt, st.sigma);
+#endif
+    st.flags = flags;
+    return true;
+}
+
+// Prep, scalar half (after twist_prep_key; `flags` = its st.flags): r / s range checks
+// (ecdsa_impl.h:216-222), u1 / u2, GLV split of u2, the odd fix-ups.  Returns false (st.flags
+// = 0) when the tuple is rejected outright.
+BCC_HD bool twist_prep_scalars(u32 flags, const sc& r_in, const sc& s_in, const sc& m_in,
+                               const sc* sinv_pre, TwistState& st) {
+    const u32 N[8] = BCC_N_LIMBS;
+    st.flags = 0;
+    if (!(flags & LS_VALID)) return false;
     if (u256_is_zero(r_in.v) || u256_is_zero(s_in.v)) return false;
     if (!u256_lt(r_in.v, N) || !u256_lt(s_in.v, N)) return false;
     sc m = m_in;
@@ -165,17 +185,15 @@ BCC_HD bool twist_prep_lane(u32 tag, const fe& px, const fe& py, const sc& r_in,
     }
     st.flags = flags;
     st.r = r_in;
-    st.v = v;
-    // Q_w = (x v, v^2): Q on E_w; the table lands on E_w scaled once more by st.sigma
-    fe qx, qy;
-    fe_mul(qx, px, v);
-    fe_sqr(qy, v);
-#if BCC_QTAB_COZ
-    build_q_table_coz(qx, qy, qt, st.sigma);
-#else
-    build_q_table(qx, qy, qt, st.sigma);
-#endif
     return true;
+}
+
+// Prep: both halves (the rejections of either set st.flags = 0).
+template <class QT>
+BCC_HD bool twist_prep_lane(u32 tag, const fe& px, const fe& py, const sc& r_in, const sc& s_in,
+                            const sc& m_in, const sc* sinv_pre, QT& qt, TwistState& st) {
+    if (!twist_prep_key(tag, px, py, qt, st)) return false;
+    return twist_prep_scalars(st.flags, r_in, s_in, m_in, sinv_pre, st);
 }
 
 // B = u2 Q_w: Strauss over the two GLV halves with shared doublings (the Q slots of

@@ -551,6 +551,54 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
     tw_store(w, T_Y, st.ychk.v);
 }
 
+// The same prep in two halves (ecdsa_launch_key): K_tkey reads only the tag and key rows (it may
+// run beside the sighash kernels and K_inv), K_tscal the r / s / m / s^-1 rows after them.
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void ecdsa_tkey_kernel(
+    const uint8_t* __restrict__ tag, const uint8_t* __restrict__ px,
+    const uint8_t* __restrict__ py, size_t cnt, u32* __restrict__ qtab, u32* __restrict__ state) {
+    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= cnt) return;
+    fe x, y;
+    load_be32(x, px + 32 * t);
+    load_be32(y, py + 32 * t);
+    QTableGlobal qt{lane_table(qtab, t)};
+    TwistState st;
+    const bool ok = twist_prep_key(tag[t], x, y, qt, st);
+    u32* w = lane_words(state, t, TSTATE_WORDS);
+    w[T_FLAGS * LANE_STRIDE] = ok ? st.flags : 0u;
+    if (!ok) return;
+    tw_store(w, T_SIGMA, st.sigma.v);
+    tw_store(w, T_V, st.v.v);
+    tw_store(w, T_Y, st.ychk.v);
+}
+
+__global__ __launch_bounds__(256) void ecdsa_tscal_kernel(
+    const uint8_t* __restrict__ pr, const uint8_t* __restrict__ ps,
+    const uint8_t* __restrict__ pm, const u32* __restrict__ psinv, size_t cnt,
+    u32* __restrict__ state) {
+    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= cnt) return;
+    u32* w = lane_words(state, t, TSTATE_WORDS);
+    const u32 kflags = w[T_FLAGS * LANE_STRIDE];
+    if (!(kflags & LS_VALID)) return;  // K_tkey rejected the key (flags 0)
+    sc r, s, m, si;
+    load_be32(r, pr + 32 * t);
+    load_be32(s, ps + 32 * t);
+    load_be32(m, pm + 32 * t);
+    load_limbs(si, psinv + 8 * t);
+    TwistState st;
+    if (!twist_prep_scalars(kflags, r, s, m, &si, st)) {
+        w[T_FLAGS * LANE_STRIDE] = 0u;
+        return;
+    }
+#pragma unroll
+    for (int a = 0; a < 4; a++)
+#pragma unroll
+        for (int b = 0; b < 4; b++) w[(T_K + a * 4 + b) * LANE_STRIDE] = st.k[a][b];
+    w[T_FLAGS * LANE_STRIDE] = st.flags;
+    tw_store(w, T_R, st.r.v);
+}
+
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void schnorr_tprep_kernel(
     const uint8_t* __restrict__ psig, const uint8_t* __restrict__ pm,
     const uint8_t* __restrict__ ppk, size_t base, size_t cnt, u32* __restrict__ qtab,
@@ -859,9 +907,32 @@ int ecdsa_launch_pre(SigScratch& sc, const uint8_t* d_tag, const uint8_t* d_x,
     return 0;
 }
 
+int ecdsa_launch_key(SigScratch& sc, const uint8_t* d_tag, const uint8_t* d_x,
+                     const uint8_t* d_y, size_t n, void* stream) {
+    static const bool off = [] {  // BCC_KEY_AHEAD=0: the whole prep after K_inv (A/B runs)
+        const char* e = getenv("BCC_KEY_AHEAD");
+        return e && atoi(e) == 0;
+    }();
+    sc.key_ready = 0;
+    if (n == 0 || off || !ecdsa_twist() || n > chunk_lanes()) return 0;
+    int dev = 0, cus = 0;
+    fe* gtab = nullptr;
+    size_t C = 0;
+    if (int e = device_tables(&dev, &gtab, &cus)) return e;
+    if (int e = ensure_scratch(sc, dev, n, true, &C)) return e;
+    u32* qtab = (u32*)sc.chunk;
+    u32* state = qtab + C * QTABLE_WORDS;
+    hipLaunchKernelGGL(ecdsa_tkey_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)stream, d_tag, d_x, d_y, n, qtab, state);
+    BCC_HIP_TRY(hipGetLastError());
+    sc.key_ready = n;
+    return 0;
+}
+
 int ecdsa_launch(SigScratch& sc, const uint8_t* d_tag, const uint8_t* d_x, const uint8_t* d_y,
                  const uint8_t* d_r, const uint8_t* d_s, const uint8_t* d_m, uint8_t* d_verdict,
                  size_t n, void* stream) {
+    sc.key_ready = 0;  // the whole prep runs after K_inv here
     if (int e = ecdsa_launch_pre(sc, d_tag, d_x, d_y, d_s, n, stream)) return e;
     return ecdsa_launch_after_pre(sc, d_tag, d_x, d_y, d_r, d_s, d_m, d_verdict, n, stream);
 }
@@ -882,10 +953,18 @@ int ecdsa_launch_after_pre(SigScratch& sc, const uint8_t* d_tag, const uint8_t* 
         u32* qtab = (u32*)sc.chunk;
         u32* state = qtab + C * QTABLE_WORDS;
         const u32* gcomb = g_gcomb[dev];
+        const bool key_ahead = sc.key_ready == n && n <= C;
+        sc.key_ready = 0;
         for (size_t base = 0; base < n; base += C) {
             const size_t cnt = std::min(C, n - base);
-            hipLaunchKernelGGL(ecdsa_tprep_kernel, dim3((unsigned)((cnt + 255) / 256)), dim3(256),
-                               0, sm, d_tag, d_x, d_y, d_r, d_s, d_m, sinv, base, cnt, qtab, state);
+            if (key_ahead) {
+                hipLaunchKernelGGL(ecdsa_tscal_kernel, dim3((unsigned)((cnt + 255) / 256)),
+                                   dim3(256), 0, sm, d_r, d_s, d_m, sinv, cnt, state);
+            } else {
+                hipLaunchKernelGGL(ecdsa_tprep_kernel, dim3((unsigned)((cnt + 255) / 256)),
+                                   dim3(256), 0, sm, d_tag, d_x, d_y, d_r, d_s, d_m, sinv, base,
+                                   cnt, qtab, state);
+            }
             BCC_HIP_TRY(hipGetLastError());
             if (ev_rows_read && base + cnt >= n)
                 BCC_HIP_TRY(hipEventRecord((hipEvent_t)ev_rows_read, sm));

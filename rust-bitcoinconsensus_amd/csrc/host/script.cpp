@@ -599,6 +599,7 @@ bool verify_witness_program(const std::vector<Span>& witness, int version, const
             sha256(sc.p, sc.n, h);
             if (memcmp(h, program.data(), 32) != 0) return fail(serror, SERR_WITNESS_PROGRAM_MISMATCH);
             std::vector<Bytes> stack;
+            stack.reserve(witness.size() + 4);  // no regrowth in the common scripts
             for (size_t k = 0; k + 1 < witness.size(); k++)
                 stack.emplace_back(witness[k].p, witness[k].p + witness[k].n);
             return execute_witness_script(std::move(stack), sc.p, sc.n, flags, checker, serror);
@@ -608,9 +609,30 @@ bool verify_witness_program(const std::vector<Span>& witness, int version, const
             memcpy(sc + 3, program.data(), 20);
             sc[23] = OP_EQUALVERIFY;
             sc[24] = OP_CHECKSIG;
-            std::vector<Bytes> stack;
-            for (const auto& w : witness) stack.emplace_back(w.p, w.p + w.n);
-            return execute_witness_script(std::move(stack), sc, 25, flags, checker, serror);
+            // execute_witness_script on [sig, key] with this script, unrolled: the same checks in
+            // the same order with the same errors (none of eval_script's size / op-count / stack
+            // limits can trip on this script and a two-element stack)
+            for (const auto& w : witness)
+                if (w.n > MAX_SCRIPT_ELEMENT_SIZE) return fail(serror, SERR_PUSH_SIZE);
+            const Span& ws = witness[0];
+            const Span& wk = witness[1];
+            uint8_t h[20];  // OP_DUP, OP_HASH160
+            const uint8_t* hk = checker.cached_hash160(wk.p, wk.n);
+            if (!hk) {
+                hash160(wk.p, wk.n, h);
+                hk = h;
+            }
+            // <20> OP_EQUALVERIFY
+            if (memcmp(hk, program.data(), 20) != 0) return fail(serror, SERR_EQUALVERIFY);
+            // OP_CHECKSIG (witness v0: no FindAndDelete; scriptCode = the whole script)
+            const Bytes sig(ws.p, ws.p + ws.n), pub(wk.p, wk.p + wk.n), code(sc, sc + 25);
+            if (!sig.empty() && (flags & FLAG_DERSIG) && !is_valid_signature_encoding(sig))
+                return fail(serror, SERR_SIG_DER);
+            // the stack is [result]: clean; false -> EVAL_FALSE
+            if (!checker.check_ecdsa(sig, pub, code, SIGVERSION_WITNESS_V0))
+                return fail(serror, SERR_EVAL_FALSE);
+            if (serror) *serror = SERR_OK;
+            return true;
         }
         return fail(serror, SERR_WITNESS_PROGRAM_WRONG_LENGTH);
     }
@@ -702,6 +724,7 @@ bool verify_script(const Span& script_sig, const Span& spk, const std::vector<Sp
     if (serror) *serror = SERR_UNKNOWN;
     bool had_witness = false;
     std::vector<Bytes> stack, stack_copy;
+    stack.reserve(8);
     if (!eval_script(stack, script_sig.p, script_sig.n, flags, checker, SIGVERSION_BASE, serror))
         return false;
     if (flags & FLAG_P2SH) stack_copy = stack;

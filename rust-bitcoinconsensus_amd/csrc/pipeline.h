@@ -225,6 +225,7 @@ struct SigScratch {
     size_t sinv_cap = 0;   // tuples
     void* chunk = nullptr;
     size_t chunk_cap = 0;  // lanes
+    size_t key_ready = 0;  // tuples whose key half of the prep ran ahead (ecdsa_launch_key)
     SigScratch() = default;
     SigScratch(const SigScratch&) = delete;
     SigScratch& operator=(const SigScratch&) = delete;
@@ -241,6 +242,12 @@ int ecdsa_launch(SigScratch& sc, const uint8_t* d_tag, const uint8_t* d_x, const
 // after them (must be ordered after both, and after the sighash kernels that write m).
 int ecdsa_launch_pre(SigScratch& sc, const uint8_t* d_tag, const uint8_t* d_x,
                      const uint8_t* d_y, const uint8_t* d_s, size_t n, void* stream);
+// The key half of the twist-path prep (K_tkey: key parse and Q_w table, which read only the tag and
+// key rows) launched ahead on `stream`, e.g. beside the sighash kernels; the next
+// ecdsa_launch_after_pre for the same n (ordered after it) then runs only the scalar half.  A no-op
+// (returns 0) on the legacy path or when n needs more than one scratch chunk.
+int ecdsa_launch_key(SigScratch& sc, const uint8_t* d_tag, const uint8_t* d_x, const uint8_t* d_y,
+                     size_t n, void* stream);
 // ev_rows_read (optional hipEvent_t) is recorded on `stream` once the last kernel that reads the
 // s / m / key rows and the s^-1 rows has been launched (the prep kernel): later writers of those
 // rows (the next run's front kernels) need only wait for it, not for the ladder.
@@ -299,6 +306,7 @@ private:
     void* ev_block_ = nullptr;     // hipEvent_t (blocking sync): host waits sleep, not spin
     int wait(void* stream);
     void* ev_front_ = nullptr;     // hipEvent_t: this run's sighash kernels done (overlap mode)
+    void* ev_key_ = nullptr;       // hipEvent_t: K_tkey (the key half of the prep) done
     bool rows_pending_ = false;    // ev_rows_ recorded by an earlier run (on rows_stream_)
     void* rows_stream_ = nullptr;
     SigScratch scratch_;

@@ -617,6 +617,7 @@ DeviceBatch::~DeviceBatch() {
     if (ev_rows_) (void)hipEventDestroy((hipEvent_t)ev_rows_);
     if (ev_block_) (void)hipEventDestroy((hipEvent_t)ev_block_);
     if (ev_front_) (void)hipEventDestroy((hipEvent_t)ev_front_);
+    if (ev_key_) (void)hipEventDestroy((hipEvent_t)ev_key_);
     if (arena_) (void)hipFree(arena_);
     if (host_image_) (void)hipHostFree(host_image_);
     if (vbuf_) (void)hipHostFree(vbuf_);
@@ -988,15 +989,25 @@ int DeviceBatch::run(void* stream) {
     BCC_HIP_TRY(hipStreamWaitEvent(side, (hipEvent_t)ev_fork_, 0));
     // K_wtx on a stream of its own (a many-input tx's serial hash chains overlap K1 + K3' on the
     // main stream and K_inv + K_key on the side stream)
+    // and the key half of the prep (K_tkey) after it there, beside K_win on the main stream and
+    // K_inv on the side stream; the scalar half waits for all three
+    BCC_HIP_TRY(hipStreamWaitEvent(ws, (hipEvent_t)ev_fork_, 0));
     if (n_wtx_) {
-        BCC_HIP_TRY(hipStreamWaitEvent(ws, (hipEvent_t)ev_fork_, 0));
         if (int e = launch_wtx(ws)) return e;
         BCC_HIP_TRY(hipEventRecord((hipEvent_t)ev_wtx_, ws));
     }
+    if (!ev_key_) {
+        hipEvent_t e = nullptr;
+        BCC_HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        ev_key_ = e;
+    }
+    if (int e = ecdsa_launch_key(scratch_, d_tag, d_x, d_y, n_rows_, ws)) return e;
+    BCC_HIP_TRY(hipEventRecord((hipEvent_t)ev_key_, ws));
     if (int e = ecdsa_launch_pre(scratch_, d_tag, d_x, d_y, d_s, n_rows_, side)) return e;
     BCC_HIP_TRY(hipEventRecord((hipEvent_t)ev_join_, side));
     if (int e = launch_sighash(st, ev_wtx_)) return e;
     BCC_HIP_TRY(hipStreamWaitEvent(st, (hipEvent_t)ev_join_, 0));
+    BCC_HIP_TRY(hipStreamWaitEvent(st, (hipEvent_t)ev_key_, 0));
     return ecdsa_launch_after_pre(scratch_, d_tag, d_x, d_y, d_r, d_s, d_m, d_v, n_rows_, st);
 }
 
