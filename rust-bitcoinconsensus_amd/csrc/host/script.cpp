@@ -579,6 +579,50 @@ bool eval_script(std::vector<Bytes>& stack, const uint8_t* script, size_t script
     return true;
 }
 
+// eval_script of a P2PKH scriptPubKey (DUP HASH160 <20> EQUALVERIFY CHECKSIG, SIGVERSION_BASE) on
+// a stack of 2..100 elements, unrolled: the same checks in the same order with the same errors and
+// the same resulting stack.  With that depth none of eval_script's size / op-count / stack limits
+// can trip, and the script has no OP_CODESEPARATOR, so the scriptCode is the whole script (after
+// FindAndDelete of the signature push, as for any BASE CHECKSIG).  Returns false when the shape
+// does not apply (the caller then runs eval_script); *res holds eval_script's result otherwise.
+bool eval_p2pkh(std::vector<Bytes>& stack, const Span& spk, unsigned flags, SigChecker& checker,
+                ScriptErr* serror, bool* res) {
+    const uint8_t* s = spk.p;
+    if (spk.n != 25 || s[0] != OP_DUP || s[1] != OP_HASH160 || s[2] != 0x14 ||
+        s[23] != OP_EQUALVERIFY || s[24] != OP_CHECKSIG)
+        return false;
+    if (stack.size() < 2 || stack.size() > 100) return false;
+    static const Bytes vch_false;
+    static const Bytes vch_true(1, 1);
+    const Bytes& sig = stack[stack.size() - 2];
+    const Bytes& pub = stack[stack.size() - 1];
+    uint8_t h[20];  // OP_DUP, OP_HASH160
+    const uint8_t* hk = checker.cached_hash160(pub.data(), pub.size());
+    if (!hk) {
+        hash160(pub.data(), pub.size(), h);
+        hk = h;
+    }
+    if (memcmp(hk, s + 3, 20) != 0) {  // <20> OP_EQUALVERIFY
+        *res = fail(serror, SERR_EQUALVERIFY);
+        return true;
+    }
+    Bytes code(s, s + 25);  // OP_CHECKSIG (EvalChecksigPreTapscript, interpreter.cpp:345-369)
+    Bytes pushed;
+    push_data(pushed, sig.data(), sig.size());
+    find_and_delete(code, pushed);
+    if (!sig.empty() && (flags & FLAG_DERSIG) && !is_valid_signature_encoding(sig)) {
+        *res = fail(serror, SERR_SIG_DER);
+        return true;
+    }
+    const bool ok = checker.check_ecdsa(sig, pub, code, SIGVERSION_BASE);
+    popstack(stack);
+    popstack(stack);
+    stack.push_back(ok ? vch_true : vch_false);
+    if (serror) *serror = SERR_OK;
+    *res = true;
+    return true;
+}
+
 bool execute_witness_script(std::vector<Bytes> stack, const uint8_t* script, size_t len,
                             unsigned flags, SigChecker& checker, ScriptErr* serror) {
     for (const auto& e : stack)
@@ -728,7 +772,10 @@ bool verify_script(const Span& script_sig, const Span& spk, const std::vector<Sp
     if (!eval_script(stack, script_sig.p, script_sig.n, flags, checker, SIGVERSION_BASE, serror))
         return false;
     if (flags & FLAG_P2SH) stack_copy = stack;
-    if (!eval_script(stack, spk.p, spk.n, flags, checker, SIGVERSION_BASE, serror)) return false;
+    bool spk_ok;
+    if (!eval_p2pkh(stack, spk, flags, checker, serror, &spk_ok))
+        spk_ok = eval_script(stack, spk.p, spk.n, flags, checker, SIGVERSION_BASE, serror);
+    if (!spk_ok) return false;
     if (stack.empty() || !cast_to_bool(stack.back())) return fail(serror, SERR_EVAL_FALSE);
 
     int wv;
