@@ -131,7 +131,8 @@ int bcc_set_pipeline_chunk(size_t items);
 
 /* bitcoinconsensus_verify_batch keeps its host-side state (items, parsed transactions, job
  * buffers) with the calling thread for reuse by its next call; batches above 4M items release it
- * on return.  This releases the calling thread's state now. */
+ * on return.  bcc_taproot_verify_batch keeps its job buffers the same way.  This releases the
+ * calling thread's state of both now. */
 void bcc_release_thread_state(void);
 
 typedef struct bcc_batch_stats {

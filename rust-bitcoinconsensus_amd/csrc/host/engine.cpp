@@ -966,6 +966,7 @@ int bcc_set_pipeline_chunk(size_t items) {
 
 void bcc_release_thread_state(void) {
     for (auto& c : tl_chunk) c = ChunkRun();
+    bcc::host::taproot_release_thread_state();
 }
 
 int bcc_set_device(int device) {

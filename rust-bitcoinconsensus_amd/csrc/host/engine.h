@@ -20,5 +20,8 @@ size_t build_first_round(const bcc_batch_item* items, size_t n, unsigned flags, 
 void append_round(SighashJobs& dst, TupleRows& dst_rows, const SighashJobs& src,
                   const TupleRows& src_rows);
 
+// Frees the calling thread's Taproot job buffers (host/taproot.cpp).
+void taproot_release_thread_state();
+
 }  // namespace host
 }  // namespace bcc

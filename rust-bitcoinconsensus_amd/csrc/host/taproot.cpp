@@ -17,6 +17,7 @@
 
 #include "bcc_amd.h"
 #include "devices.h"
+#include "engine.h"
 #include "tuples.h"
 #include "tx.h"
 
@@ -37,6 +38,9 @@ struct Part {
     TaprootJobs jobs;
     std::vector<uint32_t> item_of_row;  // row -> item index (absolute)
 };
+
+// job parts of the calling thread (run_range; released by bcc_release_thread_state)
+thread_local std::vector<Part> tl_parts;
 
 // The parsed tx (and spent outputs) an adjacent run of items shares, plus the aux message
 // index of each per-tx hash in the current part (-1: not added yet).
@@ -103,6 +107,8 @@ uint32_t tx_aux(TxState& s, TaprootJobs& J, int kind, std::vector<uint8_t>& scra
 void build_part(const bcc_taproot_check* items, size_t lo, size_t hi, int* ret, int* serr,
                 Part& P) {
     TaprootJobs& J = P.jobs;
+    J.clear();
+    P.item_of_row.clear();
     const size_t cnt = hi - lo;  // capacity for the common shape (a key path spend of its own tx)
     J.aux.reserve(cnt * 5 * 64);
     J.aux_off.reserve(cnt * 5);
@@ -224,18 +230,22 @@ int run_range(const bcc_taproot_check* items, size_t lo, size_t hi, int* ret, in
         if (c > cut.back() && c < hi) cut.push_back(c);
     }
     cut.push_back(hi);
-    std::vector<Part> parts(cut.size() - 1);
+    // the parts live with the calling thread and keep their capacity across calls: a 1M-check
+    // round fills ~650 MB of job blobs, which fresh vectors would page-fault in every call
+    std::vector<Part>& parts = tl_parts;
+    if (parts.size() < cut.size() - 1) parts.resize(cut.size() - 1);
     {
         std::vector<std::thread> th;
-        for (size_t p = 1; p < parts.size(); p++)
+        for (size_t p = 1; p + 1 < cut.size(); p++)
             th.emplace_back(build_part, items, cut[p], cut[p + 1], ret, serr, std::ref(parts[p]));
         build_part(items, cut[0], cut[1], ret, serr, parts[0]);
         for (auto& x : th) x.join();
     }
+    const size_t NP = cut.size() - 1;
     size_t aux_b = 0, msg_b = 0;
-    for (const Part& p : parts) {
-        aux_b += p.jobs.aux.size();
-        msg_b += p.jobs.msg.size();
+    for (size_t p = 0; p < NP; p++) {
+        aux_b += parts[p].jobs.aux.size();
+        msg_b += parts[p].jobs.msg.size();
     }
     if ((aux_b >= ((size_t)1 << 32) || msg_b >= ((size_t)1 << 32)) && hi - lo > 1) {
         const size_t mid = lo + (hi - lo) / 2;
@@ -244,7 +254,8 @@ int run_range(const bcc_taproot_check* items, size_t lo, size_t hi, int* ret, in
     }
     std::vector<const TaprootJobs*> pj;
     std::vector<uint32_t> item_of_row;
-    for (const Part& q : parts) {
+    for (size_t p = 0; p < NP; p++) {
+        const Part& q = parts[p];
         pj.push_back(&q.jobs);
         item_of_row.insert(item_of_row.end(), q.item_of_row.begin(), q.item_of_row.end());
     }
@@ -266,6 +277,9 @@ int run_range(const bcc_taproot_check* items, size_t lo, size_t hi, int* ret, in
 }
 
 }  // namespace
+
+void taproot_release_thread_state() { std::vector<Part>().swap(tl_parts); }
+
 }  // namespace host
 }  // namespace bcc
 

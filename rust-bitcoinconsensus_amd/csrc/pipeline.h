@@ -189,6 +189,10 @@ struct TaprootJobs {
     std::vector<PatchRec> patches;                   // aux digest -> msg blob byte offset
     std::vector<uint8_t> sig64, pk32;                // BIP340 rows
     size_t rows() const { return pk32.size() / 32; }
+    void clear() {  // keeps the capacity (a caller's next round reuses it)
+        aux.clear(); msg.clear(); aux_off.clear(); aux_nblk.clear(); msg_off.clear();
+        msg_nblk.clear(); msg_row.clear(); patches.clear(); sig64.clear(); pk32.clear();
+    }
     uint32_t add_aux(const uint8_t* m, size_t n) {
         aux_off.push_back((uint32_t)(aux.size() / 64));
         sha_append_padded(aux, m, n);
