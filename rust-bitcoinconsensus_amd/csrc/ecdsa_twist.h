@@ -30,14 +30,14 @@
 namespace bcc {
 
 #ifndef BCC_COMB_BITS
-#define BCC_COMB_BITS 12  // 22 windows x 2048 points = 2.75 MiB of tables (L2-resident per XCD)
+#define BCC_COMB_BITS 13  // 20 windows x 4096 points = 5 MiB of tables (MALL-resident)
 #endif
 #ifndef BCC_QTAB_COZ
 #define BCC_QTAB_COZ 1  // the Q_w table by co-Z additions (build_q_table_coz)
 #endif
 constexpr int WC = BCC_COMB_BITS;                 // comb window: 2^(WC-1) odd multiples per window
 constexpr int CTAB = 1 << (WC - 1);
-constexpr int CTOP = (256 + WC - 1) / WC - 1;     // top window index (21 for WC = 12)
+constexpr int CTOP = (256 + WC - 1) / WC - 1;     // top window index (19 for WC = 13)
 constexpr int CWIN = CTOP + 1;                    // windows
 static_assert(WC * CTOP + 1 + (WC - 1) >= 256, "top comb digit must cover bit 255");
 
