@@ -55,8 +55,8 @@ SEEDS = {"c2": 0x5EED0001, "c3": 0x5EED0003, "c4": 0x5EED0004, "c5": 0x5EED0005,
 # the ECDSA stage's kernels: the square-root-free path (default) or the round-1 path
 _LEGACY = os.environ.get("BCC_ECDSA_PATH") == "legacy"
 ECDSA_KERNELS = ("ecdsa (batch_sinv + ecdsa_key + ecdsa_prep + ecdsa_ladder)" if _LEGACY else
-                 "ecdsa (batch_sinv + ecdsa_tprep + twist_ladder<ecdsa> + twist_fin<ecdsa>; "
-                 "no key square root)")
+                 "ecdsa (batch_sinv + ecdsa_tkey/tscal (or ecdsa_tprep) + twist_ladder<ecdsa> + "
+                 "twist_fin<ecdsa>; no key square root)")
 SCHNORR_KERNELS = ("schnorr (prep + ladder + y-parity batch inversion)" if _LEGACY else
                    "schnorr (schnorr_tprep + twist_ladder<bip340> + twist_fin<bip340>; "
                    "no lift_x square root)")
