@@ -553,80 +553,69 @@ BCC_HD void sc_cond_sub_n(sc& r, u32 carry_in) {
     for (int i = 0; i < 8; i++) r.v[i] = take ? t[i] : r.v[i];
 }
 
-// reduce a 512-bit value mod n: fold 2^256 == NC (129 bits) three times, then subtract
+// Column accumulator (acc: 64 bits, nh: the carry word above it) of the mod-n reduction.
+#if defined(__HIP_DEVICE_COMPILE__)
+__device__ __forceinline__ void sc_mac(u64& acc, u32& nh, u32 a, u32 b) {
+    asm("v_mad_u64_u32 %[acc], vcc, %[a], %[b], %[acc]\n\tv_addc_co_u32_e32 %[nh], vcc, 0, %[nh], vcc"
+        : [acc] "+v"(acc), [nh] "+v"(nh) : [a] "v"(a), [b] "v"(b) : "vcc");
+}
+#else
+inline void sc_mac(u64& acc, u32& nh, u32 a, u32 b) {
+    const u64 p = (u64)a * b;
+    acc += p;
+    nh += acc < p ? 1u : 0u;
+}
+#endif
+BCC_HD void sc_acc(u64& acc, u32& nh, u32 a) { sc_mac(acc, nh, a, 1u); }
+BCC_HD u32 sc_col_out(u64& acc, u32& nh) {  // the column's word; acc moves to the next column
+    const u32 w = lo32(acc);
+    acc = (acc >> 32) | ((u64)nh << 32);
+    nh = 0;
+    return w;
+}
+
+// reduce a 512-bit value mod n: fold 2^256 == NC (129 bits: four limbs and a top 1) three times,
+// each fold by product scanning (one accumulator over the columns, no per-row carry walks), then
+// subtract n at most twice.  Bounds: m < 2^386 (13 limbs), q < 2^260 (9 limbs), s < 2^256 + 2^133.
 BCC_HD void sc_reduce512(sc& r, const u32 (&t)[16]) {
     const u32 NC[5] = BCC_NC_LIMBS;
-    // step 1: m = lo(8) + hi(8) * NC(5)  -> up to 14 limbs (< 2^(256+129+1))
-    u32 m[14];
+    u64 acc = 0;
+    u32 nh = 0;
+    // step 1: m = t_lo + t_hi * NC
+    u32 m[13];
 #pragma unroll
-    for (int i = 0; i < 8; i++) m[i] = t[i];
+    for (int k = 0; k < 13; k++) {
 #pragma unroll
-    for (int i = 8; i < 14; i++) m[i] = 0;
-#pragma unroll
-    for (int i = 0; i < 8; i++) {
-        u64 c = 0;
-#pragma unroll
-        for (int j = 0; j < 5; j++) {
-            c = (u64)t[8 + i] * NC[j] + m[i + j] + (c >> 32);
-            m[i + j] = lo32(c);
-        }
-        // propagate
-#pragma unroll
-        for (int k = i + 5; k < 14; k++) {
-            c = (u64)m[k] + (c >> 32);
-            m[k] = lo32(c);
-        }
+        for (int j = 0; j < 4; j++)
+            if (k - j >= 0 && k - j < 8) sc_mac(acc, nh, t[8 + k - j], NC[j]);
+        if (k >= 4 && k < 12) sc_acc(acc, nh, t[8 + k - 4]);
+        if (k < 8) sc_acc(acc, nh, t[k]);
+        m[k] = sc_col_out(acc, nh);
     }
-    // step 2: q = m_lo(8) + m_hi(6) * NC -> up to 10 limbs (< 2^(256+1) + 2^(192+129+1))
-    u32 q[10];
+    // step 2: q = m_lo + m_hi * NC (m_hi = m[8..12] < 2^130)
+    acc = 0;
+    nh = 0;
+    u32 q[9];
 #pragma unroll
-    for (int i = 0; i < 8; i++) q[i] = m[i];
-    q[8] = q[9] = 0;
+    for (int k = 0; k < 9; k++) {
 #pragma unroll
-    for (int i = 0; i < 6; i++) {
-        u64 c = 0;
-#pragma unroll
-        for (int j = 0; j < 5; j++) {
-            if (i + j < 10) {
-                c = (u64)m[8 + i] * NC[j] + q[i + j] + (c >> 32);
-                q[i + j] = lo32(c);
-            }
-        }
-#pragma unroll
-        for (int k = i + 5; k < 10; k++) {
-            c = (u64)q[k] + (c >> 32);
-            q[k] = lo32(c);
-        }
+        for (int j = 0; j < 4; j++)
+            if (k - j >= 0 && k - j < 5) sc_mac(acc, nh, m[8 + k - j], NC[j]);
+        if (k >= 4) sc_acc(acc, nh, m[8 + k - 4]);
+        if (k < 8) sc_acc(acc, nh, m[k]);
+        q[k] = sc_col_out(acc, nh);
     }
-    // step 3: s = q_lo(8) + q_hi(2) * NC -> < 2^257
-    u32 s8[8];
+    // step 3: s = q_lo + q[8] * NC (q[8] < 16)
+    acc = 0;
+    nh = 0;
 #pragma unroll
-    for (int i = 0; i < 8; i++) s8[i] = q[i];
-    u32 carry = 0;
-    {
-        u64 c = 0;
-        u32 add[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        // hi2 * NC (2 limbs x 5 limbs -> 7 limbs)
-#pragma unroll
-        for (int i = 0; i < 2; i++) {
-            c = 0;
-#pragma unroll
-            for (int j = 0; j < 5; j++) {
-                c = (u64)q[8 + i] * NC[j] + add[i + j] + (c >> 32);
-                add[i + j] = lo32(c);
-            }
-            add[i + 5] = lo32((u64)add[i + 5] + (c >> 32));
-        }
-        c = 0;
-#pragma unroll
-        for (int i = 0; i < 8; i++) {
-            c = (u64)s8[i] + add[i] + (c >> 32);
-            s8[i] = lo32(c);
-        }
-        carry = hi32(c);
+    for (int k = 0; k < 8; k++) {
+        if (k < 4) sc_mac(acc, nh, q[8], NC[k]);
+        if (k == 4) sc_acc(acc, nh, q[8]);
+        sc_acc(acc, nh, q[k]);
+        r.v[k] = sc_col_out(acc, nh);
     }
-#pragma unroll
-    for (int i = 0; i < 8; i++) r.v[i] = s8[i];
+    const u32 carry = lo32(acc);  // bit 256 of s
     sc_cond_sub_n(r, carry);
     sc_cond_sub_n(r, 0);
 }

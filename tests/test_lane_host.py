@@ -180,3 +180,21 @@ def test_lane_schnorr_twist_random_vs_legacy_lane(lane):
             bad.append((i, mode, got, exp))
     assert not bad, bad[:10]
     assert (0, 1) in seen and (1, 0) in seen
+
+
+def test_lane_scalar_mul_inv_mod_n(lane):
+    """sc_mul / sc_inv (the mod-n product-scanning reduction) against Python integers: random
+    operands, the edge values 0, 1, n - 1, n - 2 and operands just below 2^256 (reduced inputs
+    are < n, but the fold must hold for any 512-bit product)."""
+    rnd = random.Random(0x5C)
+    edge = [0, 1, 2, N - 1, N - 2, (1 << 255), N >> 1, (1 << 256) - 1]
+    pairs = [(a, b) for a in edge for b in edge]
+    pairs += [(rnd.getrandbits(256), rnd.getrandbits(256)) for _ in range(3000)]
+    out = ctypes.create_string_buffer(32)
+    for a, b in pairs:
+        lane.lane_sc_mul(a.to_bytes(32, "big"), b.to_bytes(32, "big"), out)
+        assert int.from_bytes(out.raw, "big") == (a * b) % N, (hex(a), hex(b))
+    for _ in range(200):
+        a = rnd.randrange(1, N)
+        lane.lane_sc_inv(a.to_bytes(32, "big"), out)
+        assert int.from_bytes(out.raw, "big") == pow(a, -1, N)
