@@ -104,6 +104,27 @@ void bcc_workload_shape(const bcc_workload* w, size_t* tuples, size_t* sighash_b
 size_t bcc_workload_item(const bcc_workload* w, size_t i, uint8_t* spk, size_t* spk_len,
                          int64_t* amount, uint8_t* tx, size_t cap);
 
+/* ---- the GPU sighash stage alone (tests) ----------------------------------------------------
+ * One signature check's SignatureHash inputs (interpreter.cpp:1576-1642): the spending tx, the
+ * input index, the scriptCode as the checker receives it (OP_CODESEPARATORs still in for legacy:
+ * the serializer drops them), the full 32-bit hash type, the amount (BIP143) and the SigVersion
+ * (0 BASE, 1 WITNESS_V0). */
+typedef struct bcc_sighash_check {
+    const uint8_t* tx;
+    size_t tx_len;
+    const uint8_t* script_code;
+    size_t script_code_len;
+    unsigned int n_in;
+    int32_t hashtype;
+    int64_t amount;
+    int sigversion;
+} bcc_sighash_check;
+/* Builds each check's device job exactly as the batch engine's deferring checker does and runs
+ * only the sighash kernels on `device`; msg32_out receives the n message rows the ECDSA kernels
+ * would read (the SHA-256d sighash as raw uint256 bytes; uint256 ONE for the SIGHASH_SINGLE bug).
+ * Returns 0, -1 for a tx that does not parse / a bad index or sigversion, or a HIP error. */
+int bcc_debug_sighash(const bcc_sighash_check* checks, size_t n, uint8_t* msg32_out, int device);
+
 /* ---- generator kernels (synthetic inputs; not on the verification path) -------------------- */
 int mi_gen_pubkeys(const uint8_t* d32, size_t n, uint8_t* x32, uint8_t* y32, uint8_t* ok,
                    int device);
@@ -115,6 +136,16 @@ int mi_gen_schnorr_sign(const uint8_t* d32, const uint8_t* m32, const uint8_t* k
 
 /* ---- integer-ALU microbenchmark (the roofline peak) ---------------------------------------- */
 int mi_microbench(int op, int iters, double* rate);
+/* Sustained form (the roofline peak): waves_per_simd waves of op per SIMD, launches of about
+ * target_ms back to back for warm_s seconds, then reps timed launches; median lane-instructions/s,
+ * median in-kernel clock (GHz, s_memtime / s_memrealtime stamps per wave) and launch time. */
+int mi_microbench_sustained(int op, int waves_per_simd, double target_ms, double warm_s, int reps,
+                            double* rate, double* clock_ghz, double* ms);
+
+/* Per-primitive cost (tests of the ladder's cost model): prim 0 fe_mul, 1 fe_sqr, 2 fe_add,
+ * 3 fe_sub, 4 fe_shl<1>, 5 gej_double, 6 gej_add_zinv (mixed), looped iters times per lane at
+ * 4 waves per SIMD; *cycles = median SIMD-clock cycles per primitive per wave. */
+int mi_primbench(int prim, int iters, int warm, double* cycles, double* ms);
 
 /* ---- field self-test (tests only): one device Fp operation over n operand pairs ------------
  * a, b, out: n x 8 little-endian u32 limbs.  op: 0 add, 1 sub, 2 mul, 3 sqr, 4/5/6 shift by

@@ -16,6 +16,8 @@
 //                            tx's PrecomputedTransactionData initialised with its spent outputs
 //                            (interpreter.cpp:1422-1472, 1491-1574, 1678-1704); the signature hash
 //                            is captured at VerifySchnorrSignature
+//   * ref_check_sighash   -> SignatureHash as CheckECDSASignature computes it for one check
+//                            (interpreter.cpp:1576-1642, 1656-1676)
 //   * ref_sign / ref_pubkey_create / ref_schnorr_sign: fixture generation only
 //   * ref_bench_* / ref_bulk_* -> dynamically chunked std::thread pool over the reference entry
 //                            points (cpu_baseline timing, bulk agreement checks)
@@ -263,6 +265,34 @@ int ref_taproot_check(const unsigned char* txb, size_t txlen, const unsigned cha
         *hashed = chk.called ? 1 : 0;
         if (chk.called) memcpy(sighash32, chk.sighash.begin(), 32);
         return ok ? 1 : 0;
+    } catch (const std::exception&) {
+        return -1;
+    }
+}
+
+// The reference's SignatureHash (interpreter.cpp:1576-1642) for one ECDSA check, obtained the way
+// the interpreter obtains it: GenericTransactionSignatureChecker::CheckECDSASignature
+// (:1656-1676) with a placeholder signature ending in `hashtype` and a placeholder 33-byte key,
+// the sighash captured at VerifyECDSASignature.  sigversion 0 = BASE, 1 = WITNESS_V0.  Returns 1
+// with sighash32 written, or -1 if the tx does not deserialize / nIn is out of range.
+int ref_check_sighash(const unsigned char* txb, size_t txlen, unsigned int nIn,
+                      const unsigned char* script, size_t scriptlen, unsigned int hashtype,
+                      int64_t amount, int sigversion, unsigned char* sighash32) {
+    try {
+        ByteReader ss(txb, txlen);
+        CTransaction tx(deserialize, ss);
+        if (nIn >= tx.vin.size()) return -1;
+        PrecomputedTransactionData txdata(tx);
+        CapturingChecker chk(&tx, nIn, amount, txdata);
+        std::vector<unsigned char> sig = {0x30, 0x06, 0x02, 0x01, 0x01, 0x02, 0x01, 0x01,
+                                          (unsigned char)hashtype};
+        std::vector<unsigned char> pub(33, 0x11);
+        pub[0] = 0x02;
+        chk.CheckECDSASignature(sig, pub, CScript(script, script + scriptlen),
+                                sigversion == 1 ? SigVersion::WITNESS_V0 : SigVersion::BASE);
+        if (chk.log.size() != 1) return -1;
+        memcpy(sighash32, chk.log[0].sighash.begin(), 32);
+        return 1;
     } catch (const std::exception&) {
         return -1;
     }

@@ -94,6 +94,10 @@ def blib():
         L = ctypes.CDLL(BENCH_LIB_PATH)
         u8p, sz, vp, ui = ctypes.c_char_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_uint
         L.mi_microbench.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_double)]
+        dp = ctypes.POINTER(ctypes.c_double)
+        L.mi_primbench.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, dp, dp]
+        L.mi_microbench_sustained.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_double,
+                                              ctypes.c_double, ctypes.c_int, dp, dp, dp]
         L.bcc_tupleset_c4.argtypes = [sz, ctypes.c_uint64, ctypes.c_int]
         L.bcc_tupleset_c4.restype = vp
         L.bcc_tupleset_c4_range.argtypes = [sz, ctypes.c_uint64, sz, sz, ctypes.c_int]
@@ -134,6 +138,7 @@ def blib():
         L.bcc_workload_sighash_bytes.restype = sz
         L.bcc_workload_item.argtypes = [vp, sz, u8p, szp, ctypes.POINTER(ctypes.c_int64), u8p, sz]
         L.bcc_workload_item.restype = sz
+        L.bcc_debug_sighash.argtypes = [ctypes.POINTER(SighashCheck), sz, u8p, ctypes.c_int]
         L.mi_gen_pubkeys.argtypes = [u8p, sz, u8p, u8p, u8p, ctypes.c_int]
         L.mi_gen_sign.argtypes = [u8p, u8p, u8p, sz, u8p, u8p, u8p, ctypes.c_int]
         L.mi_gen_schnorr_sign.argtypes = [u8p, u8p, u8p, sz, u8p, u8p, u8p, ctypes.c_int]
@@ -152,6 +157,37 @@ class BatchItem(ctypes.Structure):
     _fields_ = [("script_pubkey", ctypes.c_void_p), ("script_pubkey_len", ctypes.c_uint),
                 ("amount", ctypes.c_int64), ("tx_to", ctypes.c_void_p),
                 ("tx_to_len", ctypes.c_uint), ("n_in", ctypes.c_uint)]
+
+
+class SighashCheck(ctypes.Structure):
+    """struct bcc_sighash_check (include/bcc_bench.h)."""
+    _fields_ = [("tx", ctypes.c_void_p), ("tx_len", ctypes.c_size_t),
+                ("script_code", ctypes.c_void_p), ("script_code_len", ctypes.c_size_t),
+                ("n_in", ctypes.c_uint), ("hashtype", ctypes.c_int32), ("amount", ctypes.c_int64),
+                ("sigversion", ctypes.c_int)]
+
+
+def debug_sighash(checks, device=0):
+    """The GPU sighash stage alone (bcc_debug_sighash): checks = [(tx, script_code, n_in,
+    hashtype, amount, sigversion)], each built into a device job exactly as the batch engine's
+    deferring checker builds it.  Returns the n 32-byte message rows (raw uint256 bytes)."""
+    n = len(checks)
+    if n == 0:
+        return []
+    arr = (SighashCheck * n)()
+    keep = []
+    for i, (tx, code, nin, ht, amount, sv) in enumerate(checks):
+        tb, cb = ctypes.create_string_buffer(bytes(tx), max(1, len(tx))), \
+            ctypes.create_string_buffer(bytes(code), max(1, len(code)))
+        keep += [tb, cb]
+        ht = int(ht) & 0xffffffff
+        arr[i] = SighashCheck(ctypes.addressof(tb), len(tx), ctypes.addressof(cb), len(code), nin,
+                              ht - (1 << 32) if ht >= 1 << 31 else ht, amount, sv)
+    out = ctypes.create_string_buffer(32 * n)
+    rc = blib().bcc_debug_sighash(arr, n, out, device)
+    if rc != 0:
+        raise RuntimeError(f"bcc_debug_sighash failed: {rc}")
+    return [out.raw[32 * i:32 * i + 32] for i in range(n)]
 
 
 class TuplesetHost(ctypes.Structure):
@@ -622,6 +658,26 @@ def gen_schnorr_sign(d32, m32, k32, device=0):
 def set_chunk_lanes(lanes):
     """Lanes per signature-kernel launch (0 restores the default); results never depend on it."""
     lib().bcc_set_chunk_lanes(ctypes.c_size_t(lanes))
+
+
+def microbench_sustained(op, waves_per_simd=8, target_ms=20.0, warm_s=1.0, reps=5):
+    """Sustained issue rate of microbenchmark `op` (lane-instructions/s), the in-kernel clock it
+    ran at (GHz) and the launch time (ms): mi_microbench_sustained."""
+    r, c, m = ctypes.c_double(0), ctypes.c_double(0), ctypes.c_double(0)
+    rc = blib().mi_microbench_sustained(op, waves_per_simd, target_ms, warm_s, reps,
+                                        ctypes.byref(r), ctypes.byref(c), ctypes.byref(m))
+    if rc != 0:
+        raise RuntimeError(f"mi_microbench_sustained failed: {rc}")
+    return r.value, c.value, m.value
+
+
+def primbench(prim, iters=4096, warm=3):
+    """(cycles per primitive per wave at 4 waves/SIMD, launch ms): mi_primbench."""
+    c, m = ctypes.c_double(0), ctypes.c_double(0)
+    rc = blib().mi_primbench(prim, iters, warm, ctypes.byref(c), ctypes.byref(m))
+    if rc != 0:
+        raise RuntimeError(f"mi_primbench failed: {rc}")
+    return c.value, m.value
 
 
 def microbench(op, iters=4096):

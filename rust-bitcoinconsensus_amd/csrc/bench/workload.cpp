@@ -756,3 +756,26 @@ extern "C" bcc_workload* bcc_workload_block(const uint32_t* tx_nin, const uint32
     if (finish(w)) return nullptr;
     return w;
 }
+
+// The GPU sighash stage alone over n checks built by the engine's own job builder
+// (host/engine.cpp add_sighash_job via build_sighash_checks): legacy SIGHASH_ALL template jobs
+// (K3'), host-serialized legacy preimages (K3), the SIGHASH_SINGLE bug (row stays ONE), BIP143
+// raw-tx jobs (K_wtx + K_win) and BIP143 SIGHASH_SINGLE preimages (K1 + K2 + K3).
+int bcc_debug_sighash(const bcc_sighash_check* checks, size_t n, uint8_t* msg32_out, int device) {
+    if (n == 0) return 0;
+    if (!checks || !msg32_out) return -1;
+    std::vector<bcc::host::SighashCheck> c(n);
+    for (size_t i = 0; i < n; i++)
+        c[i] = bcc::host::SighashCheck{checks[i].tx,       checks[i].tx_len,
+                                       checks[i].script_code, checks[i].script_code_len,
+                                       checks[i].n_in,     checks[i].hashtype,
+                                       checks[i].amount,   checks[i].sigversion};
+    bcc::SighashJobs jobs;
+    bcc::TupleRows rows;
+    if (bcc::host::build_sighash_checks(c.data(), n, jobs, rows) != n) return -1;
+    bcc::DeviceBatch batch(device);
+    int e = batch.stage(jobs, rows);
+    if (!e) e = batch.run_sighash(nullptr);
+    if (!e) e = batch.fetch_msgs(msg32_out);
+    return e;
+}

@@ -129,6 +129,95 @@ uint32_t append_key(std::vector<uint8_t>& a, const Bytes& pub, const Bytes& sig,
     return (uint32_t)(a.size() - k0);
 }
 
+// The sighash job of one deferred check: what GenericTransactionSignatureChecker would hash
+// (SignatureHash, interpreter.cpp:1576-1642) for input in.n_in of te's tx, as a device job whose
+// digest lands in tuple row `row` (legacy SIGHASH_ALL: template job; other legacy hashtypes: host
+// preimage, SINGLE bug -> the row keeps ONE; BIP143: raw-tx job, SIGHASH_SINGLE: host preimage +
+// aux messages).  te's per-round slots (template, aux, raw tx) are filled on first use and te is
+// then appended to `touched` (Round::reset clears them).
+void add_sighash_job(SighashJobs& jobs, TxEntry& te, const bcc_batch_item& in, const Bytes& code,
+                     SigVersion sv, int hashtype, uint32_t row, std::vector<uint8_t>& scratch,
+                     Bip143Job& bip143, std::vector<TxEntry*>& touched) {
+    const Tx& tx = te.tx;
+    const unsigned nin = in.n_in;
+    if (sv == SIGVERSION_BASE && legacy_all_type(hashtype)) {
+        // device-assembled from the tx template (pipeline.h TplJob)
+        if (te.tpl < 0) {
+            build_legacy_template(tx, scratch);
+            te.tpl = jobs.add_tpl(scratch.data(), scratch.size());
+            te.tpl_len = (uint32_t)scratch.size();
+            touched.push_back(&te);
+        }
+        build_script_code_field(code, scratch);
+        TplJob tj;
+        tj.tpl_off = (uint32_t)te.tpl;
+        tj.tpl_len = te.tpl_len;
+        tj.pos = (uint32_t)legacy_template_pos(tx, nin);
+        tj.code_off = jobs.add_code(scratch.data(), scratch.size());
+        tj.code_len = (uint32_t)scratch.size();
+        tj.hashtype = (uint32_t)hashtype;
+        tj.row = row;
+        tj.nblk = SighashJobs::tpl_nblk(tj.tpl_len, tj.code_len);
+        jobs.tjobs.push_back(tj);
+    } else if (sv == SIGVERSION_BASE) {
+        if (build_legacy_preimage(tx, nin, code, hashtype, scratch))
+            jobs.add_pre(scratch.data(), scratch.size(), row);
+        // else: SIGHASH_SINGLE bug, msg stays ONE
+    } else if ((hashtype & 0x1f) != 3) {
+        // BIP143 assembled on the device from the raw tx bytes (pipeline.h WinJob): the
+        // host appends the tx once per round and a record per check
+        if (te.wtx < 0) {
+            const uint8_t* raw = in.tx_to;
+            const size_t len = in.tx_to_len;
+            if (tx.has_witness() && !tx.vout.empty() && len > 10) {
+                // upload the tx without marker, flag and witnesses (BIP144 layout: the
+                // inputs start at byte 6, the outputs end where the witnesses begin)
+                const Span& last = tx.vout.back().ser;
+                const size_t mid = (size_t)(last.p + last.n - (raw + 6));
+                te.wtx = (int32_t)jobs.add_wtx3(raw, 4, raw + 6, mid, raw + len - 4, 4,
+                                                tx.vin.size());
+            } else {
+                te.wtx = (int32_t)jobs.add_wtx(raw, len, tx.vin.size());
+            }
+            touched.push_back(&te);
+        }
+        scratch.clear();
+        put_compact_size(scratch, code.size());
+        scratch.insert(scratch.end(), code.begin(), code.end());
+        WinJob wj{};
+        wj.tx = (uint32_t)te.wtx;
+        wj.nin = nin;
+        wj.code_off = jobs.add_code(scratch.data(), scratch.size());
+        wj.code_len = (uint32_t)scratch.size();
+        wj.hashtype = (uint32_t)hashtype;
+        wj.row = row;
+        wj.amount_lo = (uint32_t)(uint64_t)in.amount;
+        wj.amount_hi = (uint32_t)((uint64_t)in.amount >> 32);
+        jobs.wjobs.push_back(wj);
+    } else {  // SIGHASH_SINGLE: host preimage, single-output aux message
+        Bip143Job& job = bip143;
+        build_bip143_preimage(tx, nin, code, hashtype, in.amount, job);
+        uint32_t pre = jobs.add_pre(job.preimage.data(), job.preimage.size(), row);
+        size_t base = (size_t)jobs.pre_off[pre] * 64;
+        for (int k = 0; k < 3; k++) {
+            if (!job.need[k]) continue;
+            int32_t aux;
+            if (k == AUX_OUTPUTS && job.single_output) {
+                const Span& o = tx.vout[nin].ser;
+                aux = (int32_t)jobs.add_aux(o.p, o.n);
+            } else {
+                if (te.aux[k] < 0) {
+                    build_aux_message(tx, (AuxKind)k, scratch);
+                    te.aux[k] = (int32_t)jobs.add_aux(scratch.data(), scratch.size());
+                    touched.push_back(&te);
+                }
+                aux = te.aux[k];
+            }
+            jobs.patches.push_back(PatchRec{(uint32_t)(base + job.off[k]), (uint32_t)aux});
+        }
+    }
+}
+
 class Round;
 
 // The deferral seam (BaseSignatureChecker::CheckECDSASignature, interpreter.h:227)
@@ -195,8 +284,6 @@ public:
             host_rejected++;
             return false;
         }
-        const Tx& tx = it.tx->tx;
-        const unsigned nin = it.in->n_in;
         const int hashtype = sig.back();
         uint8_t one[32] = {0};
         one[0] = 1;  // uint256::ONE as raw bytes: the SIGHASH_SINGLE-bug message
@@ -204,82 +291,7 @@ public:
         const uint8_t* y = pub.size() == 65 ? pub.data() + 33 : ybuf;  // y unused for 02/03
         uint32_t row = rows.add(pub[0], pub.data() + 1, y, r, s, one);
         if (pub.size() == 65) rows.y_unused = false;
-        if (sv == SIGVERSION_BASE && legacy_all_type(hashtype)) {
-            // device-assembled from the tx template (pipeline.h TplJob)
-            if (it.tx->tpl < 0) {
-                build_legacy_template(tx, scratch);
-                it.tx->tpl = jobs.add_tpl(scratch.data(), scratch.size());
-                it.tx->tpl_len = (uint32_t)scratch.size();
-                touched.push_back(it.tx);
-            }
-            build_script_code_field(code, scratch);
-            TplJob tj;
-            tj.tpl_off = (uint32_t)it.tx->tpl;
-            tj.tpl_len = it.tx->tpl_len;
-            tj.pos = (uint32_t)legacy_template_pos(tx, nin);
-            tj.code_off = jobs.add_code(scratch.data(), scratch.size());
-            tj.code_len = (uint32_t)scratch.size();
-            tj.hashtype = (uint32_t)hashtype;
-            tj.row = row;
-            tj.nblk = SighashJobs::tpl_nblk(tj.tpl_len, tj.code_len);
-            jobs.tjobs.push_back(tj);
-        } else if (sv == SIGVERSION_BASE) {
-            if (build_legacy_preimage(tx, nin, code, hashtype, scratch))
-                jobs.add_pre(scratch.data(), scratch.size(), row);
-            // else: SIGHASH_SINGLE bug, msg stays ONE
-        } else if ((hashtype & 0x1f) != 3) {
-            // BIP143 assembled on the device from the raw tx bytes (pipeline.h WinJob): the
-            // host appends the tx once per round and a record per check
-            if (it.tx->wtx < 0) {
-                const uint8_t* raw = it.in->tx_to;
-                const size_t len = it.in->tx_to_len;
-                if (tx.has_witness() && !tx.vout.empty() && len > 10) {
-                    // upload the tx without marker, flag and witnesses (BIP144 layout: the
-                    // inputs start at byte 6, the outputs end where the witnesses begin)
-                    const Span& last = tx.vout.back().ser;
-                    const size_t mid = (size_t)(last.p + last.n - (raw + 6));
-                    it.tx->wtx = (int32_t)jobs.add_wtx3(raw, 4, raw + 6, mid, raw + len - 4, 4,
-                                                        tx.vin.size());
-                } else {
-                    it.tx->wtx = (int32_t)jobs.add_wtx(raw, len, tx.vin.size());
-                }
-                touched.push_back(it.tx);
-            }
-            scratch.clear();
-            put_compact_size(scratch, code.size());
-            scratch.insert(scratch.end(), code.begin(), code.end());
-            WinJob wj{};
-            wj.tx = (uint32_t)it.tx->wtx;
-            wj.nin = nin;
-            wj.code_off = jobs.add_code(scratch.data(), scratch.size());
-            wj.code_len = (uint32_t)scratch.size();
-            wj.hashtype = (uint32_t)hashtype;
-            wj.row = row;
-            wj.amount_lo = (uint32_t)(uint64_t)it.in->amount;
-            wj.amount_hi = (uint32_t)((uint64_t)it.in->amount >> 32);
-            jobs.wjobs.push_back(wj);
-        } else {  // SIGHASH_SINGLE: host preimage, single-output aux message
-            Bip143Job& job = bip143;
-            build_bip143_preimage(tx, nin, code, hashtype, it.in->amount, job);
-            uint32_t pre = jobs.add_pre(job.preimage.data(), job.preimage.size(), row);
-            size_t base = (size_t)jobs.pre_off[pre] * 64;
-            for (int k = 0; k < 3; k++) {
-                if (!job.need[k]) continue;
-                int32_t aux;
-                if (k == AUX_OUTPUTS && job.single_output) {
-                    const Span& o = tx.vout[nin].ser;
-                    aux = (int32_t)jobs.add_aux(o.p, o.n);
-                } else {
-                    if (it.tx->aux[k] < 0) {
-                        build_aux_message(tx, (AuxKind)k, scratch);
-                        it.tx->aux[k] = (int32_t)jobs.add_aux(scratch.data(), scratch.size());
-                        touched.push_back(it.tx);
-                    }
-                    aux = it.tx->aux[k];
-                }
-                jobs.patches.push_back(PatchRec{(uint32_t)(base + job.off[k]), (uint32_t)aux});
-            }
-        }
+        add_sighash_job(jobs, *it.tx, *it.in, code, sv, hashtype, row, scratch, bip143, touched);
         it.cache.push_back(Item::Check{koff, klen, -2 - (int32_t)pending.size()});
         if (consult) it.pending.push_back((uint32_t)pending.size());
         pending.push_back(Pending{item_idx, (uint32_t)(it.cache.size() - 1)});
@@ -839,6 +851,33 @@ size_t build_first_round(const bcc_batch_item* items, size_t n, unsigned flags, 
     jobs = std::move(rd.jobs);
     rows = std::move(rd.rows);
     return rows.size();
+}
+
+size_t build_sighash_checks(const SighashCheck* checks, size_t n, SighashJobs& jobs,
+                            TupleRows& rows) {
+    jobs.clear();
+    rows.clear();
+    rows.msg_one = true;
+    rows.y_unused = true;
+    std::vector<TxEntry> txs(n);
+    std::vector<TxEntry*> touched;
+    std::vector<uint8_t> scratch;
+    Bip143Job bip143;
+    const uint8_t zero[32] = {0};
+    uint8_t one[32] = {0};
+    one[0] = 1;
+    for (size_t i = 0; i < n; i++) {
+        const SighashCheck& c = checks[i];
+        if (!c.tx || !parse_tx(c.tx, c.tx_len, txs[i].tx) || c.nin >= txs[i].tx.vin.size())
+            return i;
+        if (c.sigversion != SIGVERSION_BASE && c.sigversion != SIGVERSION_WITNESS_V0) return i;
+        bcc_batch_item in{nullptr, 0, c.amount, c.tx, (unsigned)c.tx_len, c.nin};
+        const Bytes code(c.code, c.code + c.code_len);
+        const uint32_t row = rows.add(0x02, zero, zero, zero, zero, one);
+        add_sighash_job(jobs, txs[i], in, code, (SigVersion)c.sigversion, c.hashtype, row, scratch,
+                        bip143, touched);
+    }
+    return n;
 }
 
 void append_round(SighashJobs& dst, TupleRows& drows, const SighashJobs& src,

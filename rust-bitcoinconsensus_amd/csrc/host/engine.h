@@ -1,6 +1,7 @@
 // Internal interface of the batch engine (engine.cpp), shared with the workload builder.
 #pragma once
 #include <cstddef>
+#include <cstdint>
 #include <vector>
 
 #include "../pipeline.h"
@@ -15,6 +16,26 @@ namespace host {
 // Returns the number of deferred tuples.
 size_t build_first_round(const bcc_batch_item* items, size_t n, unsigned flags, SighashJobs& jobs,
                          TupleRows& rows, std::vector<uint32_t>* tuple_item = nullptr);
+
+// One signature check's sighash inputs (tests / debugging of the sighash kernels): the spending
+// tx, the input index, the scriptCode as GenericTransactionSignatureChecker receives it, the full
+// 32-bit hash type, the spent amount (BIP143) and the SigVersion (0 BASE, 1 WITNESS_V0).
+struct SighashCheck {
+    const uint8_t* tx;
+    size_t tx_len;
+    const uint8_t* code;
+    size_t code_len;
+    unsigned nin;
+    int hashtype;
+    int64_t amount;
+    int sigversion;
+};
+
+// Builds the device sighash jobs of n checks exactly as the deferring checker builds them for a
+// deferred tuple (one row per check, msg = ONE unless a kernel overwrites it).  Returns n, or the
+// index of the first check whose tx does not parse / whose nin or sigversion is out of range.
+size_t build_sighash_checks(const SighashCheck* checks, size_t n, SighashJobs& jobs,
+                            TupleRows& rows);
 
 // Appends src (jobs + rows) to dst, fixing offsets / indices.
 void append_round(SighashJobs& dst, TupleRows& dst_rows, const SighashJobs& src,

@@ -10,6 +10,7 @@
 
 #include "../../oracle/bcc_oracle.h"
 #include "../../rust-bitcoinconsensus_amd/csrc/pipeline.h"
+#include "../../rust-bitcoinconsensus_amd/csrc/host/engine.h"
 
 namespace bcc {
 
@@ -31,7 +32,8 @@ int gpu_verify_parts(int dev, const SighashJobs* const* jobs, const TupleRows* c
     return 0;
 }
 
-int gpu_verify_batch(int, const SighashJobs& j, const TupleRows& rows, uint8_t* verdict, double*) {
+// The sighash stage: msg rows (entering as rows.msg) overwritten by every job's digest.
+static void stub_sighash(const SighashJobs& j, std::vector<uint8_t>& msg) {
     std::vector<uint8_t> auxd(32 * j.aux_off.size());
     for (size_t a = 0; a < j.aux_off.size(); a++) {
         const uint8_t* m = &j.aux[(size_t)j.aux_off[a] * 64];
@@ -40,7 +42,6 @@ int gpu_verify_batch(int, const SighashJobs& j, const TupleRows& rows, uint8_t* 
     }
     std::vector<uint8_t> pre = j.pre;
     for (const auto& p : j.patches) memcpy(&pre[p.pre_byte], &auxd[32 * p.aux], 32);
-    std::vector<uint8_t> msg = rows.msg;
     for (size_t k = 0; k < j.pre_off.size(); k++) {
         const uint8_t* m = &pre[(size_t)j.pre_off[k] * 64];
         size_t L = (size_t)j.pre_nblk[k] * 64;
@@ -62,6 +63,11 @@ int gpu_verify_batch(int, const SighashJobs& j, const TupleRows& rows, uint8_t* 
         bcco_sighash(&j.txraw[r.tx_off], r.tx_len, w.nin, c + hdr, w.code_len - hdr,
                      (int)w.hashtype, amount, 1, &msg[32 * w.row]);
     }
+}
+
+int gpu_verify_batch(int, const SighashJobs& j, const TupleRows& rows, uint8_t* verdict, double*) {
+    std::vector<uint8_t> msg = rows.msg;
+    stub_sighash(j, msg);
     for (size_t i = 0; i < rows.size(); i++) {
         uint8_t pub[65];
         pub[0] = rows.tag[i];
@@ -119,3 +125,15 @@ int gpu_taproot_verify(int, const TaprootJobs& j, uint8_t* verdict, uint8_t* msg
 }
 
 }  // namespace bcc
+
+// bcc_debug_sighash's host half (the job builder) with the stub sighash stage: the CPU suite
+// checks the jobs the engine builds for the reference's sighash goldens.
+extern "C" int stub_debug_sighash(const bcc::host::SighashCheck* c, size_t n, uint8_t* out) {
+    bcc::SighashJobs jobs;
+    bcc::TupleRows rows;
+    if (bcc::host::build_sighash_checks(c, n, jobs, rows) != n) return -1;
+    std::vector<uint8_t> msg = rows.msg;
+    bcc::stub_sighash(jobs, msg);
+    memcpy(out, msg.data(), msg.size());
+    return 0;
+}
