@@ -42,12 +42,6 @@ sys.path.insert(0, os.path.join(ROOT, "rust-bitcoinconsensus_amd"))
 
 MADS_PER_VERIFY = 144448          # 2,257 modmuls x 64 (32x32->64) products
 MADS_PER_SCHNORR = 142848         # 2,232 modmuls x 64
-UBENCH_OPS = {0: "v_mad_u64_u32", 1: "v_mul_lo_u32", 2: "v_mul_hi_u32", 3: "v_add_co_u32 (sgpr)",
-              4: "v_addc_co_u32", 5: "v_mad_u32_u24", 6: "v_lshl_add_u64", 7: "v_fma_f64",
-              8: "v_add_u32", 9: "v_add3_u32", 10: "v_mul_u32_u24", 11: "v_mul_hi_u32_u24",
-              12: "v_alignbit_b32", 13: "v_lshrrev_b64", 14: "v_add_co_u32 (vcc)",
-              15: "v_cndmask_b32", 16: "mad_u64_u32+addc pair", 17: "mul_lo+mul_hi pair",
-              18: "mad_u64_u32+add_u32 pair"}
 METRIC = "ECDSA verifies/sec (node) at 1/2/4/8 MI355X; % of int-ALU roofline"
 DEFAULT_N = {"c2": 1_000_000, "c3": 4000, "c4": 8_000_000, "c5": 16_000_000, "c5t": 1_000_000}
 SEEDS = {"c2": 0x5EED0001, "c3": 0x5EED0003, "c4": 0x5EED0004, "c5": 0x5EED0005,
@@ -207,6 +201,42 @@ def gather_verdicts(local, world, device="cuda"):
     return np.concatenate([np.unpackbits(allb[r])[: ns[r]] for r in range(world)])
 
 
+def c1_vector():
+    """Config C1: the README P2PKH spend (lib.rs:223-231), as committed in crate_vectors.json."""
+    v = next(x for x in json.load(open(os.path.join(ROOT, "tests", "golden", "crate_vectors.json")))
+             if x["name"] == "p2pkh")
+    return bytes.fromhex(v["spk"]), v["amount"], bytes.fromhex(v["tx"]), v["nin"], v["flags"]
+
+
+def single_call_latency(B, calls=200):
+    """Latency of ONE bitcoinconsensus_verify_script_with_amount call on C1 (what an unchanged Rust
+    caller of verify() sees, lib.rs:103-139): its round on the GPU (default), and with
+    bcc_set_host_small_round routing rounds of <= 64 checks to the engine's host code."""
+    import statistics
+    spk, amount, tx, nin, flags = c1_vector()
+
+    def lat():
+        ts = []
+        for _ in range(calls):
+            t0 = time.perf_counter()
+            r = B.verify_script_with_amount(spk, amount, tx, nin, flags)
+            ts.append(time.perf_counter() - t0)
+            assert r == (1, 0)
+        return statistics.median(ts) * 1e6
+    B.verify_script_with_amount(spk, amount, tx, nin, flags)  # warm
+    gpu_us = lat()
+    B.set_host_small_round(64)
+    try:
+        B.verify_script_with_amount(spk, amount, tx, nin, flags)
+        host_us = lat()
+    finally:
+        B.set_host_small_round(0)
+    return dict(config="C1: README P2PKH tx, input 0", calls=calls, gpu_round_us=gpu_us,
+                host_small_round_us=host_us,
+                note="median per-call latency; the reference's own per-call latency is in "
+                     "cpu_baseline.single_call_us")
+
+
 # ---- per-config jobs: stage inputs, run one step, time the dominant kernels, CPU baseline ----
 
 class C2:
@@ -256,6 +286,7 @@ class C2:
                                      achieved_GBps=b / (sighash_ms * 1e-3) / 1e9, peak_GBps=8000.0)}
         if type(self) is C2:
             out["drop_in_end_to_end"] = self.end_to_end()
+            out["single_call"] = single_call_latency(self.B)
         return out
 
     def end_to_end(self, reps=3):
@@ -280,9 +311,21 @@ class C2:
         item_v = bytearray(self.n)
         for t, i in enumerate(self.wl.tuple_items()):
             item_v[i] = v[t]
-        return cpu_baseline_script([self.wl.item(i) for i in range(sample)],
-                                   f"C2 inputs (first {sample} of rank 0's workload)",
-                                   unit="verifies/s", gpu_verdicts=item_v[:sample])
+        cb = cpu_baseline_script([self.wl.item(i) for i in range(sample)],
+                                 f"C2 inputs (first {sample} of rank 0's workload)",
+                                 unit="verifies/s", gpu_verdicts=item_v[:sample])
+        R = _reference()
+        if cb is not None and R is not None:
+            import statistics
+            spk, amount, tx, nin, flags = c1_vector()
+            ts = []
+            for _ in range(2000):
+                t0 = time.perf_counter()
+                R.verify_script_with_amount(spk, amount, tx, nin, flags)
+                ts.append(time.perf_counter() - t0)
+            cb["single_call_us"] = statistics.median(ts) * 1e6
+            cb["single_call"] = "C1 README tx, one bitcoinconsensus_verify_script_with_amount call, median of 2000"
+        return cb
 
     def config(self, world):
         return {"workload": "C2: synthetic P2WPKH inputs, BIP143 sighash + ECDSA verify "
@@ -363,6 +406,7 @@ class TupleJob:
             from fixtures import bip340_vectors
             vec = [(t["sig"], t["msg"], t["pub"], t["verdict"]) for t in bip340_vectors()]
         self.kind = kind
+        self.dev = dev
         self.ts = BB.TupleSet(n, kind=kind, seed=seed, device=dev, vectors=vec, first=first,
                               total=total)
         self.units = self.n = n
@@ -397,9 +441,40 @@ class TupleJob:
     def extra(self, sighash_ms):
         import numpy as np
         h = self.ts.host()
-        return {"expected_valid": int(h["expect"].sum()),
-                "mismatch_vs_construction": self.mismatch_vs_construction,
-                "class_counts": np.bincount(h["cls"]).tolist()}
+        out = {"expected_valid": int(h["expect"].sum()),
+               "mismatch_vs_construction": self.mismatch_vs_construction,
+               "class_counts": np.bincount(h["cls"]).tolist()}
+        if self.kind == "c4":
+            out["drop_in_end_to_end"] = self.end_to_end(h)
+        return out
+
+    def end_to_end(self, h, reps=2):
+        """The same n tuples through bcc_pubkey_verify_batch from host buffers: N x
+        CPubKey(pub).Verify(hash, sig) (pubkey.cpp:191-207): host length filter + lax DER, H2D,
+        kernels, verdicts back.  Reported beside value, never as value."""
+        import ctypes
+        import numpy as np
+        import bitcoinconsensus_amd as BB
+        L = BB.lib()
+        u64p = ctypes.POINTER(ctypes.c_uint64)
+        L.bcc_pubkey_verify_batch.argtypes = [ctypes.c_void_p, u64p, ctypes.c_void_p,
+                                              ctypes.c_void_p, u64p, ctypes.c_void_p,
+                                              ctypes.c_size_t, ctypes.c_int]
+        out = np.zeros(self.n, np.uint8)
+        best = None
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            rc = L.bcc_pubkey_verify_batch(
+                h["pub_blob"].ctypes.data, h["pub_off"].ctypes.data_as(u64p), h["msg32"].ctypes.data,
+                h["sig_blob"].ctypes.data, h["sig_off"].ctypes.data_as(u64p), out.ctypes.data,
+                self.n, self.dev)
+            dt = time.perf_counter() - t0
+            assert rc == 0
+            best = dt if best is None else min(best, dt)
+        v = np.frombuffer(self.ts.verdicts(), np.uint8)
+        return dict(verifies_per_s=self.n / best, ms=best * 1e3,
+                    mismatches_vs_staged=int((out != v).sum()),
+                    entry="bcc_pubkey_verify_batch (CPubKey::Verify semantics) from host buffers")
 
     def cpu(self, sample):
         import numpy as np
@@ -703,35 +778,46 @@ def main():
     total = job.units * world * args.steps
     value = total / elapsed
     if rank == 0:
-        peak = B.microbench(0, 4096)  # v_mad_u64_u32 lane-ops/s, measured on this GPU
-        rates = {UBENCH_OPS[op]: round(B.microbench(op, 2048) / 1e12, 2) for op in UBENCH_OPS}
+        # peak: the v_mad_u64_u32 issue limit at the spec clock (MI355X_MICROARCH.md: 2400 MHz max;
+        # a wave64 v_mad_u64_u32 occupies its SIMD 4 cycles: 16 lanes/clk/SIMD x 4 SIMDs x CUs);
+        # beside it the sustained on-box rate (8 independent mads per asm block, 8 waves/SIMD,
+        # >= 1 s of back-to-back ~20 ms launches) and the clock it held (s_memtime stamps)
+        cus = torch.cuda.get_device_properties(dev).multi_processor_count
+        peak = 2.4e9 * cus * 4 * 16
+        m_rate, m_clk, m_ms = B.microbench_sustained(25, 8, 20.0, 1.0, 3)
         achieved = sig_units * job.mads / (sig_ms * 1e-3)
         traffic, tsrc = args.traffic, "--traffic" if args.traffic else None
-        mix = None
         tf = os.path.join(ROOT, "profiles", "traffic.json")
         if traffic is None and os.path.exists(tf):
             tj = json.load(open(tf))
             t = tj.get(f"{args.config}@{sig_units}") or tj.get(args.config)
             if t and t.get("units") == sig_units and t.get("kernel") == job.kernel:
                 traffic, tsrc = t["traffic_bytes"], t["source"]
-                mix = t.get("instruction_mix")
         roof = dict(bound="int-alu", kernel=job.kernel,
                     achieved=achieved / 1e12, peak=peak / 1e12, unit="T(v_mad_u64_u32)/s",
                     frac=achieved / peak, traffic=traffic, traffic_source=tsrc,
-                    issue_rates_T_per_s=rates,
+                    peak_source=f"spec: 2.4 GHz x {cus} CUs x 4 SIMDs x 16 lanes/clk "
+                                "(v_mad_u64_u32, 4 cycles per wave64)",
+                    peak_measured=dict(T_per_s=m_rate / 1e12, clock_GHz=m_clk,
+                                       T_per_s_at_2_4GHz=m_rate / 1e12 * 2.4 / m_clk,
+                                       launch_ms=m_ms, frac_vs_measured=achieved / m_rate,
+                                       source="mi_microbench_sustained(op 25: 8 v_mad_u64_u32 with "
+                                              "own SGPR carries per asm block, 8 waves/SIMD)"),
                     per_launch=dict(verifies=sig_units, mads=sig_units * job.mads, avg_ms=sig_ms,
                                     verifies_per_s=sig_units / (sig_ms * 1e-3)))
-        if mix:
-            # the instruction mix behind frac (committed SQ counter pass): the stage is VALU-issue-
-            # bound, so frac ~= (counted mads / issued VALU instructions) x (the mix's issue rate /
-            # the v_mad_u64_u32 peak); raising frac means issuing fewer non-mad instructions
-            share = job.mads / mix["valu_lane_instructions_per_verify"]
-            roof["instruction_mix"] = dict(
-                valu_lane_instructions_per_verify=mix["valu_lane_instructions_per_verify"],
-                ladder_valu_per_verify=mix["ladder_valu_per_verify"],
-                counted_mad_share=share, issue_rate_T_per_s=mix["ladder_issue_rate_T_per_s"],
-                frac_estimate=share * mix["ladder_issue_rate_T_per_s"] * 1e12 / peak,
-                source=mix["source"])
+        cm = os.path.join(ROOT, "profiles", "r03", "ladder_cost_model.json")
+        if args.config == "c2" and os.path.exists(cm):
+            # why frac stops where it does (committed PMC passes + microbenchmark): the ladder is
+            # VALU-issue-bound; its cycles split by instruction class at the measured issue costs
+            d = json.load(open(cm))
+            k = d["kernels"].get("bench:twist_ladder_kernel<false>")
+            if k:
+                roof["cost_model"] = dict(
+                    kernel="twist_ladder_kernel<false>", cycle_share=k["cycle_share"],
+                    valu_per_verify=k["valu_per_wave"],
+                    issue_cost_cycles=d["issue_cost_cycles_per_wave_instr"],
+                    predicted_over_measured_cycles=k["predicted_over_measured"],
+                    source="profiles/r03/ladder_cost_model.json (tools/isa/cost_model.py)")
         cpu = None
         if world == 1 and not args.no_cpu:
             default_sample = {"c2": 200_000, "c3": 100_000, "c4": 400_000, "c5": 400_000,

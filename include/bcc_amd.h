@@ -131,8 +131,15 @@ int bcc_set_pipeline_chunk(size_t items);
 
 /* bitcoinconsensus_verify_batch keeps its host-side state (items, parsed transactions, job
  * buffers) with the calling thread for reuse by its next call; batches above 4M items release it
- * on return.  bcc_taproot_verify_batch keeps its job buffers the same way.  This releases the
- * calling thread's state of both now. */
+ * on return.  bcc_taproot_verify_batch keeps its job buffers the same way, and every entry point
+ * keeps a device batch (HBM arena, pinned staging image, streams, kernel scratch) per (thread,
+ * GPU).  This releases the calling thread's state, and the state the library's own worker threads
+ * keep (the per-GPU workers of a bcc_set_devices() list and the pipeline worker run rounds for
+ * their callers), now.
+ * Threads: with one device and no pipelining a call runs on the calling thread with that
+ * thread's own device state, so concurrent callers share nothing.  With several devices
+ * configured, or pipelining on, device rounds run on one shared worker thread per GPU: the results
+ * are the same, but concurrent callers' rounds queue on those workers. */
 void bcc_release_thread_state(void);
 
 typedef struct bcc_batch_stats {
@@ -144,16 +151,46 @@ typedef struct bcc_batch_stats {
     double total_seconds; /* the whole call, teardown included */
     size_t device_retries; /* device rounds that failed once and were re-run on a fresh batch */
     size_t devices;        /* GPUs a device round was spread over (max over the call's rounds) */
+    size_t host_rounds;    /* rounds (or device groups) verified on the host CPU: small rounds
+                            * (bcc_set_host_small_round) and device-failure fallbacks */
 } bcc_batch_stats;
 /* Statistics of the calling thread's last bitcoinconsensus_verify_batch / verify call. */
 void bcc_last_batch_stats(bcc_batch_stats* out);
 
+/* ---- host verification: the engine's own code on the CPU ------------------------------------
+ * A device round (sighash jobs + ECDSA tuples) can be evaluated on the host with the engine's own
+ * preimage builders, host SHA-256 and the kernels' lane code compiled for the CPU
+ * (csrc/host/host_verify.cpp); the verdicts are the same.
+ *
+ * Device failure policy.  A failed device round is retried once on a fresh device batch when the
+ * HIP error is transient (out of memory, not ready); a sticky error (launch failure, illegal
+ * address, no device, ...) leaves the HIP context unusable, so it is not retried.  Then:
+ *   BCC_DEVICE_FAILURE_HOST  (default; BCC_DEVICE_FAILURE=host) the round is verified on the host
+ *                            CPU (logged on stderr, counted by bcc_host_fallback_rounds) and every
+ *                            entry point returns its normal, exact result;
+ *   BCC_DEVICE_FAILURE_ERROR (BCC_DEVICE_FAILURE=error) bitcoinconsensus_verify_batch returns -1
+ *                            (unfinished items: BCC_ERR_DEVICE_FAILURE) and the single-item ABI
+ *                            aborts, as there is no verdict (see bitcoinconsensus.h). */
+#define BCC_DEVICE_FAILURE_HOST 0
+#define BCC_DEVICE_FAILURE_ERROR 1
+int bcc_set_device_failure_policy(int policy);
+/* Device rounds of at most `tuples` signature checks are verified on the host CPU instead of the
+ * GPU (0, the default, or BCC_HOST_SMALL_ROUND: every round on the GPU).  One lane of the GPU
+ * ladder is a single wave issuing a few hundred thousand dependent instructions, so a lone
+ * verify()'s latency is lower on the host. */
+int bcc_set_host_small_round(size_t tuples);
+/* Device rounds (or per-GPU groups) verified on the host after a device failure, process-wide. */
+size_t bcc_host_fallback_rounds(void);
+/* mi_ecdsa_verify_tuples' contract on the host CPU (threads >= 1). */
+int bcc_host_verify_tuples(const uint8_t* pub65, const uint8_t* msg32, const uint8_t* r32,
+                           const uint8_t* s32, uint8_t* verdict, size_t n, unsigned threads);
+
 /* Fault injection (tests): the next `rounds` device rounds of any thread fail as if the HIP
- * runtime had returned an error, without touching the GPU (also: BCC_FAULT_INJECT=rounds in the
- * environment at load time).  A failed round is retried once on a fresh device batch; a second
- * failure makes bitcoinconsensus_verify_batch return -1 (unfinished items: BCC_ERR_DEVICE_FAILURE)
- * and the single-item ABI abort (see bitcoinconsensus.h). */
+ * runtime had returned a transient error (hipErrorOutOfMemory), without touching the GPU (also:
+ * BCC_FAULT_INJECT=rounds in the environment at load time); _code injects the given HIP error
+ * (e.g. 719, hipErrorLaunchFailure: sticky, never retried). */
 void bcc_debug_fail_device_rounds(int rounds);
+void bcc_debug_fail_device_rounds_code(int rounds, int hip_error);
 
 #ifdef __cplusplus
 }

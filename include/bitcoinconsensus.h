@@ -21,10 +21,13 @@
  * staging buffer and kernel scratch per device (created on its first call, reused afterwards), so
  * concurrent callers never share mutable device state; the only shared state is the read-only
  * G table per device, built once under a lock.
- * Device failure: a failed device round is retried once on a fresh batch.  If it fails again,
- * bitcoinconsensus_verify_script[_with_amount] abort() the process (there is no verdict, and
- * returning 0 would report a consensus failure for a transaction that may be valid);
- * bitcoinconsensus_verify_batch returns -1 instead (see below).
+ * Device failure: a failed device round is retried once on a fresh batch when the error is
+ * transient.  If the device still cannot deliver, the round is verified on the host CPU with the
+ * engine's own code (bcc_amd.h: BCC_DEVICE_FAILURE_HOST, the default) and every entry point
+ * returns its exact result.  Under BCC_DEVICE_FAILURE_ERROR there is no verdict:
+ * bitcoinconsensus_verify_script[_with_amount] abort() the process (returning 0 would report a
+ * consensus failure for a transaction that may be valid) and bitcoinconsensus_verify_batch returns
+ * -1 instead (see below).
  */
 #ifndef BCC_AMD_BITCOINCONSENSUS_H
 #define BCC_AMD_BITCOINCONSENSUS_H
@@ -87,13 +90,15 @@ typedef struct bcc_batch_item {
     unsigned int n_in;
 } bcc_batch_item;
 
-/* Engine-specific error code, written ONLY by bitcoinconsensus_verify_batch, for items whose
- * verdict the device could not deliver (never by the single-item ABI, which aborts instead). */
+/* Engine-specific error code, written ONLY by bitcoinconsensus_verify_batch under
+ * BCC_DEVICE_FAILURE_ERROR, for items whose verdict the device could not deliver (never by the
+ * single-item ABI, which aborts instead). */
 #define BCC_ERR_DEVICE_FAILURE 6
 
 /* Verifies n items with `flags`.  ret_out[i] / err_out[i] (err_out may be NULL) receive exactly
  * what bitcoinconsensus_verify_script_with_amount would return / write for item i.
- * Returns the number of valid items, or -1 if the device pipeline failed twice in a row: then
+ * Returns the number of valid items, or -1 if the device pipeline failed (BCC_DEVICE_FAILURE_ERROR
+ * only; the default verifies such a round on the host): then
  * items the failed round left unfinished get ret_out 0 and err_out BCC_ERR_DEVICE_FAILURE, and
  * every other item carries its final result. */
 long bitcoinconsensus_verify_batch(const bcc_batch_item* items, size_t n, unsigned int flags,

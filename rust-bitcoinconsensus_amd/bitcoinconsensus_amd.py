@@ -205,7 +205,7 @@ class BatchStats(ctypes.Structure):
                 ("prepare_seconds", ctypes.c_double), ("interpret_seconds", ctypes.c_double),
                 ("merge_seconds", ctypes.c_double), ("stage_seconds", ctypes.c_double),
                 ("total_seconds", ctypes.c_double), ("device_retries", ctypes.c_size_t),
-                ("devices", ctypes.c_size_t)]
+                ("devices", ctypes.c_size_t), ("host_rounds", ctypes.c_size_t)]
 
 
 def _bind_consensus(L):
@@ -223,6 +223,11 @@ def _bind_consensus(L):
     L.bcc_set_devices.argtypes = [ctypes.POINTER(ctypes.c_int), ctypes.c_int]
     L.bcc_get_devices.argtypes = [ctypes.POINTER(ctypes.c_int), ctypes.c_int]
     L.bcc_last_batch_stats.argtypes = [ctypes.POINTER(BatchStats)]
+    L.bcc_set_device_failure_policy.argtypes = [ctypes.c_int]
+    L.bcc_set_host_small_round.argtypes = [ctypes.c_size_t]
+    L.bcc_host_fallback_rounds.restype = ctypes.c_size_t
+    L.bcc_debug_fail_device_rounds_code.argtypes = [ctypes.c_int, ctypes.c_int]
+    L.bcc_host_verify_tuples.argtypes = [ctypes.c_char_p] * 5 + [ctypes.c_size_t, ctypes.c_uint]
 
 
 class Workload:
@@ -406,6 +411,35 @@ def last_batch_stats():
 def debug_fail_device_rounds(rounds):
     """Fault injection (tests): the next `rounds` device rounds fail (include/bcc_amd.h)."""
     lib().bcc_debug_fail_device_rounds(rounds)
+
+
+DEVICE_FAILURE_HOST, DEVICE_FAILURE_ERROR = 0, 1
+
+
+def set_device_failure_policy(policy):
+    """bcc_set_device_failure_policy: DEVICE_FAILURE_HOST (default) verifies a round the GPU could
+    not deliver on the host CPU; DEVICE_FAILURE_ERROR reports it (-1 / abort)."""
+    if lib().bcc_set_device_failure_policy(policy) != 0:
+        raise ValueError(policy)
+
+
+def set_host_small_round(tuples):
+    """bcc_set_host_small_round: device rounds of at most `tuples` checks run on the host CPU."""
+    lib().bcc_set_host_small_round(tuples)
+
+
+def host_fallback_rounds():
+    """Rounds verified on the host after a device failure, process-wide."""
+    return lib().bcc_host_fallback_rounds()
+
+
+def host_verify_tuples(pub65, msg32, r32, s32, threads=1):
+    """bcc_host_verify_tuples: mi_ecdsa_verify_tuples' contract on the host CPU."""
+    n = len(msg32) // 32
+    out = ctypes.create_string_buffer(max(1, n))
+    if lib().bcc_host_verify_tuples(pub65, msg32, r32, s32, out, n, threads) != 0:
+        raise RuntimeError("bcc_host_verify_tuples failed")
+    return out.raw[:n]
 
 
 def set_device(device):

@@ -1096,8 +1096,15 @@ struct ThreadCtx {
     }
 };
 
+thread_local std::unique_ptr<ThreadCtx> tl_ctx[64];
+
+// Frees the calling thread's tuple-path contexts (bcc_release_thread_state).
+void release_tuple_thread_state() {
+    for (auto& c : tl_ctx) c.reset();
+}
+
 static int thread_ctx(int device, ThreadCtx** out) {
-    thread_local std::unique_ptr<ThreadCtx> ctx[64];
+    auto& ctx = tl_ctx;
     if (device < 0 || device >= 64) return (int)hipErrorInvalidDevice;
     if (!ctx[device]) {
         auto c = std::make_unique<ThreadCtx>();

@@ -123,6 +123,21 @@ int run_on_devices(const std::vector<int>& devs, const std::vector<std::function
     return rc;
 }
 
+void run_on_all_workers(const std::function<void()>& f) {
+    std::vector<Worker*> ws;
+    {
+        std::lock_guard<std::mutex> lk(g_workers_mu);
+        for (auto& kv : workers())
+            if (kv.second) ws.push_back(kv.second.get());
+    }
+    std::vector<std::future<int>> fut;
+    for (Worker* w : ws) fut.push_back(w->submit([f] {
+        f();
+        return 0;
+    }));
+    for (auto& x : fut) x.get();
+}
+
 std::future<int> run_async(std::function<int()> job) {
     return worker(-1).submit(std::move(job));  // key -1: the pipeline worker (no device of its own)
 }
@@ -149,13 +164,16 @@ using namespace bcc::host;
 extern "C" {
 
 int bcc_set_devices(const int* devices, int n) {
-    std::lock_guard<std::mutex> lk(g_devs_mu);
-    g_devs.clear();
-    g_devs_env_read = true;  // an explicit call overrides BCC_DEVICES
+    // validate everything first: a rejected call leaves the configured list unchanged
+    if (n < 0 || (n > 0 && !devices)) return -1;
+    std::vector<int> next;
     for (int i = 0; i < n; i++) {
         if (devices[i] < 0) return -1;
-        g_devs.push_back(devices[i]);
+        next.push_back(devices[i]);
     }
+    std::lock_guard<std::mutex> lk(g_devs_mu);
+    g_devs.swap(next);
+    g_devs_env_read = true;  // an explicit call overrides BCC_DEVICES
     return 0;
 }
 

@@ -23,6 +23,10 @@ int run_on_devices(const std::vector<int>& devs, const std::vector<std::function
 // batch is the pipeline's arena).
 std::future<int> run_async(std::function<int()> job);
 
+// Runs f() once on every persistent worker thread that exists (device workers and the pipeline
+// worker) and waits: releases the state those threads keep for themselves.
+void run_on_all_workers(const std::function<void()>& f);
+
 // Contiguous split of `weights` (in order) into k groups of about equal total weight; returns the
 // k + 1 group boundaries (indices into weights).
 std::vector<size_t> split_balanced(const std::vector<size_t>& weights, size_t k);

@@ -27,6 +27,7 @@
 #include "devices.h"
 #include "engine.h"
 #include "hashes.h"
+#include "host_verify.h"
 #include "script.h"
 #include "sighash.h"
 
@@ -52,11 +53,20 @@ namespace {
 thread_local bcc_batch_stats t_stats;
 
 // Fault injection (tests): the next N device rounds of any thread fail as if the HIP runtime had
-// returned an error (bcc_debug_fail_device_rounds, or BCC_FAULT_INJECT at load time).
+// returned g_fail_code (bcc_debug_fail_device_rounds[_code], or BCC_FAULT_INJECT at load time).
 std::atomic<int> g_fail_rounds{[] {
     const char* e = getenv("BCC_FAULT_INJECT");
     return e ? atoi(e) : 0;
 }()};
+std::atomic<int> g_fail_code{2};  // hipErrorOutOfMemory: transient
+
+// A HIP error worth one retry on a fresh device batch: allocation / readiness trouble.  Anything
+// else (launch failure, illegal address, no device, ECC, ...) leaves the context unusable, so the
+// round goes straight to the failure policy.
+bool retryable(int hip_error) {
+    return hip_error == 2 /* hipErrorOutOfMemory */ || hip_error == 600 /* hipErrorNotReady */ ||
+           hip_error == 1 /* hipErrorInvalidValue: staging limits */;
+}
 
 // Largest padded-message / template / code blob one device round may stage: the device job
 // records address them with 32-bit byte offsets (pipeline.h PatchRec / TplJob).
@@ -486,18 +496,20 @@ std::vector<std::vector<uint32_t>> make_shards(const BatchState& b, unsigned T) 
 int device_round(int dev, const SighashJobs* const* pj, const TupleRows* const* pr, size_t P,
                  uint8_t* verdict, double* stage_s) {
     for (int f = g_fail_rounds.load(); f > 0;)
-        if (g_fail_rounds.compare_exchange_weak(f, f - 1)) return 719;  // hipErrorLaunchFailure
+        if (g_fail_rounds.compare_exchange_weak(f, f - 1)) return g_fail_code.load();
     return gpu_verify_parts(dev, pj, pr, P, verdict, stage_s);
 }
 
 // Shards [t0, t1) of the round on device `dev`, as device batches whose blobs stay under
 // ROUND_BLOB_LIMIT (the device job records use 32-bit byte offsets): consecutive shards are
 // grouped greedily; a single shard above the limit is an error (reported, never silently
-// truncated).  A failed batch is retried once on a fresh device batch (gpu_verify_parts drops the
-// failed one); *retries counts those.  Returns 0 or the error.
+// truncated).  A batch failing with a transient error is retried once on a fresh device batch
+// (gpu_verify_parts drops the failed one); *retries counts those.  If the device still cannot
+// deliver, the failure policy decides: the batch is verified on the host (*host_rounds counts
+// those) or the error is returned.  Returns 0 or the error.
 int run_device_group(int dev, const std::vector<Round>& rds, unsigned t0, unsigned t1,
                      const std::vector<size_t>& row0, uint8_t* verdict, double* stage_total,
-                     size_t* retries) {
+                     size_t* retries, size_t* host_rounds) {
     unsigned g0 = t0;
     while (g0 < t1) {
         size_t sz[5] = {0, 0, 0, 0, 0};
@@ -511,10 +523,11 @@ int run_device_group(int dev, const std::vector<Round>& rds, unsigned t0, unsign
             if (!fits) break;
             for (int k = 0; k < 5; k++) sz[k] += add[k];
         }
-        if (g1 == g0) {
+        const bool too_big = g1 == g0;
+        if (too_big) {
             fprintf(stderr, "[bcc] verify_batch: one shard's sighash jobs exceed %zu bytes\n",
                     ROUND_BLOB_LIMIT);
-            return (int)1;  // hipErrorInvalidValue
+            g1 = g0 + 1;
         }
         std::vector<const SighashJobs*> pj;
         std::vector<const TupleRows*> pr;
@@ -523,17 +536,25 @@ int run_device_group(int dev, const std::vector<Round>& rds, unsigned t0, unsign
             pr.push_back(&rds[t].rows);
         }
         double st = 0;
-        int e = device_round(dev, pj.data(), pr.data(), pj.size(), verdict + row0[g0], &st);
-        if (e != 0) {
+        int e = too_big ? 1 : device_round(dev, pj.data(), pr.data(), pj.size(), verdict + row0[g0], &st);
+        if (e != 0 && retryable(e) && !too_big) {
             fprintf(stderr, "[bcc] verify_batch: device %d round failed (hip error %d), retrying\n",
                     dev, e);
             (*retries)++;
             e = device_round(dev, pj.data(), pr.data(), pj.size(), verdict + row0[g0], &st);
-            if (e != 0) {
-                fprintf(stderr, "[bcc] verify_batch: device %d round failed again (hip error %d)\n",
-                        dev, e);
+        }
+        if (e != 0) {
+            if (!host_fallback_enabled()) {
+                fprintf(stderr, "[bcc] verify_batch: device %d round failed (hip error %d), no "
+                                "verdict (BCC_DEVICE_FAILURE_ERROR)\n", dev, e);
                 return e;
             }
+            fprintf(stderr, "[bcc] verify_batch: device %d round failed (hip error %d): verifying "
+                            "its %zu checks on the host CPU\n",
+                    dev, e, row0[g1] - row0[g0]);
+            host_verify_parts(pj.data(), pr.data(), pj.size(), verdict + row0[g0], host_threads());
+            note_host_fallback();
+            (*host_rounds)++;
         }
         *stage_total += st;
         g0 = g1;
@@ -547,14 +568,24 @@ int run_device_group(int dev, const std::vector<Round>& rds, unsigned t0, unsign
 // the GPUs' worker threads and write their verdicts at their row offsets.
 int run_device_round(const std::vector<Round>& rds, unsigned T, const std::vector<size_t>& row0,
                      uint8_t* verdict, double* stage_total, size_t* devices_used,
-                     size_t* retries) {
+                     size_t* retries, size_t* host_rounds) {
+    if (row0[T] <= host_small_round()) {  // a small round: lower latency on the host CPU
+        std::vector<const SighashJobs*> pj;
+        std::vector<const TupleRows*> pr;
+        for (unsigned t = 0; t < T; t++) {
+            pj.push_back(&rds[t].jobs);
+            pr.push_back(&rds[t].rows);
+        }
+        (*host_rounds)++;
+        return host_verify_parts(pj.data(), pr.data(), T, verdict, host_threads());
+    }
     const std::vector<int> devs = device_list();
     std::vector<size_t> w(T);
     for (unsigned t = 0; t < T; t++) w[t] = rds[t].pending.size();
     const size_t D = std::min<size_t>(devs.size(), T);
     const std::vector<size_t> cut = split_balanced(w, D);
     std::vector<double> st(D, 0);
-    std::vector<size_t> rt(D, 0);
+    std::vector<size_t> rt(D, 0), hr(D, 0);
     std::vector<std::function<int()>> jobs;
     std::vector<int> jd;
     for (size_t d = 0; d < D; d++) {
@@ -562,13 +593,14 @@ int run_device_round(const std::vector<Round>& rds, unsigned T, const std::vecto
         jd.push_back(devs[d]);
         jobs.push_back([&, d] {
             return run_device_group(devs[d], rds, (unsigned)cut[d], (unsigned)cut[d + 1], row0,
-                                    verdict, &st[d], &rt[d]);
+                                    verdict, &st[d], &rt[d], &hr[d]);
         });
     }
     const int e = jobs.empty() ? 0 : run_on_devices(jd, jobs);
     for (size_t d = 0; d < D; d++) {
         *stage_total += st[d];
         *retries += rt[d];
+        *host_rounds += hr[d];
     }
     *devices_used = std::max(*devices_used, jobs.size());
     return e;
@@ -588,7 +620,7 @@ struct ChunkRun {
     std::future<int> fut;        // the device round in flight (pipelined)
     int sync_rc = 0;             // result of a synchronous device round
     double stage_s = 0;
-    size_t devices_used = 0, retries = 0;
+    size_t devices_used = 0, retries = 0, host_rounds = 0;
 };
 
 // Host state of bitcoinconsensus_verify_batch, per calling thread, reused across its calls: two
@@ -658,7 +690,7 @@ void chunk_start(ChunkRun& c, const bcc_batch_item* items, size_t n, unsigned fl
 // The chunk's pending device round (its arguments stay valid until the chunk's next pass).
 int chunk_device_round(ChunkRun& c) {
     return run_device_round(c.rds, c.T, c.row0, c.verdict.data(), &c.stage_s, &c.devices_used,
-                            &c.retries);
+                            &c.retries, &c.host_rounds);
 }
 
 // Stitches a device round's verdicts into the items; the items whose speculation failed get
@@ -705,9 +737,11 @@ long chunk_finish(ChunkRun& c, int* ret_out, bitcoinconsensus_error* err_out, bo
         *gpu_s += since(g0);
         t_stats.stage_seconds += c.stage_s;
         t_stats.device_retries += c.retries;
+        t_stats.host_rounds += c.host_rounds;
         t_stats.devices = std::max(t_stats.devices, c.devices_used);
         c.stage_s = 0;
         c.retries = 0;
+        c.host_rounds = 0;
         c.pending_round = false;
         if (e != 0) {
             status = -1;
@@ -953,11 +987,12 @@ int bitcoinconsensus_verify_script_with_amount(const unsigned char* scriptPubKey
         return set_err(err, bitcoinconsensus_ERR_TX_DESERIALIZE);
     }
     if (rc < 0) {
-        // The device failed twice in a row: there is no verdict, and the reference ABI has no
-        // code for "no verdict" (every error it reports is about the transaction, bitcoinconsensus.cpp
-        // :83-100).  Reporting 0 would reject a possibly valid spend as a consensus failure, so the
-        // call fails loudly instead, as libsecp256k1's illegal-argument callback does
-        // (secp256k1.c:45-54).  bitcoinconsensus_verify_batch reports the same condition as -1.
+        // Only under BCC_DEVICE_FAILURE_ERROR (the default policy verifies a failed round on the
+        // host): there is no verdict, and the reference ABI has no code for "no verdict" (every
+        // error it reports is about the transaction, bitcoinconsensus.cpp:83-100).  Reporting 0
+        // would reject a possibly valid spend as a consensus failure, so the call fails loudly
+        // instead, as libsecp256k1's illegal-argument callback does (secp256k1.c:45-54).
+        // bitcoinconsensus_verify_batch reports the same condition as -1.
         fprintf(stderr, "[bcc] bitcoinconsensus_verify_script_with_amount: GPU unavailable, no "
                         "verdict; aborting\n");
         abort();
@@ -996,7 +1031,15 @@ long bitcoinconsensus_verify_batch(const bcc_batch_item* items, size_t n, unsign
     }
 }
 
-void bcc_debug_fail_device_rounds(int rounds) { g_fail_rounds.store(rounds > 0 ? rounds : 0); }
+void bcc_debug_fail_device_rounds(int rounds) {
+    g_fail_code.store(2);
+    g_fail_rounds.store(rounds > 0 ? rounds : 0);
+}
+
+void bcc_debug_fail_device_rounds_code(int rounds, int hip_error) {
+    g_fail_code.store(hip_error ? hip_error : 2);
+    g_fail_rounds.store(rounds > 0 ? rounds : 0);
+}
 
 int bcc_set_pipeline_chunk(size_t items) {
     g_pipeline_chunk.store(items, std::memory_order_relaxed);
@@ -1006,6 +1049,14 @@ int bcc_set_pipeline_chunk(size_t items) {
 void bcc_release_thread_state(void) {
     for (auto& c : tl_chunk) c = ChunkRun();
     bcc::host::taproot_release_thread_state();
+    bcc::release_device_thread_state();
+    bcc::release_tuple_thread_state();
+    // the state the per-GPU and pipeline workers keep for the rounds they ran for callers
+    bcc::host::run_on_all_workers([] {
+        bcc::host::taproot_release_thread_state();
+        bcc::release_device_thread_state();
+        bcc::release_tuple_thread_state();
+    });
 }
 
 int bcc_set_device(int device) {

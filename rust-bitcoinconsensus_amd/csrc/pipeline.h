@@ -341,6 +341,11 @@ private:
 // throttled for the rest of the quota period.
 void set_stage_threads(unsigned n);
 
+// Free the calling thread's cached device state: the verify_batch / Taproot device batches and
+// contexts (sighash.hip) and the tuple-path contexts (ecdsa_verify.hip).
+void release_device_thread_state();
+void release_tuple_thread_state();
+
 // One-shot helper: stage + run + fetch on `device` (synchronous).
 // *stage_seconds (optional) receives the host -> HBM staging time.
 int gpu_verify_batch(int device, const SighashJobs& jobs, const TupleRows& rows, uint8_t* verdict,

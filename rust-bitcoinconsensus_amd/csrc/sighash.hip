@@ -845,6 +845,9 @@ int DeviceBatch::stage_parts(const SighashJobs* const* J, const TupleRows* const
     } else if (R) {  // every row's msg is uint256 ONE (byte 0 = 1); the sighash kernels overwrite theirs
         BCC_HIP_TRY(hipMemset(a + off[M], 0, 32 * R));
         BCC_HIP_TRY(hipMemset2D(a + off[M], 32, 1, 1, R));
+        // device memsets are asynchronous on the null stream, which the batch's non-blocking run
+        // streams do not wait for: finish them before any run can write the rows
+        BCC_HIP_TRY(hipStreamSynchronize(nullptr));
     }
     return 0;
 }
@@ -1043,14 +1046,16 @@ int gpu_verify_batch(int device, const SighashJobs& jobs, const TupleRows& rows,
     return gpu_verify_parts(device, &jp, &rp, 1, verdict, stage_seconds);
 }
 
+// one cached batch per (thread, device): repeated calls reuse the device arena, the pinned host
+// image, scratch and streams, and concurrent callers never share any of them
+thread_local std::vector<std::unique_ptr<DeviceBatch>> tl_batches;
+
 int gpu_verify_parts(int device, const SighashJobs* const* jobs, const TupleRows* const* rows,
                      size_t parts, uint8_t* verdict, double* stage_seconds) {
     size_t n = 0;
     for (size_t p = 0; p < parts; p++) n += rows[p]->size();
     if (n == 0) return 0;
-    // one cached batch per (thread, device): repeated calls reuse the device arena, the pinned
-    // host image, scratch and streams, and concurrent callers never share any of them
-    thread_local std::vector<std::unique_ptr<DeviceBatch>> cache;
+    auto& cache = tl_batches;
     if (device < 0) return (int)hipErrorInvalidDevice;
     if ((int)cache.size() <= device) cache.resize(device + 1);
     if (!cache[device]) cache[device] = std::make_unique<DeviceBatch>(device);
@@ -1108,6 +1113,14 @@ int gpu_taproot_verify(int device, const TaprootJobs& J, uint8_t* verdict, uint8
 
 // The parts (one per host thread) are concatenated straight into the pinned image, each part by
 // its own thread with its index fix-ups (no merged host copy), then go to HBM in one DMA copy.
+thread_local std::unique_ptr<TaprootCtx> tl_taproot_ctxs[64];
+
+// Frees the calling thread's device batches and Taproot contexts (bcc_release_thread_state).
+void release_device_thread_state() {
+    tl_batches.clear();
+    for (auto& c : tl_taproot_ctxs) c.reset();
+}
+
 int gpu_taproot_verify_parts(int device, const TaprootJobs* const* Jp, size_t P, uint8_t* verdict,
                              uint8_t* msg32_out) {
     std::vector<size_t> row0(P + 1, 0), aux0(P + 1, 0), msg0(P + 1, 0), auxi0(P + 1, 0),
@@ -1127,7 +1140,7 @@ int gpu_taproot_verify_parts(int device, const TaprootJobs* const* Jp, size_t P,
         fprintf(stderr, "[bcc] gpu_taproot_verify: a message blob exceeds 4 GiB; split the batch\n");
         return (int)hipErrorInvalidValue;
     }
-    thread_local std::unique_ptr<TaprootCtx> ctxs[64];
+    auto& ctxs = tl_taproot_ctxs;
     if (!ctxs[device]) {
         auto c = std::make_unique<TaprootCtx>();
         c->dev = device;

@@ -8,5 +8,22 @@ for p in (ROOT, PKG, os.path.dirname(os.path.abspath(__file__))):
         sys.path.insert(0, p)
 
 
+import pytest  # noqa: E402
+
+
+@pytest.fixture(autouse=True)
+def _gpu_rounds_ran_on_the_gpu(request):
+    """Every -m gpu test must exercise the HIP kernels: a device round that failed and was
+    verified on the host CPU (the library's failure policy) fails the test."""
+    if request.node.get_closest_marker("gpu") is None:
+        yield
+        return
+    import bitcoinconsensus_amd as B
+    before = B.host_fallback_rounds()
+    yield
+    assert B.host_fallback_rounds() == before, \
+        "a device round failed and was verified on the host CPU (see stderr)"
+
+
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs through the HIP C-ABI)")

@@ -32,6 +32,8 @@ def load():
     L = ctypes.CDLL(SO)
     L.bitcoinconsensus_verify_batch.restype = ctypes.c_long
     L.bcc_debug_fail_device_rounds.argtypes = [ctypes.c_int]
+    L.bcc_set_device_failure_policy.argtypes = [ctypes.c_int]
+    L.bcc_get_devices.argtypes = [ctypes.POINTER(ctypes.c_int), ctypes.c_int]
     L.bcc_set_devices.argtypes = [ctypes.POINTER(ctypes.c_int), ctypes.c_int]
     u64p = ctypes.POINTER(ctypes.c_uint64)
     L.bcc_pubkey_verify_batch.argtypes = [ctypes.c_char_p, u64p, ctypes.c_char_p, ctypes.c_char_p,

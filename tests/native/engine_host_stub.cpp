@@ -22,6 +22,8 @@ static size_t unpadded_len(const uint8_t* m, size_t padded) {
 
 int gpu_verify_batch(int, const SighashJobs& j, const TupleRows& rows, uint8_t* verdict, double*);
 void set_stage_threads(unsigned) {}  // the device batch is stubbed out
+void release_device_thread_state() {}
+void release_tuple_thread_state() {}
 int gpu_verify_parts(int dev, const SighashJobs* const* jobs, const TupleRows* const* rows, size_t parts,
                      uint8_t* verdict, double*) {
     size_t r0 = 0;

@@ -157,7 +157,8 @@ class Stats(ctypes.Structure):
         (k, ctypes.c_double) for k in ("host_seconds", "gpu_seconds", "prepare_seconds",
                                        "interpret_seconds", "merge_seconds", "stage_seconds",
                                        "total_seconds")] + [("device_retries", ctypes.c_size_t),
-                                                             ("devices", ctypes.c_size_t)]
+                                                             ("devices", ctypes.c_size_t),
+                                                             ("host_rounds", ctypes.c_size_t)]
 
 
 def test_device_failure_retried_once(eng):
@@ -173,13 +174,17 @@ def test_device_failure_retried_once(eng):
 
 
 def test_device_failure_never_reported_as_invalid(eng):
-    """Two failures in a row: verify_batch returns -1; items whose verdict needed the device get
-    ret 0 / BCC_ERR_DEVICE_FAILURE (6), never a consensus error; items decided on the host before
-    the device (here: bad flags) keep their reference result."""
+    """BCC_DEVICE_FAILURE_ERROR, two failures in a row: verify_batch returns -1; items whose
+    verdict needed the device get ret 0 / BCC_ERR_DEVICE_FAILURE (6), never a consensus error;
+    items decided on the host before the device (here: bad flags) keep their reference result."""
     vs = [v for v in load_json("crate_vectors.json") if v["flags"] == 0xE15]
-    eng.bcc_debug_fail_device_rounds(2)
-    rc, got = _batch(eng, vs)
-    eng.bcc_debug_fail_device_rounds(0)
+    assert eng.bcc_set_device_failure_policy(1) == 0
+    try:
+        eng.bcc_debug_fail_device_rounds(2)
+        rc, got = _batch(eng, vs)
+        eng.bcc_debug_fail_device_rounds(0)
+    finally:
+        eng.bcc_set_device_failure_policy(0)
     assert rc == -1
     for v, (r, e) in zip(vs, got):
         assert r == 0
@@ -191,9 +196,89 @@ def test_device_failure_never_reported_as_invalid(eng):
     assert rc == 0 and all(g == (0, 5) for g in got)
 
 
+def test_device_failure_verified_on_host(eng):
+    """The default policy (BCC_DEVICE_FAILURE_HOST): a round the device cannot deliver (a transient
+    error twice, or one sticky error, which is not retried) is verified on the host with the
+    engine's own code, and every item gets exactly the reference's result."""
+    vs = [v for v in load_json("crate_vectors.json") if v["flags"] == 0xE15]
+    exp = [(v["ret"], v["err"]) for v in vs]
+    eng.bcc_debug_fail_device_rounds_code.argtypes = [ctypes.c_int, ctypes.c_int]
+    eng.bcc_host_fallback_rounds.restype = ctypes.c_size_t
+    before = eng.bcc_host_fallback_rounds()
+    for inject, retries in ((lambda: eng.bcc_debug_fail_device_rounds(2), 1),
+                            (lambda: eng.bcc_debug_fail_device_rounds_code(1, 719), 0)):
+        inject()
+        rc, got = _batch(eng, vs)
+        eng.bcc_debug_fail_device_rounds(0)
+        st = Stats()
+        eng.bcc_last_batch_stats(ctypes.byref(st))
+        assert got == exp
+        assert rc == sum(v["ret"] for v in vs)
+        assert st.device_retries == retries and st.host_rounds == 1
+    assert eng.bcc_host_fallback_rounds() == before + 2
+    # the script-level goldens with every device round failing (one batch per flag set)
+    eng.bcc_debug_fail_device_rounds_code(1 << 20, 719)
+    try:
+        test_script_cases_as_batches(eng)
+    finally:
+        eng.bcc_debug_fail_device_rounds(0)
+
+
+def test_small_rounds_on_host(eng):
+    """bcc_set_host_small_round: rounds of at most that many checks run on the host CPU with the
+    same results (every script-level golden, single calls and batches)."""
+    eng.bcc_set_host_small_round.argtypes = [ctypes.c_size_t]
+    try:
+        eng.bcc_set_host_small_round(1 << 30)
+        test_script_cases_as_batches(eng)
+        vs = load_json("crate_vectors.json")
+        for v in vs:
+            got = call(eng, bytes.fromhex(v["spk"]), v["amount"], bytes.fromhex(v["tx"]), v["nin"],
+                       v["flags"])
+            assert got == (v["ret"], v["err"]), v["name"]
+            st = Stats()
+            eng.bcc_last_batch_stats(ctypes.byref(st))
+            assert st.host_rounds == st.rounds
+    finally:
+        eng.bcc_set_host_small_round(0)
+
+
+def test_set_devices_rejects_without_side_effect(eng):
+    """A rejected bcc_set_devices call (negative id anywhere) leaves the device list unchanged."""
+    engine_stub.set_devices(eng, [3, 4])
+    arr = (ctypes.c_int * 2)(0, -1)
+    assert eng.bcc_set_devices(arr, 2) == -1
+    out = (ctypes.c_int * 8)()
+    n = eng.bcc_get_devices(out, 8)
+    assert list(out)[:n] == [3, 4]
+    engine_stub.set_devices(eng, [])
+
+
+def test_single_call_with_device_failure_verified_on_host():
+    """Default policy: the single-item ABI returns the exact verdict after device failures."""
+    import sys
+    code = f"""
+import ctypes, json, os, sys
+sys.path.insert(0, {HERE!r})
+from fixtures import load_json
+L = ctypes.CDLL({SO!r})
+for v in load_json("crate_vectors.json"):
+    spk, tx = bytes.fromhex(v["spk"]), bytes.fromhex(v["tx"])
+    L.bcc_debug_fail_device_rounds(2)
+    e = ctypes.c_int(-1)
+    r = L.bitcoinconsensus_verify_script_with_amount(spk, len(spk), ctypes.c_int64(v["amount"]),
+                                                     tx, len(tx), v["nin"], v["flags"], ctypes.byref(e))
+    assert (r, e.value) == (v["ret"], v["err"]), v["name"]
+print("ok")
+"""
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0 and "ok" in p.stdout, (p.returncode, p.stdout, p.stderr)
+
+
 def test_single_call_aborts_without_verdict():
-    """The single-item ABI has no 'no verdict' code: after two device failures it aborts
-    (libsecp256k1's illegal-argument behaviour) rather than report a valid spend as invalid."""
+    """Under BCC_DEVICE_FAILURE=error the single-item ABI has no 'no verdict' code: after the
+    device fails it aborts (libsecp256k1's illegal-argument behaviour) rather than report a valid
+    spend as invalid."""
     import signal
     import sys
     code = f"""
@@ -209,7 +294,9 @@ r = L.bitcoinconsensus_verify_script_with_amount(spk, len(spk), ctypes.c_int64(v
                                                  len(tx), v["nin"], v["flags"], ctypes.byref(e))
 print("returned", r, e.value)
 """
-    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+    env = dict(os.environ, BCC_DEVICE_FAILURE="error")
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120,
+                       env=env)
     assert p.returncode == -signal.SIGABRT, (p.returncode, p.stdout, p.stderr)
     assert "GPU unavailable" in p.stderr
 
