@@ -302,7 +302,8 @@ class C2:
                 best, st = dt, self.B.last_batch_stats()
         return dict(inputs_per_s=self.n / best, ms=best * 1e3, valid=nv,
                     host_ms=st["host_seconds"] * 1e3, gpu_ms=st["gpu_seconds"] * 1e3,
-                    h2d_ms=st["stage_seconds"] * 1e3, host_threads="min(16, cores)")
+                    h2d_ms=st["stage_seconds"] * 1e3, host_threads=B.host_threads(),
+                    cpu_share=B.cpu_share())
 
     def cpu(self, sample):
         sample = min(sample, self.n)
@@ -374,7 +375,7 @@ class C3(C2):
                                                "aux_messages", "host_rejected", "host_seconds",
                                                "gpu_seconds", "prepare_seconds",
                                                "interpret_seconds", "merge_seconds",
-                                               "stage_seconds", "total_seconds")}
+                                               "stage_seconds", "total_seconds", "host_hashed")}
         e["note"] = ("value = inputs/s of bitcoinconsensus_verify_batch end to end from host "
                      "buffers (host deserialize + interpreter + preimage building on up to 16 "
                      "threads, H2D, GPU sighash + ECDSA, re-run rounds for CHECKMULTISIG key "

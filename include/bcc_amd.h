@@ -129,6 +129,20 @@ int bcc_set_chunk_lanes(size_t lanes);
  * DESIGN.md).  Results never depend on it. */
 int bcc_set_pipeline_chunk(size_t items);
 
+/* Signature checks whose serial SHA-256 chain is longer than `blocks` 64-byte blocks (the legacy
+ * preimages and BIP143 per-tx hashes of many-input transactions) are hashed on the host CPU
+ * instead of in one GPU lane each (default 32, or BCC_HOST_CHAIN_BLOCKS; 0: every chain on the
+ * GPU).  Results never depend on it. */
+int bcc_set_host_chain_blocks(unsigned blocks);
+
+/* Host worker threads of a batch pass (verify_batch interpreter shards, tuple / Taproot front
+ * ends, host-verified rounds).  0 restores the default: BCC_HOST_THREADS, else the process's CPU
+ * share (bcc_cpu_share, at most 64).  Results never depend on it. */
+int bcc_set_host_threads(unsigned n);
+unsigned bcc_get_host_threads(void);
+/* CPUs this process can keep busy: min(affinity mask, cgroup CPU quota). */
+unsigned bcc_cpu_share(void);
+
 /* bitcoinconsensus_verify_batch keeps its host-side state (items, parsed transactions, job
  * buffers) with the calling thread for reuse by its next call; batches above 4M items release it
  * on return.  bcc_taproot_verify_batch keeps its job buffers the same way, and every entry point
@@ -153,6 +167,8 @@ typedef struct bcc_batch_stats {
     size_t devices;        /* GPUs a device round was spread over (max over the call's rounds) */
     size_t host_rounds;    /* rounds (or device groups) verified on the host CPU: small rounds
                             * (bcc_set_host_small_round) and device-failure fallbacks */
+    size_t host_hashed;    /* deferred checks whose sighash the host computed (SHA chains longer
+                            * than bcc_set_host_chain_blocks) */
 } bcc_batch_stats;
 /* Statistics of the calling thread's last bitcoinconsensus_verify_batch / verify call. */
 void bcc_last_batch_stats(bcc_batch_stats* out);

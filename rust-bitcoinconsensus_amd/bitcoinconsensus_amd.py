@@ -205,7 +205,8 @@ class BatchStats(ctypes.Structure):
                 ("prepare_seconds", ctypes.c_double), ("interpret_seconds", ctypes.c_double),
                 ("merge_seconds", ctypes.c_double), ("stage_seconds", ctypes.c_double),
                 ("total_seconds", ctypes.c_double), ("device_retries", ctypes.c_size_t),
-                ("devices", ctypes.c_size_t), ("host_rounds", ctypes.c_size_t)]
+                ("devices", ctypes.c_size_t), ("host_rounds", ctypes.c_size_t),
+                ("host_hashed", ctypes.c_size_t)]
 
 
 def _bind_consensus(L):
@@ -426,6 +427,43 @@ def set_device_failure_policy(policy):
 def set_host_small_round(tuples):
     """bcc_set_host_small_round: device rounds of at most `tuples` checks run on the host CPU."""
     lib().bcc_set_host_small_round(tuples)
+
+
+def set_host_threads(n):
+    """bcc_set_host_threads: host worker threads of a batch pass (0: the default, cpu_share())."""
+    L = lib()
+    L.bcc_set_host_threads.argtypes = [ctypes.c_uint]
+    if L.bcc_set_host_threads(n) != 0:
+        raise ValueError(n)
+
+
+def host_threads():
+    L = lib()
+    L.bcc_get_host_threads.restype = ctypes.c_uint
+    return L.bcc_get_host_threads()
+
+
+def cpu_share():
+    """CPUs this process can keep busy: min(affinity, cgroup CPU quota) (bcc_cpu_share)."""
+    L = lib()
+    L.bcc_cpu_share.restype = ctypes.c_uint
+    return L.bcc_cpu_share()
+
+
+def set_host_chain_blocks(blocks):
+    """bcc_set_host_chain_blocks: checks whose SHA-256 chain exceeds `blocks` blocks are hashed on
+    the host CPU (0: every chain on the GPU)."""
+    L = lib()
+    L.bcc_set_host_chain_blocks.argtypes = [ctypes.c_uint]
+    L.bcc_set_host_chain_blocks(blocks)
+
+
+def set_pipeline_chunk(items):
+    """bcc_set_pipeline_chunk: verify_batch overlaps chunk k's device round with chunk k+1's host
+    pass (0 disables)."""
+    L = lib()
+    L.bcc_set_pipeline_chunk.argtypes = [ctypes.c_size_t]
+    L.bcc_set_pipeline_chunk(items)
 
 
 def host_fallback_rounds():

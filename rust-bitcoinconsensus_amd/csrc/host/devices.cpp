@@ -9,7 +9,12 @@
 // array at each group's row offset (the host-side gather).  No collective sits on this path.
 #include "devices.h"
 
+#include <sched.h>
+
+#include <algorithm>
+#include <atomic>
 #include <condition_variable>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <deque>
@@ -142,6 +147,56 @@ std::future<int> run_async(std::function<int()> job) {
     return worker(-1).submit(std::move(job));  // key -1: the pipeline worker (no device of its own)
 }
 
+namespace {
+
+// cgroup v2 "max 100000" / "1600000 100000", or v1 quota / period files; 0 = no quota
+double cgroup_quota_cpus() {
+    if (FILE* f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
+        char q[32] = {0};
+        long long period = 0;
+        const int k = fscanf(f, "%31s %lld", q, &period);
+        fclose(f);
+        if (k == 2 && strcmp(q, "max") != 0 && period > 0) return (double)atoll(q) / (double)period;
+        if (k >= 1) return 0;
+    }
+    long long quota = -1, period = 0;
+    if (FILE* f = fopen("/sys/fs/cgroup/cpu/cpu.cfs_quota_us", "r")) {
+        if (fscanf(f, "%lld", &quota) != 1) quota = -1;
+        fclose(f);
+    }
+    if (FILE* f = fopen("/sys/fs/cgroup/cpu/cpu.cfs_period_us", "r")) {
+        if (fscanf(f, "%lld", &period) != 1) period = 0;
+        fclose(f);
+    }
+    return quota > 0 && period > 0 ? (double)quota / (double)period : 0;
+}
+
+std::atomic<unsigned> g_host_threads{0};  // bcc_set_host_threads (0: default)
+
+}  // namespace
+
+unsigned cpu_share() {
+    static const unsigned share = [] {
+        unsigned n = std::max(1u, std::thread::hardware_concurrency());
+        cpu_set_t set;
+        if (sched_getaffinity(0, sizeof(set), &set) == 0) n = std::max(1, CPU_COUNT(&set));
+        const double q = cgroup_quota_cpus();
+        if (q > 0) n = std::min<unsigned>(n, std::max(1u, (unsigned)q));
+        return n;
+    }();
+    return share;
+}
+
+unsigned host_threads() {
+    if (unsigned v = g_host_threads.load(std::memory_order_relaxed)) return v;
+    static const unsigned dflt = [] {
+        if (const char* e = getenv("BCC_HOST_THREADS"))
+            if (atoi(e) > 0) return (unsigned)atoi(e);
+        return std::min(64u, cpu_share());
+    }();
+    return dflt;
+}
+
 std::vector<size_t> split_balanced(const std::vector<size_t>& w, size_t k) {
     size_t total = 0;
     for (size_t x : w) total += x;
@@ -176,6 +231,16 @@ int bcc_set_devices(const int* devices, int n) {
     g_devs_env_read = true;  // an explicit call overrides BCC_DEVICES
     return 0;
 }
+
+int bcc_set_host_threads(unsigned n) {
+    if (n > 1024) return -1;
+    g_host_threads.store(n, std::memory_order_relaxed);
+    return 0;
+}
+
+unsigned bcc_get_host_threads(void) { return host_threads(); }
+
+unsigned bcc_cpu_share(void) { return cpu_share(); }
 
 int bcc_get_devices(int* out, int cap) {
     const std::vector<int> d = device_list();

@@ -31,5 +31,16 @@ void run_on_all_workers(const std::function<void()>& f);
 // k + 1 group boundaries (indices into weights).
 std::vector<size_t> split_balanced(const std::vector<size_t>& weights, size_t k);
 
+// The CPUs this process may actually keep busy: the smaller of its affinity mask and its cgroup
+// CPU bandwidth quota (cgroup v2 cpu.max, or v1 cfs_quota_us / cfs_period_us), rounded down, at
+// least 1.  A quota is a per-period budget: more runnable threads than the quota do not run
+// faster, they exhaust the budget early and the whole cgroup is throttled until the period ends.
+unsigned cpu_share();
+
+// Host worker threads of one batch pass (verify_batch's interpreter shards, the tuple and Taproot
+// front ends, host-verified rounds): bcc_set_host_threads(), else BCC_HOST_THREADS, else
+// cpu_share() (capped at 64).
+unsigned host_threads();
+
 }  // namespace host
 }  // namespace bcc

@@ -30,6 +30,7 @@
 #include "host_verify.h"
 #include "script.h"
 #include "sighash.h"
+#include "team.h"
 
 namespace bcc {
 namespace host {
@@ -79,7 +80,40 @@ struct TxEntry {
     int64_t tpl = -1;               // legacy template offset in the current round (-1: none)
     uint32_t tpl_len = 0;
     int32_t wtx = -1;               // WtxRec index in the current round (-1: none)
+    int64_t htpl = -1;              // host-kept legacy template offset (HostJobs::tpl), -1: none
+    int32_t hdig = -1;              // host-computed BIP143 per-tx digests (HostJobs::dig), -1: none
 };
+
+// Long serial SHA chains stay on the host.  One GPU lane compresses one block
+// in ~6.5 us (the SHA-256 rounds are a dependent chain; a lone wave cannot hide their latency), the
+// host's SHA extensions in ~35 ns.  A many-input transaction (block413567's 442-input tx) has
+// chains of ~250-290 blocks -- its legacy preimages (every input's template is ~18 KB) and its
+// BIP143 hashPrevouts -- which would set the whole device round's front at ~2 ms while the rest of
+// the round's thousands of short chains finish in microseconds.  A check whose chain exceeds
+// host_chain_blocks() blocks is therefore hashed on the host: BIP143 checks of such a tx inline
+// (the per-tx digests once, then a ~4-block preimage each), legacy template / host-preimage jobs in
+// a parallel pass over all shards after the interpreter pass (run_host_jobs).  Their tuple rows
+// then carry the sighash in msg (uploaded); everything else is unchanged.
+struct HostJobs {
+    uint32_t chain_blocks = 0;       // offload threshold in 64-byte blocks (0: never)
+    std::vector<uint8_t> tpl, code;  // templates / code fields of offloaded legacy ALL jobs
+    std::vector<TplJob> tjobs;       // offsets into tpl / code, row = the tuple row
+    std::vector<uint8_t> pre;        // offloaded host preimages (NONE / SINGLE / ACP), unpadded
+    std::vector<uint64_t> pre_off;   // pre_off[k] .. pre_off[k + 1]: preimage k
+    std::vector<uint32_t> pre_row;
+    std::vector<uint8_t> dig;        // 96 bytes per long BIP143 tx: prevouts / sequence / outputs
+    size_t inline_rows = 0;          // rows whose msg add_sighash_job wrote itself
+    size_t pending() const { return tjobs.size() + pre_row.size(); }
+    void clear() {
+        tpl.clear(); code.clear(); tjobs.clear(); pre.clear(); pre_off.assign(1, 0); pre_row.clear();
+        dig.clear(); inline_rows = 0;
+    }
+};
+
+std::atomic<uint32_t> g_host_chain_blocks{[] {
+    const char* e = getenv("BCC_HOST_CHAIN_BLOCKS");
+    return e ? (uint32_t)atoi(e) : 32u;
+}()};
 
 struct Item {
     const bcc_batch_item* in;
@@ -145,34 +179,97 @@ uint32_t append_key(std::vector<uint8_t>& a, const Bytes& pub, const Bytes& sig,
 // preimage, SINGLE bug -> the row keeps ONE; BIP143: raw-tx job, SIGHASH_SINGLE: host preimage +
 // aux messages).  te's per-round slots (template, aux, raw tx) are filled on first use and te is
 // then appended to `touched` (Round::reset clears them).
+// BIP143 per-tx chains (hashPrevouts / hashSequence / hashOutputs) of tx, in 64-byte blocks
+uint32_t bip143_tx_chain_blocks(const Tx& tx) {
+    size_t out = 0;
+    for (const TxOut& o : tx.vout) out += o.ser.n;
+    return (uint32_t)(sha_padded_len(std::max<size_t>(36 * tx.vin.size(), out)) / 64);
+}
+
+// The BIP143 sighash of a long tx's check on the host: the tx's three digests once per round
+// (te.hdig), then the check's own preimage.
+void host_bip143_sighash(HostJobs& host, TxEntry& te, unsigned nin, const Bytes& code, int hashtype,
+                         int64_t amount, std::vector<uint8_t>& scratch, Bip143Job& job,
+                         std::vector<TxEntry*>& touched, uint8_t* out32) {
+    const Tx& tx = te.tx;
+    if (te.hdig < 0) {
+        te.hdig = (int32_t)(host.dig.size() / 96);
+        host.dig.resize(host.dig.size() + 96);
+        for (int k = 0; k < 3; k++) {
+            build_aux_message(tx, (AuxKind)k, scratch);
+            sha256d(scratch.data(), scratch.size(), &host.dig[96 * (size_t)te.hdig + 32 * k]);
+        }
+        touched.push_back(&te);
+    }
+    build_bip143_preimage(tx, nin, code, hashtype, amount, job);
+    for (int k = 0; k < 3; k++) {
+        if (!job.need[k]) continue;
+        if (k == AUX_OUTPUTS && job.single_output) {
+            const Span& o = tx.vout[nin].ser;
+            sha256d(o.p, o.n, &job.preimage[job.off[k]]);
+        } else {
+            memcpy(&job.preimage[job.off[k]], &host.dig[96 * (size_t)te.hdig + 32 * k], 32);
+        }
+    }
+    sha256d(job.preimage.data(), job.preimage.size(), out32);
+    host.inline_rows++;
+}
+
+// `host` (optional): checks whose SHA chain exceeds host->chain_blocks are hashed on the host
+// (HostJobs); `msg_row` = the tuple row's msg (BIP143 offloads write it at once).
 void add_sighash_job(SighashJobs& jobs, TxEntry& te, const bcc_batch_item& in, const Bytes& code,
                      SigVersion sv, int hashtype, uint32_t row, std::vector<uint8_t>& scratch,
-                     Bip143Job& bip143, std::vector<TxEntry*>& touched) {
+                     Bip143Job& bip143, std::vector<TxEntry*>& touched, HostJobs* host = nullptr,
+                     uint8_t* msg_row = nullptr) {
     const Tx& tx = te.tx;
     const unsigned nin = in.n_in;
+    const uint32_t hb = host && msg_row ? host->chain_blocks : 0;
     if (sv == SIGVERSION_BASE && legacy_all_type(hashtype)) {
-        // device-assembled from the tx template (pipeline.h TplJob)
-        if (te.tpl < 0) {
+        // device-assembled from the tx template (pipeline.h TplJob), or a host job (long template)
+        if (te.tpl < 0 && te.htpl < 0) {
             build_legacy_template(tx, scratch);
-            te.tpl = jobs.add_tpl(scratch.data(), scratch.size());
             te.tpl_len = (uint32_t)scratch.size();
+            if (hb && SighashJobs::tpl_nblk(te.tpl_len, 1) > hb) {
+                te.htpl = (int64_t)host->tpl.size();
+                host->tpl.insert(host->tpl.end(), scratch.begin(), scratch.end());
+            } else {
+                te.tpl = jobs.add_tpl(scratch.data(), scratch.size());
+            }
             touched.push_back(&te);
         }
         build_script_code_field(code, scratch);
         TplJob tj;
-        tj.tpl_off = (uint32_t)te.tpl;
         tj.tpl_len = te.tpl_len;
         tj.pos = (uint32_t)legacy_template_pos(tx, nin);
-        tj.code_off = jobs.add_code(scratch.data(), scratch.size());
         tj.code_len = (uint32_t)scratch.size();
         tj.hashtype = (uint32_t)hashtype;
         tj.row = row;
         tj.nblk = SighashJobs::tpl_nblk(tj.tpl_len, tj.code_len);
-        jobs.tjobs.push_back(tj);
+        if (te.htpl >= 0) {
+            tj.tpl_off = (uint32_t)te.htpl;
+            tj.code_off = (uint32_t)host->code.size();
+            host->code.insert(host->code.end(), scratch.begin(), scratch.end());
+            host->tjobs.push_back(tj);
+        } else {
+            tj.tpl_off = (uint32_t)te.tpl;
+            tj.code_off = jobs.add_code(scratch.data(), scratch.size());
+            jobs.tjobs.push_back(tj);
+        }
     } else if (sv == SIGVERSION_BASE) {
-        if (build_legacy_preimage(tx, nin, code, hashtype, scratch))
-            jobs.add_pre(scratch.data(), scratch.size(), row);
+        if (build_legacy_preimage(tx, nin, code, hashtype, scratch)) {
+            if (hb && sha_padded_len(scratch.size()) / 64 > hb) {
+                host->pre.insert(host->pre.end(), scratch.begin(), scratch.end());
+                host->pre_off.push_back(host->pre.size());
+                host->pre_row.push_back(row);
+            } else {
+                jobs.add_pre(scratch.data(), scratch.size(), row);
+            }
+        }
         // else: SIGHASH_SINGLE bug, msg stays ONE
+    } else if (hb && (te.hdig >= 0 || (te.wtx < 0 && bip143_tx_chain_blocks(tx) > hb))) {
+        // a long BIP143 tx: every check of it on the host, at once
+        host_bip143_sighash(*host, te, nin, code, hashtype, in.amount, scratch, bip143, touched,
+                            msg_row);
     } else if ((hashtype & 0x1f) != 3) {
         // BIP143 assembled on the device from the raw tx bytes (pipeline.h WinJob): the
         // host appends the tx once per round and a record per check
@@ -260,6 +357,7 @@ public:
     std::vector<uint8_t> keys;  // check identities of this shard's items (whole call, all rounds)
     Bip143Job bip143;
     std::vector<TxEntry*> touched;
+    HostJobs host;  // checks whose sighash the host computes (long chains)
     size_t host_rejected = 0;
 
     // GenericTransactionSignatureChecker::CheckECDSASignature (interpreter.cpp:1656-1676) up to
@@ -301,7 +399,8 @@ public:
         const uint8_t* y = pub.size() == 65 ? pub.data() + 33 : ybuf;  // y unused for 02/03
         uint32_t row = rows.add(pub[0], pub.data() + 1, y, r, s, one);
         if (pub.size() == 65) rows.y_unused = false;
-        add_sighash_job(jobs, *it.tx, *it.in, code, sv, hashtype, row, scratch, bip143, touched);
+        add_sighash_job(jobs, *it.tx, *it.in, code, sv, hashtype, row, scratch, bip143, touched,
+                        &host, &rows.msg[32 * (size_t)row]);
         it.cache.push_back(Item::Check{koff, klen, -2 - (int32_t)pending.size()});
         if (consult) it.pending.push_back((uint32_t)pending.size());
         pending.push_back(Pending{item_idx, (uint32_t)(it.cache.size() - 1)});
@@ -314,14 +413,63 @@ public:
         rows.msg_one = true;   // every row enters with msg = ONE (defer)
         rows.y_unused = true;  // until a 65-byte key is deferred
         pending.clear();
+        host.clear();
+        host.chain_blocks = g_host_chain_blocks.load(std::memory_order_relaxed);
         for (auto* t : touched) {
             t->aux[0] = t->aux[1] = t->aux[2] = -1;
             t->tpl = -1;
             t->wtx = -1;
+            t->htpl = -1;
+            t->hdig = -1;
         }
         touched.clear();
     }
 };
+
+// The offloaded legacy jobs of every shard, hashed in parallel on the calling thread's team (their
+// rows' msg receive the sighash).  Marks the rows of every shard with host-written messages for
+// upload.
+void run_host_jobs(std::vector<Round>& rds, unsigned T) {
+    std::vector<std::pair<uint32_t, uint32_t>> work;  // (shard, job): tjobs first, then pre
+    for (unsigned t = 0; t < T; t++) {
+        HostJobs& h = rds[t].host;
+        if (h.pending() || h.inline_rows) rds[t].rows.msg_one = false;
+        for (uint32_t k = 0; k < h.pending(); k++) work.emplace_back(t, k);
+    }
+    if (work.empty()) return;
+    size_t blocks = 0;
+    for (const auto& w : work) {
+        const HostJobs& h = rds[w.first].host;
+        blocks += w.second < h.tjobs.size() ? h.tjobs[w.second].nblk : 8;
+    }
+    const unsigned W = (unsigned)std::max<size_t>(1, std::min<size_t>(std::min<size_t>(T, host_threads()),
+                                                                         blocks / 256 + 1));
+    // jobs are dealt round-robin: the long ones of one tx are spread over every worker
+    run_team(W, [&](unsigned w) {
+        for (size_t i = w; i < work.size(); i += W) {
+            Round& rd = rds[work[i].first];
+            HostJobs& h = rd.host;
+            uint8_t* out = rd.rows.msg.data();
+            const uint32_t k = work[i].second;
+            uint8_t d[32];
+            if (k < h.tjobs.size()) {
+                const TplJob& t = h.tjobs[k];
+                const uint8_t* T0 = &h.tpl[t.tpl_off];
+                uint8_t ht[4];
+                for (int b = 0; b < 4; b++) ht[b] = (uint8_t)(t.hashtype >> (8 * b));
+                Sha256 x;
+                x.write(T0, t.pos).write(&h.code[t.code_off], t.code_len);
+                x.write(T0 + t.pos + 1, t.tpl_len - t.pos - 1).write(ht, 4);
+                x.finalize(d);
+                sha256(d, 32, out + 32 * (size_t)t.row);
+            } else {
+                const size_t j = k - h.tjobs.size();
+                sha256d(&h.pre[h.pre_off[j]], h.pre_off[j + 1] - h.pre_off[j],
+                        out + 32 * (size_t)h.pre_row[j]);
+            }
+        }
+    });
+}
 
 bool DeferringChecker::check_ecdsa(const Bytes& sig, const Bytes& pub, const Bytes& code,
                                    SigVersion sv) {
@@ -348,27 +496,10 @@ struct BatchState {
     unsigned flags = 0;
 };
 
-unsigned host_threads() {
-    static const unsigned t = [] {
-        const char* e = getenv("BCC_HOST_THREADS");
-        unsigned v = e ? (unsigned)atoi(e) : std::min(16u, std::thread::hardware_concurrency());
-        return std::max(1u, v);
-    }();
-    return t;
-}
-
-// Runs f(t) for t in [0, T) on T threads (inline when T == 1).
+// Runs f(t) for t in [0, T) on the calling thread's persistent team (inline when T == 1).
 template <class F>
 void run_threads(unsigned T, F f) {
-    if (T <= 1) {
-        f(0u);
-        return;
-    }
-    std::vector<std::thread> th;
-    th.reserve(T - 1);
-    for (unsigned t = 1; t < T; t++) th.emplace_back(f, t);
-    f(0u);
-    for (auto& x : th) x.join();
+    run_team(T, std::function<void(unsigned)>(f));
 }
 
 // Contiguous [lo, hi) share t of T over n units.
@@ -638,6 +769,7 @@ void chunk_interpret(ChunkRun& c) {
         c.rds[t].reset();
         ran[t] = interpret_shard(c.b, c.run_list[t], c.rds[t]);
     });
+    run_host_jobs(c.rds, c.T);
     t_stats.interpret_seconds += since(i0);
     size_t npend = 0;
     bool any = false;
@@ -654,6 +786,7 @@ void chunk_interpret(ChunkRun& c) {
         t_stats.preimages += c.rds[t].jobs.pre_off.size() + c.rds[t].jobs.tjobs.size() +
                              c.rds[t].jobs.wjobs.size();
         t_stats.aux_messages += c.rds[t].jobs.aux_off.size() + 3 * c.rds[t].jobs.wtx.size();
+        t_stats.host_hashed += c.rds[t].host.pending() + c.rds[t].host.inline_rows;
     }
     t_stats.rounds++;
     t_stats.tuples += npend;
@@ -1041,6 +1174,11 @@ void bcc_debug_fail_device_rounds_code(int rounds, int hip_error) {
     g_fail_rounds.store(rounds > 0 ? rounds : 0);
 }
 
+int bcc_set_host_chain_blocks(unsigned blocks) {
+    bcc::host::g_host_chain_blocks.store(blocks, std::memory_order_relaxed);
+    return 0;
+}
+
 int bcc_set_pipeline_chunk(size_t items) {
     g_pipeline_chunk.store(items, std::memory_order_relaxed);
     return 0;
@@ -1051,11 +1189,13 @@ void bcc_release_thread_state(void) {
     bcc::host::taproot_release_thread_state();
     bcc::release_device_thread_state();
     bcc::release_tuple_thread_state();
+    bcc::host::release_team();
     // the state the per-GPU and pipeline workers keep for the rounds they ran for callers
     bcc::host::run_on_all_workers([] {
         bcc::host::taproot_release_thread_state();
         bcc::release_device_thread_state();
         bcc::release_tuple_thread_state();
+        bcc::host::release_team();
     });
 }
 

@@ -31,6 +31,7 @@
 #include "hashes.h"
 #include "host_verify.h"
 #include "sighash.h"
+#include "team.h"
 #include "tx.h"
 
 namespace bcc {
@@ -69,12 +70,9 @@ void parallel_for(size_t n, unsigned T, F f) {
         for (size_t i = 0; i < n; i++) f(i);
         return;
     }
-    std::vector<std::thread> th;
-    for (unsigned t = 0; t < T; t++)
-        th.emplace_back([&, t] {
-            for (size_t i = n * t / T; i < n * (t + 1) / T; i++) f(i);
-        });
-    for (auto& x : th) x.join();
+    run_team(T, [&](unsigned t) {
+        for (size_t i = n * t / T; i < n * (t + 1) / T; i++) f(i);
+    });
 }
 
 }  // namespace

@@ -18,6 +18,7 @@
 #include "bcc_amd.h"
 #include "devices.h"
 #include "engine.h"
+#include "team.h"
 #include "tuples.h"
 #include "tx.h"
 
@@ -234,13 +235,9 @@ int run_range(const bcc_taproot_check* items, size_t lo, size_t hi, int* ret, in
     // round fills ~650 MB of job blobs, which fresh vectors would page-fault in every call
     std::vector<Part>& parts = tl_parts;
     if (parts.size() < cut.size() - 1) parts.resize(cut.size() - 1);
-    {
-        std::vector<std::thread> th;
-        for (size_t p = 1; p + 1 < cut.size(); p++)
-            th.emplace_back(build_part, items, cut[p], cut[p + 1], ret, serr, std::ref(parts[p]));
-        build_part(items, cut[0], cut[1], ret, serr, parts[0]);
-        for (auto& x : th) x.join();
-    }
+    run_team((unsigned)(cut.size() - 1), [&](unsigned p) {
+        build_part(items, cut[p], cut[p + 1], ret, serr, parts[p]);
+    });
     const size_t NP = cut.size() - 1;
     size_t aux_b = 0, msg_b = 0;
     for (size_t p = 0; p < NP; p++) {

@@ -18,8 +18,7 @@ namespace bcc {
 namespace host {
 
 unsigned pool_threads(size_t n, size_t grain) {
-    unsigned T = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-    return (unsigned)std::max<size_t>(1, std::min<size_t>(T, n / grain));
+    return (unsigned)std::max<size_t>(1, std::min<size_t>(host_threads(), n / grain));
 }
 
 // One tuple's host half of CPubKey::Verify into row i of preallocated rows.  A tuple the host

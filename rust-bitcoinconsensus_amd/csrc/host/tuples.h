@@ -7,11 +7,12 @@
 #include <vector>
 
 #include "../pipeline.h"
+#include "team.h"
 
 namespace bcc {
 namespace host {
 
-// Threaded pool helpers (up to 16 threads, at least `grain` items per thread).
+// Threaded pool helpers (up to host_threads() threads, at least `grain` items per thread).
 unsigned pool_threads(size_t n, size_t grain);
 // f(lo, hi) over contiguous chunks of [0, n) on pool_threads(n, grain) threads
 template <class F>
@@ -21,9 +22,7 @@ void pfor(size_t n, size_t grain, F f) {
         f(0, n);
         return;
     }
-    std::vector<std::thread> th;
-    for (unsigned t = 0; t < T; t++) th.emplace_back([=]() { f(n * t / T, n * (t + 1) / T); });
-    for (auto& x : th) x.join();
+    run_team(T, [&](unsigned t) { f(n * t / T, n * (t + 1) / T); });
 }
 
 // rows[i] for tuple i (rows resized to n): tag 0 (rejected on the host) unless the pubkey passes

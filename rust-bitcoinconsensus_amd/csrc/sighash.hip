@@ -15,6 +15,7 @@
 #include "pipeline.h"
 #include "sha256_device.h"
 #include "host/hashes.h"
+#include "host/team.h"
 
 namespace bcc {
 
@@ -829,13 +830,9 @@ int DeviceBatch::stage_parts(const SighashJobs* const* J, const TupleRows* const
     if (nth <= 1 || upload < ((size_t)1 << 20)) {
         for (size_t p = 0; p < P; p++) fill(p);
     } else {
-        auto fill_some = [&](size_t t) {
+        host::run_team((unsigned)nth, [&](unsigned t) {
             for (size_t p = t; p < P; p += nth) fill(p);
-        };
-        std::vector<std::thread> th;
-        for (size_t t = 1; t < nth; t++) th.emplace_back(fill_some, t);
-        fill_some(0);
-        for (auto& x : th) x.join();
+        });
     }
     BCC_HIP_TRY(hipSetDevice(dev_));
     BCC_HIP_TRY(hipMemcpy(arena_, host_image_, upload, hipMemcpyHostToDevice));

@@ -28,10 +28,18 @@ def wl():
     return B.Workload(kind="block", shape=sub, seed=0x5EED0003)
 
 
-def test_block_workload_all_valid_and_matches_reference(wl):
+@pytest.mark.parametrize("chain_blocks", [32, 0])
+def test_block_workload_all_valid_and_matches_reference(wl, chain_blocks):
+    """chain_blocks 32 (default): the big tx's long SHA chains hashed on the host; 0: every
+    chain in a GPU lane."""
     import bitcoinconsensus_amd as B
-    n_valid, ret = wl.verify_batch()
-    st = B.last_batch_stats()
+    B.set_host_chain_blocks(chain_blocks)
+    try:
+        n_valid, ret = wl.verify_batch()
+        st = B.last_batch_stats()
+    finally:
+        B.set_host_chain_blocks(32)
+    assert (st["host_hashed"] > 0) == (chain_blocks > 0)
     assert n_valid == wl.n and all(r == 1 for r in ret)
     assert st["rounds"] == 1          # multisig candidate pairs are queued up front: no re-run
     assert st["tuples"] > wl.n        # multisig inputs verify 2-3 signatures

@@ -71,7 +71,7 @@ def test_script_cases_single_calls(eng):
     assert not bad, bad[:10]
 
 
-def test_script_cases_as_batches(eng):
+def test_script_cases_as_batches(eng, stats=None):
     """verify_batch per flag set == single calls (shared tx buffers parsed once)."""
     allc = cases()
     by_flags = {}
@@ -93,6 +93,10 @@ def test_script_cases_as_batches(eng):
         got = list(zip(ret, err))
         assert got == exp
         assert nvalid == sum(r for r, _ in exp)
+        if stats is not None:
+            st = Stats()
+            eng.bcc_last_batch_stats(ctypes.byref(st))
+            stats.append(st.host_hashed)
 
 
 def test_script_cases_pipelined(eng):
@@ -111,6 +115,24 @@ def test_script_cases_pipelined(eng):
     finally:
         engine_stub.set_devices(eng, [])
         eng.bcc_set_pipeline_chunk(0)
+
+
+@pytest.mark.parametrize("blocks", [1, 2, 5])
+def test_script_cases_host_hashed_chains(eng, blocks):
+    """Checks whose SHA chain exceeds `blocks` blocks hashed on the host (legacy template and
+    preimage jobs in the parallel pass, long-tx BIP143 checks inline): identical results, as
+    batches and as single calls."""
+    eng.bcc_set_host_chain_blocks.argtypes = [ctypes.c_uint]
+    try:
+        eng.bcc_set_host_chain_blocks(blocks)
+        hashed = []
+        test_script_cases_as_batches(eng, hashed)
+        assert sum(hashed) > 0  # the offload ran
+        if blocks == 1:
+            test_script_cases_single_calls(eng)
+            test_crate_vectors(eng)
+    finally:
+        eng.bcc_set_host_chain_blocks(32)
 
 
 def test_pubkey_verify_batch_front_end(eng):
@@ -158,7 +180,8 @@ class Stats(ctypes.Structure):
                                        "interpret_seconds", "merge_seconds", "stage_seconds",
                                        "total_seconds")] + [("device_retries", ctypes.c_size_t),
                                                              ("devices", ctypes.c_size_t),
-                                                             ("host_rounds", ctypes.c_size_t)]
+                                                             ("host_rounds", ctypes.c_size_t),
+                                                             ("host_hashed", ctypes.c_size_t)]
 
 
 def test_device_failure_retried_once(eng):
