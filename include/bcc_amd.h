@@ -131,8 +131,7 @@ int bcc_set_pipeline_chunk(size_t items);
 
 /* Signature checks whose serial SHA-256 chain is longer than `blocks` 64-byte blocks (the legacy
  * preimages and BIP143 per-tx hashes of many-input transactions) are hashed on the host CPU
- * instead of in one GPU lane each (default 32, or BCC_HOST_CHAIN_BLOCKS; 0: every chain on the
- * GPU).  Results never depend on it. */
+ * instead of in one GPU lane each (BCC_HOST_CHAIN_BLOCKS; default 0: every chain on the GPU).  Results never depend on it. */
 int bcc_set_host_chain_blocks(unsigned blocks);
 
 /* Host worker threads of a batch pass (verify_batch interpreter shards, tuple / Taproot front
@@ -169,6 +168,9 @@ typedef struct bcc_batch_stats {
                             * (bcc_set_host_small_round) and device-failure fallbacks */
     size_t host_hashed;    /* deferred checks whose sighash the host computed (SHA chains longer
                             * than bcc_set_host_chain_blocks) */
+    /* more of the host pass: shard / run lists, stitching verdicts into items, writing ret / err,
+     * the host-hashed long chains */
+    double shard_seconds, stitch_seconds, finish_seconds, host_jobs_seconds;
 } bcc_batch_stats;
 /* Statistics of the calling thread's last bitcoinconsensus_verify_batch / verify call. */
 void bcc_last_batch_stats(bcc_batch_stats* out);

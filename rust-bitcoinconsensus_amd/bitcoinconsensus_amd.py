@@ -206,7 +206,9 @@ class BatchStats(ctypes.Structure):
                 ("merge_seconds", ctypes.c_double), ("stage_seconds", ctypes.c_double),
                 ("total_seconds", ctypes.c_double), ("device_retries", ctypes.c_size_t),
                 ("devices", ctypes.c_size_t), ("host_rounds", ctypes.c_size_t),
-                ("host_hashed", ctypes.c_size_t)]
+                ("host_hashed", ctypes.c_size_t), ("shard_seconds", ctypes.c_double),
+                ("stitch_seconds", ctypes.c_double), ("finish_seconds", ctypes.c_double),
+                ("host_jobs_seconds", ctypes.c_double)]
 
 
 def _bind_consensus(L):

@@ -134,26 +134,21 @@ BCC_HD bool twist_prep_key(u32 tag, const fe& px, const fe& py, QT& qt, TwistSta
     return true;
 }
 
-// Prep, scalar half (after twist_prep_key; `flags` = its st.flags): r / s range checks
-// (ecdsa_impl.h:216-222), u1 / u2, GLV split of u2, the odd fix-ups.  Returns false (st.flags
-// = 0) when the tuple is rejected outright.
-BCC_HD bool twist_prep_scalars(u32 flags, const sc& r_in, const sc& s_in, const sc& m_in,
-                               const sc* sinv_pre, TwistState& st) {
+// Prep, the signature half (after twist_prep_key; `flags` = its st.flags): r / s range checks
+// (ecdsa_impl.h:216-222), u2 = r s^-1 and its GLV split, the odd fix-ups.  Nothing here reads the
+// message, so the Q ladder (B = u2 Q_w) can run beside the sighash kernels.  Returns false
+// (st.flags = 0) when the tuple is rejected outright; *sinv_out (optional) receives s^-1.
+BCC_HD bool twist_prep_u2(u32 flags, const sc& r_in, const sc& s_in, const sc* sinv_pre,
+                          TwistState& st, sc* sinv_out = nullptr) {
     const u32 N[8] = BCC_N_LIMBS;
     st.flags = 0;
     if (!(flags & LS_VALID)) return false;
     if (u256_is_zero(r_in.v) || u256_is_zero(s_in.v)) return false;
     if (!u256_lt(r_in.v, N) || !u256_lt(s_in.v, N)) return false;
-    sc m = m_in;
-    if (!u256_lt(m.v, N)) {
-        u32 tmp[8];
-        u256_sub(tmp, m.v, N);
-        for (int i = 0; i < 8; i++) m.v[i] = tmp[i];
-    }
-    sc sinv, u1, u2, k1, k2;
+    sc sinv, u2, k1, k2;
     if (sinv_pre) sinv = *sinv_pre;
     else sc_inv(sinv, s_in);
-    sc_mul(u1, m, sinv);
+    if (sinv_out) *sinv_out = sinv;
     sc_mul(u2, r_in, sinv);
     // u2 = k1 + lambda k2 for the Q ladder, both halves odd (corrections at the end)
     sc_split_lambda(k1, k2, u2);
@@ -165,19 +160,9 @@ BCC_HD bool twist_prep_scalars(u32 flags, const sc& r_in, const sc& s_in, const 
         sc_neg(k2, k2);
         flags |= LS_NEG1;
     }
-    // u1 for the comb: odd by negation (u1 G = -((n - u1) G)), so A needs no correction
-    if (sc_is_zero(u1)) {
-        flags |= LS_U1ZERO;
-        u1.v[0] = 1u;
-    } else if ((u1.v[0] & 1u) == 0) {
-        sc_neg(u1, u1);
-        flags |= LS_NEGU1;
-    }
     for (int i = 0; i < 4; i++) {
         st.k[0][i] = k1.v[i];
         st.k[1][i] = k2.v[i];
-        st.k[2][i] = u1.v[i];
-        st.k[3][i] = u1.v[4 + i];
     }
     for (int s = 0; s < 2; s++) {
         if ((st.k[s][0] & 1u) == 0) flags |= LS_CORR0 << s;
@@ -185,6 +170,40 @@ BCC_HD bool twist_prep_scalars(u32 flags, const sc& r_in, const sc& s_in, const 
     }
     st.flags = flags;
     st.r = r_in;
+    return true;
+}
+
+// Prep, the message half: u1 = (m mod n) s^-1 for the comb, odd by negation (u1 G = -((n - u1) G),
+// so A needs no correction); sets LS_U1ZERO / LS_NEGU1 in *flags and the u1 words k2 (0..3) and
+// k3 (4..7).
+BCC_HD void twist_prep_u1(const sc& m_in, const sc& sinv, u32* flags, u32 (&k2)[4], u32 (&k3)[4]) {
+    const u32 N[8] = BCC_N_LIMBS;
+    sc m = m_in, u1;
+    if (!u256_lt(m.v, N)) {
+        u32 tmp[8];
+        u256_sub(tmp, m.v, N);
+        for (int i = 0; i < 8; i++) m.v[i] = tmp[i];
+    }
+    sc_mul(u1, m, sinv);
+    if (sc_is_zero(u1)) {
+        *flags |= LS_U1ZERO;
+        u1.v[0] = 1u;
+    } else if ((u1.v[0] & 1u) == 0) {
+        sc_neg(u1, u1);
+        *flags |= LS_NEGU1;
+    }
+    for (int i = 0; i < 4; i++) {
+        k2[i] = u1.v[i];
+        k3[i] = u1.v[4 + i];
+    }
+}
+
+// Prep, scalar half: both of the above.
+BCC_HD bool twist_prep_scalars(u32 flags, const sc& r_in, const sc& s_in, const sc& m_in,
+                               const sc* sinv_pre, TwistState& st) {
+    sc sinv;
+    if (!twist_prep_u2(flags, r_in, s_in, sinv_pre, st, &sinv)) return false;
+    twist_prep_u1(m_in, sinv, &st.flags, st.k[2], st.k[3]);
     return true;
 }
 

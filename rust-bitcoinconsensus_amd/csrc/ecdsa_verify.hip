@@ -599,6 +599,34 @@ __global__ __launch_bounds__(256) void ecdsa_tscal_kernel(
     tw_store(w, T_R, st.r.v);
 }
 
+// The signature half of K_tscal alone (K_tscal_q): r / s checks, u2 and its GLV split -- no
+// message, so it and the Q ladder after it run beside the sighash kernels; u1 is formed by the G
+// ladder kernel once the sighashes exist.
+__global__ __launch_bounds__(256) void ecdsa_tscal_q_kernel(
+    const uint8_t* __restrict__ pr, const uint8_t* __restrict__ ps,
+    const u32* __restrict__ psinv, size_t cnt, u32* __restrict__ state) {
+    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= cnt) return;
+    u32* w = lane_words(state, t, TSTATE_WORDS);
+    const u32 kflags = w[T_FLAGS * LANE_STRIDE];
+    if (!(kflags & LS_VALID)) return;  // K_tkey rejected the key (flags 0)
+    sc r, s, si;
+    load_be32(r, pr + 32 * t);
+    load_be32(s, ps + 32 * t);
+    load_limbs(si, psinv + 8 * t);
+    TwistState st;
+    if (!twist_prep_u2(kflags, r, s, &si, st)) {
+        w[T_FLAGS * LANE_STRIDE] = 0u;
+        return;
+    }
+#pragma unroll
+    for (int a = 0; a < 2; a++)
+#pragma unroll
+        for (int b = 0; b < 4; b++) w[(T_K + a * 4 + b) * LANE_STRIDE] = st.k[a][b];
+    w[T_FLAGS * LANE_STRIDE] = st.flags;
+    tw_store(w, T_R, st.r.v);
+}
+
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void schnorr_tprep_kernel(
     const uint8_t* __restrict__ psig, const uint8_t* __restrict__ pm,
     const uint8_t* __restrict__ ppk, size_t base, size_t cnt, u32* __restrict__ qtab,
@@ -634,31 +662,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
 #endif
 constexpr int TLADDER_WG = BCC_TLADDER_WG;
 
+// The Q half of the ladder: B = u2 Q_w (or the BIP340 e P_w), parked in the lane's own table
+// words (dead after the Q loop) for the G half.
+__device__ __forceinline__ void twist_q_part(u32* lt, const TwistStateView& st) {
+    gej B;
+    const bool binf = twist_accumulate_q(st, QTableGlobal{lt}, B);
+    park_gej(lt + PARK_B, B, binf);
+}
+
+// The G half: A = u1 G by the comb, B back from the table, the w-free combine; writes the lane's
+// status (and alpha / beta / K, or the parked A for the exact fallback).
 template <bool BIP340>
-__global__ __launch_bounds__(TLADDER_WG) __attribute__((amdgpu_waves_per_eu(BCC_LADDER_WAVES, BCC_LADDER_WAVES))) void twist_ladder_kernel(
-    u32* __restrict__ state, u32* __restrict__ qtab, const u32* __restrict__ gcomb, size_t cnt) {
-    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= cnt) return;
-    u32* w = lane_words(state, t, TSTATE_WORDS);
-    TwistStateView st;
-    st.p = w;
-    st.flags = w[T_FLAGS * LANE_STRIDE];
-    if (!(st.flags & LS_VALID)) {
-        w[T_STAT * LANE_STRIDE] = TW_REJECT;
-        return;
-    }
-    tw_load(st.sigma.v, w, T_SIGMA);
-    u32* lt = lane_table(qtab, t);
-    QTableGlobal qt{lt};
-    GCombGlobal gc{gcomb};
+__device__ __forceinline__ void twist_g_part(u32* w, u32* lt, const u32* gcomb, TwistStateView& st) {
     u32 stat = TW_NORMAL;
-    {
-        gej B;
-        const bool binf = twist_accumulate_q(st, qt, B);
-        park_gej(lt + PARK_B, B, binf);
-    }
     gej A, B;
-    const bool ainf = twist_accumulate_g(st, gc, A);
+    const bool ainf = twist_accumulate_g(st, GCombGlobal{gcomb}, A);
     const bool binf = unpark_gej(lt + PARK_B, B);
     fe v, al, be, K;
     sc r;
@@ -686,6 +704,72 @@ __global__ __launch_bounds__(TLADDER_WG) __attribute__((amdgpu_waves_per_eu(BCC_
         tw_store(w, T_KK, K.v);  // BIP340: Dd
     }
     w[T_STAT * LANE_STRIDE] = stat;
+}
+
+template <bool BIP340>
+__global__ __launch_bounds__(TLADDER_WG) __attribute__((amdgpu_waves_per_eu(BCC_LADDER_WAVES, BCC_LADDER_WAVES))) void twist_ladder_kernel(
+    u32* __restrict__ state, u32* __restrict__ qtab, const u32* __restrict__ gcomb, size_t cnt) {
+    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= cnt) return;
+    u32* w = lane_words(state, t, TSTATE_WORDS);
+    TwistStateView st;
+    st.p = w;
+    st.flags = w[T_FLAGS * LANE_STRIDE];
+    if (!(st.flags & LS_VALID)) {
+        w[T_STAT * LANE_STRIDE] = TW_REJECT;
+        return;
+    }
+    tw_load(st.sigma.v, w, T_SIGMA);
+    u32* lt = lane_table(qtab, t);
+    twist_q_part(lt, st);
+    twist_g_part<BIP340>(w, lt, gcomb, st);
+}
+
+// The ECDSA ladder in two launches (ecdsa_launch_q / ecdsa_launch_after_pre): K_tladder_q needs
+// only the key and u2, so it runs on the side stream beside the sighash kernels; K_tladder_g
+// forms u1 = m s^-1 from the sighash row (twist_prep_u1) and finishes the lane.
+__global__ __launch_bounds__(TLADDER_WG) __attribute__((amdgpu_waves_per_eu(BCC_LADDER_WAVES, BCC_LADDER_WAVES))) void twist_ladder_q_kernel(
+    u32* __restrict__ state, u32* __restrict__ qtab, size_t cnt) {
+    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= cnt) return;
+    u32* w = lane_words(state, t, TSTATE_WORDS);
+    TwistStateView st;
+    st.p = w;
+    st.flags = w[T_FLAGS * LANE_STRIDE];
+    if (!(st.flags & LS_VALID)) return;  // K_tladder_g writes the status
+    tw_load(st.sigma.v, w, T_SIGMA);
+    twist_q_part(lane_table(qtab, t), st);
+}
+
+__global__ __launch_bounds__(TLADDER_WG) __attribute__((amdgpu_waves_per_eu(BCC_LADDER_WAVES, BCC_LADDER_WAVES))) void twist_ladder_g_kernel(
+    u32* __restrict__ state, u32* __restrict__ qtab, const u32* __restrict__ gcomb,
+    const uint8_t* __restrict__ pm, const u32* __restrict__ psinv, size_t cnt) {
+    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= cnt) return;
+    u32* w = lane_words(state, t, TSTATE_WORDS);
+    u32 flags = w[T_FLAGS * LANE_STRIDE];
+    if (!(flags & LS_VALID)) {
+        w[T_STAT * LANE_STRIDE] = TW_REJECT;
+        return;
+    }
+    {
+        sc m, si;
+        load_be32(m, pm + 32 * t);
+        load_limbs(si, psinv + 8 * t);
+        u32 k2[4], k3[4];
+        twist_prep_u1(m, si, &flags, k2, k3);
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+            w[(T_K + 8 + b) * LANE_STRIDE] = k2[b];
+            w[(T_K + 12 + b) * LANE_STRIDE] = k3[b];
+        }
+        w[T_FLAGS * LANE_STRIDE] = flags;
+    }
+    TwistStateView st;
+    st.p = w;
+    st.flags = flags;
+    tw_load(st.sigma.v, w, T_SIGMA);
+    twist_g_part<false>(w, lane_table(qtab, t), gcomb, st);
 }
 
 // beta^-1 for every normal lane of a chunk by Montgomery's trick over the strided sub-chunk
@@ -929,10 +1013,42 @@ int ecdsa_launch_key(SigScratch& sc, const uint8_t* d_tag, const uint8_t* d_x,
     return 0;
 }
 
+// BCC_LADDER_SPLIT=0: the fused ladder after the sighash kernels (A/B runs)
+static bool ladder_split() {
+    static const bool on = [] {
+        const char* e = getenv("BCC_LADDER_SPLIT");
+        return !(e && atoi(e) == 0);
+    }();
+    return on;
+}
+
+int ecdsa_launch_q(SigScratch& sc, const uint8_t* d_r, const uint8_t* d_s, size_t n, void* stream) {
+    sc.q_ready = 0;
+    if (n == 0 || !ladder_split() || sc.key_ready != n || n > chunk_lanes()) return 0;
+    int dev = 0, cus = 0;
+    fe* gtab = nullptr;
+    size_t C = 0;
+    if (int e = device_tables(&dev, &gtab, &cus)) return e;
+    if (int e = ensure_scratch(sc, dev, n, true, &C)) return e;
+    if (n > C) return 0;
+    u32* qtab = (u32*)sc.chunk;
+    u32* state = qtab + C * QTABLE_WORDS;
+    hipStream_t st = (hipStream_t)stream;
+    hipLaunchKernelGGL(ecdsa_tscal_q_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
+                       d_r, d_s, (const u32*)sc.sinv, n, state);
+    BCC_HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(twist_ladder_q_kernel, dim3((unsigned)((n + TLADDER_WG - 1) / TLADDER_WG)),
+                       dim3(TLADDER_WG), 0, st, state, qtab, n);
+    BCC_HIP_TRY(hipGetLastError());
+    sc.q_ready = n;
+    return 0;
+}
+
 int ecdsa_launch(SigScratch& sc, const uint8_t* d_tag, const uint8_t* d_x, const uint8_t* d_y,
                  const uint8_t* d_r, const uint8_t* d_s, const uint8_t* d_m, uint8_t* d_verdict,
                  size_t n, void* stream) {
     sc.key_ready = 0;  // the whole prep runs after K_inv here
+    sc.q_ready = 0;
     if (int e = ecdsa_launch_pre(sc, d_tag, d_x, d_y, d_s, n, stream)) return e;
     return ecdsa_launch_after_pre(sc, d_tag, d_x, d_y, d_r, d_s, d_m, d_verdict, n, stream);
 }
@@ -954,7 +1070,20 @@ int ecdsa_launch_after_pre(SigScratch& sc, const uint8_t* d_tag, const uint8_t* 
         u32* state = qtab + C * QTABLE_WORDS;
         const u32* gcomb = g_gcomb[dev];
         const bool key_ahead = sc.key_ready == n && n <= C;
+        const bool q_ahead = sc.q_ready == n && n <= C;
         sc.key_ready = 0;
+        sc.q_ready = 0;
+        if (q_ahead) {  // K_tkey, K_tscal_q and K_tladder_q ran ahead (ecdsa_launch_q)
+            hipLaunchKernelGGL(twist_ladder_g_kernel, dim3((unsigned)((n + TLADDER_WG - 1) / TLADDER_WG)),
+                               dim3(TLADDER_WG), 0, sm, state, qtab, gcomb, d_m, sinv, n);
+            BCC_HIP_TRY(hipGetLastError());
+            if (ev_rows_read) BCC_HIP_TRY(hipEventRecord((hipEvent_t)ev_rows_read, sm));
+            const size_t T = std::max<size_t>((n + 15) / 16, std::min<size_t>(n, (size_t)cus * 256));
+            hipLaunchKernelGGL(twist_fin_kernel<false>, dim3((unsigned)((T + 255) / 256)), dim3(256), 0,
+                               sm, state, qtab, d_verdict, 0, n, T);
+            BCC_HIP_TRY(hipGetLastError());
+            return 0;
+        }
         for (size_t base = 0; base < n; base += C) {
             const size_t cnt = std::min(C, n - base);
             if (key_ahead) {

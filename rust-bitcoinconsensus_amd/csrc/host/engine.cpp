@@ -112,7 +112,7 @@ struct HostJobs {
 
 std::atomic<uint32_t> g_host_chain_blocks{[] {
     const char* e = getenv("BCC_HOST_CHAIN_BLOCKS");
-    return e ? (uint32_t)atoi(e) : 32u;
+    return e ? (uint32_t)atoi(e) : 0u;
 }()};
 
 struct Item {
@@ -606,21 +606,20 @@ bool interpret_shard(BatchState& b, const std::vector<uint32_t>& idx, Round& rd)
     return any;
 }
 
-// Splits the items into T contiguous shards of whole transactions (items of one tx share its
-// TxEntry, whose BIP143 aux slots and legacy template the shard's Round owns), balanced by count.
-std::vector<std::vector<uint32_t>> make_shards(const BatchState& b, unsigned T) {
+// Boundaries of T contiguous shards of whole transactions (items of one tx share its TxEntry,
+// whose BIP143 aux slots and legacy template the shard's Round owns), balanced by count: shard t
+// is items [bound[t], bound[t + 1]).
+std::vector<size_t> shard_bounds(const BatchState& b, unsigned T) {
     const size_t n = b.st.size(), E = b.tx_first.size();
-    std::vector<std::vector<uint32_t>> sh(T);
+    std::vector<size_t> bound(T + 1, n);
+    bound[0] = 0;
     size_t k = 0;
     for (unsigned t = 0; t < T; t++) {
         const size_t want = share_lo(n, t + 1, T);
-        size_t lo = k < E ? b.tx_first[k] : n;
         while (k < E && (t + 1 == T || b.tx_first[k] < want)) k++;
-        size_t hi = k < E ? b.tx_first[k] : n;
-        sh[t].reserve(hi - lo);
-        for (size_t i = lo; i < hi; i++) sh[t].push_back((uint32_t)i);
+        bound[t + 1] = k < E ? b.tx_first[k] : n;
     }
-    return sh;
+    return bound;
 }
 
 // One device round over the parts [p0, p1): fault injection first, then the device pipeline.
@@ -769,8 +768,10 @@ void chunk_interpret(ChunkRun& c) {
         c.rds[t].reset();
         ran[t] = interpret_shard(c.b, c.run_list[t], c.rds[t]);
     });
-    run_host_jobs(c.rds, c.T);
     t_stats.interpret_seconds += since(i0);
+    auto h0 = clk::now();
+    run_host_jobs(c.rds, c.T);
+    t_stats.host_jobs_seconds += since(h0);
     size_t npend = 0;
     bool any = false;
     for (unsigned t = 0; t < c.T; t++) {
@@ -801,12 +802,24 @@ void chunk_start(ChunkRun& c, const bcc_batch_item* items, size_t n, unsigned fl
     const unsigned T = c.T;
     prepare(c.b, items, n, flags, T);
     t_stats.prepare_seconds += since(t0);
-    c.shards = make_shards(c.b, T);
-    c.run_list.assign(T, {});
-    c.next_list.assign(T, {});
-    for (unsigned t = 0; t < T; t++)
-        for (uint32_t i : c.shards[t])
-            if (c.b.st[i].active) c.run_list[t].push_back(i);
+    auto s0 = clk::now();
+    const std::vector<size_t> bound = shard_bounds(c.b, T);
+    // the shard / run lists keep their capacity from call to call; filled in parallel
+    c.shards.resize(T);
+    c.run_list.resize(T);
+    c.next_list.resize(T);
+    run_threads(T, [&](unsigned t) {
+        auto& sh = c.shards[t];
+        auto& rl = c.run_list[t];
+        sh.clear();
+        rl.clear();
+        c.next_list[t].clear();
+        for (size_t i = bound[t]; i < bound[t + 1]; i++) {
+            sh.push_back((uint32_t)i);
+            if (c.b.st[i].active) rl.push_back((uint32_t)i);
+        }
+    });
+    t_stats.shard_seconds += since(s0);
     if (c.rds.size() < T) c.rds.resize(T);
     for (unsigned t = 0; t < T; t++) {
         c.rds[t].keys.clear();
@@ -888,18 +901,28 @@ long chunk_finish(ChunkRun& c, int* ret_out, bitcoinconsensus_error* err_out, bo
                 }
             break;
         }
+        auto s1 = clk::now();
         chunk_stitch(c);
+        t_stats.stitch_seconds += since(s1);
         chunk_interpret(c);
     }
     for (unsigned t = 0; t < c.T; t++) t_stats.host_rejected += c.rds[t].host_rejected;
+    auto f0 = clk::now();
+    std::vector<long> vt(c.T, 0);
+    run_threads(c.T, [&](unsigned t) {  // the shards cover [0, n) contiguously
+        long v = 0;
+        for (uint32_t i : c.shards[t]) {
+            Item& it = st[i];
+            int ret = (it.err == bitcoinconsensus_ERR_OK && it.result) ? 1 : 0;
+            ret_out[i] = ret;
+            if (err_out) err_out[i] = it.err;
+            v += ret;
+        }
+        vt[t] = v;
+    });
     long valid = 0;
-    for (size_t i = 0; i < c.n; i++) {
-        Item& it = st[i];
-        int ret = (it.err == bitcoinconsensus_ERR_OK && it.result) ? 1 : 0;
-        ret_out[i] = ret;
-        if (err_out) err_out[i] = it.err;
-        valid += ret;
-    }
+    for (long v : vt) valid += v;
+    t_stats.finish_seconds += since(f0);
     return status < 0 ? -1 : valid;
 }
 

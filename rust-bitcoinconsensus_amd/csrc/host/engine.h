@@ -44,5 +44,9 @@ void append_round(SighashJobs& dst, TupleRows& dst_rows, const SighashJobs& src,
 // Frees the calling thread's Taproot job buffers (host/taproot.cpp).
 void taproot_release_thread_state();
 
+// The SigMsg digests of a part's device-built Taproot jobs computed on the host (the CPU twin of
+// sighash.hip taproot_tx_kernel + taproot_msg_kernel: tests, stub device): msg + 32 row.
+void taproot_dev_sigmsg_host(const TaprootTxJobs& jobs, uint8_t* msg);
+
 }  // namespace host
 }  // namespace bcc

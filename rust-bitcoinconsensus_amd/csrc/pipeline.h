@@ -177,6 +177,37 @@ struct TupleRows {
     }
 };
 
+// The device-built SigMsg path (sighash.hip taproot_tx_kernel / taproot_msg_kernel): per tx its
+// bytes without marker / flag / witnesses and the serialized outputs it spends (both 4-aligned in
+// txraw), per check a TapJob.
+struct TtxRec {
+    uint32_t tx_off, tx_len;  // the tx in txraw
+    uint32_t sp_off, sp_len;  // the spent outputs (std::vector<CTxOut> serialization) in txraw
+    uint32_t in_base, n_in;   // input table entries [in_base, in_base + n_in)
+    uint32_t pad[2];
+};
+struct TapJob {
+    uint32_t ttx, nin, hash_type;
+    uint32_t spend_type;  // (ext_flag << 1) | annex present (interpreter.cpp:1534)
+    uint32_t row;         // BIP340 row whose msg receives the sighash
+    uint32_t ext_off;     // byte offset in the ext blob: [sha_annex] [sha_single_output] [tapleaf]
+    uint32_t codesep;     // BIP342 codesep_pos
+    uint32_t flags;       // 1: BIP342 (tapleaf hash, key_version, codesep_pos follow)
+};
+struct TaprootTxJobs {
+    std::vector<uint8_t> txraw, ext;
+    std::vector<TtxRec> ttx;
+    std::vector<TapJob> jobs;
+    uint32_t in_entries = 0;
+    void clear() {
+        txraw.clear(); ext.clear(); ttx.clear(); jobs.clear(); in_entries = 0;
+    }
+    void put_raw(const uint8_t* p, size_t n) {
+        txraw.insert(txraw.end(), p, p + n);
+    }
+    void align4() { txraw.resize((txraw.size() + 3) & ~(size_t)3, 0); }
+};
+
 // BIP341 / BIP342 signature checks (host/taproot.cpp): single-SHA256 aux messages (a tx's
 // sha_prevouts / sha_amounts / sha_scriptpubkeys / sha_sequences / sha_outputs, a check's
 // sha_annex / sha_single_output), SigMsg messages hashed as TapSighash tagged hashes (the
@@ -188,10 +219,12 @@ struct TaprootJobs {
     std::vector<uint32_t> msg_off, msg_nblk, msg_row;
     std::vector<PatchRec> patches;                   // aux digest -> msg blob byte offset
     std::vector<uint8_t> sig64, pk32;                // BIP340 rows
+    TaprootTxJobs dev;                               // device-built SigMsgs (the default path)
     size_t rows() const { return pk32.size() / 32; }
     void clear() {  // keeps the capacity (a caller's next round reuses it)
         aux.clear(); msg.clear(); aux_off.clear(); aux_nblk.clear(); msg_off.clear();
         msg_nblk.clear(); msg_row.clear(); patches.clear(); sig64.clear(); pk32.clear();
+        dev.clear();
     }
     uint32_t add_aux(const uint8_t* m, size_t n) {
         aux_off.push_back((uint32_t)(aux.size() / 64));
@@ -230,6 +263,7 @@ struct SigScratch {
     void* chunk = nullptr;
     size_t chunk_cap = 0;  // lanes
     size_t key_ready = 0;  // tuples whose key half of the prep ran ahead (ecdsa_launch_key)
+    size_t q_ready = 0;    // tuples whose Q ladder ran ahead (ecdsa_launch_q)
     SigScratch() = default;
     SigScratch(const SigScratch&) = delete;
     SigScratch& operator=(const SigScratch&) = delete;
@@ -252,6 +286,13 @@ int ecdsa_launch_pre(SigScratch& sc, const uint8_t* d_tag, const uint8_t* d_x,
 // (returns 0) on the legacy path or when n needs more than one scratch chunk.
 int ecdsa_launch_key(SigScratch& sc, const uint8_t* d_tag, const uint8_t* d_x, const uint8_t* d_y,
                      size_t n, void* stream);
+// The message-free part of the ECDSA lane ahead of the sighash kernels: the r / s half of the
+// prep (u2 = r s^-1, GLV split) and the Q ladder B = u2 Q_w, on `stream` after K_inv and K_tkey
+// (ecdsa_launch_pre / ecdsa_launch_key for the same n, ordered before it); the next
+// ecdsa_launch_after_pre for the same n then forms u1 from the sighash rows and runs only the G
+// ladder, the combine and K_tfin.  A no-op (returns 0) unless the key half ran ahead and n fits one
+// scratch chunk, or with BCC_LADDER_SPLIT=0.
+int ecdsa_launch_q(SigScratch& sc, const uint8_t* d_r, const uint8_t* d_s, size_t n, void* stream);
 // ev_rows_read (optional hipEvent_t) is recorded on `stream` once the last kernel that reads the
 // s / m / key rows and the s^-1 rows has been launched (the prep kernel): later writers of those
 // rows (the next run's front kernels) need only wait for it, not for the ladder.
@@ -310,7 +351,6 @@ private:
     void* ev_block_ = nullptr;     // hipEvent_t (blocking sync): host waits sleep, not spin
     int wait(void* stream);
     void* ev_front_ = nullptr;     // hipEvent_t: this run's sighash kernels done (overlap mode)
-    void* ev_key_ = nullptr;       // hipEvent_t: K_tkey (the key half of the prep) done
     bool rows_pending_ = false;    // ev_rows_ recorded by an earlier run (on rows_stream_)
     void* rows_stream_ = nullptr;
     SigScratch scratch_;

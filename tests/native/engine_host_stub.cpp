@@ -112,6 +112,7 @@ int gpu_taproot_verify(int, const TaprootJobs& j, uint8_t* verdict, uint8_t* msg
     bcco_sha256(reinterpret_cast<const uint8_t*>("TapSighash"), 10, tag);
     const size_t n = j.rows();
     std::vector<uint8_t> h(32 * n, 0);
+    bcc::host::taproot_dev_sigmsg_host(j.dev, h.data());  // the device-built SigMsg path
     for (size_t k = 0; k < j.msg_off.size(); k++) {
         const uint8_t* m = &msgs[(size_t)j.msg_off[k] * 64];
         size_t L = unpadded_len(m, (size_t)j.msg_nblk[k] * 64) - 64;

@@ -30,7 +30,7 @@ def wl():
 
 @pytest.mark.parametrize("chain_blocks", [32, 0])
 def test_block_workload_all_valid_and_matches_reference(wl, chain_blocks):
-    """chain_blocks 32 (default): the big tx's long SHA chains hashed on the host; 0: every
+    """chain_blocks 32: the big txs' long SHA chains hashed on the host; 0 (default): every
     chain in a GPU lane."""
     import bitcoinconsensus_amd as B
     B.set_host_chain_blocks(chain_blocks)
@@ -38,7 +38,7 @@ def test_block_workload_all_valid_and_matches_reference(wl, chain_blocks):
         n_valid, ret = wl.verify_batch()
         st = B.last_batch_stats()
     finally:
-        B.set_host_chain_blocks(32)
+        B.set_host_chain_blocks(0)
     assert (st["host_hashed"] > 0) == (chain_blocks > 0)
     assert n_valid == wl.n and all(r == 1 for r in ret)
     assert st["rounds"] == 1          # multisig candidate pairs are queued up front: no re-run

@@ -132,7 +132,7 @@ def test_script_cases_host_hashed_chains(eng, blocks):
             test_script_cases_single_calls(eng)
             test_crate_vectors(eng)
     finally:
-        eng.bcc_set_host_chain_blocks(32)
+        eng.bcc_set_host_chain_blocks(0)
 
 
 def test_pubkey_verify_batch_front_end(eng):
@@ -181,7 +181,9 @@ class Stats(ctypes.Structure):
                                        "total_seconds")] + [("device_retries", ctypes.c_size_t),
                                                              ("devices", ctypes.c_size_t),
                                                              ("host_rounds", ctypes.c_size_t),
-                                                             ("host_hashed", ctypes.c_size_t)]
+                                                             ("host_hashed", ctypes.c_size_t)] + [
+        (k, ctypes.c_double) for k in ("shard_seconds", "stitch_seconds", "finish_seconds",
+                                       "host_jobs_seconds")]
 
 
 def test_device_failure_retried_once(eng):

@@ -59,3 +59,33 @@ def test_pubkey_verify_batch_sharded(two_workers):
     one = B.pubkey_verify_batch(tuples, device=0)
     assert many == one
     assert list(one) == [t["verdict"] for t in ts]
+
+
+def test_rank_partition_of_one_global_set():
+    """bench.py's multi-GPU partition: rank r stages items [r n, (r + 1) n) of ONE
+    global set (Workload(n, first=r n), TupleSet(n, first=r n, total=N n)).  Two ranges must be
+    exactly the items, sighashes and verdicts of the single 2n set -- no overlap, no gap, no
+    rank-dependent content."""
+    import bitcoinconsensus_amd as B
+    n, seed = 2500, 0x5EED0001
+    full = B.Workload(2 * n, seed=seed)
+    parts = [B.Workload(n, seed=seed, first=0), B.Workload(n, seed=seed, first=n)]
+    assert [full.item(i) for i in range(2 * n)] == [p.item(i) for p in parts for i in range(n)]
+    full.run()
+    for p in parts:
+        p.run()
+    assert full.msgs() == b"".join(p.msgs() for p in parts)
+    assert full.verdicts() == b"".join(p.verdicts() for p in parts)
+    assert all(full.verdicts())
+    # the C4 tuple sets the same way (10 % adversarial classes drawn per global row)
+    t_full = B.TupleSet(2 * n, kind="c4")
+    t_parts = [B.TupleSet(n, kind="c4", first=0, total=2 * n),
+               B.TupleSet(n, kind="c4", first=n, total=2 * n)]
+    hf = t_full.host()
+    hp = [t.host() for t in t_parts]
+    assert bytes(hf["msg32"]) == b"".join(bytes(h["msg32"]) for h in hp)
+    assert bytes(hf["cls"]) == b"".join(bytes(h["cls"]) for h in hp)
+    for t in [t_full] + t_parts:
+        t.run()
+    assert t_full.verdicts() == b"".join(t.verdicts() for t in t_parts)
+    assert t_full.verdicts() == bytes(hf["expect"])

@@ -59,7 +59,11 @@ def main():
                        gpu_wait_ms=round(1e3 * st["gpu_seconds"], 1),
                        prepare_ms=round(1e3 * st["prepare_seconds"], 1),
                        interpret_ms=round(1e3 * st["interpret_seconds"], 1),
-                       stage_ms=round(1e3 * st["stage_seconds"], 1))
+                       stage_ms=round(1e3 * st["stage_seconds"], 1),
+                       shard_ms=round(1e3 * st["shard_seconds"], 1),
+                       stitch_ms=round(1e3 * st["stitch_seconds"], 1),
+                       finish_ms=round(1e3 * st["finish_seconds"], 1),
+                       host_jobs_ms=round(1e3 * st["host_jobs_seconds"], 1))
             for k in ("usage_usec", "user_usec", "system_usec", "nr_periods", "nr_throttled",
                       "throttled_usec"):
                 if k in c0 and k in c1:
