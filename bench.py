@@ -302,8 +302,8 @@ class C2:
                 best, st = dt, self.B.last_batch_stats()
         return dict(inputs_per_s=self.n / best, ms=best * 1e3, valid=nv,
                     host_ms=st["host_seconds"] * 1e3, gpu_ms=st["gpu_seconds"] * 1e3,
-                    h2d_ms=st["stage_seconds"] * 1e3, host_threads=B.host_threads(),
-                    cpu_share=B.cpu_share())
+                    h2d_ms=st["stage_seconds"] * 1e3, host_threads=self.B.host_threads(),
+                    cpu_share=self.B.cpu_share())
 
     def cpu(self, sample):
         sample = min(sample, self.n)

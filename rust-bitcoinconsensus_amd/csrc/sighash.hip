@@ -661,7 +661,10 @@ __global__ __launch_bounds__(XS_WG) void taproot_tx_kernel(const uint8_t* __rest
         }
     } else {
         pos = 4;
-        const uint32_t nin = min(wire_cs(x, pos), r.n_in);
+        uint32_t nin = wire_cs(x, pos);
+        // a segwit tx uploaded whole (no outputs to cut the witnesses at): marker 0x00, flag
+        if (nin == 0 && xw_byte(x, pos++) != 0) nin = wire_cs(x, pos);
+        nin = min(nin, r.n_in);
         if (role == 4) {  // sha_outputs: the serialized outputs, one contiguous range
             for (uint32_t k = 0; k < nin; k++) {
                 uint32_t sq;
