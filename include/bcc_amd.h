@@ -171,6 +171,9 @@ typedef struct bcc_batch_stats {
     /* more of the host pass: shard / run lists, stitching verdicts into items, writing ret / err,
      * the host-hashed long chains */
     double shard_seconds, stitch_seconds, finish_seconds, host_jobs_seconds;
+    /* the deserialization pass per worker, max over workers (summed over chunks): dispatch -> start
+     * lag, tx parsing + pre-checks, the batched HASH160 of P2WPKH keys */
+    double prepare_lag_seconds, prepare_parse_seconds, prepare_hash_seconds;
 } bcc_batch_stats;
 /* Statistics of the calling thread's last bitcoinconsensus_verify_batch / verify call. */
 void bcc_last_batch_stats(bcc_batch_stats* out);

@@ -208,7 +208,8 @@ class BatchStats(ctypes.Structure):
                 ("devices", ctypes.c_size_t), ("host_rounds", ctypes.c_size_t),
                 ("host_hashed", ctypes.c_size_t), ("shard_seconds", ctypes.c_double),
                 ("stitch_seconds", ctypes.c_double), ("finish_seconds", ctypes.c_double),
-                ("host_jobs_seconds", ctypes.c_double)]
+                ("host_jobs_seconds", ctypes.c_double), ("prepare_lag_seconds", ctypes.c_double),
+                ("prepare_parse_seconds", ctypes.c_double), ("prepare_hash_seconds", ctypes.c_double)]
 
 
 def _bind_consensus(L):

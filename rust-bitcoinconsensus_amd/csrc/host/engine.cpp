@@ -493,6 +493,7 @@ struct BatchState {
     // buffer repeated non-adjacently is merely parsed again (same result)
     std::vector<TxEntry> txs;
     std::vector<uint32_t> tx_first;  // first item of each entry
+    std::vector<std::vector<uint32_t>> tx_slices;  // per-thread scans building tx_first
     unsigned flags = 0;
 };
 
@@ -512,13 +513,40 @@ void prepare(BatchState& b, const bcc_batch_item* items, size_t n, unsigned flag
     b.flags = flags;
     auto& st = b.st;
     const bool flags_ok = (flags & ~(unsigned)FLAGS_VERIFY_ALL) == 0;
+    // runs of adjacent items with the same tx buffer: scanned in T slices, then concatenated
+    auto starts_tx = [&](size_t i) {
+        return i == 0 || items[i].tx_to != items[i - 1].tx_to || items[i].tx_to_len != items[i - 1].tx_to_len;
+    };
     b.tx_first.clear();
-    for (size_t i = 0; i < n; i++)
-        if (i == 0 || items[i].tx_to != items[i - 1].tx_to || items[i].tx_to_len != items[i - 1].tx_to_len)
-            b.tx_first.push_back((uint32_t)i);
+    if (T <= 1 || n < 1024) {
+        for (size_t i = 0; i < n; i++)
+            if (starts_tx(i)) b.tx_first.push_back((uint32_t)i);
+    } else {
+        b.tx_slices.resize(T);
+        run_threads(T, [&](unsigned t) {
+            auto& v = b.tx_slices[t];
+            v.clear();
+            for (size_t i = share_lo(n, t, T); i < share_lo(n, t + 1, T); i++)
+                if (starts_tx(i)) v.push_back((uint32_t)i);
+        });
+        size_t total = 0;
+        for (unsigned t = 0; t < T; t++) total += b.tx_slices[t].size();
+        b.tx_first.resize(total);
+        size_t at = 0;
+        for (unsigned t = 0; t < T; t++) {
+            std::copy(b.tx_slices[t].begin(), b.tx_slices[t].end(), b.tx_first.begin() + at);
+            at += b.tx_slices[t].size();
+        }
+    }
     const size_t E = b.tx_first.size();
     b.txs.resize(E);
+    // per-thread timing (bcc_batch_stats prepare_*): dispatch -> start lag, parse, batched HASH160
+    using pclk = std::chrono::steady_clock;
+    std::vector<double> lag(T, 0), tparse(T, 0), thash(T, 0);
+    const auto d0 = pclk::now();
     run_threads(T, [&](unsigned t) {
+        const auto s0 = pclk::now();
+        lag[t] = std::chrono::duration<double>(s0 - d0).count();
         for (size_t k = share_lo(E, t, T); k < share_lo(E, t + 1, T); k++) {
             const bcc_batch_item* in = &items[b.tx_first[k]];
             TxEntry& e = b.txs[k];
@@ -547,6 +575,8 @@ void prepare(BatchState& b, const bcc_batch_item* items, size_t n, unsigned flag
                 }
             }
         }
+        const auto s1 = pclk::now();
+        tparse[t] = std::chrono::duration<double>(s1 - s0).count();
         // HASH160 of every P2WPKH witness key of this thread's share, eight at a time (the
         // interpreter's OP_HASH160 finds it by content, DeferringChecker::cached_hash160)
         const size_t i0 = share_lo(E, t, T) < E ? b.tx_first[share_lo(E, t, T)] : n;
@@ -577,7 +607,13 @@ void prepare(BatchState& b, const bcc_batch_item* items, size_t n, unsigned flag
             if (++k == BATCH) flush();
         }
         flush();
+        thash[t] = std::chrono::duration<double>(pclk::now() - s1).count();
     });
+    for (unsigned t = 0; t < T; t++) {
+        t_stats.prepare_lag_seconds = std::max(t_stats.prepare_lag_seconds, lag[t]);
+        t_stats.prepare_parse_seconds = std::max(t_stats.prepare_parse_seconds, tparse[t]);
+        t_stats.prepare_hash_seconds = std::max(t_stats.prepare_hash_seconds, thash[t]);
+    }
 }
 
 // Interpreter pass over the active items of one shard (idx: the shard's items that need a run);

@@ -183,7 +183,8 @@ class Stats(ctypes.Structure):
                                                              ("host_rounds", ctypes.c_size_t),
                                                              ("host_hashed", ctypes.c_size_t)] + [
         (k, ctypes.c_double) for k in ("shard_seconds", "stitch_seconds", "finish_seconds",
-                                       "host_jobs_seconds")]
+                                       "host_jobs_seconds", "prepare_lag_seconds",
+                                       "prepare_parse_seconds", "prepare_hash_seconds")]
 
 
 def test_device_failure_retried_once(eng):

@@ -63,7 +63,10 @@ def main():
                        shard_ms=round(1e3 * st["shard_seconds"], 1),
                        stitch_ms=round(1e3 * st["stitch_seconds"], 1),
                        finish_ms=round(1e3 * st["finish_seconds"], 1),
-                       host_jobs_ms=round(1e3 * st["host_jobs_seconds"], 1))
+                       host_jobs_ms=round(1e3 * st["host_jobs_seconds"], 1),
+                       prep_lag_ms=round(1e3 * st["prepare_lag_seconds"], 2),
+                       prep_parse_ms=round(1e3 * st["prepare_parse_seconds"], 2),
+                       prep_hash_ms=round(1e3 * st["prepare_hash_seconds"], 2))
             for k in ("usage_usec", "user_usec", "system_usec", "nr_periods", "nr_throttled",
                       "throttled_usec"):
                 if k in c0 and k in c1:
