@@ -649,12 +649,12 @@ std::vector<size_t> shard_bounds(const BatchState& b, unsigned T) {
     const size_t n = b.st.size(), E = b.tx_first.size();
     std::vector<size_t> bound(T + 1, n);
     bound[0] = 0;
-    size_t k = 0;
-    for (unsigned t = 0; t < T; t++) {
+    for (unsigned t = 0; t + 1 < T; t++) {  // the first tx starting at or after the even split
         const size_t want = share_lo(n, t + 1, T);
-        while (k < E && (t + 1 == T || b.tx_first[k] < want)) k++;
-        bound[t + 1] = k < E ? b.tx_first[k] : n;
+        auto it = std::lower_bound(b.tx_first.begin(), b.tx_first.end(), (uint32_t)want);
+        bound[t + 1] = std::max(bound[t], it == b.tx_first.end() ? n : (size_t)*it);
     }
+    (void)E;
     return bound;
 }
 

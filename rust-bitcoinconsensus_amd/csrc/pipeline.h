@@ -338,6 +338,8 @@ private:
     void* pick(void* stream);
     int launch_wtx(void* stream);
     int launch_sighash(struct ihipStream_t* st, void* ev_wtx);
+    int launch_front(struct ihipStream_t* st);        // K_wtx + K3' + K1 fused, then the rest
+    int launch_after_front(struct ihipStream_t* st);  // K_win, K2, K3
     int dev_;
     void* own_stream_ = nullptr;   // hipStream_t, created on first use
     void* last_stream_ = nullptr;  // stream of the last run

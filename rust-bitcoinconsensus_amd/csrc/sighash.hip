@@ -423,19 +423,16 @@ __device__ __forceinline__ uint32_t wire_input(XWin& x, uint32_t& pos, uint32_t*
 //                                                              input table K_win reads)
 //   txd[32:64] hashSequence  = SHA256d(nSequence_0 || ... )  (one word per input)
 //   txd[64:96] hashOutputs   = SHA256d(the serialized outputs: one contiguous range of the tx)
-__global__ __launch_bounds__(XS_WG) void bip143_tx_kernel(const uint8_t* __restrict__ txraw,
-                                                          const WtxRec* __restrict__ recs,
-                                                          uint32_t n, uint32_t* __restrict__ intab,
-                                                          uint8_t* __restrict__ txd) {
-    __shared__ __attribute__((aligned(16))) uint8_t lds[XS_WG * (XW_BYTES + 4)];
-    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-    if (g >= 3 * n) return;
+__device__ __forceinline__ void bip143_tx_lane(const uint8_t* __restrict__ txraw,
+                                               const WtxRec* __restrict__ recs, uint32_t n,
+                                               uint32_t g, uint32_t* __restrict__ intab,
+                                               uint8_t* __restrict__ txd, uint8_t* win) {
     const uint32_t role = g / n, i = g - role * n;
     const WtxRec r = recs[i];
     const uint8_t* t = txraw + r.tx_off;
     const uint32_t* t4 = reinterpret_cast<const uint32_t*>(t);
     XWin x;
-    x.w = lds + threadIdx.x * (XW_BYTES + 4);
+    x.w = win;
     x.t4 = t4;
     x.nd = (r.tx_len + 3) >> 2;
     x.base = 0;
@@ -533,6 +530,39 @@ __global__ __launch_bounds__(XS_WG) void bip143_tx_kernel(const uint8_t* __restr
     uint4* o = reinterpret_cast<uint4*>(d + 32 * role);
     o[0] = make_uint4(bswap_u32(dd[0]), bswap_u32(dd[1]), bswap_u32(dd[2]), bswap_u32(dd[3]));
     o[1] = make_uint4(bswap_u32(dd[4]), bswap_u32(dd[5]), bswap_u32(dd[6]), bswap_u32(dd[7]));
+}
+
+__global__ __launch_bounds__(XS_WG) void bip143_tx_kernel(const uint8_t* __restrict__ txraw,
+                                                          const WtxRec* __restrict__ recs,
+                                                          uint32_t n, uint32_t* __restrict__ intab,
+                                                          uint8_t* __restrict__ txd) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[XS_WG * (XW_BYTES + 4)];
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g < 3 * n) bip143_tx_lane(txraw, recs, n, g, intab, txd, lds + threadIdx.x * (XW_BYTES + 4));
+}
+
+// The whole sighash front of a round in ONE launch (round 3): K_wtx's role lanes first (a
+// many-input tx's hashPrevouts is the longest serial chain of a block), then the K3' template jobs,
+// then the K1 aux messages -- every one a single-lane serial SHA chain, latency-bound, so one grid
+// runs them all side by side on the main stream, and the signature side stream (K_inv, K_tkey,
+// the Q ladder) keeps a hardware queue of its own: with K_wtx on a third stream, the box's 4
+// hardware queues per process put it on the side stream's queue, and K_inv waited 1.75 ms for
+// a C3 block's K_wtx (profiles/r03/c3_trace_before_front_fusion.txt).
+__global__ __launch_bounds__(XS_WG) void sighash_front_kernel(
+    const uint8_t* __restrict__ txraw, const WtxRec* __restrict__ recs, uint32_t nwtx,
+    uint32_t* __restrict__ intab, uint8_t* __restrict__ txd, const uint8_t* __restrict__ tpl,
+    const uint8_t* __restrict__ code, const TplJob* __restrict__ tjobs, uint32_t ntpl,
+    const uint8_t* __restrict__ aux, const uint32_t* __restrict__ aux_off,
+    const uint32_t* __restrict__ aux_nblk, uint32_t naux, uint8_t* __restrict__ auxd,
+    uint8_t* __restrict__ msg) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[XS_WG * (XW_BYTES + 4)];
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x, nw = 3 * nwtx;
+    if (g < nw)
+        bip143_tx_lane(txraw, recs, nwtx, g, intab, txd, lds + threadIdx.x * (XW_BYTES + 4));
+    else if (g - nw < ntpl)
+        sha256d_tpl_lane(tpl, code, tjobs, g - nw, msg);
+    else if (g - nw - ntpl < naux)
+        sha256d_msg_lane(aux, aux_off, aux_nblk, g - nw - ntpl, auxd, nullptr);
 }
 
 // K_win: one lane per BIP143 check (not SIGHASH_SINGLE).  SignatureHash WITNESS_V0
@@ -1047,6 +1077,11 @@ int DeviceBatch::launch_sighash(hipStream_t st, void* ev_wtx) {
     } else if (int e = launch_wtx(st)) {
         return e;
     }
+    return launch_after_front(st);
+}
+
+// K_win, K2, K3: everything of the sighash stage after K_wtx / K1 / K3'.
+int DeviceBatch::launch_after_front(hipStream_t st) {
     if (n_wjob_) {  // K_win: BIP143 preimages assembled from the raw tx bytes and hashed
         hipLaunchKernelGGL(bip143_in_kernel, dim3((unsigned)((n_wjob_ + XS_WG - 1) / XS_WG)),
                            dim3(XS_WG), 0, st, d_txraw_, d_wtx_, d_wjob_, (uint32_t)n_wjob_,
@@ -1067,11 +1102,24 @@ int DeviceBatch::launch_sighash(hipStream_t st, void* ev_wtx) {
     return 0;
 }
 
+// The sighash stage with the front fused (sighash_front_kernel), then K_win, K2, K3.
+int DeviceBatch::launch_front(hipStream_t st) {
+    const size_t lanes = 3 * n_wtx_ + n_tjob_ + n_aux_;
+    if (lanes) {
+        hipLaunchKernelGGL(sighash_front_kernel, dim3((unsigned)((lanes + XS_WG - 1) / XS_WG)),
+                           dim3(XS_WG), 0, st, d_txraw_, d_wtx_, (uint32_t)n_wtx_, d_intab_, d_txd_,
+                           d_tpl_, d_code_, d_tjob_, (uint32_t)n_tjob_, d_aux_, d_aux_off_,
+                           d_aux_nblk_, (uint32_t)n_aux_, d_auxd_, d_m);
+        BCC_HIP_TRY(hipGetLastError());
+    }
+    return launch_after_front(st);
+}
+
 int DeviceBatch::run_sighash(void* stream) {
     BCC_HIP_TRY(hipSetDevice(dev_));
     hipStream_t st = (hipStream_t)pick(stream);
     if (!st) return (int)hipErrorOutOfMemory;
-    return launch_sighash(st, nullptr);
+    return launch_front(st);
 }
 
 int DeviceBatch::run_ecdsa(void* stream) {
@@ -1107,7 +1155,8 @@ int DeviceBatch::run(void* stream) {
         hipStream_t s = nullptr, s2 = nullptr;
         hipEvent_t a = nullptr, b = nullptr, c = nullptr;
         BCC_HIP_TRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-        BCC_HIP_TRY(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
+        // a third stream only for the overlap mode: every stream beyond two shares a hardware queue
+        if (overlap_runs()) BCC_HIP_TRY(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
         BCC_HIP_TRY(hipEventCreateWithFlags(&a, hipEventDisableTiming));
         BCC_HIP_TRY(hipEventCreateWithFlags(&b, hipEventDisableTiming));
         BCC_HIP_TRY(hipEventCreateWithFlags(&c, hipEventDisableTiming));
@@ -1160,21 +1209,16 @@ int DeviceBatch::run(void* stream) {
     }
     BCC_HIP_TRY(hipEventRecord((hipEvent_t)ev_fork_, st));
     BCC_HIP_TRY(hipStreamWaitEvent(side, (hipEvent_t)ev_fork_, 0));
-    // K_wtx on a stream of its own (a many-input tx's serial hash chains overlap K1 + K3' on the
-    // main stream and the signature kernels on the side stream)
-    BCC_HIP_TRY(hipStreamWaitEvent(ws, (hipEvent_t)ev_fork_, 0));
-    if (n_wtx_) {
-        if (int e = launch_wtx(ws)) return e;
-        BCC_HIP_TRY(hipEventRecord((hipEvent_t)ev_wtx_, ws));
-    }
-    // the side stream: K_inv, the key half of the prep (K_tkey), then everything the message does
-    // not enter -- the signature half of the prep and the Q ladder (ecdsa_launch_q) -- beside the
-    // sighash kernels on the main stream; the G ladder and K_tfin wait for both
+    // two streams: the sighash stage on the main stream (K_wtx + K3' + K1 fused into one front
+    // launch, then K_win / K2 / K3), and on the side stream K_inv, the key half of the prep
+    // (K_tkey) and everything the message does not enter -- the signature half of the prep and
+    // the Q ladder (ecdsa_launch_q); the G ladder and K_tfin wait for both
+    (void)ws;
     if (int e = ecdsa_launch_pre(scratch_, d_tag, d_x, d_y, d_s, n_rows_, side)) return e;
     if (int e = ecdsa_launch_key(scratch_, d_tag, d_x, d_y, n_rows_, side)) return e;
     if (int e = ecdsa_launch_q(scratch_, d_r, d_s, n_rows_, side)) return e;
     BCC_HIP_TRY(hipEventRecord((hipEvent_t)ev_join_, side));
-    if (int e = launch_sighash(st, ev_wtx_)) return e;
+    if (int e = launch_front(st)) return e;
     BCC_HIP_TRY(hipStreamWaitEvent(st, (hipEvent_t)ev_join_, 0));
     return ecdsa_launch_after_pre(scratch_, d_tag, d_x, d_y, d_r, d_s, d_m, d_v, n_rows_, st);
 }
