@@ -506,9 +506,29 @@ void run_threads(unsigned T, F f) {
 // Contiguous [lo, hi) share t of T over n units.
 inline size_t share_lo(size_t n, unsigned t, unsigned T) { return n * t / T; }
 
+// Boundaries of T contiguous shards of whole transactions (items of one tx share its TxEntry,
+// whose BIP143 aux slots and legacy template the shard's Round owns), balanced by count: shard t
+// is items [bound[t], bound[t + 1]).
+std::vector<size_t> shard_bounds(const BatchState& b, unsigned T) {
+    const size_t n = b.st.size(), E = b.tx_first.size();
+    std::vector<size_t> bound(T + 1, n);
+    bound[0] = 0;
+    for (unsigned t = 0; t + 1 < T; t++) {  // the first tx starting at or after the even split
+        const size_t want = share_lo(n, t + 1, T);
+        auto it = std::lower_bound(b.tx_first.begin(), b.tx_first.end(), (uint32_t)want);
+        bound[t + 1] = std::max(bound[t], it == b.tx_first.end() ? n : (size_t)*it);
+    }
+    (void)E;
+    return bound;
+}
+
 // verify_script's pre-checks (bitcoinconsensus.cpp:83-95) in reference order.  Tx buffers are
 // deserialized once per adjacent run of items, in parallel over T threads.
-void prepare(BatchState& b, const bcc_batch_item* items, size_t n, unsigned flags, unsigned T) {
+// With `shards` / `runs`, the workers' shares are the shard_bounds() shards, and each worker also
+// fills its shard's item list and run list (the items that passed the pre-checks).
+void prepare(BatchState& b, const bcc_batch_item* items, size_t n, unsigned flags, unsigned T,
+             std::vector<std::vector<uint32_t>>* shards = nullptr,
+             std::vector<std::vector<uint32_t>>* runs = nullptr) {
     b.st.resize(n);  // the state is reused across calls: every field is (re)set below
     b.flags = flags;
     auto& st = b.st;
@@ -544,10 +564,26 @@ void prepare(BatchState& b, const bcc_batch_item* items, size_t n, unsigned flag
     using pclk = std::chrono::steady_clock;
     std::vector<double> lag(T, 0), tparse(T, 0), thash(T, 0);
     const auto d0 = pclk::now();
+    const std::vector<size_t> bound = shard_bounds(b, T);
+    if (shards) {
+        shards->resize(T);
+        runs->resize(T);
+    }
     run_threads(T, [&](unsigned t) {
         const auto s0 = pclk::now();
         lag[t] = std::chrono::duration<double>(s0 - d0).count();
-        for (size_t k = share_lo(E, t, T); k < share_lo(E, t + 1, T); k++) {
+        // this worker's txs: the entries starting in its shard [bound[t], bound[t + 1])
+        const size_t klo = (size_t)(std::lower_bound(b.tx_first.begin(), b.tx_first.end(),
+                                                     (uint32_t)bound[t]) - b.tx_first.begin());
+        const size_t khi = (size_t)(std::lower_bound(b.tx_first.begin(), b.tx_first.end(),
+                                                     (uint32_t)bound[t + 1]) - b.tx_first.begin());
+        std::vector<uint32_t>* sh = shards ? &(*shards)[t] : nullptr;
+        std::vector<uint32_t>* rl = shards ? &(*runs)[t] : nullptr;
+        if (sh) {
+            sh->clear();
+            rl->clear();
+        }
+        for (size_t k = klo; k < khi; k++) {
             const bcc_batch_item* in = &items[b.tx_first[k]];
             TxEntry& e = b.txs[k];
             e.aux[0] = e.aux[1] = e.aux[2] = -1;
@@ -573,14 +609,17 @@ void prepare(BatchState& b, const bcc_batch_item* items, size_t n, unsigned flag
                     it.err = bitcoinconsensus_ERR_OK;
                     it.active = true;
                 }
+                if (sh) {
+                    sh->push_back((uint32_t)i);
+                    if (it.active) rl->push_back((uint32_t)i);
+                }
             }
         }
         const auto s1 = pclk::now();
         tparse[t] = std::chrono::duration<double>(s1 - s0).count();
         // HASH160 of every P2WPKH witness key of this thread's share, eight at a time (the
         // interpreter's OP_HASH160 finds it by content, DeferringChecker::cached_hash160)
-        const size_t i0 = share_lo(E, t, T) < E ? b.tx_first[share_lo(E, t, T)] : n;
-        const size_t i1 = share_lo(E, t + 1, T) < E ? b.tx_first[share_lo(E, t + 1, T)] : n;
+        const size_t i0 = bound[t], i1 = bound[t + 1];
         constexpr size_t BATCH = 64;
         const uint8_t* hp[BATCH];
         size_t hn[BATCH];
@@ -640,22 +679,6 @@ bool interpret_shard(BatchState& b, const std::vector<uint32_t>& idx, Round& rd)
         it.active = false;
     }
     return any;
-}
-
-// Boundaries of T contiguous shards of whole transactions (items of one tx share its TxEntry,
-// whose BIP143 aux slots and legacy template the shard's Round owns), balanced by count: shard t
-// is items [bound[t], bound[t + 1]).
-std::vector<size_t> shard_bounds(const BatchState& b, unsigned T) {
-    const size_t n = b.st.size(), E = b.tx_first.size();
-    std::vector<size_t> bound(T + 1, n);
-    bound[0] = 0;
-    for (unsigned t = 0; t + 1 < T; t++) {  // the first tx starting at or after the even split
-        const size_t want = share_lo(n, t + 1, T);
-        auto it = std::lower_bound(b.tx_first.begin(), b.tx_first.end(), (uint32_t)want);
-        bound[t + 1] = std::max(bound[t], it == b.tx_first.end() ? n : (size_t)*it);
-    }
-    (void)E;
-    return bound;
 }
 
 // One device round over the parts [p0, p1): fault injection first, then the device pipeline.
@@ -836,26 +859,10 @@ void chunk_start(ChunkRun& c, const bcc_batch_item* items, size_t n, unsigned fl
     c.n = n;
     c.T = n >= 256 ? std::min<unsigned>(host_threads(), (unsigned)(n / 64)) : 1u;
     const unsigned T = c.T;
-    prepare(c.b, items, n, flags, T);
+    prepare(c.b, items, n, flags, T, &c.shards, &c.run_list);  // + the shard / run lists
     t_stats.prepare_seconds += since(t0);
-    auto s0 = clk::now();
-    const std::vector<size_t> bound = shard_bounds(c.b, T);
-    // the shard / run lists keep their capacity from call to call; filled in parallel
-    c.shards.resize(T);
-    c.run_list.resize(T);
     c.next_list.resize(T);
-    run_threads(T, [&](unsigned t) {
-        auto& sh = c.shards[t];
-        auto& rl = c.run_list[t];
-        sh.clear();
-        rl.clear();
-        c.next_list[t].clear();
-        for (size_t i = bound[t]; i < bound[t + 1]; i++) {
-            sh.push_back((uint32_t)i);
-            if (c.b.st[i].active) rl.push_back((uint32_t)i);
-        }
-    });
-    t_stats.shard_seconds += since(s0);
+    for (auto& v : c.next_list) v.clear();
     if (c.rds.size() < T) c.rds.resize(T);
     for (unsigned t = 0; t < T; t++) {
         c.rds[t].keys.clear();

@@ -9,13 +9,15 @@ mkdir -p $O
 FULL=1 bash tools/profile_c2.sh $T > $O/profile.txt 2>&1 || { tail -20 $O/profile.txt; exit 1; }
 tail -14 $O/profile.txt
 timeout -k 10 400 python bench.py > $O/bench_c2.json 2> $O/bench_c2.err || { tail -20 $O/bench_c2.err; exit 2; }
-for c in c4 c5 c5t; do
+for c in c3 c4 c5 c5t; do
   timeout -k 10 400 python bench.py --config $c > $O/bench_$c.json 2> $O/bench_$c.err || { tail -20 $O/bench_$c.err; exit 3; }
 done
-python3 - "$O" <<'PY'
+python3 - "$O" <<'PY
+timeout -k 10 200 python -u tools/e2e_cgroup.py 1000000 0:0 > $O/e2e.txt 2>&1 || { tail -5 $O/e2e.txt; exit 4; }
+grep best_ms $O/e2e.txt'
 import json, sys
 O = sys.argv[1]
-for f in ("c2", "c4", "c5", "c5t"):
+for f in ("c2", "c3", "c4", "c5", "c5t"):
     d = json.load(open(f"{O}/bench_{f}.json"))
     cb = d.get("cpu_baseline") or {}
     print(f, round(d["value"] / 1e6, 2), d["unit"], "ms", round(d["ms_per_step"], 3), "frac",
