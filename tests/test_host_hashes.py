@@ -78,17 +78,29 @@ def test_host_sha256_portable_path(so):
     assert r.stdout.strip() == "0"
 
 
+def test_host_hash160_batch_other_paths(so):
+    """The same check with AVX-512 off (eight RIPEMD-160s per AVX2 pass) and with both off."""
+    for env in ({"BCC_NO_AVX512": "1"}, {"BCC_NO_AVX512": "1", "BCC_NO_AVX2": "1"}):
+        code = ("import sys; sys.path.insert(0, %r); import test_host_hashes as T; "
+                "T.test_host_hash160_batch_matches_scalar(%r); print('ok')" % (os.path.dirname(__file__), so))
+        r = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, **env),
+                           capture_output=True, text=True)
+        assert r.returncode == 0 and r.stdout.strip().endswith("ok"), (env, r.stderr[-2000:])
+
+
 def test_host_hash160_batch_matches_scalar(so):
-    """hash160_batch (eight RIPEMD-160s per AVX2 pass when the CPU has it, the scalar path for the
-    rest) against hash160 on the same messages: key-sized and odd-sized inputs, batch sizes that
-    leave remainders."""
+    """hash160_batch (sixteen SHA-256s and RIPEMD-160s per AVX-512 pass, eight RIPEMD-160s per AVX2
+    pass, the scalar path for the rest) against hash160 on the same messages: key-sized and
+    odd-sized inputs, batch sizes that leave remainders."""
     import ctypes
     import random
     L = ctypes.CDLL(so)
     rng = random.Random(160)
-    for count in (1, 7, 8, 9, 16, 23, 64):
-        msgs = [rng.randbytes(rng.choice([33, 65, 0, 1, 31, 32, 55, 56, 64, 100, 200]))
-                for _ in range(count)]
+    cases = [(count, [33, 65, 0, 1, 31, 32, 55, 56, 64, 100, 200]) for count in (1, 7, 8, 9, 16, 23, 64)]
+    cases += [(count, [33, 0, 1, 20, 32, 54, 55]) for count in (16, 17, 33, 64)]  # one-block SHA-256s
+    cases += [(64, [33])]
+    for count, sizes in cases:
+        msgs = [rng.randbytes(rng.choice(sizes)) for _ in range(count)]
         n = (ctypes.c_ulong * count)(*[len(m) for m in msgs])
         out = ctypes.create_string_buffer(20 * count)
         L.th_hash160_batch(b"".join(msgs), n, ctypes.c_ulong(count), out)

@@ -1,6 +1,7 @@
 #!/bin/bash
 # Round evidence on the current build (run via gpurun): C2 rocprof trace + SQ / FETCH / WRITE
-# passes, then the default bench line (with the CPU baseline) and C4 / C5 / C5T lines.
+# passes, then the default bench line (with the CPU baseline) and the C3 / C4 / C5 / C5T lines,
+# then the drop-in end to end with cgroup accounting.
 # usage: tools/round_evidence.sh TAG
 export TMPDIR=/tmp
 T=${1:-r02x}
@@ -12,9 +13,7 @@ timeout -k 10 400 python bench.py > $O/bench_c2.json 2> $O/bench_c2.err || { tai
 for c in c3 c4 c5 c5t; do
   timeout -k 10 400 python bench.py --config $c > $O/bench_$c.json 2> $O/bench_$c.err || { tail -20 $O/bench_$c.err; exit 3; }
 done
-python3 - "$O" <<'PY
-timeout -k 10 200 python -u tools/e2e_cgroup.py 1000000 0:0 > $O/e2e.txt 2>&1 || { tail -5 $O/e2e.txt; exit 4; }
-grep best_ms $O/e2e.txt'
+python3 - "$O" <<'PY'
 import json, sys
 O = sys.argv[1]
 for f in ("c2", "c3", "c4", "c5", "c5t"):
@@ -24,3 +23,5 @@ for f in ("c2", "c3", "c4", "c5", "c5t"):
           round(d["roofline"]["frac"], 4), "cpu", cb.get("value"), "mism", cb.get("gpu_verdict_mismatches"),
           "e2e", (d.get("drop_in_end_to_end") or {}).get("inputs_per_s"))
 PY
+timeout -k 10 200 python -u tools/e2e_cgroup.py 1000000 0:0 > $O/e2e.txt 2>&1 || { tail -5 $O/e2e.txt; exit 4; }
+grep best_ms $O/e2e.txt
