@@ -728,7 +728,10 @@ __global__ __launch_bounds__(TLADDER_WG) __attribute__((amdgpu_waves_per_eu(BCC_
 // The ECDSA ladder in two launches (ecdsa_launch_q / ecdsa_launch_after_pre): K_tladder_q needs
 // only the key and u2, so it runs on the side stream beside the sighash kernels; K_tladder_g
 // forms u1 = m s^-1 from the sighash row (twist_prep_u1) and finishes the lane.
-__global__ __launch_bounds__(TLADDER_WG) __attribute__((amdgpu_waves_per_eu(BCC_LADDER_WAVES, BCC_LADDER_WAVES))) void twist_ladder_q_kernel(
+#ifndef BCC_LADDERQ_WAVES
+#define BCC_LADDERQ_WAVES BCC_LADDER_WAVES
+#endif
+__global__ __launch_bounds__(TLADDER_WG) __attribute__((amdgpu_waves_per_eu(BCC_LADDERQ_WAVES, BCC_LADDERQ_WAVES))) void twist_ladder_q_kernel(
     u32* __restrict__ state, u32* __restrict__ qtab, size_t cnt) {
     const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= cnt) return;
@@ -1047,9 +1050,13 @@ int ecdsa_launch_q(SigScratch& sc, const uint8_t* d_r, const uint8_t* d_s, size_
 int ecdsa_launch(SigScratch& sc, const uint8_t* d_tag, const uint8_t* d_x, const uint8_t* d_y,
                  const uint8_t* d_r, const uint8_t* d_s, const uint8_t* d_m, uint8_t* d_verdict,
                  size_t n, void* stream) {
-    sc.key_ready = 0;  // the whole prep runs after K_inv here
+    sc.key_ready = 0;
     sc.q_ready = 0;
     if (int e = ecdsa_launch_pre(sc, d_tag, d_x, d_y, d_s, n, stream)) return e;
+    if (ladder_split()) {  // the same split kernels as DeviceBatch::run, on one stream
+        if (int e = ecdsa_launch_key(sc, d_tag, d_x, d_y, n, stream)) return e;
+        if (int e = ecdsa_launch_q(sc, d_r, d_s, n, stream)) return e;
+    }
     return ecdsa_launch_after_pre(sc, d_tag, d_x, d_y, d_r, d_s, d_m, d_verdict, n, stream);
 }
 
