@@ -339,6 +339,10 @@ private:
     int launch_wtx(void* stream);
     int launch_sighash(struct ihipStream_t* st, void* ev_wtx);
     int launch_front(struct ihipStream_t* st);        // K_wtx + K3' + K1 fused, then the rest
+    static bool async_upload();
+    int upload_on(struct ihipStream_t* rows_stream, struct ihipStream_t* rest_stream);
+    bool up_pending_ = false;      // the staged image is not on the device yet (async_upload)
+    size_t up_rows_ = 0, up_total_ = 0;
     int launch_after_front(struct ihipStream_t* st);  // K_win, K2, K3
     int dev_;
     void* own_stream_ = nullptr;   // hipStream_t, created on first use

@@ -1038,7 +1038,16 @@ int DeviceBatch::stage_parts(const SighashJobs* const* J, const TupleRows* const
         });
     }
     BCC_HIP_TRY(hipSetDevice(dev_));
-    BCC_HIP_TRY(hipMemcpy(arena_, host_image_, upload, hipMemcpyHostToDevice));
+    if (async_upload()) {
+        // the copy is issued by the next run, in two parts on the two streams that need them
+        // first (upload_on): the tuple rows on the side stream ahead of K_inv / K_tkey / the Q
+        // ladder, the sighash inputs on the main stream ahead of the front kernel
+        up_pending_ = true;
+        up_rows_ = off[AUX];
+        up_total_ = upload;
+    } else {
+        BCC_HIP_TRY(hipMemcpy(arena_, host_image_, upload, hipMemcpyHostToDevice));
+    }
     if (need_y) BCC_HIP_TRY(hipMemcpy(a + off[Y], h + off[Y], 32 * R, hipMemcpyHostToDevice));
     if (need_m) {
         BCC_HIP_TRY(hipMemcpy(a + off[M], h + off[M], 32 * R, hipMemcpyHostToDevice));
@@ -1049,6 +1058,34 @@ int DeviceBatch::stage_parts(const SighashJobs* const* J, const TupleRows* const
         // streams do not wait for: finish them before any run can write the rows
         BCC_HIP_TRY(hipStreamSynchronize(nullptr));
     }
+    return 0;
+}
+
+// BCC_ASYNC_UPLOAD=0: stage_parts copies the whole image synchronously (the round-2 way; A/B).
+bool DeviceBatch::async_upload() {
+    static const bool on = [] {
+        const char* e = getenv("BCC_ASYNC_UPLOAD");
+        return !(e && atoi(e) == 0);
+    }();
+    return on;
+}
+
+// The staged image's pending upload: all of it on `rows_stream` when `rest_stream` is null, else
+// the tuple rows on `rows_stream` and the rest on `rest_stream`.  Stream order puts every kernel
+// launched after it on the same stream behind its bytes.
+int DeviceBatch::upload_on(hipStream_t rows_stream, hipStream_t rest_stream) {
+    if (!up_pending_) return 0;
+    up_pending_ = false;
+    uint8_t* a = (uint8_t*)arena_;
+    const uint8_t* h = (const uint8_t*)host_image_;
+    if (!rest_stream) {
+        BCC_HIP_TRY(hipMemcpyAsync(a, h, up_total_, hipMemcpyHostToDevice, rows_stream));
+        return 0;
+    }
+    BCC_HIP_TRY(hipMemcpyAsync(a, h, up_rows_, hipMemcpyHostToDevice, rows_stream));
+    if (up_total_ > up_rows_)
+        BCC_HIP_TRY(hipMemcpyAsync(a + up_rows_, h + up_rows_, up_total_ - up_rows_,
+                                   hipMemcpyHostToDevice, rest_stream));
     return 0;
 }
 
@@ -1119,6 +1156,7 @@ int DeviceBatch::run_sighash(void* stream) {
     BCC_HIP_TRY(hipSetDevice(dev_));
     hipStream_t st = (hipStream_t)pick(stream);
     if (!st) return (int)hipErrorOutOfMemory;
+    if (int e = upload_on(st, nullptr)) return e;
     return launch_front(st);
 }
 
@@ -1126,6 +1164,7 @@ int DeviceBatch::run_ecdsa(void* stream) {
     BCC_HIP_TRY(hipSetDevice(dev_));
     void* st = pick(stream);
     if (!st) return (int)hipErrorOutOfMemory;
+    if (int e = upload_on((hipStream_t)st, nullptr)) return e;
     return ecdsa_launch(scratch_, d_tag, d_x, d_y, d_r, d_s, d_m, d_v, n_rows_, st);
 }
 
@@ -1168,6 +1207,7 @@ int DeviceBatch::run(void* stream) {
     }
     hipStream_t side = (hipStream_t)side_stream_, ws = (hipStream_t)wtx_stream_;
     if (overlap_runs()) {
+        if (int e = upload_on(st, nullptr)) return e;
         // Run-to-run overlap: this run's front (K_inv; K_wtx then the other sighash kernels) waits
         // only for the previous run's prep kernel -- the last reader of the rows it rewrites --
         // not for that run's ladder, so it fills the ladder's tail.  Prep waits for the front.
@@ -1214,6 +1254,7 @@ int DeviceBatch::run(void* stream) {
     // (K_tkey) and everything the message does not enter -- the signature half of the prep and
     // the Q ladder (ecdsa_launch_q); the G ladder and K_tfin wait for both
     (void)ws;
+    if (int e = upload_on(side, st)) return e;
     if (int e = ecdsa_launch_pre(scratch_, d_tag, d_x, d_y, d_s, n_rows_, side)) return e;
     if (int e = ecdsa_launch_key(scratch_, d_tag, d_x, d_y, n_rows_, side)) return e;
     if (int e = ecdsa_launch_q(scratch_, d_r, d_s, n_rows_, side)) return e;
@@ -1243,6 +1284,11 @@ int DeviceBatch::fetch_verdicts(uint8_t* out) {
 }
 
 int DeviceBatch::fetch_msgs(uint8_t* out) {
+    if (up_pending_) {  // staged but never run: the rows are still the host's
+        BCC_HIP_TRY(hipSetDevice(dev_));
+        hipStream_t st = (hipStream_t)pick(last_stream_);
+        if (int e = upload_on(st, nullptr)) return e;
+    }
     if (int e = sync()) return e;
     if (n_rows_) BCC_HIP_TRY(hipMemcpy(out, d_m, 32 * n_rows_, hipMemcpyDeviceToHost));
     return 0;
