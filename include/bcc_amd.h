@@ -134,6 +134,14 @@ int bcc_set_pipeline_chunk(size_t items);
  * instead of in one GPU lane each (BCC_HOST_CHAIN_BLOCKS; default 0: every chain on the GPU).  Results never depend on it. */
 int bcc_set_host_chain_blocks(unsigned blocks);
 
+/* Key-hash spends (P2WPKH, and P2PKH scriptPubKeys): on an input's first interpreter run the
+ * HASH160(pubkey) == program comparison of OP_EQUALVERIFY is checked on the device beside the
+ * signature (the row's verdict = signature valid AND hash equal); a false verdict re-runs the
+ * input on the host with the comparison done there, so the error codes are the reference's.
+ * on = 0: the host hashes every P2WPKH key before the run (BCC_DEVICE_KEY_HASH; default 1).
+ * Results never depend on it. */
+int bcc_set_device_key_hash(int on);
+
 /* Host worker threads of a batch pass (verify_batch interpreter shards, tuple / Taproot front
  * ends, host-verified rounds).  0 restores the default: BCC_HOST_THREADS, else the process's CPU
  * share (bcc_cpu_share, at most 64).  Results never depend on it. */
@@ -174,6 +182,9 @@ typedef struct bcc_batch_stats {
     /* the deserialization pass per worker, max over workers (summed over chunks): dispatch -> start
      * lag, tx parsing + pre-checks, the batched HASH160 of P2WPKH keys */
     double prepare_lag_seconds, prepare_parse_seconds, prepare_hash_seconds;
+    /* key-hash conditions (HASH160(pubkey) == program) checked on the device beside their
+     * signature (bcc_set_device_key_hash) */
+    size_t device_key_hashes;
 } bcc_batch_stats;
 /* Statistics of the calling thread's last bitcoinconsensus_verify_batch / verify call. */
 void bcc_last_batch_stats(bcc_batch_stats* out);

@@ -209,7 +209,8 @@ class BatchStats(ctypes.Structure):
                 ("host_hashed", ctypes.c_size_t), ("shard_seconds", ctypes.c_double),
                 ("stitch_seconds", ctypes.c_double), ("finish_seconds", ctypes.c_double),
                 ("host_jobs_seconds", ctypes.c_double), ("prepare_lag_seconds", ctypes.c_double),
-                ("prepare_parse_seconds", ctypes.c_double), ("prepare_hash_seconds", ctypes.c_double)]
+                ("prepare_parse_seconds", ctypes.c_double), ("prepare_hash_seconds", ctypes.c_double),
+                ("device_key_hashes", ctypes.c_size_t)]
 
 
 def _bind_consensus(L):
@@ -459,6 +460,15 @@ def set_host_chain_blocks(blocks):
     L = lib()
     L.bcc_set_host_chain_blocks.argtypes = [ctypes.c_uint]
     L.bcc_set_host_chain_blocks(blocks)
+
+
+def set_device_key_hash(on):
+    """bcc_set_device_key_hash: on an input's first run the HASH160(pubkey) == program check of a
+    P2WPKH / P2PKH spend runs on the device beside the signature (default on); off: the host
+    hashes every P2WPKH key before the run.  Results never depend on it."""
+    L = lib()
+    L.bcc_set_device_key_hash.argtypes = [ctypes.c_int]
+    L.bcc_set_device_key_hash(1 if on else 0)
 
 
 def set_pipeline_chunk(items):

@@ -115,6 +115,15 @@ std::atomic<uint32_t> g_host_chain_blocks{[] {
     return e ? (uint32_t)atoi(e) : 0u;
 }()};
 
+// Key-hash spends (P2WPKH, P2PKH): the first run leaves HASH160(key) == program to the device,
+// which checks it beside the signature (DeferringChecker::defer_key_hash, sighash.hip
+// key_hash_kernel); prepare() then hashes nothing.  BCC_DEVICE_KEY_HASH=0 / bcc_set_device_key_hash(0):
+// the host hashes every P2WPKH key in prepare() (the round-3 way).
+std::atomic<bool> g_device_key_hash{[] {
+    const char* e = getenv("BCC_DEVICE_KEY_HASH");
+    return !(e && atoi(e) == 0);
+}()};
+
 struct Item {
     const bcc_batch_item* in;
     TxEntry* tx = nullptr;
@@ -338,6 +347,21 @@ public:
         return it_.h160_src && n == it_.h160_len && memcmp(p, it_.h160_src, n) == 0 ? it_.h160
                                                                                      : nullptr;
     }
+    // first runs only: a re-run (the device found the check or the hash false) compares on the host
+    bool defer_key_hash(const uint8_t* key, size_t n, const uint8_t* prog20) override {
+        if (it_.runs != 1 || !g_device_key_hash.load(std::memory_order_relaxed) ||
+            cached_hash160(key, n))
+            return false;
+        kh_prog_ = prog20;
+        kh_taken_ = false;
+        return true;
+    }
+    bool key_hash_taken() override {
+        const bool t = kh_taken_;
+        kh_prog_ = nullptr;
+        kh_taken_ = false;
+        return t;
+    }
     bool check_locktime(int64_t n) override { return tx_check_locktime(it_.tx->tx, it_.in->n_in, n); }
     bool check_sequence(int64_t n) override { return tx_check_sequence(it_.tx->tx, it_.in->n_in, n); }
 
@@ -345,6 +369,8 @@ private:
     Round& rd_;
     uint32_t idx_;
     Item& it_;
+    const uint8_t* kh_prog_ = nullptr;  // a key-hash condition for the next check_ecdsa
+    bool kh_taken_ = false;             // ... which a new device row carries
 };
 
 // One GPU round: the tuples deferred by this round's interpreter runs.
@@ -359,13 +385,17 @@ public:
     std::vector<TxEntry*> touched;
     HostJobs host;  // checks whose sighash the host computes (long chains)
     size_t host_rejected = 0;
+    size_t key_hashes = 0;  // key-hash conditions deferred (whole call)
 
     // GenericTransactionSignatureChecker::CheckECDSASignature (interpreter.cpp:1656-1676) up to
     // the point where the sighash + secp256k1 verify would run; those become a GPU tuple.
     // consult = false queues a check the run may reach later (a CHECKMULTISIG candidate pair)
     // without making the item's finality depend on it.
+    // key_prog (with key_taken): a key-hash condition the new row carries (TupleRows::hrow); a
+    // check answered from the item's cache or rejected on the host leaves it to the caller.
     bool defer(uint32_t item_idx, Item& it, const Bytes& sig, const Bytes& pub, const Bytes& code,
-               SigVersion sv, bool consult) {
+               SigVersion sv, bool consult, const uint8_t* key_prog = nullptr,
+               bool* key_taken = nullptr) {
         const uint64_t koff = keys.size();
         const uint32_t klen = append_key(keys, pub, sig, code, sv);
         for (const Item::Check& c : it.cache) {
@@ -399,6 +429,11 @@ public:
         const uint8_t* y = pub.size() == 65 ? pub.data() + 33 : ybuf;  // y unused for 02/03
         uint32_t row = rows.add(pub[0], pub.data() + 1, y, r, s, one);
         if (pub.size() == 65) rows.y_unused = false;
+        if (key_prog) {
+            rows.add_key_hash(row, key_prog);
+            *key_taken = true;
+            key_hashes++;
+        }
         add_sighash_job(jobs, *it.tx, *it.in, code, sv, hashtype, row, scratch, bip143, touched,
                         &host, &rows.msg[32 * (size_t)row]);
         it.cache.push_back(Item::Check{koff, klen, -2 - (int32_t)pending.size()});
@@ -473,7 +508,9 @@ void run_host_jobs(std::vector<Round>& rds, unsigned T) {
 
 bool DeferringChecker::check_ecdsa(const Bytes& sig, const Bytes& pub, const Bytes& code,
                                    SigVersion sv) {
-    return rd_.defer(idx_, it_, sig, pub, code, sv, true);
+    const uint8_t* kp = kh_prog_;
+    kh_prog_ = nullptr;
+    return rd_.defer(idx_, it_, sig, pub, code, sv, true, kp, &kh_taken_);
 }
 
 void DeferringChecker::hint_ecdsa(const Bytes& sig, const Bytes& pub, const Bytes& code,
@@ -620,6 +657,7 @@ void prepare(BatchState& b, const bcc_batch_item* items, size_t n, unsigned flag
         // HASH160 of every P2WPKH witness key of this thread's share, eight at a time (the
         // interpreter's OP_HASH160 finds it by content, DeferringChecker::cached_hash160)
         const size_t i0 = bound[t], i1 = bound[t + 1];
+        const bool hash_here = !g_device_key_hash.load(std::memory_order_relaxed);
         constexpr size_t BATCH = 64;
         const uint8_t* hp[BATCH];
         size_t hn[BATCH];
@@ -632,7 +670,7 @@ void prepare(BatchState& b, const bcc_batch_item* items, size_t n, unsigned flag
         for (size_t i = i0; i < i1; i++) {
             Item& it = st[i];
             it.h160_src = nullptr;
-            if (!it.active) continue;
+            if (!it.active || !hash_here) continue;
             const bcc_batch_item* in = it.in;
             const uint8_t* spk = in->script_pubkey;
             if (in->script_pubkey_len != 22 || spk[0] != 0x00 || spk[1] != 0x14) continue;
@@ -868,6 +906,7 @@ void chunk_start(ChunkRun& c, const bcc_batch_item* items, size_t n, unsigned fl
         c.rds[t].keys.clear();
         c.rds[t].touched.clear();  // pointers into a previous call's tx entries: never followed
         c.rds[t].host_rejected = 0;
+        c.rds[t].key_hashes = 0;
     }
     c.row0.assign(T + 1, 0);
     c.stage_s = 0;
@@ -949,7 +988,10 @@ long chunk_finish(ChunkRun& c, int* ret_out, bitcoinconsensus_error* err_out, bo
         t_stats.stitch_seconds += since(s1);
         chunk_interpret(c);
     }
-    for (unsigned t = 0; t < c.T; t++) t_stats.host_rejected += c.rds[t].host_rejected;
+    for (unsigned t = 0; t < c.T; t++) {
+        t_stats.host_rejected += c.rds[t].host_rejected;
+        t_stats.device_key_hashes += c.rds[t].key_hashes;
+    }
     auto f0 = clk::now();
     std::vector<long> vt(c.T, 0);
     run_threads(c.T, [&](unsigned t) {  // the shards cover [0, n) contiguously
@@ -1238,6 +1280,11 @@ void bcc_debug_fail_device_rounds(int rounds) {
 void bcc_debug_fail_device_rounds_code(int rounds, int hip_error) {
     g_fail_code.store(hip_error ? hip_error : 2);
     g_fail_rounds.store(rounds > 0 ? rounds : 0);
+}
+
+int bcc_set_device_key_hash(int on) {
+    bcc::host::g_device_key_hash.store(on != 0, std::memory_order_relaxed);
+    return 0;
 }
 
 int bcc_set_host_chain_blocks(unsigned blocks) {

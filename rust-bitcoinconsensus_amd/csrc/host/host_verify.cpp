@@ -13,6 +13,7 @@
 //   preimages      aux digests patched in, SHA-256d                   (K2, K3)
 //   template jobs  T[0, pos) || code || T[pos + 1, len) || le32(type) (K3')
 //   BIP143 jobs    BIP143 preimage of the raw tx (interpreter.cpp:1581-1625), SHA-256d (K_wtx, K_win)
+//   key hashes     HASH160 of the row's key against the program                        (K_h160)
 // Nothing here is test infrastructure: tests/test_host_verify.py pins it against the reference's
 // fixtures; the oracle is never linked.
 #include <algorithm>
@@ -156,6 +157,22 @@ void host_verify_rows(const TupleRows& rows, const uint8_t* msg, uint8_t* verdic
     });
 }
 
+void apply_key_hashes(const TupleRows& R, uint8_t* verdict) {
+    for (size_t k = 0; k < R.hrow.size(); k++) {
+        const uint32_t row = R.hrow[k];
+        uint8_t key[65], h[20];
+        key[0] = R.tag[row];
+        memcpy(key + 1, &R.x[32 * (size_t)row], 32);
+        size_t n = 33;
+        if (key[0] != 2 && key[0] != 3) {
+            memcpy(key + 33, &R.y[32 * (size_t)row], 32);
+            n = 65;
+        }
+        hash160(key, n, h);
+        if (memcmp(h, &R.hprog[20 * k], 20) != 0) verdict[row] = 0;
+    }
+}
+
 int host_verify_parts(const SighashJobs* const* jobs, const TupleRows* const* rows, size_t P,
                       uint8_t* verdict, unsigned threads) {
     size_t r0 = 0;
@@ -169,6 +186,7 @@ int host_verify_parts(const SighashJobs* const* jobs, const TupleRows* const* ro
         }
         host_sighash(*jobs[p], msg.data());
         host_verify_rows(R, msg.data(), verdict + r0, threads);
+        apply_key_hashes(R, verdict + r0);
         r0 += R.size();
     }
     return 0;

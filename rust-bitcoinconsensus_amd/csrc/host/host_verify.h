@@ -16,6 +16,9 @@ int host_verify_tuple(uint8_t tag, const uint8_t* x32, const uint8_t* y32, const
                       const uint8_t* s32, const uint8_t* m32);
 void host_verify_rows(const TupleRows& rows, const uint8_t* msg, uint8_t* verdict, unsigned threads);
 // gpu_verify_parts on the host: the same verdicts for the concatenation of P parts.
+// The key-hash conditions of R (TupleRows::hrow / hprog, the device's key_hash_kernel): clears
+// verdict[row] where HASH160(the row's key) != the program.
+void apply_key_hashes(const TupleRows& R, uint8_t* verdict);
 int host_verify_parts(const SighashJobs* const* jobs, const TupleRows* const* rows, size_t P,
                       uint8_t* verdict, unsigned threads);
 

@@ -585,6 +585,17 @@ bool eval_script(std::vector<Bytes>& stack, const uint8_t* script, size_t script
 // can trip, and the script has no OP_CODESEPARATOR, so the scriptCode is the whole script (after
 // FindAndDelete of the signature push, as for any BASE CHECKSIG).  Returns false when the shape
 // does not apply (the caller then runs eval_script); *res holds eval_script's result otherwise.
+// HASH160(key) == prog20 (the checker's batched hash when it holds one)
+bool key_hash_equal(SigChecker& checker, const uint8_t* key, size_t n, const uint8_t* prog20) {
+    uint8_t h[20];
+    const uint8_t* hk = checker.cached_hash160(key, n);
+    if (!hk) {
+        hash160(key, n, h);
+        hk = h;
+    }
+    return memcmp(hk, prog20, 20) == 0;
+}
+
 bool eval_p2pkh(std::vector<Bytes>& stack, const Span& spk, unsigned flags, SigChecker& checker,
                 ScriptErr* serror, bool* res) {
     const uint8_t* s = spk.p;
@@ -596,25 +607,27 @@ bool eval_p2pkh(std::vector<Bytes>& stack, const Span& spk, unsigned flags, SigC
     static const Bytes vch_true(1, 1);
     const Bytes& sig = stack[stack.size() - 2];
     const Bytes& pub = stack[stack.size() - 1];
-    uint8_t h[20];  // OP_DUP, OP_HASH160
-    const uint8_t* hk = checker.cached_hash160(pub.data(), pub.size());
-    if (!hk) {
-        hash160(pub.data(), pub.size(), h);
-        hk = h;
-    }
-    if (memcmp(hk, s + 3, 20) != 0) {  // <20> OP_EQUALVERIFY
+    const bool der_bad = !sig.empty() && (flags & FLAG_DERSIG) && !is_valid_signature_encoding(sig);
+    // OP_DUP, OP_HASH160, <20> OP_EQUALVERIFY: taken over by the checker when the run goes on to
+    // the signature check (no DER failure in between), else compared here
+    const bool taken = !der_bad && checker.defer_key_hash(pub.data(), pub.size(), s + 3);
+    if (!taken && !key_hash_equal(checker, pub.data(), pub.size(), s + 3)) {
         *res = fail(serror, SERR_EQUALVERIFY);
+        return true;
+    }
+    if (der_bad) {
+        *res = fail(serror, SERR_SIG_DER);
         return true;
     }
     Bytes code(s, s + 25);  // OP_CHECKSIG (EvalChecksigPreTapscript, interpreter.cpp:345-369)
     Bytes pushed;
     push_data(pushed, sig.data(), sig.size());
     find_and_delete(code, pushed);
-    if (!sig.empty() && (flags & FLAG_DERSIG) && !is_valid_signature_encoding(sig)) {
-        *res = fail(serror, SERR_SIG_DER);
+    const bool ok = checker.check_ecdsa(sig, pub, code, SIGVERSION_BASE);
+    if (taken && !checker.key_hash_taken() && !key_hash_equal(checker, pub.data(), pub.size(), s + 3)) {
+        *res = fail(serror, SERR_EQUALVERIFY);
         return true;
     }
-    const bool ok = checker.check_ecdsa(sig, pub, code, SIGVERSION_BASE);
     popstack(stack);
     popstack(stack);
     stack.push_back(ok ? vch_true : vch_false);
@@ -660,21 +673,21 @@ bool verify_witness_program(const std::vector<Span>& witness, int version, const
                 if (w.n > MAX_SCRIPT_ELEMENT_SIZE) return fail(serror, SERR_PUSH_SIZE);
             const Span& ws = witness[0];
             const Span& wk = witness[1];
-            uint8_t h[20];  // OP_DUP, OP_HASH160
-            const uint8_t* hk = checker.cached_hash160(wk.p, wk.n);
-            if (!hk) {
-                hash160(wk.p, wk.n, h);
-                hk = h;
-            }
-            // <20> OP_EQUALVERIFY
-            if (memcmp(hk, program.data(), 20) != 0) return fail(serror, SERR_EQUALVERIFY);
+            const Bytes sig(ws.p, ws.p + ws.n);
+            const bool der_bad = !sig.empty() && (flags & FLAG_DERSIG) && !is_valid_signature_encoding(sig);
+            // OP_DUP, OP_HASH160, <20> OP_EQUALVERIFY: taken over by the checker when the run goes
+            // on to the signature check, else compared here
+            const bool taken = !der_bad && checker.defer_key_hash(wk.p, wk.n, program.data());
+            if (!taken && !key_hash_equal(checker, wk.p, wk.n, program.data()))
+                return fail(serror, SERR_EQUALVERIFY);
             // OP_CHECKSIG (witness v0: no FindAndDelete; scriptCode = the whole script)
-            const Bytes sig(ws.p, ws.p + ws.n), pub(wk.p, wk.p + wk.n), code(sc, sc + 25);
-            if (!sig.empty() && (flags & FLAG_DERSIG) && !is_valid_signature_encoding(sig))
-                return fail(serror, SERR_SIG_DER);
+            if (der_bad) return fail(serror, SERR_SIG_DER);
+            const Bytes pub(wk.p, wk.p + wk.n), code(sc, sc + 25);
+            const bool ok = checker.check_ecdsa(sig, pub, code, SIGVERSION_WITNESS_V0);
+            if (taken && !checker.key_hash_taken() && !key_hash_equal(checker, wk.p, wk.n, program.data()))
+                return fail(serror, SERR_EQUALVERIFY);
             // the stack is [result]: clean; false -> EVAL_FALSE
-            if (!checker.check_ecdsa(sig, pub, code, SIGVERSION_WITNESS_V0))
-                return fail(serror, SERR_EVAL_FALSE);
+            if (!ok) return fail(serror, SERR_EVAL_FALSE);
             if (serror) *serror = SERR_OK;
             return true;
         }

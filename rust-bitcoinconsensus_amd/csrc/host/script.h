@@ -91,6 +91,14 @@ public:
     // HASH160 of `p` if the checker already holds it (computed ahead in a batch for exactly these
     // bytes), else nullptr; OP_HASH160 then uses it instead of hashing again.
     virtual const uint8_t* cached_hash160(const uint8_t*, size_t) const { return nullptr; }
+    // The <20> OP_EQUALVERIFY of a key-hash spend (P2WPKH, P2PKH): HASH160(key) == prog20.  A
+    // batching checker may take it over: it returns true and the script goes on as if the hashes
+    // matched; the checker then ties the condition to the NEXT check_ecdsa of this run (the
+    // check's verdict becomes "signature valid AND hashes match").  key_hash_taken() after that
+    // check_ecdsa says whether it did; when not, the script compares the hash itself before using
+    // the check's result.  false (the default): the script hashes now.
+    virtual bool defer_key_hash(const uint8_t*, size_t, const uint8_t*) { return false; }
+    virtual bool key_hash_taken() { return false; }
     virtual bool check_locktime(int64_t n) = 0;
     virtual bool check_sequence(int64_t n) = 0;
 };

@@ -160,7 +160,16 @@ struct TupleRows {
     // keep it; the device initialises the msg rows itself), y_unused = no 65-byte key (the y
     // rows are never read).  clear() resets both.
     bool msg_one = false, y_unused = false;
+    // Key-hash conditions (the <20> OP_EQUALVERIFY of a P2WPKH / P2PKH spend taken over by the
+    // device, engine.cpp DeferringChecker::defer_key_hash): row hrow[k] is valid only if
+    // HASH160(its key) == hprog[20k, 20k + 20); the device ANDs that into the row's verdict.
+    std::vector<uint32_t> hrow;
+    std::vector<uint8_t> hprog;
     size_t size() const { return tag.size(); }
+    void add_key_hash(uint32_t row, const uint8_t* prog20) {
+        hrow.push_back(row);
+        hprog.insert(hprog.end(), prog20, prog20 + 20);
+    }
     uint32_t add(uint8_t t, const uint8_t* x32, const uint8_t* y32, const uint8_t* r32,
                  const uint8_t* s32, const uint8_t* m32) {
         tag.push_back(t);
@@ -173,6 +182,7 @@ struct TupleRows {
     }
     void clear() {
         tag.clear(); x.clear(); y.clear(); r.clear(); s.clear(); msg.clear();
+        hrow.clear(); hprog.clear();
         msg_one = y_unused = false;
     }
 };
@@ -319,6 +329,7 @@ public:
     int fetch_verdicts(uint8_t* out);            // synchronous D2H (waits for the last run)
     int fetch_msgs(uint8_t* out);                // synchronous D2H (tests)
     size_t n_tuples() const { return n_rows_; }
+    size_t n_key_hashes() const { return n_hash_; }  // TupleRows::hrow conditions staged
     size_t n_pre() const { return n_pre_ + n_tjob_ + n_wjob_; }  // sighash messages (all kinds)
     size_t n_wtx() const { return n_wtx_; }
     // Algorithmic bytes of one run of the sighash stage: padded messages + digests of the host-built
@@ -344,6 +355,8 @@ private:
     bool up_pending_ = false;      // the staged image is not on the device yet (async_upload)
     size_t up_rows_ = 0, up_total_ = 0;
     int launch_after_front(struct ihipStream_t* st);  // K_win, K2, K3
+    int launch_key_hash(struct ihipStream_t* st);     // K_h160: key-hash conditions into the verdicts
+    int run_stages(void* stream);                     // run() up to K_tfin
     int dev_;
     void* own_stream_ = nullptr;   // hipStream_t, created on first use
     void* last_stream_ = nullptr;  // stream of the last run
@@ -379,6 +392,9 @@ private:
     WtxRec* d_wtx_ = nullptr;
     WinJob* d_wjob_ = nullptr;
     uint32_t* d_intab_ = nullptr;
+    size_t n_hash_ = 0;
+    uint32_t* d_hrow_ = nullptr;
+    uint8_t* d_hprog_ = nullptr;
 };
 
 // Threads the calling thread's device batches use to fill their pinned staging image (0: one per

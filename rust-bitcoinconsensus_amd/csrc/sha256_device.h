@@ -63,4 +63,104 @@ SHA_HD void sha256_of_digest(uint32_t out[8], const uint32_t d[8]) {
     sha256_compress(out, w);
 }
 
+// RIPEMD-160 compression for one lane (restates crypto/ripemd160.cpp:20-239: two lines of 80
+// steps over the little-endian words X[16]; the fully unrolled tables fold into constants).
+SHA_HD uint32_t rmd_rol(uint32_t x, int n) { return (x << n) | (x >> (32 - n)); }
+
+SHA_HD uint32_t rmd_f(int j, uint32_t x, uint32_t y, uint32_t z) {
+    return j < 16 ? x ^ y ^ z
+         : j < 32 ? (x & y) | (~x & z)
+         : j < 48 ? (x | ~y) ^ z
+         : j < 64 ? (x & z) | (y & ~z)
+                  : x ^ (y | ~z);
+}
+
+SHA_HD void ripemd160_compress(uint32_t h[5], const uint32_t X[16]) {
+    const uint8_t RL[80] = {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15,
+                            7, 4, 13, 1, 10, 6, 15, 3, 12, 0, 9, 5, 2, 14, 11, 8,
+                            3, 10, 14, 4, 9, 15, 8, 1, 2, 7, 0, 6, 13, 11, 5, 12,
+                            1, 9, 11, 10, 0, 8, 12, 4, 13, 3, 7, 15, 14, 5, 6, 2,
+                            4, 0, 5, 9, 7, 12, 2, 10, 14, 1, 3, 8, 11, 6, 15, 13};
+    const uint8_t RR[80] = {5, 14, 7, 0, 9, 2, 11, 4, 13, 6, 15, 8, 1, 10, 3, 12,
+                            6, 11, 3, 7, 0, 13, 5, 10, 14, 15, 8, 12, 4, 9, 1, 2,
+                            15, 5, 1, 3, 7, 14, 6, 9, 11, 8, 12, 2, 10, 0, 4, 13,
+                            8, 6, 4, 1, 3, 11, 15, 0, 5, 12, 2, 13, 9, 7, 10, 14,
+                            12, 15, 10, 4, 1, 5, 8, 7, 6, 2, 13, 14, 0, 3, 9, 11};
+    const uint8_t SL[80] = {11, 14, 15, 12, 5, 8, 7, 9, 11, 13, 14, 15, 6, 7, 9, 8,
+                            7, 6, 8, 13, 11, 9, 7, 15, 7, 12, 15, 9, 11, 7, 13, 12,
+                            11, 13, 6, 7, 14, 9, 13, 15, 14, 8, 13, 6, 5, 12, 7, 5,
+                            11, 12, 14, 15, 14, 15, 9, 8, 9, 14, 5, 6, 8, 6, 5, 12,
+                            9, 15, 5, 11, 6, 8, 13, 12, 5, 12, 13, 14, 11, 8, 5, 6};
+    const uint8_t SR[80] = {8, 9, 9, 11, 13, 15, 15, 5, 7, 7, 8, 11, 14, 14, 12, 6,
+                            9, 13, 15, 7, 12, 8, 9, 11, 7, 7, 12, 7, 6, 15, 13, 11,
+                            9, 7, 15, 11, 8, 6, 6, 14, 12, 13, 5, 14, 13, 13, 7, 5,
+                            15, 5, 8, 11, 14, 14, 6, 14, 6, 9, 12, 9, 12, 5, 15, 8,
+                            8, 5, 12, 9, 12, 5, 14, 6, 8, 13, 6, 5, 15, 13, 11, 11};
+    const uint32_t KL[5] = {0u, 0x5a827999u, 0x6ed9eba1u, 0x8f1bbcdcu, 0xa953fd4eu};
+    const uint32_t KR[5] = {0x50a28be6u, 0x5c4dd124u, 0x6d703ef3u, 0x7a6d76e9u, 0u};
+    uint32_t a1 = h[0], b1 = h[1], c1 = h[2], d1 = h[3], e1 = h[4];
+    uint32_t a2 = a1, b2 = b1, c2 = c1, d2 = d1, e2 = e1;
+#pragma unroll
+    for (int j = 0; j < 80; j++) {
+        uint32_t t = rmd_rol(a1 + rmd_f(j, b1, c1, d1) + X[RL[j]] + KL[j >> 4], SL[j]) + e1;
+        a1 = e1; e1 = d1; d1 = rmd_rol(c1, 10); c1 = b1; b1 = t;
+        t = rmd_rol(a2 + rmd_f(79 - j, b2, c2, d2) + X[RR[j]] + KR[j >> 4], SR[j]) + e2;
+        a2 = e2; e2 = d2; d2 = rmd_rol(c2, 10); c2 = b2; b2 = t;
+    }
+    const uint32_t t = h[1] + c1 + d2;
+    h[1] = h[2] + d1 + e2;
+    h[2] = h[3] + e1 + a2;
+    h[3] = h[4] + a1 + b2;
+    h[4] = h[0] + b1 + c2;
+    h[0] = t;
+}
+
+SHA_HD uint32_t sha_bswap(uint32_t x) {
+    return (x >> 24) | ((x >> 8) & 0xff00u) | ((x << 8) & 0xff0000u) | (x << 24);
+}
+
+// HASH160 (RIPEMD160(SHA256(k)), crypto/hash.h CHash160) of a public key held as a tuple row:
+// k = tag || x (33 bytes) for tag 2 / 3, tag || x || y (65 bytes) otherwise; x, y are the big-endian
+// coordinates as eight words each (xw[0] = bytes 0-3).  out[5] = the digest as little-endian
+// words (out[0] = digest bytes 0-3, the byte order of the 20-byte program).
+SHA_HD void key_hash160(uint32_t tag, const uint32_t xw[8], const uint32_t yw[8], uint32_t out[5]) {
+    const bool cmp = tag == 2 || tag == 3;
+    uint32_t w[16], s[8];
+    // bytes: tag, x[0..31] (, y[0..31]) -> big-endian words shifted by one byte
+    w[0] = (tag << 24) | (xw[0] >> 8);
+#pragma unroll
+    for (int i = 1; i < 8; i++) w[i] = (xw[i - 1] << 24) | (xw[i] >> 8);
+    sha256_init_state(s);
+    if (cmp) {
+        w[8] = (xw[7] << 24) | 0x00800000u;
+#pragma unroll
+        for (int i = 9; i < 15; i++) w[i] = 0;
+        w[15] = 33 * 8;
+        sha256_compress(s, w);
+    } else {
+        w[8] = (xw[7] << 24) | (yw[0] >> 8);
+#pragma unroll
+        for (int i = 9; i < 16; i++) w[i] = (yw[i - 9] << 24) | (yw[i - 8] >> 8);
+        const uint32_t last = yw[7] << 24;
+        sha256_compress(s, w);
+        w[0] = last | 0x00800000u;
+#pragma unroll
+        for (int i = 1; i < 15; i++) w[i] = 0;
+        w[15] = 65 * 8;
+        sha256_compress(s, w);
+    }
+    // RIPEMD-160 of the 32-byte digest: one block, little-endian words
+    uint32_t X[16];
+#pragma unroll
+    for (int i = 0; i < 8; i++) X[i] = sha_bswap(s[i]);
+    X[8] = 0x80u;
+#pragma unroll
+    for (int i = 9; i < 14; i++) X[i] = 0;
+    X[14] = 256;
+    X[15] = 0;
+    out[0] = 0x67452301u; out[1] = 0xefcdab89u; out[2] = 0x98badcfeu; out[3] = 0x10325476u;
+    out[4] = 0xc3d2e1f0u;
+    ripemd160_compress(out, X);
+}
+
 }  // namespace bcc

@@ -879,7 +879,7 @@ int DeviceBatch::stage_parts(const SighashJobs* const* J, const TupleRows* const
     rows_pending_ = false;
     std::vector<size_t> row0(P + 1, 0), auxb0(P + 1, 0), preb0(P + 1, 0), auxi0(P + 1, 0),
         prei0(P + 1, 0), pat0(P + 1, 0), tpl0(P + 1, 0), code0(P + 1, 0), tj0(P + 1, 0),
-        raw0(P + 1, 0), wtx0(P + 1, 0), wj0(P + 1, 0), win0(P + 1, 0);
+        raw0(P + 1, 0), wtx0(P + 1, 0), wj0(P + 1, 0), win0(P + 1, 0), h0(P + 1, 0);
     size_t tjblk = 0;
     for (size_t p = 0; p < P; p++) {
         row0[p + 1] = row0[p] + Rw[p]->size();
@@ -895,6 +895,7 @@ int DeviceBatch::stage_parts(const SighashJobs* const* J, const TupleRows* const
         wtx0[p + 1] = wtx0[p] + J[p]->wtx.size();
         wj0[p + 1] = wj0[p] + J[p]->wjobs.size();
         win0[p + 1] = win0[p] + J[p]->win_entries;
+        h0[p + 1] = h0[p] + Rw[p]->hrow.size();
         for (const auto& t : J[p]->tjobs) tjblk += t.nblk;
     }
     const size_t LIM = (size_t)1 << 32;
@@ -915,6 +916,7 @@ int DeviceBatch::stage_parts(const SighashJobs* const* J, const TupleRows* const
     n_wtx_ = wtx0[P];
     n_wjob_ = wj0[P];
     n_win_ = win0[P];
+    n_hash_ = h0[P];
     sighash_bytes_ = 64 * (pre_blocks_ + aux_blocks_ + tjob_blocks_) + 32 * (n_pre_ + n_aux_ + n_tjob_);
     for (size_t p = 0; p < P; p++) {
         for (const WtxRec& r : J[p]->wtx) sighash_bytes_ += r.tx_len + 96;
@@ -924,7 +926,7 @@ int DeviceBatch::stage_parts(const SighashJobs* const* J, const TupleRows* const
     // regions filled from the host image first (one copy), device-written ones after them
     // Y and M go up only when some part needs them (TupleRows::y_unused / msg_one)
     enum { TAG, X, RR, S, AUX, PRE, AUX_OFF, AUX_NBLK, PRE_OFF, PRE_NBLK, PRE_ROW, PATCH,
-           TPL, CODE, TJOB, TXRAW, WTX, WJOB, ZEROS, UPLOADED, Y = UPLOADED, M, V, AUXD, INTAB, TXD,
+           TPL, CODE, TJOB, TXRAW, WTX, WJOB, HROW, HPROG, ZEROS, UPLOADED, Y = UPLOADED, M, V, AUXD, INTAB, TXD,
            NB };
     bool need_y = false, need_m = false;
     for (size_t p = 0; p < P; p++) {
@@ -939,6 +941,7 @@ int DeviceBatch::stage_parts(const SighashJobs* const* J, const TupleRows* const
     sizes[PATCH] = sizeof(PatchRec) * n_patch_;
     sizes[TPL] = tpl0[P]; sizes[CODE] = code0[P]; sizes[TJOB] = sizeof(TplJob) * n_tjob_;
     sizes[TXRAW] = raw0[P]; sizes[WTX] = sizeof(WtxRec) * n_wtx_; sizes[WJOB] = sizeof(WinJob) * n_wjob_;
+    sizes[HROW] = 4 * n_hash_; sizes[HPROG] = 20 * n_hash_;
     sizes[ZEROS] = 64;
     sizes[V] = R; sizes[AUXD] = 32 * n_aux_; sizes[INTAB] = 8 * n_win_; sizes[TXD] = 96 * n_wtx_;
     size_t off[NB], total = 0;
@@ -970,6 +973,7 @@ int DeviceBatch::stage_parts(const SighashJobs* const* J, const TupleRows* const
     d_pre_row_ = (uint32_t*)(a + off[PRE_ROW]); d_patch_ = (PatchRec*)(a + off[PATCH]);
     d_tpl_ = a + off[TPL]; d_code_ = a + off[CODE]; d_tjob_ = (TplJob*)(a + off[TJOB]);
     d_txraw_ = a + off[TXRAW]; d_wtx_ = (WtxRec*)(a + off[WTX]); d_wjob_ = (WinJob*)(a + off[WJOB]);
+    d_hrow_ = (uint32_t*)(a + off[HROW]); d_hprog_ = a + off[HPROG];
     d_zeros_ = a + off[ZEROS]; d_intab_ = (uint32_t*)(a + off[INTAB]); d_txd_ = a + off[TXD];
     uint8_t* h = (uint8_t*)host_image_;
     memset(h + off[ZEROS], 0, 64);
@@ -1028,6 +1032,9 @@ int DeviceBatch::stage_parts(const SighashJobs* const* J, const TupleRows* const
             t.row += (uint32_t)r0;
             wj[k] = t;
         }
+        uint32_t* hr = (uint32_t*)(h + off[HROW]) + h0[p];
+        for (size_t k = 0; k < rw.hrow.size(); k++) hr[k] = rw.hrow[k] + (uint32_t)r0;
+        cp(HPROG, 20 * h0[p], rw.hprog.data(), rw.hprog.size());
     };
     const size_t nth = std::min<size_t>(P, tl_stage_threads ? tl_stage_threads : P);
     if (nth <= 1 || upload < ((size_t)1 << 20)) {
@@ -1165,7 +1172,51 @@ int DeviceBatch::run_ecdsa(void* stream) {
     void* st = pick(stream);
     if (!st) return (int)hipErrorOutOfMemory;
     if (int e = upload_on((hipStream_t)st, nullptr)) return e;
-    return ecdsa_launch(scratch_, d_tag, d_x, d_y, d_r, d_s, d_m, d_v, n_rows_, st);
+    if (int e = ecdsa_launch(scratch_, d_tag, d_x, d_y, d_r, d_s, d_m, d_v, n_rows_, st)) return e;
+    return launch_key_hash((hipStream_t)st);
+}
+
+// K_h160: per key-hash condition (TupleRows::hrow) the HASH160 of the row's key, rebuilt from its
+// tag / x / y rows, against the 20-byte program; a mismatch clears the row's verdict.  Runs after
+// K_tfin on the same stream.  ~1 SHA-256 block (2 for a 65-byte key) + 1 RIPEMD-160 block a lane.
+__global__ void __launch_bounds__(256) key_hash_kernel(const uint8_t* __restrict__ tag,
+                                                       const uint8_t* __restrict__ x,
+                                                       const uint8_t* __restrict__ y,
+                                                       const uint32_t* __restrict__ hrow,
+                                                       const uint8_t* __restrict__ hprog,
+                                                       uint32_t n, uint8_t* __restrict__ verdict) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    const uint32_t row = hrow[k];
+    const uint32_t t = tag[row];
+    uint32_t xw[8], yw[8], d[5];
+    const uint4* xp = (const uint4*)(x + 32 * (size_t)row);
+    const uint4 x0 = xp[0], x1 = xp[1];
+    xw[0] = sha_bswap(x0.x); xw[1] = sha_bswap(x0.y); xw[2] = sha_bswap(x0.z); xw[3] = sha_bswap(x0.w);
+    xw[4] = sha_bswap(x1.x); xw[5] = sha_bswap(x1.y); xw[6] = sha_bswap(x1.z); xw[7] = sha_bswap(x1.w);
+    if (t == 2 || t == 3) {
+#pragma unroll
+        for (int i = 0; i < 8; i++) yw[i] = 0;
+    } else {
+        const uint4* yp = (const uint4*)(y + 32 * (size_t)row);
+        const uint4 y0 = yp[0], y1 = yp[1];
+        yw[0] = sha_bswap(y0.x); yw[1] = sha_bswap(y0.y); yw[2] = sha_bswap(y0.z); yw[3] = sha_bswap(y0.w);
+        yw[4] = sha_bswap(y1.x); yw[5] = sha_bswap(y1.y); yw[6] = sha_bswap(y1.z); yw[7] = sha_bswap(y1.w);
+    }
+    key_hash160(t, xw, yw, d);
+    const uint8_t* pg = hprog + 20 * (size_t)k;
+    uint32_t diff = 0;
+#pragma unroll
+    for (int i = 0; i < 20; i++) diff |= (uint32_t)pg[i] ^ ((d[i / 4] >> (8 * (i % 4))) & 0xffu);
+    if (diff) verdict[row] = 0;
+}
+
+int DeviceBatch::launch_key_hash(hipStream_t st) {
+    if (!n_hash_) return 0;
+    hipLaunchKernelGGL(key_hash_kernel, dim3((unsigned)((n_hash_ + 255) / 256)), dim3(256), 0, st,
+                       d_tag, d_x, d_y, d_hrow_, d_hprog_, (uint32_t)n_hash_, d_v);
+    BCC_HIP_TRY(hipGetLastError());
+    return 0;
 }
 
 // Consecutive run()s of a resident batch may overlap (BCC_OVERLAP_RUNS=1): see DeviceBatch::run.
@@ -1188,8 +1239,14 @@ int DeviceBatch::run(void* stream) {
     if (!st) return (int)hipErrorOutOfMemory;
     if (n_rows_ == 0 || n_aux_ + n_tjob_ + n_pre_ + n_wjob_ == 0) {
         if (int e = run_sighash(st)) return e;
-        return run_ecdsa(st);
+        return run_ecdsa(st);  // K_h160 included
     }
+    if (int e = run_stages(st)) return e;
+    return launch_key_hash(st);
+}
+
+int DeviceBatch::run_stages(void* stream) {
+    hipStream_t st = (hipStream_t)stream;
     if (!side_stream_) {
         hipStream_t s = nullptr, s2 = nullptr;
         hipEvent_t a = nullptr, b = nullptr, c = nullptr;

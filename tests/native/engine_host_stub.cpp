@@ -11,6 +11,7 @@
 #include "../../oracle/bcc_oracle.h"
 #include "../../rust-bitcoinconsensus_amd/csrc/pipeline.h"
 #include "../../rust-bitcoinconsensus_amd/csrc/host/engine.h"
+#include "../../rust-bitcoinconsensus_amd/csrc/host/host_verify.h"
 
 namespace bcc {
 
@@ -84,6 +85,7 @@ int gpu_verify_batch(int, const SighashJobs& j, const TupleRows& rows, uint8_t* 
         verdict[i] = (uint8_t)bcco_ecdsa_verify_raw(qx, qy, &rows.r[32 * i], &rows.s[32 * i],
                                                     &msg[32 * i]);
     }
+    bcc::host::apply_key_hashes(rows, verdict);  // the device's key_hash_kernel
     return 0;
 }
 

@@ -159,3 +159,57 @@ def build_script_test_tx(script_sig, spk, witness, value):
     txid = sha256d(credit)
     prevout = txid + struct.pack("<I", 0)
     return ser_tx(1, [(prevout, script_sig, 0xffffffff)], [(value, b"")], 0, [witness])
+
+
+def _ripemd160(m):
+    """RIPEMD-160 (Dobbertin, Bosselaers, Preneel 1996) in plain Python, for test inputs only
+    (this image's hashlib has no ripemd160); pinned by the published vectors in
+    tests/test_key_hash.py."""
+    M = 0xFFFFFFFF
+    rol = lambda x, n: ((x << n) | (x >> (32 - n))) & M  # noqa: E731
+    RL = [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 7, 4, 13, 1, 10, 6, 15, 3, 12, 0, 9,
+          5, 2, 14, 11, 8, 3, 10, 14, 4, 9, 15, 8, 1, 2, 7, 0, 6, 13, 11, 5, 12, 1, 9, 11, 10, 0, 8,
+          12, 4, 13, 3, 7, 15, 14, 5, 6, 2, 4, 0, 5, 9, 7, 12, 2, 10, 14, 1, 3, 8, 11, 6, 15, 13]
+    RR = [5, 14, 7, 0, 9, 2, 11, 4, 13, 6, 15, 8, 1, 10, 3, 12, 6, 11, 3, 7, 0, 13, 5, 10, 14, 15, 8,
+          12, 4, 9, 1, 2, 15, 5, 1, 3, 7, 14, 6, 9, 11, 8, 12, 2, 10, 0, 4, 13, 8, 6, 4, 1, 3, 11, 15,
+          0, 5, 12, 2, 13, 9, 7, 10, 14, 12, 15, 10, 4, 1, 5, 8, 7, 6, 2, 13, 14, 0, 3, 9, 11]
+    SL = [11, 14, 15, 12, 5, 8, 7, 9, 11, 13, 14, 15, 6, 7, 9, 8, 7, 6, 8, 13, 11, 9, 7, 15, 7, 12,
+          15, 9, 11, 7, 13, 12, 11, 13, 6, 7, 14, 9, 13, 15, 14, 8, 13, 6, 5, 12, 7, 5, 11, 12, 14,
+          15, 14, 15, 9, 8, 9, 14, 5, 6, 8, 6, 5, 12, 9, 15, 5, 11, 6, 8, 13, 12, 5, 12, 13, 14, 11,
+          8, 5, 6]
+    SR = [8, 9, 9, 11, 13, 15, 15, 5, 7, 7, 8, 11, 14, 14, 12, 6, 9, 13, 15, 7, 12, 8, 9, 11, 7, 7,
+          12, 7, 6, 15, 13, 11, 9, 7, 15, 11, 8, 6, 6, 14, 12, 13, 5, 14, 13, 13, 7, 5, 15, 5, 8, 11,
+          14, 14, 6, 14, 6, 9, 12, 9, 12, 5, 15, 8, 8, 5, 12, 9, 12, 5, 14, 6, 8, 13, 6, 5, 15, 13,
+          11, 11]
+    KL = [0, 0x5A827999, 0x6ED9EBA1, 0x8F1BBCDC, 0xA953FD4E]
+    KR = [0x50A28BE6, 0x5C4DD124, 0x6D703EF3, 0x7A6D76E9, 0]
+
+    def f(j, x, y, z):
+        if j < 16:
+            return x ^ y ^ z
+        if j < 32:
+            return (x & y) | (~x & z)
+        if j < 48:
+            return (x | ~y & M) ^ z
+        if j < 64:
+            return (x & z) | (y & ~z)
+        return x ^ (y | ~z & M)
+
+    h = [0x67452301, 0xEFCDAB89, 0x98BADCFE, 0x10325476, 0xC3D2E1F0]
+    m = m + b"\x80" + b"\x00" * ((55 - len(m)) % 64) + struct.pack("<Q", 8 * len(m))
+    for o in range(0, len(m), 64):
+        X = struct.unpack("<16I", m[o:o + 64])
+        a1, b1, c1, d1, e1 = h
+        a2, b2, c2, d2, e2 = h
+        for j in range(80):
+            t = (rol((a1 + (f(j, b1, c1, d1) & M) + X[RL[j]] + KL[j >> 4]) & M, SL[j]) + e1) & M
+            a1, e1, d1, c1, b1 = e1, d1, rol(c1, 10), b1, t
+            t = (rol((a2 + (f(79 - j, b2, c2, d2) & M) + X[RR[j]] + KR[j >> 4]) & M, SR[j]) + e2) & M
+            a2, e2, d2, c2, b2 = e2, d2, rol(c2, 10), b2, t
+        h = [(h[1] + c1 + d2) & M, (h[2] + d1 + e2) & M, (h[3] + e1 + a2) & M,
+             (h[4] + a1 + b2) & M, (h[0] + b1 + c2) & M]
+    return struct.pack("<5I", *h)
+
+
+def hash160(b):
+    return _ripemd160(hashlib.sha256(b).digest())

@@ -135,6 +135,46 @@ def test_script_cases_host_hashed_chains(eng, blocks):
         eng.bcc_set_host_chain_blocks(0)
 
 
+@pytest.mark.parametrize("on", [0, 1])
+def test_script_cases_key_hash_where(eng, on):
+    """The HASH160(pubkey) == program check of P2WPKH / P2PKH spends on the device beside the
+    signature (on: the stub applies the rows' key-hash conditions like key_hash_kernel; a false
+    verdict re-runs the input with the host comparison) or on the host before the run (off):
+    identical results, batched and single; the deferred path carried conditions."""
+    eng.bcc_set_device_key_hash.argtypes = [ctypes.c_int]
+    try:
+        eng.bcc_set_device_key_hash(on)
+        allc = cases()
+        n = [0]
+
+        def count():
+            st = Stats()
+            eng.bcc_last_batch_stats(ctypes.byref(st))
+            n[0] += st.device_key_hashes
+
+        by_flags = {}
+        for c in allc:
+            by_flags.setdefault(c["flags"], []).append(c)
+        for flags, cs in by_flags.items():
+            keep, arr = [], (Item * len(cs))()
+            for i, c in enumerate(cs):
+                spk, tx = bytes.fromhex(c["spk"]), bytes.fromhex(c["tx"])
+                bs = ctypes.create_string_buffer(spk, max(1, len(spk)))
+                bt = ctypes.create_string_buffer(tx, max(1, len(tx)))
+                keep += [bs, bt]
+                arr[i] = Item(ctypes.addressof(bs), len(spk), c["amount"], ctypes.addressof(bt), len(tx), c["nin"])
+            ret = (ctypes.c_int * len(cs))()
+            err = (ctypes.c_int * len(cs))()
+            eng.bitcoinconsensus_verify_batch(arr, len(cs), flags, ret, err)
+            assert list(zip(ret, err)) == [(c["ret"], c["err"]) for c in cs]
+            count()
+        assert (n[0] > 0) == bool(on)
+        test_script_cases_single_calls(eng)
+        test_crate_vectors(eng)
+    finally:
+        eng.bcc_set_device_key_hash(1)
+
+
 def test_pubkey_verify_batch_front_end(eng):
     """bcc_pubkey_verify_batch's host front end (CPubKey length filter, lax DER, r/s == 0; the
     curve work stubbed by the oracle) on the reference-labelled adversarial tuple fixtures."""
@@ -184,7 +224,8 @@ class Stats(ctypes.Structure):
                                                              ("host_hashed", ctypes.c_size_t)] + [
         (k, ctypes.c_double) for k in ("shard_seconds", "stitch_seconds", "finish_seconds",
                                        "host_jobs_seconds", "prepare_lag_seconds",
-                                       "prepare_parse_seconds", "prepare_hash_seconds")]
+                                       "prepare_parse_seconds", "prepare_hash_seconds")] + [
+        ("device_key_hashes", ctypes.c_size_t)]
 
 
 def test_device_failure_retried_once(eng):

@@ -15,6 +15,7 @@ ROOT = os.path.dirname(HERE)
 SO = os.path.join(HERE, "native", "_build", "hash_test.so")
 SRC = [os.path.join(HERE, "native", "hash_test.cpp"),
        os.path.join(ROOT, "rust-bitcoinconsensus_amd", "csrc", "host", "hashes.cpp")]
+DEPS = SRC + [os.path.join(ROOT, "rust-bitcoinconsensus_amd", "csrc", "sha256_device.h")]
 
 # Dobbertin-Bosselaers-Preneel, "RIPEMD-160: A Strengthened Version of RIPEMD", test vectors
 RIPEMD_VECTORS = [
@@ -33,7 +34,7 @@ RIPEMD_VECTORS = [
 
 @pytest.fixture(scope="module")
 def so():
-    if not os.path.exists(SO) or any(os.path.getmtime(s) > os.path.getmtime(SO) for s in SRC):
+    if not os.path.exists(SO) or any(os.path.getmtime(s) > os.path.getmtime(SO) for s in DEPS):
         os.makedirs(os.path.dirname(SO), exist_ok=True)
         subprocess.check_call(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-o", SO] + SRC)
     return SO
@@ -108,3 +109,21 @@ def test_host_hash160_batch_matches_scalar(so):
             exp = ctypes.create_string_buffer(20)
             L.th_hash160(m, len(m), exp)
             assert out.raw[20 * i: 20 * i + 20] == exp.raw, (count, i, len(m))
+
+
+def test_device_key_hash160(so):
+    """The device-side key HASH160 (sha256_device.h key_hash160: SHA-256 of the 33- / 65-byte key
+    built from a tuple row, then RIPEMD-160, the P2WPKH / P2PKH EQUALVERIFY check deferred to the
+    GPU) compiled as host code, against the host HASH160 of the same key bytes."""
+    L = ctypes.CDLL(so)
+    rng = random.Random(23)
+    out = ctypes.create_string_buffer(20)
+    ref = ctypes.create_string_buffer(32)
+    for i in range(400):
+        tag = (2, 3, 4, 6, 7)[i % 5]
+        x = bytes(rng.getrandbits(8) for _ in range(32))
+        y = bytes(rng.getrandbits(8) for _ in range(32))
+        key = bytes([tag]) + x + (y if tag >= 4 else b"")
+        L.th_key_hash160(tag, x, y, out)
+        L.th_hash160(key, len(key), ref)
+        assert out.raw == ref.raw[:20], (tag, i)

@@ -123,13 +123,20 @@ def test_c2_staged_mutated_matches_reference(wl):
         if i not in kinds:
             assert by_item.get(i) == [(by_item[i][0][0], 1)], i
     # mutated items: every GPU tuple is one of the reference's checks with the same verdict, and
-    # every check the reference accepted was deferred to the GPU
-    n_false = 0
+    # every check the reference accepted was deferred to the GPU.  The one exception is the
+    # device key-hash check (bcc_set_device_key_hash): a first run defers the signature check
+    # with HASH160(key) == program attached, so an item whose key no longer hashes to its program
+    # has a tuple the reference never reached (it stopped at OP_EQUALVERIFY, no checks): that
+    # tuple's verdict must be 0.
+    n_false = n_keyhash = 0
     for i in kinds:
         r, _, recs = R.capture_script(*items[i], B.VERIFY_ALL)
         gpu = by_item.get(i, [])
         ref_pairs = [(c["sighash"], c["verdict"]) for c in recs]
         for pair in gpu:
+            if pair not in ref_pairs and not recs and r == 0 and pair[1] == 0:
+                n_keyhash += 1
+                continue
             assert pair in ref_pairs, (i, kinds[i])
             n_false += pair[1] == 0
         for pair in ref_pairs:

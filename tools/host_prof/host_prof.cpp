@@ -19,6 +19,8 @@ int gpu_verify_batch(int, const SighashJobs&, const TupleRows& rows, uint8_t* ve
     return 0;
 }
 void set_stage_threads(unsigned) {}  // the device batch is stubbed out
+void release_device_thread_state() {}
+void release_tuple_thread_state() {}
 int gpu_verify_parts(int, const SighashJobs* const*, const TupleRows* const* rows, size_t parts,
                      uint8_t* verdict, double*) {
     size_t n = 0;
