@@ -175,11 +175,21 @@ std::atomic<unsigned> g_host_threads{0};  // bcc_set_host_threads (0: default)
 
 }  // namespace
 
+namespace {
+unsigned affinity_cpus() {
+    static const unsigned n = [] {
+        unsigned c = std::max(1u, std::thread::hardware_concurrency());
+        cpu_set_t set;
+        if (sched_getaffinity(0, sizeof(set), &set) == 0) c = std::max(1, CPU_COUNT(&set));
+        return c;
+    }();
+    return n;
+}
+}  // namespace
+
 unsigned cpu_share() {
     static const unsigned share = [] {
-        unsigned n = std::max(1u, std::thread::hardware_concurrency());
-        cpu_set_t set;
-        if (sched_getaffinity(0, sizeof(set), &set) == 0) n = std::max(1, CPU_COUNT(&set));
+        unsigned n = affinity_cpus();
         const double q = cgroup_quota_cpus();
         if (q > 0) n = std::min<unsigned>(n, std::max(1u, (unsigned)q));
         return n;
@@ -187,12 +197,20 @@ unsigned cpu_share() {
     return share;
 }
 
+// Default: the CPUs the process may run on, and under a CFS quota (cpu.max) three times the quota.
+// The quota bounds the AVERAGE over a period, and a verify_batch call alternates a parallel host
+// pass with a device wait on one thread, so a host pass on quota-many threads leaves half the
+// quota unused: in 20 back-to-back 1M-input C2 calls on the GPU box (quota 16 of 256 CPUs,
+// profiles/r03/threads) 16 threads kept 8 CPUs busy (12.8-14.5 M inputs/s), 48 threads 15.8 of 16
+// (20.1-21.3 M/s, a few throttled periods), 64 threads hit the quota hard (17.2-19.0 M/s).
 unsigned host_threads() {
     if (unsigned v = g_host_threads.load(std::memory_order_relaxed)) return v;
     static const unsigned dflt = [] {
         if (const char* e = getenv("BCC_HOST_THREADS"))
             if (atoi(e) > 0) return (unsigned)atoi(e);
-        return std::min(64u, cpu_share());
+        const unsigned aff = affinity_cpus(), share = cpu_share();
+        const unsigned n = share < aff ? std::min(aff, 3 * share) : aff;
+        return std::min(64u, n);
     }();
     return dflt;
 }

@@ -33,13 +33,13 @@ std::vector<size_t> split_balanced(const std::vector<size_t>& weights, size_t k)
 
 // The CPUs this process may actually keep busy: the smaller of its affinity mask and its cgroup
 // CPU bandwidth quota (cgroup v2 cpu.max, or v1 cfs_quota_us / cfs_period_us), rounded down, at
-// least 1.  A quota is a per-period budget: more runnable threads than the quota do not run
-// faster, they exhaust the budget early and the whole cgroup is throttled until the period ends.
+// least 1.  A quota is a per-period budget: a process that keeps more threads than the quota busy
+// for a whole period exhausts it early and is throttled until the period ends.
 unsigned cpu_share();
 
 // Host worker threads of one batch pass (verify_batch's interpreter shards, the tuple and Taproot
-// front ends, host-verified rounds): bcc_set_host_threads(), else BCC_HOST_THREADS, else
-// cpu_share() (capped at 64).
+// front ends, host-verified rounds): bcc_set_host_threads(), else BCC_HOST_THREADS, else the
+// affinity CPUs, or 3 x cpu_share() under a smaller quota (capped at 64; devices.cpp says why).
 unsigned host_threads();
 
 }  // namespace host

@@ -77,15 +77,17 @@ int num_getint(int64_t v) {
     return (int)v;
 }
 
-bool cast_to_bool(const Bytes& v) {
-    for (size_t i = 0; i < v.size(); i++) {
+bool cast_to_bool(const uint8_t* v, size_t n) {
+    for (size_t i = 0; i < n; i++) {
         if (v[i] != 0) {
-            if (i == v.size() - 1 && v[i] == 0x80) return false;  // negative zero
+            if (i == n - 1 && v[i] == 0x80) return false;  // negative zero
             return true;
         }
     }
     return false;
 }
+
+bool cast_to_bool(const Bytes& v) { return cast_to_bool(v.data(), v.size()); }
 
 bool fail(ScriptErr* e, ScriptErr code) {
     if (e) *e = code;
@@ -646,24 +648,24 @@ bool execute_witness_script(std::vector<Bytes> stack, const uint8_t* script, siz
     return true;
 }
 
-bool verify_witness_program(const std::vector<Span>& witness, int version, const Bytes& program,
+bool verify_witness_program(const std::vector<Span>& witness, int version, const Span& program,
                             unsigned flags, SigChecker& checker, ScriptErr* serror) {
     if (version == 0) {
-        if (program.size() == 32) {  // P2WSH
+        if (program.n == 32) {  // P2WSH
             if (witness.empty()) return fail(serror, SERR_WITNESS_PROGRAM_WITNESS_EMPTY);
             const Span& sc = witness.back();
             uint8_t h[32];
             sha256(sc.p, sc.n, h);
-            if (memcmp(h, program.data(), 32) != 0) return fail(serror, SERR_WITNESS_PROGRAM_MISMATCH);
+            if (memcmp(h, program.p, 32) != 0) return fail(serror, SERR_WITNESS_PROGRAM_MISMATCH);
             std::vector<Bytes> stack;
             stack.reserve(witness.size() + 4);  // no regrowth in the common scripts
             for (size_t k = 0; k + 1 < witness.size(); k++)
                 stack.emplace_back(witness[k].p, witness[k].p + witness[k].n);
             return execute_witness_script(std::move(stack), sc.p, sc.n, flags, checker, serror);
-        } else if (program.size() == 20) {  // P2WPKH: DUP HASH160 <20> EQUALVERIFY CHECKSIG
+        } else if (program.n == 20) {  // P2WPKH: DUP HASH160 <20> EQUALVERIFY CHECKSIG
             if (witness.size() != 2) return fail(serror, SERR_WITNESS_PROGRAM_MISMATCH);
             uint8_t sc[25] = {OP_DUP, OP_HASH160, 0x14};
-            memcpy(sc + 3, program.data(), 20);
+            memcpy(sc + 3, program.p, 20);
             sc[23] = OP_EQUALVERIFY;
             sc[24] = OP_CHECKSIG;
             // execute_witness_script on [sig, key] with this script, unrolled: the same checks in
@@ -677,14 +679,14 @@ bool verify_witness_program(const std::vector<Span>& witness, int version, const
             const bool der_bad = !sig.empty() && (flags & FLAG_DERSIG) && !is_valid_signature_encoding(sig);
             // OP_DUP, OP_HASH160, <20> OP_EQUALVERIFY: taken over by the checker when the run goes
             // on to the signature check, else compared here
-            const bool taken = !der_bad && checker.defer_key_hash(wk.p, wk.n, program.data());
-            if (!taken && !key_hash_equal(checker, wk.p, wk.n, program.data()))
+            const bool taken = !der_bad && checker.defer_key_hash(wk.p, wk.n, program.p);
+            if (!taken && !key_hash_equal(checker, wk.p, wk.n, program.p))
                 return fail(serror, SERR_EQUALVERIFY);
             // OP_CHECKSIG (witness v0: no FindAndDelete; scriptCode = the whole script)
             if (der_bad) return fail(serror, SERR_SIG_DER);
             const Bytes pub(wk.p, wk.p + wk.n), code(sc, sc + 25);
             const bool ok = checker.check_ecdsa(sig, pub, code, SIGVERSION_WITNESS_V0);
-            if (taken && !checker.key_hash_taken() && !key_hash_equal(checker, wk.p, wk.n, program.data()))
+            if (taken && !checker.key_hash_taken() && !key_hash_equal(checker, wk.p, wk.n, program.p))
                 return fail(serror, SERR_EQUALVERIFY);
             // the stack is [result]: clean; false -> EVAL_FALSE
             if (!ok) return fail(serror, SERR_EVAL_FALSE);
@@ -779,6 +781,17 @@ bool tx_check_sequence(const Tx& tx, unsigned nin, int64_t sq) {
 bool verify_script(const Span& script_sig, const Span& spk, const std::vector<Span>& witness,
                    unsigned flags, SigChecker& checker, ScriptErr* serror) {
     if (serror) *serror = SERR_UNKNOWN;
+    // Native P2WPKH with an empty scriptSig: the general path below evaluates nothing, then pushes
+    // OP_0 and the 20-byte program (no error is possible), tests the program with CastToBool,
+    // finds a v0 program and runs it; P2SH does not apply.  The same steps without the stacks.
+    if ((flags & FLAG_WITNESS) && script_sig.n == 0 && spk.n == 22 && spk.p[0] == 0 &&
+        spk.p[1] == 0x14) {
+        const Span prog{spk.p + 2, 20};
+        if (!cast_to_bool(prog.p, prog.n)) return fail(serror, SERR_EVAL_FALSE);
+        if (!verify_witness_program(witness, 0, prog, flags, checker, serror)) return false;
+        if (serror) *serror = SERR_OK;
+        return true;
+    }
     bool had_witness = false;
     std::vector<Bytes> stack, stack_copy;
     stack.reserve(8);
@@ -796,7 +809,8 @@ bool verify_script(const Span& script_sig, const Span& spk, const std::vector<Sp
     if ((flags & FLAG_WITNESS) && is_witness_program(spk.p, spk.n, wv, wp)) {
         had_witness = true;
         if (script_sig.n != 0) return fail(serror, SERR_WITNESS_MALLEATED);
-        if (!verify_witness_program(witness, wv, wp, flags, checker, serror)) return false;
+        if (!verify_witness_program(witness, wv, Span{wp.data(), wp.size()}, flags, checker, serror))
+            return false;
         stack.resize(1);
     }
 
@@ -814,7 +828,8 @@ bool verify_script(const Span& script_sig, const Span& spk, const std::vector<Sp
             push_data(expect, redeem.data(), redeem.size());
             if (script_sig.n != expect.size() || memcmp(script_sig.p, expect.data(), expect.size()) != 0)
                 return fail(serror, SERR_WITNESS_MALLEATED_P2SH);
-            if (!verify_witness_program(witness, wv, wp, flags, checker, serror)) return false;
+            if (!verify_witness_program(witness, wv, Span{wp.data(), wp.size()}, flags, checker, serror))
+                return false;
             stack.resize(1);
         }
     }

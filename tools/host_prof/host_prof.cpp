@@ -87,10 +87,10 @@ int main(int argc, char** argv) {
         bcc_batch_stats st;
         bcc_last_batch_stats(&st);
         printf("n %zu valid %ld  %.1f ms  %.2f M items/s | prepare %.1f interpret %.1f merge %.1f "
-               "stage %.1f gpu %.1f host %.1f total %.1f ms\n", n, v, 1e3 * s, n / s / 1e6,
+               "stage %.1f gpu %.1f host %.1f total %.1f ms | key hashes on the device %zu\n", n, v, 1e3 * s, n / s / 1e6,
                1e3 * st.prepare_seconds, 1e3 * st.interpret_seconds, 1e3 * st.merge_seconds,
                1e3 * st.stage_seconds, 1e3 * st.gpu_seconds, 1e3 * st.host_seconds,
-               1e3 * st.total_seconds);
+               1e3 * st.total_seconds, st.device_key_hashes);
     }
     return 0;
 }
