@@ -162,24 +162,26 @@ struct Pending {
 uint32_t append_key(std::vector<uint8_t>& a, const Bytes& pub, const Bytes& sig, const Bytes& code,
                     SigVersion sv) {
     const size_t k0 = a.size();
-    auto put = [&](const uint8_t* p, size_t len) {
-        uint32_t n = (uint32_t)len;
-        a.insert(a.end(), (const uint8_t*)&n, (const uint8_t*)&n + 4);
-        a.insert(a.end(), p, p + len);
+    uint8_t d[32];
+    const bool hashed = code.size() > 64;
+    if (hashed) sha256(code.data(), code.size(), d);
+    const uint8_t* cp = hashed ? d : code.data();
+    const size_t cn = hashed ? 32 : code.size();
+    const size_t len = 1 + 4 + pub.size() + 4 + sig.size() + 1 + 4 + cn;
+    a.resize(k0 + len);  // one growth check, then plain stores
+    uint8_t* o = &a[k0];
+    auto put = [&](const uint8_t* p, size_t n) {
+        const uint32_t n32 = (uint32_t)n;
+        memcpy(o, &n32, 4);
+        if (n) memcpy(o + 4, p, n);
+        o += 4 + n;
     };
-    a.push_back((uint8_t)sv);
+    *o++ = (uint8_t)sv;
     put(pub.data(), pub.size());
     put(sig.data(), sig.size());
-    if (code.size() > 64) {
-        uint8_t d[32];
-        sha256(code.data(), code.size(), d);
-        a.push_back(1);
-        put(d, 32);
-    } else {
-        a.push_back(0);
-        put(code.data(), code.size());
-    }
-    return (uint32_t)(a.size() - k0);
+    *o++ = hashed ? 1 : 0;
+    put(cp, cn);
+    return (uint32_t)len;
 }
 
 // The sighash job of one deferred check: what GenericTransactionSignatureChecker would hash
@@ -297,14 +299,11 @@ void add_sighash_job(SighashJobs& jobs, TxEntry& te, const bcc_batch_item& in, c
             }
             touched.push_back(&te);
         }
-        scratch.clear();
-        put_compact_size(scratch, code.size());
-        scratch.insert(scratch.end(), code.begin(), code.end());
         WinJob wj{};
         wj.tx = (uint32_t)te.wtx;
         wj.nin = nin;
-        wj.code_off = jobs.add_code(scratch.data(), scratch.size());
-        wj.code_len = (uint32_t)scratch.size();
+        wj.code_off = jobs.add_code_field(code.data(), code.size());  // compactsize || code
+        wj.code_len = (uint32_t)(code.size() + (code.size() < 253 ? 1 : code.size() <= 0xFFFF ? 3 : 5));
         wj.hashtype = (uint32_t)hashtype;
         wj.row = row;
         wj.amount_lo = (uint32_t)(uint64_t)in.amount;
@@ -410,12 +409,11 @@ public:
         bool reject = !pubkey_size_valid(pub.data(), pub.size()) || sig.empty() ||
                       !der_parse_lax(sig.data(), sig.size() - 1, r, s);
         if (!reject) {
-            bool rz = true, sz = true;
-            for (int i = 0; i < 32; i++) {
-                rz &= r[i] == 0;
-                sz &= s[i] == 0;
-            }
-            reject = rz || sz;  // secp256k1_ecdsa_sig_verify rejects r == 0 || s == 0
+            uint64_t rw[4], sw[4];
+            memcpy(rw, r, 32);
+            memcpy(sw, s, 32);
+            // secp256k1_ecdsa_sig_verify rejects r == 0 || s == 0
+            reject = (rw[0] | rw[1] | rw[2] | rw[3]) == 0 || (sw[0] | sw[1] | sw[2] | sw[3]) == 0;
         }
         if (reject) {
             it.cache.push_back(Item::Check{koff, klen, 0});
@@ -425,17 +423,19 @@ public:
         const int hashtype = sig.back();
         uint8_t one[32] = {0};
         one[0] = 1;  // uint256::ONE as raw bytes: the SIGHASH_SINGLE-bug message
-        uint8_t ybuf[32] = {0};
-        const uint8_t* y = pub.size() == 65 ? pub.data() + 33 : ybuf;  // y unused for 02/03
-        uint32_t row = rows.add(pub[0], pub.data() + 1, y, r, s, one);
-        if (pub.size() == 65) rows.y_unused = false;
+        // y only for a 65-byte key, msg only when the host may write it (long chains on the host):
+        // the device initialises every msg row to ONE itself (TupleRows::add_lazy)
+        const bool key65 = pub.size() == 65;
+        const uint32_t row = rows.add_lazy(pub[0], pub.data() + 1, r, s, key65 ? pub.data() + 33 : nullptr,
+                                           host.chain_blocks ? one : nullptr);
+        if (key65) rows.y_unused = false;
         if (key_prog) {
             rows.add_key_hash(row, key_prog);
             *key_taken = true;
             key_hashes++;
         }
         add_sighash_job(jobs, *it.tx, *it.in, code, sv, hashtype, row, scratch, bip143, touched,
-                        &host, &rows.msg[32 * (size_t)row]);
+                        &host, host.chain_blocks ? &rows.msg[32 * (size_t)row] : nullptr);
         it.cache.push_back(Item::Check{koff, klen, -2 - (int32_t)pending.size()});
         if (consult) it.pending.push_back((uint32_t)pending.size());
         pending.push_back(Pending{item_idx, (uint32_t)(it.cache.size() - 1)});
@@ -468,7 +468,10 @@ void run_host_jobs(std::vector<Round>& rds, unsigned T) {
     std::vector<std::pair<uint32_t, uint32_t>> work;  // (shard, job): tjobs first, then pre
     for (unsigned t = 0; t < T; t++) {
         HostJobs& h = rds[t].host;
-        if (h.pending() || h.inline_rows) rds[t].rows.msg_one = false;
+        if (h.pending() || h.inline_rows) {
+            rds[t].rows.msg_one = false;
+            rds[t].rows.pad_msg(rds[t].rows.size());
+        }
         for (uint32_t k = 0; k < h.pending(); k++) work.emplace_back(t, k);
     }
     if (work.empty()) return;
@@ -1125,6 +1128,7 @@ size_t build_first_round(const bcc_batch_item* items, size_t n, unsigned flags, 
     }
     jobs = std::move(rd.jobs);
     rows = std::move(rd.rows);
+    rows.materialize();  // full y / msg rows for the bench and test consumers
     return rows.size();
 }
 

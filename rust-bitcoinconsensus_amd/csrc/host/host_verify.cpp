@@ -179,10 +179,14 @@ int host_verify_parts(const SighashJobs* const* jobs, const TupleRows* const* ro
     std::vector<uint8_t> msg;
     for (size_t p = 0; p < P; p++) {
         const TupleRows& R = *rows[p];
-        msg.assign(R.msg.begin(), R.msg.end());
-        if (R.msg_one || msg.size() != 32 * R.size()) {  // the device initialises these rows: ONE
-            msg.assign(32 * R.size(), 0);
-            for (size_t i = 0; i < R.size(); i++) msg[32 * i] = 1;
+        msg.resize(32 * R.size());
+        if (R.msg_one) {  // the device initialises these rows: ONE
+            for (size_t i = 0; i < R.size(); i++) {
+                memset(&msg[32 * i], 0, 32);
+                msg[32 * i] = 1;
+            }
+        } else {
+            R.copy_msg(msg.data());  // rows past the stored prefix: ONE
         }
         host_sighash(*jobs[p], msg.data());
         host_verify_rows(R, msg.data(), verdict + r0, threads);

@@ -8,6 +8,7 @@
 #pragma once
 #include <cstddef>
 #include <cstdint>
+#include <algorithm>
 #include <cstring>
 #include <vector>
 
@@ -121,6 +122,21 @@ struct SighashJobs {
         tpl.resize(off + ((n + 3) & ~(size_t)3) + 8, 0);
         return off;
     }
+    // compactsize(n) || m, 4-aligned: a scriptCode field (BIP143 / legacy serialization)
+    uint32_t add_code_field(const uint8_t* m, size_t n) {
+        const uint32_t off = (uint32_t)code.size();
+        const size_t h = n < 253 ? 1 : n <= 0xFFFF ? 3 : 5;
+        code.resize(off + ((h + n + 3) & ~(size_t)3), 0);
+        uint8_t* o = &code[off];
+        if (h == 1) {
+            o[0] = (uint8_t)n;
+        } else {
+            o[0] = h == 3 ? 253 : 254;
+            for (size_t i = 0; i + 1 < h; i++) o[1 + i] = (uint8_t)(n >> (8 * i));
+        }
+        if (n) memcpy(o + h, m, n);
+        return off;
+    }
     uint32_t add_code(const uint8_t* m, size_t n) {
         uint32_t off = (uint32_t)code.size();
         code.insert(code.end(), m, m + n);
@@ -166,6 +182,49 @@ struct TupleRows {
     std::vector<uint32_t> hrow;
     std::vector<uint8_t> hprog;
     size_t size() const { return tag.size(); }
+    // A row that stores its y / msg only when given: y32 == nullptr reads as zero (a 33-byte key),
+    // m32 == nullptr as uint256 ONE.  y and msg may then hold only a prefix of the rows; readers
+    // go through copy_y / copy_msg (or materialize() first).
+    uint32_t add_lazy(uint8_t t, const uint8_t* x32, const uint8_t* r32, const uint8_t* s32,
+                      const uint8_t* y32, const uint8_t* m32) {
+        const size_t row = tag.size();
+        tag.push_back(t);
+        x.insert(x.end(), x32, x32 + 32);
+        r.insert(r.end(), r32, r32 + 32);
+        s.insert(s.end(), s32, s32 + 32);
+        if (y32) {
+            y.resize(32 * row, 0);
+            y.insert(y.end(), y32, y32 + 32);
+        }
+        if (m32) {
+            pad_msg(row);
+            msg.insert(msg.end(), m32, m32 + 32);
+        }
+        return (uint32_t)row;
+    }
+    void pad_msg(size_t rows) {  // msg rows [msg.size() / 32, rows) = ONE
+        size_t k = msg.size() / 32;
+        if (k >= rows) return;
+        msg.resize(32 * rows, 0);
+        for (; k < rows; k++) msg[32 * k] = 1;
+    }
+    void materialize() {
+        y.resize(32 * size(), 0);
+        pad_msg(size());
+    }
+    void copy_y(uint8_t* out) const {  // 32 * size() bytes
+        const size_t n = std::min(y.size(), 32 * size());
+        if (n) memcpy(out, y.data(), n);
+        memset(out + n, 0, 32 * size() - n);
+    }
+    void copy_msg(uint8_t* out) const {  // 32 * size() bytes
+        const size_t n = std::min(msg.size(), 32 * size());
+        if (n) memcpy(out, msg.data(), n);
+        for (size_t k = n / 32; k < size(); k++) {
+            memset(out + 32 * k, 0, 32);
+            out[32 * k] = 1;
+        }
+    }
     void add_key_hash(uint32_t row, const uint8_t* prog20) {
         hrow.push_back(row);
         hprog.insert(hprog.end(), prog20, prog20 + 20);

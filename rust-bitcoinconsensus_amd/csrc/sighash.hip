@@ -986,10 +986,10 @@ int DeviceBatch::stage_parts(const SighashJobs* const* J, const TupleRows* const
         };
         cp(TAG, r0, rw.tag.data(), nr);
         cp(X, 32 * r0, rw.x.data(), 32 * nr);
-        if (need_y) cp(Y, 32 * r0, rw.y.data(), 32 * nr);
+        if (need_y && nr) rw.copy_y(h + off[Y] + 32 * r0);  // rows past the stored prefix: zero
         cp(RR, 32 * r0, rw.r.data(), 32 * nr);
         cp(S, 32 * r0, rw.s.data(), 32 * nr);
-        if (need_m) cp(M, 32 * r0, rw.msg.data(), 32 * nr);
+        if (need_m && nr) rw.copy_msg(h + off[M] + 32 * r0);  // rows past the stored prefix: ONE
         cp(AUX, auxb0[p], j.aux.data(), j.aux.size());
         cp(PRE, preb0[p], j.pre.data(), j.pre.size());
         const uint32_t ablk = (uint32_t)(auxb0[p] / 64), pblk = (uint32_t)(preb0[p] / 64);

@@ -68,7 +68,9 @@ static void stub_sighash(const SighashJobs& j, std::vector<uint8_t>& msg) {
     }
 }
 
-int gpu_verify_batch(int, const SighashJobs& j, const TupleRows& rows, uint8_t* verdict, double*) {
+int gpu_verify_batch(int, const SighashJobs& j, const TupleRows& rows_in, uint8_t* verdict, double*) {
+    TupleRows rows = rows_in;
+    rows.materialize();  // rows stored without y / msg (TupleRows::add_lazy): zero / ONE
     std::vector<uint8_t> msg = rows.msg;
     stub_sighash(j, msg);
     for (size_t i = 0; i < rows.size(); i++) {

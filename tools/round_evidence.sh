@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round evidence on the current build (run via gpurun): C2 rocprof trace + SQ / FETCH / WRITE
 # passes, then the default bench line (with the CPU baseline) and the C3 / C4 / C5 / C5T lines,
-# then the drop-in end to end with cgroup accounting.
+# then the drop-in end to end with cgroup accounting, best of 3 and 20 calls back to back.
 # usage: tools/round_evidence.sh TAG
 export TMPDIR=/tmp
 T=${1:-r02x}
@@ -25,3 +25,5 @@ for f in ("c2", "c3", "c4", "c5", "c5t"):
 PY
 timeout -k 10 200 python -u tools/e2e_cgroup.py 1000000 0:0 > $O/e2e.txt 2>&1 || { tail -5 $O/e2e.txt; exit 4; }
 grep best_ms $O/e2e.txt
+timeout -k 10 200 python -u tools/e2e_sustained.py 1000000 20 0 > $O/e2e_sustained.txt 2>&1 || { tail -5 $O/e2e_sustained.txt; exit 5; }
+cat $O/e2e_sustained.txt
