@@ -210,8 +210,8 @@ def c1_vector():
 
 def single_call_latency(B, calls=200):
     """Latency of ONE bitcoinconsensus_verify_script_with_amount call on C1 (what an unchanged Rust
-    caller of verify() sees, lib.rs:103-139): its round on the GPU (default), and with
-    bcc_set_host_small_round routing rounds of <= 64 checks to the engine's host code."""
+    caller of verify() sees, lib.rs:103-139): its round on the GPU (bcc_set_host_small_round(0)),
+    and the default, which verifies rounds of <= 16 checks with the engine's host code."""
     import statistics
     spk, amount, tx, nin, flags = c1_vector()
 
@@ -223,14 +223,14 @@ def single_call_latency(B, calls=200):
             ts.append(time.perf_counter() - t0)
             assert r == (1, 0)
         return statistics.median(ts) * 1e6
-    B.verify_script_with_amount(spk, amount, tx, nin, flags)  # warm
-    gpu_us = lat()
-    B.set_host_small_round(64)
+    B.set_host_small_round(0)  # every round on the GPU
     try:
-        B.verify_script_with_amount(spk, amount, tx, nin, flags)
-        host_us = lat()
+        B.verify_script_with_amount(spk, amount, tx, nin, flags)  # warm
+        gpu_us = lat()
     finally:
-        B.set_host_small_round(0)
+        B.set_host_small_round(B.HOST_SMALL_ROUND_DEFAULT)  # the default: small rounds on the host
+    B.verify_script_with_amount(spk, amount, tx, nin, flags)
+    host_us = lat()
     return dict(config="C1: README P2PKH tx, input 0", calls=calls, gpu_round_us=gpu_us,
                 host_small_round_us=host_us,
                 note="median per-call latency; the reference's own per-call latency is in "

@@ -428,6 +428,9 @@ def set_device_failure_policy(policy):
         raise ValueError(policy)
 
 
+HOST_SMALL_ROUND_DEFAULT = 16  # include/bcc_amd.h BCC_HOST_SMALL_ROUND_DEFAULT
+
+
 def set_host_small_round(tuples):
     """bcc_set_host_small_round: device rounds of at most `tuples` checks run on the host CPU."""
     lib().bcc_set_host_small_round(tuples)

@@ -199,7 +199,7 @@ int host_verify_parts(const SighashJobs* const* jobs, const TupleRows* const* ro
 namespace {
 std::atomic<size_t> g_small_round{[] {
     const char* e = getenv("BCC_HOST_SMALL_ROUND");
-    return e ? (size_t)atoll(e) : (size_t)0;
+    return e ? (size_t)atoll(e) : (size_t)BCC_HOST_SMALL_ROUND_DEFAULT;
 }()};
 std::atomic<int> g_failure_policy{[] {
     const char* e = getenv("BCC_DEVICE_FAILURE");

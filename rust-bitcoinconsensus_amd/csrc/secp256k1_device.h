@@ -17,6 +17,7 @@
 //  GLV split              scalar_impl.h:342-375 (constants re-derived: tools/derive_glv_constants.py)
 #pragma once
 #include <stdint.h>
+#include <string.h>
 
 #if defined(__HIPCC__)
 #include <hip/hip_runtime.h>
@@ -194,7 +195,65 @@ BCC_HD void fe_reduce512(fe& r, const u32 (&t)[16]) {
 #define BCC_RED_V3 1
 #endif
 
+#if !defined(__HIP_DEVICE_COMPILE__) && defined(__SIZEOF_INT128__)
+// Host builds (the engine's host verification, host_verify.cpp, and tests/native): 4 x 64-bit limbs
+// with 128-bit products, the CPU's native width, over the same little-endian bytes as fe.v.
+// Same contract as the 32-bit formulation: a weak residue (< 2^256) of a * b mod p.
+#define BCC_FE_HOST64 1
+inline void mul_4x64(u64 (&t)[8], const u32 (&a)[8], const u32 (&b)[8]) {
+    typedef unsigned __int128 u128;
+    u64 x[4], y[4];
+    memcpy(x, a, 32);
+    memcpy(y, b, 32);
+    for (int i = 0; i < 8; i++) t[i] = 0;
+    for (int i = 0; i < 4; i++) {
+        u64 c = 0;
+        for (int j = 0; j < 4; j++) {
+            const u128 p = (u128)x[i] * y[j] + t[i + j] + c;
+            t[i + j] = (u64)p;
+            c = (u64)(p >> 64);
+        }
+        t[i + 4] = c;
+    }
+}
+inline void fe_mul_host64(fe& r, const fe& a, const fe& b) {
+    typedef unsigned __int128 u128;
+    u64 t[8];
+    mul_4x64(t, a.v, b.v);
+    // 2^256 == 0x1000003D1 (mod p): r = t_lo + t_hi * 0x1000003D1, folded twice
+    const u64 C = 0x1000003D1ull;
+    u64 o[4], c = 0;
+    for (int i = 0; i < 4; i++) {
+        const u128 p = (u128)t[4 + i] * C + t[i] + c;
+        o[i] = (u64)p;
+        c = (u64)(p >> 64);
+    }
+    u128 p = (u128)c * C + o[0];  // c < 2^34
+    o[0] = (u64)p;
+    u64 k = (u64)(p >> 64);
+    for (int i = 1; i < 4 && k; i++) {
+        const u128 q = (u128)o[i] + k;
+        o[i] = (u64)q;
+        k = (u64)(q >> 64);
+    }
+    if (k) {  // wrapped past 2^256 once more (the value is then tiny): add C again, no carry out
+        p = (u128)o[0] + C;
+        o[0] = (u64)p;
+        k = (u64)(p >> 64);
+        for (int i = 1; i < 4 && k; i++) {
+            const u128 q = (u128)o[i] + k;
+            o[i] = (u64)q;
+            k = (u64)(q >> 64);
+        }
+    }
+    memcpy(r.v, o, 32);
+}
+#endif
+
 BCC_HD void fe_mul(fe& r, const fe& a, const fe& b) {
+#if defined(BCC_FE_HOST64)
+    fe_mul_host64(r, a, b);
+#else
     u32 t[16];
 #if defined(__HIP_DEVICE_COMPILE__)
     mul_256x256_col(t, a.v, b.v);
@@ -209,9 +268,13 @@ BCC_HD void fe_mul(fe& r, const fe& a, const fe& b) {
     mul_256x256(t, a.v, b.v);
     fe_reduce512(r, t);
 #endif
+#endif
 }
 
 BCC_HD void fe_sqr(fe& r, const fe& a) {
+#if defined(BCC_FE_HOST64)
+    fe_mul_host64(r, a, a);
+#else
     u32 t[16];
 #if defined(__HIP_DEVICE_COMPILE__)
     sqr_256_col(t, a.v);
@@ -225,6 +288,7 @@ BCC_HD void fe_sqr(fe& r, const fe& a) {
 #else
     sqr_256(t, a.v);
     fe_reduce512(r, t);
+#endif
 #endif
 }
 
@@ -620,7 +684,60 @@ BCC_HD void sc_reduce512(sc& r, const u32 (&t)[16]) {
     sc_cond_sub_n(r, 0);
 }
 
+#if defined(BCC_FE_HOST64)
+// Host builds: the same three folds by 2^256 == NC over 64-bit words (NC = 2^256 - n, 129 bits).
+inline void sc_reduce512_host64(sc& r, const u64 (&t)[8]) {
+    typedef unsigned __int128 u128;
+    const u64 NC[3] = {0x402DA1732FC9BEBFull, 0x4551231950B75FC4ull, 1ull};
+    u64 m[7] = {t[0], t[1], t[2], t[3], 0, 0, 0};  // m = t_lo + t_hi NC < 2^386
+    for (int i = 0; i < 4; i++) {
+        u64 c = 0;
+        for (int j = 0; j < 3; j++) {
+            const u128 p = (u128)t[4 + i] * NC[j] + m[i + j] + c;
+            m[i + j] = (u64)p;
+            c = (u64)(p >> 64);
+        }
+        for (int k = i + 3; k < 7; k++) {
+            const u128 p = (u128)m[k] + c;
+            m[k] = (u64)p;
+            c = (u64)(p >> 64);
+        }
+    }
+    u64 q[5] = {m[0], m[1], m[2], m[3], 0};  // q = m_lo + m_hi NC < 2^260 (m_hi < 2^130)
+    for (int i = 0; i < 3; i++) {
+        u64 c = 0;
+        for (int j = 0; j < 3 && i + j < 5; j++) {
+            const u128 p = (u128)m[4 + i] * NC[j] + q[i + j] + c;
+            q[i + j] = (u64)p;
+            c = (u64)(p >> 64);
+        }
+        for (int k = i + 3; k < 5; k++) {
+            const u128 p = (u128)q[k] + c;
+            q[k] = (u64)p;
+            c = (u64)(p >> 64);
+        }
+    }
+    u64 w[4] = {q[0], q[1], q[2], q[3]};  // w = q_lo + q[4] NC < 2^256 + 2^133
+    u64 c = 0;
+    for (int j = 0; j < 3; j++) {
+        const u128 p = (u128)q[4] * NC[j] + w[j] + c;
+        w[j] = (u64)p;
+        c = (u64)(p >> 64);
+    }
+    const u128 p = (u128)w[3] + c;
+    w[3] = (u64)p;
+    memcpy(r.v, w, 32);
+    sc_cond_sub_n(r, (u32)(p >> 64));
+    sc_cond_sub_n(r, 0);
+}
+#endif
+
 BCC_HD void sc_mul(sc& r, const sc& a, const sc& b) {
+#if defined(BCC_FE_HOST64)
+    u64 t[8];
+    mul_4x64(t, a.v, b.v);
+    sc_reduce512_host64(r, t);
+#else
     u32 t[16];
 #if defined(__HIP_DEVICE_COMPILE__)
     mul_256x256_col(t, a.v, b.v);
@@ -628,9 +745,13 @@ BCC_HD void sc_mul(sc& r, const sc& a, const sc& b) {
     mul_256x256(t, a.v, b.v);
 #endif
     sc_reduce512(r, t);
+#endif
 }
 
 BCC_HD void sc_sqr(sc& r, const sc& a) {
+#if defined(BCC_FE_HOST64)
+    sc_mul(r, a, a);
+#else
     u32 t[16];
 #if defined(__HIP_DEVICE_COMPILE__)
     sqr_256_col(t, a.v);
@@ -638,6 +759,7 @@ BCC_HD void sc_sqr(sc& r, const sc& a) {
     sqr_256(t, a.v);
 #endif
     sc_reduce512(r, t);
+#endif
 }
 
 BCC_HD void sc_add(sc& r, const sc& a, const sc& b) {

@@ -68,3 +68,27 @@ def test_small_rounds_on_host_match_reference():
             assert st["host_rounds"] == st["rounds"]
     finally:
         B.set_host_small_round(0)
+
+
+def test_default_small_round_threshold():
+    """The library default (BCC_HOST_SMALL_ROUND_DEFAULT = 16 checks; the suite itself runs with
+    0): a lone verify() is verified on the host, a batch of more checks goes to the GPU, both with
+    the reference's results."""
+    import bitcoinconsensus_amd as B
+    vs = load_json("crate_vectors.json")
+    B.set_host_small_round(B.HOST_SMALL_ROUND_DEFAULT)
+    try:
+        for v in vs:
+            item = (bytes.fromhex(v["spk"]), v["amount"], bytes.fromhex(v["tx"]), v["nin"])
+            rc, got = B.verify_batch_raw([item], v["flags"])
+            st = B.last_batch_stats()
+            assert [tuple(g) for g in got] == [(v["ret"], v["err"])], v["name"]
+            assert st["host_rounds"] == st["rounds"]  # <= 16 checks: the host
+        v = next(x for x in vs if x["name"] == "p2pkh")
+        item = (bytes.fromhex(v["spk"]), v["amount"], bytes.fromhex(v["tx"]), v["nin"])
+        rc, got = B.verify_batch_raw([item] * 64, v["flags"])
+        st = B.last_batch_stats()
+        assert [tuple(g) for g in got] == [(v["ret"], v["err"])] * 64
+        assert st["rounds"] >= 1 and st["host_rounds"] == 0  # 64 checks: the GPU
+    finally:
+        B.set_host_small_round(0)
