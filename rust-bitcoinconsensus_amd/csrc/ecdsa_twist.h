@@ -25,12 +25,16 @@
 #pragma once
 #include <stddef.h>
 
+#include <algorithm>
+#include <thread>
+#include <vector>
+
 #include "ecdsa_lane.h"
 
 namespace bcc {
 
 #ifndef BCC_COMB_BITS
-#define BCC_COMB_BITS 13  // 20 windows x 4096 points = 5 MiB of tables (MALL-resident)
+#define BCC_COMB_BITS 16  // 16 windows x 32768 points = 32 MiB of tables (MALL-resident); 15 additions
 #endif
 #ifndef BCC_QTAB_COZ
 #define BCC_QTAB_COZ 1  // the Q_w table by co-Z additions (build_q_table_coz)
@@ -646,25 +650,13 @@ BCC_HD int schnorr_verify_twist_lane(const fe& px, const fe& rx, const sc& s, co
 }
 
 // Host build of the comb tables: per window the odd multiples of 2^(WC win) G in Jacobian
-// coordinates, then one batched normalisation (Montgomery's trick) per window.
-inline void build_g_comb(fe* xy) {
-    fe gx, gy;
+// coordinates, then one batched normalisation (Montgomery's trick) per window.  The window bases
+// come from one doubling chain; the windows themselves are independent and built on up to CWIN
+// threads (std::thread; the 16-bit comb is 0.5 M points).
+inline void build_g_comb_window(fe* xy, int win, const gej& base) {
+    std::vector<gej> pts(CTAB);
+    std::vector<fe> pre(CTAB);
     {
-        const u32 X[8] = BCC_GX_LIMBS, Y[8] = BCC_GY_LIMBS;
-        fe_set(gx, X);
-        fe_set(gy, Y);
-    }
-    gej base;
-    base.x = gx; base.y = gy; base.z = fe_one();
-    gej* pts = new gej[CTAB];
-    fe* pre = new fe[CTAB];
-    for (int win = 0; win < CWIN; win++) {
-        if (win > 0)
-            for (int i = 0; i < WC; i++) {
-                gej t;
-                gej_double(t, base);
-                base = t;
-            }
         gej b2;
         gej_double(b2, base);
         pts[0] = base;
@@ -692,10 +684,35 @@ inline void build_g_comb(fe* xy) {
             xy[((size_t)win * CTAB + i) * 2 + 0] = x;
             xy[((size_t)win * CTAB + i) * 2 + 1] = y;
         }
-        // base for the next window stays Jacobian (pts[0] == base)
     }
-    delete[] pts;
-    delete[] pre;
+}
+
+inline void build_g_comb(fe* xy) {
+    std::vector<gej> bases(CWIN);
+    {
+        const u32 X[8] = BCC_GX_LIMBS, Y[8] = BCC_GY_LIMBS;
+        fe_set(bases[0].x, X);
+        fe_set(bases[0].y, Y);
+        bases[0].z = fe_one();
+    }
+    for (int win = 1; win < CWIN; win++) {  // 2^(WC win) G, Jacobian
+        gej b = bases[win - 1];
+        for (int i = 0; i < WC; i++) {
+            gej t;
+            gej_double(t, b);
+            b = t;
+        }
+        bases[win] = b;
+    }
+    const unsigned hw = std::thread::hardware_concurrency();
+    const int nth = std::max(1, std::min<int>(CWIN, hw ? (int)hw : 1));
+    std::vector<std::thread> th;
+    for (int k = 1; k < nth; k++)
+        th.emplace_back([&, k] {
+            for (int win = k; win < CWIN; win += nth) build_g_comb_window(xy, win, bases[win]);
+        });
+    for (int win = 0; win < CWIN; win += nth) build_g_comb_window(xy, win, bases[win]);
+    for (auto& t : th) t.join();
 }
 
 }  // namespace bcc
