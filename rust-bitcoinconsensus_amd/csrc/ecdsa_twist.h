@@ -460,6 +460,96 @@ BCC_HD int ecdsa_verify_twist_lane(u32 tag, const fe& px, const fe& py, const sc
     return twist_final(al, K, binv, st.v, st.ychk, st.flags, st.r);
 }
 
+#if !defined(__HIP_DEVICE_COMPILE__)
+// Host-only form of B = u2 Q_w for one lane (the engine's host verification path): a lone CPU
+// thread pays for every addition, so the GLV halves are recoded as width-5 wNAF (digits odd in
+// [-15, 15] or 0: the same 8-entry table, ≈43 additions instead of the SIMT path's 63 + 2 fixed-
+// window ones, and no odd-fix corrections), the variable-time recoding the reference uses on the
+// CPU too (ecmult_impl.h:155-199, 531-558).  `k` are the raw halves (|k| < 2^128, their signs in
+// LS_NEG0 / LS_NEG1).  Same result as twist_accumulate_q; returns inf.
+inline int wnaf5_128(int8_t (&d)[132], const u32 (&k)[4]) {
+    typedef unsigned __int128 u128;
+    u128 lo = (u128)((uint64_t)k[2] | (uint64_t)k[3] << 32) << 64 | ((uint64_t)k[0] | (uint64_t)k[1] << 32);
+    uint64_t hi = 0;  // bits from 128 up (the value stays below 2^128 + 16)
+    int n = 0;
+    while (lo | hi) {
+        int v = 0;
+        if (lo & 1) {
+            v = (int)(lo & 31);
+            if (v >= 16) v -= 32;
+            if (v > 0) {
+                lo -= (u128)v;  // the low 5 bits are v: no borrow
+            } else {
+                const u128 o = lo;
+                lo += (u128)(-v);
+                if (lo < o) hi++;
+            }
+        }
+        d[n++] = (int8_t)v;  // at most 130 digits
+        lo = lo >> 1 | (u128)(hi & 1) << 127;
+        hi >>= 1;
+    }
+    return n;
+}
+
+template <class ST, class QT>
+inline bool twist_accumulate_q_wnaf(const ST& st, const u32 (&k1)[4], const u32 (&k2)[4], const QT& qt,
+                                    gej& acc) {
+    int8_t d[2][132];
+    const int n0 = wnaf5_128(d[0], k1), n1 = wnaf5_128(d[1], k2);
+    const bool kneg[2] = {(st.flags & LS_NEG0) != 0, (st.flags & LS_NEG1) != 0};
+    const fe one = fe_one();
+    bool inf = true;
+    acc.x = acc.y = fe_zero();
+    acc.z = one;
+    for (int i = std::max(n0, n1) - 1; i >= 0; i--) {
+        if (!inf) {
+            gej t;
+            gej_double(t, acc);
+            acc = t;
+        }
+        for (int slot = 0; slot < 2; slot++) {
+            const int v = i < (slot ? n1 : n0) ? d[slot][i] : 0;
+            if (v == 0) continue;
+            fe px, py;
+            qt.get_pair((v < 0 ? -v : v) >> 1, slot, px, py);  // (|v| - 1) / 2 for odd |v|
+            if ((v < 0) != kneg[slot]) fe_neg(py, py);
+            acc_add(acc, inf, px, py, one, false);
+        }
+    }
+    return inf;
+}
+
+// Whole ECDSA verify on one lane for the host (host_verify.cpp): the twist path with the wNAF Q
+// half above and the host's variable-time inverses (modinv_host.h).  Same verdicts as
+// ecdsa_verify_twist_lane.
+template <class QT, class GC>
+inline int ecdsa_verify_twist_host(u32 tag, const fe& px, const fe& py, const sc& r, const sc& s,
+                                   const sc& m, QT& qt, const GC& gc) {
+    TwistState st;
+    if (!twist_prep_key(tag, px, py, qt, st)) return 0;
+    sc sinv;
+    if (!twist_prep_u2(st.flags, r, s, nullptr, st, &sinv)) return 0;
+    u32 k1[4], k2[4];  // the raw GLV halves: undo twist_prep_u2's odd fix-up
+    for (int i = 0; i < 4; i++) {
+        k1[i] = st.k[0][i];
+        k2[i] = st.k[1][i];
+    }
+    if (st.flags & LS_CORR0) k1[0] &= ~1u;
+    if (st.flags & (LS_CORR0 << 1)) k2[0] &= ~1u;
+    twist_prep_u1(m, sinv, &st.flags, st.k[2], st.k[3]);
+    gej A, B;
+    const bool binf = twist_accumulate_q_wnaf(st, k1, k2, qt, B);
+    const bool ainf = twist_accumulate_g(st, gc, A);
+    fe al, be, K;
+    if (binf || ainf || !twist_combine(A, B, st.sigma, st.v, st.r, al, be, K))
+        return twist_exceptional(A, ainf, B, binf, st.sigma, st.v, st.ychk, st.flags, st.r);
+    fe binv;
+    fe_inv(binv, be);
+    return twist_final(al, K, binv, st.v, st.ychk, st.flags, st.r);
+}
+#endif
+
 // ------------------------------------------------------------------------------------------
 // BIP340 on the same path (secp256k1_schnorrsig_verify, modules/schnorrsig/main_impl.h:190-237):
 // the x-only key's even-y lift (extrakeys/main_impl.h:21-39) is never computed either.

@@ -142,6 +142,17 @@ __device__ __forceinline__ void sanitize_s(sc& s) {
     }
 }
 
+// Tuples per thread of the batched inversions (K_inv: s^-1, K_tfin: beta^-1): one Fermat
+// inversion per thread is shared by this many tuples (at least one wave per SIMD either way).
+#ifndef BCC_INV_PER_THREAD
+#define BCC_INV_PER_THREAD 16
+#endif
+#ifndef BCC_FIN_PER_THREAD
+#define BCC_FIN_PER_THREAD 16
+#endif
+constexpr size_t INV_PER_THREAD = BCC_INV_PER_THREAD;
+constexpr size_t FIN_PER_THREAD = BCC_FIN_PER_THREAD;
+
 // Montgomery's simultaneous inversion over the strided chunk {t, t+T, t+2T, ...} (coalesced:
 // at every step the wave touches 64 consecutive tuples).  s == 0 or s >= n is replaced by 1;
 // the prep kernel rejects those tuples on the original s anyway.
@@ -982,7 +993,7 @@ int ecdsa_launch_pre(SigScratch& sc, const uint8_t* d_tag, const uint8_t* d_x,
     if (int e = ensure_scratch(sc, dev, n, true, &C)) return e;
     u32* sinv = (u32*)sc.sinv;
     // K_inv: chunks of <= 16 tuples, but at least one wave per SIMD
-    size_t T = std::max<size_t>((n + 15) / 16, std::min<size_t>(n, (size_t)cus * 256));
+    size_t T = std::max<size_t>((n + INV_PER_THREAD - 1) / INV_PER_THREAD, std::min<size_t>(n, (size_t)cus * 256));
     hipLaunchKernelGGL(batch_sinv_kernel, dim3((unsigned)((T + 255) / 256)), dim3(256), 0,
                        (hipStream_t)stream, d_s, sinv, n, T);
     BCC_HIP_TRY(hipGetLastError());
@@ -1085,7 +1096,7 @@ int ecdsa_launch_after_pre(SigScratch& sc, const uint8_t* d_tag, const uint8_t* 
                                dim3(TLADDER_WG), 0, sm, state, qtab, gcomb, d_m, sinv, n);
             BCC_HIP_TRY(hipGetLastError());
             if (ev_rows_read) BCC_HIP_TRY(hipEventRecord((hipEvent_t)ev_rows_read, sm));
-            const size_t T = std::max<size_t>((n + 15) / 16, std::min<size_t>(n, (size_t)cus * 256));
+            const size_t T = std::max<size_t>((n + FIN_PER_THREAD - 1) / FIN_PER_THREAD, std::min<size_t>(n, (size_t)cus * 256));
             hipLaunchKernelGGL(twist_fin_kernel<false>, dim3((unsigned)((T + 255) / 256)), dim3(256), 0,
                                sm, state, qtab, d_verdict, 0, n, T);
             BCC_HIP_TRY(hipGetLastError());
@@ -1109,7 +1120,7 @@ int ecdsa_launch_after_pre(SigScratch& sc, const uint8_t* d_tag, const uint8_t* 
                                dim3(TLADDER_WG), 0, sm, state, qtab, gcomb, cnt);
             BCC_HIP_TRY(hipGetLastError());
             // the batched beta inversion: sub-chunks of <= 16 lanes, at least one wave per SIMD
-            const size_t T = std::max<size_t>((cnt + 15) / 16, std::min<size_t>(cnt, (size_t)cus * 256));
+            const size_t T = std::max<size_t>((cnt + FIN_PER_THREAD - 1) / FIN_PER_THREAD, std::min<size_t>(cnt, (size_t)cus * 256));
             hipLaunchKernelGGL(twist_fin_kernel<false>, dim3((unsigned)((T + 255) / 256)), dim3(256), 0,
                                sm, state, qtab, d_verdict, base, cnt, T);
             BCC_HIP_TRY(hipGetLastError());
@@ -1156,7 +1167,7 @@ int schnorr_launch(SigScratch& sc, const uint8_t* d_sig64, const uint8_t* d_msg3
                                dim3((unsigned)((cnt + TLADDER_WG - 1) / TLADDER_WG)),
                                dim3(TLADDER_WG), 0, sm, state, qtab, gcomb, cnt);
             BCC_HIP_TRY(hipGetLastError());
-            const size_t T = std::max<size_t>((cnt + 15) / 16, std::min<size_t>(cnt, (size_t)cus * 256));
+            const size_t T = std::max<size_t>((cnt + FIN_PER_THREAD - 1) / FIN_PER_THREAD, std::min<size_t>(cnt, (size_t)cus * 256));
             hipLaunchKernelGGL(twist_fin_kernel<true>, dim3((unsigned)((T + 255) / 256)), dim3(256), 0,
                                sm, state, qtab, d_verdict, base, cnt, T);
             BCC_HIP_TRY(hipGetLastError());
@@ -1174,7 +1185,7 @@ int schnorr_launch(SigScratch& sc, const uint8_t* d_sig64, const uint8_t* d_msg3
                            d_verdict, base, cnt, C);
         BCC_HIP_TRY(hipGetLastError());
         // parity: sub-chunks of <= 16 lanes, at least one wave per SIMD
-        size_t T = std::max<size_t>((cnt + 15) / 16, std::min<size_t>(cnt, (size_t)cus * 256));
+        size_t T = std::max<size_t>((cnt + FIN_PER_THREAD - 1) / FIN_PER_THREAD, std::min<size_t>(cnt, (size_t)cus * 256));
         hipLaunchKernelGGL(schnorr_parity_kernel, dim3((unsigned)((T + 255) / 256)), dim3(256), 0,
                            sm, qtab, d_verdict, base, cnt, C, T);
         BCC_HIP_TRY(hipGetLastError());

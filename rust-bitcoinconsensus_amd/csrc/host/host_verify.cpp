@@ -144,7 +144,7 @@ int host_verify_tuple(uint8_t tag, const uint8_t* x32, const uint8_t* y32, const
     load_be(m, m32);
     QTableArray qt;
     GCombArray gc{comb_tables()};
-    return ecdsa_verify_twist_lane(tag, px, py, r, s, m, qt, gc);
+    return ecdsa_verify_twist_host(tag, px, py, r, s, m, qt, gc);  // wNAF Q half, safegcd inverses
 }
 
 void host_verify_rows(const TupleRows& rows, const uint8_t* msg, uint8_t* verdict, unsigned threads) {

@@ -200,6 +200,9 @@ BCC_HD void fe_reduce512(fe& r, const u32 (&t)[16]) {
 // with 128-bit products, the CPU's native width, over the same little-endian bytes as fe.v.
 // Same contract as the 32-bit formulation: a weak residue (< 2^256) of a * b mod p.
 #define BCC_FE_HOST64 1
+}  // namespace bcc
+#include "modinv_host.h"  // variable-time inverses of the host builds (fe_inv, sc_inv)
+namespace bcc {
 inline void mul_4x64(u64 (&t)[8], const u32 (&a)[8], const u32 (&b)[8]) {
     typedef unsigned __int128 u128;
     u64 x[4], y[4];
@@ -514,8 +517,13 @@ BCC_HD bool fe_sqrt(fe& r, const fe& a) {
     return fe_equal(t, a);
 }
 
-// r = a^(p-2)
+// r = a^(p-2) (host builds: the variable-time safegcd inverse, modinv_host.h)
 BCC_HD void fe_inv(fe& r, const fe& a) {
+#if defined(BCC_FE_HOST64)
+    const u32 P[8] = BCC_P_LIMBS;
+    modinv::inverse_var(r.v, a.v, P);
+    return;
+#endif
     fe x223, x22, x2, t;
     fe_chain_x223(x223, x22, x2, a);
     fe_sqr_n(t, x223, 23);
@@ -784,6 +792,11 @@ BCC_HD bool sc_is_zero(const sc& a) { return u256_is_zero(a.v); }
 // step list is a constant table, so every branch is wave-uniform and the power table is indexed
 // by constants only (no scratch).  The batched path (batch_sinv_kernel) amortises this.
 BCC_HD void sc_inv(sc& r, const sc& a) {
+#if defined(BCC_FE_HOST64)  // host builds: the variable-time safegcd inverse (modinv_host.h)
+    const u32 N[8] = BCC_N_LIMBS;
+    modinv::inverse_var(r.v, a.v, N);
+    return;
+#endif
     // n - 2 = FFFFFFFF FFFFFFFF FFFFFFFF FFFFFFFE BAAEDCE6 AF48A03B BFD25E8C D036413F
     static constexpr uint8_t SQ[58] = {0, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4,
                                        4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 3, 5, 3, 4, 4, 5, 2, 5, 6,

@@ -17,6 +17,8 @@ def load():
     hostdir = os.path.join(ROOT, "rust-bitcoinconsensus_amd", "csrc", "host")
     srcs += [os.path.join(hostdir, f) for f in sorted(os.listdir(hostdir)) if f.endswith(".cpp")]
     deps = srcs + [os.path.join(hostdir, f) for f in os.listdir(hostdir) if f.endswith(".h")]
+    csrc = os.path.join(ROOT, "rust-bitcoinconsensus_amd", "csrc")
+    deps += [os.path.join(csrc, f) for f in os.listdir(csrc) if f.endswith(".h")]  # lane code
     deps += [os.path.join(ROOT, "oracle", "bcc_oracle.c"),
              os.path.join(ROOT, "rust-bitcoinconsensus_amd", "csrc", "pipeline.h"),
              os.path.join(ROOT, "include", "bcc_amd.h"),

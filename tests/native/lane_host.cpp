@@ -65,6 +65,26 @@ extern "C" int lane_verify_twist(unsigned tag, const unsigned char* x32, const u
     return ecdsa_verify_twist_lane(tag, px, py, r, s, m, qt, gc);
 }
 
+// the host engine's form of the same path (ecdsa_verify_twist_host: wNAF Q half, variable-time
+// inverses), same arguments
+extern "C" int lane_verify_twist_host(unsigned tag, const unsigned char* x32, const unsigned char* y32,
+                                      const unsigned char* r32, const unsigned char* s32,
+                                      const unsigned char* m32) {
+    fe px, py, t;
+    sc r, s, m;
+    fe_from_be_bytes(px, x32);
+    fe_from_be_bytes(py, y32);
+    fe_from_be_bytes(t, r32);
+    memcpy(r.v, t.v, 32);
+    fe_from_be_bytes(t, s32);
+    memcpy(s.v, t.v, 32);
+    fe_from_be_bytes(t, m32);
+    memcpy(m.v, t.v, 32);
+    QTableArray qt;
+    GCombArray gc{gcomb().data()};
+    return ecdsa_verify_twist_host(tag, px, py, r, s, m, qt, gc);
+}
+
 // BIP340 on the square-root-free path (ecdsa_twist.h)
 extern "C" int lane_schnorr_verify_twist(const unsigned char* sig64, const unsigned char* msg32,
                                          const unsigned char* xonly32) {

@@ -21,7 +21,7 @@ SO = os.path.join(HERE, "native", "_build", "lane_host.so")
 def lane():
     src = os.path.join(HERE, "native", "lane_host.cpp")
     deps = [src] + [os.path.join(HERE, "..", "rust-bitcoinconsensus_amd", "csrc", f)
-                    for f in ("ecdsa_lane.h", "ecdsa_twist.h", "secp256k1_device.h",
+                    for f in ("ecdsa_lane.h", "ecdsa_twist.h", "secp256k1_device.h", "modinv_host.h",
                               "sha256_device.h")]
     if not os.path.exists(SO) or any(os.path.getmtime(d) > os.path.getmtime(SO) for d in deps):
         os.makedirs(os.path.dirname(SO), exist_ok=True)
@@ -77,10 +77,15 @@ def test_lane_code_matches_reference_fixtures(lane):
     assert not bad, bad[:10]
 
 
-def test_lane_twist_matches_reference_fixtures(lane):
+TWIST_FORMS = ["lane_verify_twist", "lane_verify_twist_host"]  # SIMT lane code / host engine's form
+
+
+@pytest.mark.parametrize("fn", TWIST_FORMS)
+def test_lane_twist_matches_reference_fixtures(lane, fn):
     """The square-root-free path (csrc/ecdsa_twist.h) on every fixture tuple: compressed keys
     never decompressed, the key's y recovered as -alpha / beta; exceptional classes (R at
-    infinity, x(A) == x(B), u1 == 0) take the exact fallback."""
+    infinity, x(A) == x(B), u1 == 0) take the exact fallback.  Both forms: the kernels' fixed-window
+    lane code and the host engine's (wNAF Q half, variable-time inverses)."""
     O = Oracle()
     bad = []
     classes = {}
@@ -89,7 +94,7 @@ def test_lane_twist_matches_reference_fixtures(lane):
         ok, r, s = O.der_parse_lax(t["sig"])
         if not ok:
             r = s = bytes(32)
-        got = lane.lane_verify_twist(tag, x, y, r, s, t["hash"])
+        got = getattr(lane, fn)(tag, x, y, r, s, t["hash"])
         classes[t["cls"]] = classes.get(t["cls"], 0) + 1
         if got != t["verdict"]:
             bad.append((t["cls"], got, t["verdict"]))
@@ -107,7 +112,8 @@ def _der(r, s):
     return b"\x30" + bytes([len(body)]) + body
 
 
-def test_lane_twist_random_vs_oracle(lane):
+@pytest.mark.parametrize("fn", TWIST_FORMS)
+def test_lane_twist_random_vs_oracle(lane, fn):
     """Random signed tuples with mutations (flipped key parity, random x -- about half of them
     non-residues --, hybrid / uncompressed encodings, negated y, message and s flips) through
     the square-root-free lane code against the oracle's CPubKey::Verify."""
@@ -142,7 +148,7 @@ def test_lane_twist_random_vs_oracle(lane):
             pub = bytes([tag]) + qx.to_bytes(32, "big") + qy.to_bytes(32, "big")
         exp = O.pubkey_verify(pub, msg, _der(r, s))
         tag, x, y = pub_to_tuple(pub)
-        got = lane.lane_verify_twist(tag, x, y, r.to_bytes(32, "big"), s.to_bytes(32, "big"), msg)
+        got = getattr(lane, fn)(tag, x, y, r.to_bytes(32, "big"), s.to_bytes(32, "big"), msg)
         seen.add((mode, exp))
         if got != exp:
             bad.append((i, mode, got, exp))
