@@ -755,7 +755,12 @@ __global__ __launch_bounds__(TLADDER_WG) __attribute__((amdgpu_waves_per_eu(BCC_
     twist_q_part(lane_table(qtab, t), st);
 }
 
-__global__ __launch_bounds__(TLADDER_WG) __attribute__((amdgpu_waves_per_eu(BCC_LADDER_WAVES, BCC_LADDER_WAVES))) void twist_ladder_g_kernel(
+// The G half keeps the combine's temporaries live beside the comb accumulator: at four waves
+// per SIMD (128 VGPRs) it spills; BCC_LADDERG_WAVES selects its own occupancy (A/B builds).
+#ifndef BCC_LADDERG_WAVES
+#define BCC_LADDERG_WAVES BCC_LADDER_WAVES
+#endif
+__global__ __launch_bounds__(TLADDER_WG) __attribute__((amdgpu_waves_per_eu(BCC_LADDERG_WAVES, BCC_LADDERG_WAVES))) void twist_ladder_g_kernel(
     u32* __restrict__ state, u32* __restrict__ qtab, const u32* __restrict__ gcomb,
     const uint8_t* __restrict__ pm, const u32* __restrict__ psinv, size_t cnt) {
     const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;

@@ -429,6 +429,8 @@ private:
     void* ev_block_ = nullptr;     // hipEvent_t (blocking sync): host waits sleep, not spin
     int wait(void* stream);
     void* ev_front_ = nullptr;     // hipEvent_t: this run's sighash kernels done (overlap mode)
+    void* ev_up_ = nullptr;        // hipEvent_t: the tuple rows uploaded (K_inv on the main stream)
+    void* ev_inv_ = nullptr;       // hipEvent_t: K_inv done on the main stream
     bool rows_pending_ = false;    // ev_rows_ recorded by an earlier run (on rows_stream_)
     void* rows_stream_ = nullptr;
     SigScratch scratch_;

@@ -819,6 +819,8 @@ DeviceBatch::~DeviceBatch() {
     if (ev_fork_) (void)hipEventDestroy((hipEvent_t)ev_fork_);
     if (ev_join_) (void)hipEventDestroy((hipEvent_t)ev_join_);
     if (ev_wtx_) (void)hipEventDestroy((hipEvent_t)ev_wtx_);
+    if (ev_up_) (void)hipEventDestroy((hipEvent_t)ev_up_);
+    if (ev_inv_) (void)hipEventDestroy((hipEvent_t)ev_inv_);
     if (ev_rows_) (void)hipEventDestroy((hipEvent_t)ev_rows_);
     if (ev_block_) (void)hipEventDestroy((hipEvent_t)ev_block_);
     if (ev_front_) (void)hipEventDestroy((hipEvent_t)ev_front_);
@@ -1231,6 +1233,16 @@ static bool overlap_runs() {
     return on;
 }
 
+// K_inv on the main stream beside K_tkey (default since round 3: C2 +0.9..1.2 % in an interleaved
+// A/B, profiles/r03/ab/inv_main); BCC_INV_MAIN=0 puts it back ahead of K_tkey on the side stream
+static bool inv_on_main() {
+    static const bool on = [] {
+        const char* e = getenv("BCC_INV_MAIN");
+        return !(e && atoi(e) == 0);
+    }();
+    return on;
+}
+
 // K_inv and K_key read only the s and key rows, so they run on a side stream beside the sighash
 // kernels (fork / join by events: graph-capturable); prep + ladder wait for both.
 int DeviceBatch::run(void* stream) {
@@ -1312,8 +1324,26 @@ int DeviceBatch::run_stages(void* stream) {
     // the Q ladder (ecdsa_launch_q); the G ladder and K_tfin wait for both
     (void)ws;
     if (int e = upload_on(side, st)) return e;
-    if (int e = ecdsa_launch_pre(scratch_, d_tag, d_x, d_y, d_s, n_rows_, side)) return e;
-    if (int e = ecdsa_launch_key(scratch_, d_tag, d_x, d_y, n_rows_, side)) return e;
+    if (inv_on_main()) {
+        // K_inv (one latency-bound wave per SIMD) on the main stream, beside K_tkey on the side
+        // stream, instead of ahead of it: the side stream's chain to the Q ladder loses K_inv
+        if (!ev_up_) {
+            hipEvent_t a = nullptr, b = nullptr;
+            BCC_HIP_TRY(hipEventCreateWithFlags(&a, hipEventDisableTiming));
+            BCC_HIP_TRY(hipEventCreateWithFlags(&b, hipEventDisableTiming));
+            ev_up_ = a;
+            ev_inv_ = b;
+        }
+        BCC_HIP_TRY(hipEventRecord((hipEvent_t)ev_up_, side));  // the s rows are on the device
+        BCC_HIP_TRY(hipStreamWaitEvent(st, (hipEvent_t)ev_up_, 0));
+        if (int e = ecdsa_launch_pre(scratch_, d_tag, d_x, d_y, d_s, n_rows_, st)) return e;
+        BCC_HIP_TRY(hipEventRecord((hipEvent_t)ev_inv_, st));
+        if (int e = ecdsa_launch_key(scratch_, d_tag, d_x, d_y, n_rows_, side)) return e;
+        BCC_HIP_TRY(hipStreamWaitEvent(side, (hipEvent_t)ev_inv_, 0));  // K_tscal_q reads s^-1
+    } else {
+        if (int e = ecdsa_launch_pre(scratch_, d_tag, d_x, d_y, d_s, n_rows_, side)) return e;
+        if (int e = ecdsa_launch_key(scratch_, d_tag, d_x, d_y, n_rows_, side)) return e;
+    }
     if (int e = ecdsa_launch_q(scratch_, d_r, d_s, n_rows_, side)) return e;
     BCC_HIP_TRY(hipEventRecord((hipEvent_t)ev_join_, side));
     if (int e = launch_front(st)) return e;
