@@ -49,7 +49,7 @@ SEEDS = {"c2": 0x5EED0001, "c3": 0x5EED0003, "c4": 0x5EED0004, "c5": 0x5EED0005,
 # the ECDSA stage's kernels: the square-root-free path (default) or the round-1 path
 _LEGACY = os.environ.get("BCC_ECDSA_PATH") == "legacy"
 ECDSA_KERNELS = ("ecdsa (batch_sinv + ecdsa_key + ecdsa_prep + ecdsa_ladder)" if _LEGACY else
-                 "ecdsa (batch_sinv + ecdsa_tkey/tscal (or ecdsa_tprep) + twist_ladder<ecdsa> + "
+                 "ecdsa (batch_sinv + ecdsa_tkey + ecdsa_tscal_q + twist_ladder_q + twist_ladder_g + "
                  "twist_fin<ecdsa>; no key square root)")
 SCHNORR_KERNELS = ("schnorr (prep + ladder + y-parity batch inversion)" if _LEGACY else
                    "schnorr (schnorr_tprep + twist_ladder<bip340> + twist_fin<bip340>; "
@@ -719,6 +719,9 @@ def main():
     ap.add_argument("--seed", type=int, default=None)
     ap.add_argument("--cpu-sample", type=int, default=None)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-extra", action="store_true",
+                    help="skip the drop-in / single-call / host-buffer extras (profiling runs: "
+                         "every launch is then a full-size one)")
     ap.add_argument("--traffic", type=float, default=None,
                     help="HBM bytes per ECDSA launch from a rocprofv3 --pmc run (profiles/)")
     args = ap.parse_args()
@@ -819,10 +822,12 @@ def main():
             # why frac stops where it does (committed PMC passes + microbenchmark): the ladder is
             # VALU-issue-bound; its cycles split by instruction class at the measured issue costs
             d = json.load(open(cm))
-            k = d["kernels"].get("bench:twist_ladder_kernel<false>")
+            kname = next((n for n in ("twist_ladder_q_kernel", "twist_ladder_kernel<false>")
+                          if "bench:" + n in d["kernels"]), None)
+            k = d["kernels"].get("bench:" + kname) if kname else None
             if k:
                 roof["cost_model"] = dict(
-                    kernel="twist_ladder_kernel<false>", cycle_share=k["cycle_share"],
+                    kernel=kname, cycle_share=k["cycle_share"],
                     valu_per_verify=k["valu_per_wave"],
                     issue_cost_cycles=d["issue_cost_cycles_per_wave_instr"],
                     predicted_over_measured_cycles=k["predicted_over_measured"],
@@ -842,7 +847,8 @@ def main():
             "roofline": roof,
             "cpu_baseline": cpu,
         }
-        out.update(job.extra(sighash_ms))
+        if not args.no_extra:
+            out.update(job.extra(sighash_ms))
         out["source_hash"] = B.source_hash()
         out["verdicts_valid"] = n_valid_all
         out["validity_bitmap"] = bitmap

@@ -31,6 +31,7 @@
 #include "script.h"
 #include "sighash.h"
 #include "team.h"
+#include "tuples.h"
 
 namespace bcc {
 namespace host {
@@ -1306,12 +1307,14 @@ void bcc_release_thread_state(void) {
     bcc::host::taproot_release_thread_state();
     bcc::release_device_thread_state();
     bcc::release_tuple_thread_state();
+    bcc::host::release_pubkey_rows();
     bcc::host::release_team();
     // the state the per-GPU and pipeline workers keep for the rounds they ran for callers
     bcc::host::run_on_all_workers([] {
         bcc::host::taproot_release_thread_state();
         bcc::release_device_thread_state();
         bcc::release_tuple_thread_state();
+        bcc::host::release_pubkey_rows();
         bcc::host::release_team();
     });
 }

@@ -57,13 +57,23 @@ static void rows_resize(bcc::TupleRows& rows, size_t n) {
 
 void parse_rows(const uint8_t* pub_blob, const uint64_t* pub_off, const uint8_t* msg32,
                 const uint8_t* sig_blob, const uint64_t* sig_off, size_t n, bcc::TupleRows& rows) {
-    rows_resize(rows, n);
+    rows_resize(rows, n);  // every field of every row is written below (reused rows stay dirty)
+    rows.msg_one = rows.y_unused = false;
+    rows.hrow.clear();
+    rows.hprog.clear();
     pfor(n, 4096, [&](size_t lo, size_t hi) {
         for (size_t i = lo; i < hi; i++)
             parse_row(pub_blob + pub_off[i], pub_off[i + 1] - pub_off[i], msg32 + 32 * i,
                       sig_blob + sig_off[i], sig_off[i + 1] - sig_off[i], rows, i);
     });
 }
+
+// The rows of bcc_pubkey_verify_batch, kept with the thread that parsed them (the caller, or a
+// per-GPU worker) for its next call: an 8M-tuple call otherwise zero-fills and faults in 1.3 GB of
+// fresh vectors on one thread before the parallel parse, and unmaps them afterwards.
+thread_local bcc::TupleRows tl_pubkey_rows;
+
+void release_pubkey_rows() { tl_pubkey_rows = bcc::TupleRows(); }
 
 }  // namespace host
 }  // namespace bcc
@@ -80,7 +90,7 @@ extern "C" int bcc_pubkey_verify_batch(const uint8_t* pub_blob, const uint64_t* 
     for (size_t d = 0; d < D; d++) {
         const size_t lo = n * d / D, hi = n * (d + 1) / D;
         jobs.push_back([=] {  // contiguous equal range on devs[d] (offsets stay absolute)
-            bcc::TupleRows rows;
+            bcc::TupleRows& rows = bcc::host::tl_pubkey_rows;
             bcc::host::parse_rows(pub_blob, pub_off + lo, msg32 + 32 * lo, sig_blob, sig_off + lo,
                                   hi - lo, rows);
             bcc::SighashJobs none;

@@ -30,5 +30,8 @@ void pfor(size_t n, size_t grain, F f) {
 void parse_rows(const uint8_t* pub_blob, const uint64_t* pub_off, const uint8_t* msg32,
                 const uint8_t* sig_blob, const uint64_t* sig_off, size_t n, TupleRows& rows);
 
+// Frees the calling thread's reused bcc_pubkey_verify_batch rows (bcc_release_thread_state).
+void release_pubkey_rows();
+
 }  // namespace host
 }  // namespace bcc

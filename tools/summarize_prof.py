@@ -60,6 +60,7 @@ def main(d):
     # the same inputs = 7.  A stage may launch a kernel once per lane chunk (C4 at 8M, C5 at 16M).
     stages = {"ecdsa": ["batch_sinv_kernel", "ecdsa_key_kernel", "ecdsa_prep_kernel", "ecdsa_ladder_kernel",
                         "ecdsa_tprep_kernel", "ecdsa_tkey_kernel", "ecdsa_tscal_kernel",
+                        "ecdsa_tscal_q_kernel", "twist_ladder_q_kernel", "twist_ladder_g_kernel",
                         "void twist_ladder_kernel<false>", "void twist_fin_kernel<false>"],
               "schnorr": ["schnorr_prep_kernel", "schnorr_ladder_kernel", "schnorr_parity_kernel",
                           "schnorr_tprep_kernel", "void twist_ladder_kernel<true>", "void twist_fin_kernel<true>"]}
@@ -78,6 +79,12 @@ def main(d):
         wb = sum(K[k].get("write_size_bytes_total", 0) for k in ks if k in K) / n_stage
         out.setdefault("stages", {})[st] = dict(executions=n_stage, fetch_bytes=fb, fetch_bytes_x2=2 * fb,
                                                write_bytes=wb, traffic_bytes=2 * fb + wb)
+        # the same from per-launch averages (every launch full-size: bench.py --no-extra runs)
+        fl = sum(K[k].get("fetch_size_bytes_per_launch", 0) for k in ks if k in K)
+        wl = sum(K[k].get("write_size_bytes_per_launch", 0) for k in ks if k in K)
+        out["stages"][st].update(per_launch_fetch_bytes_x2=2 * fl, per_launch_write_bytes=wl,
+                                 per_launch_traffic_bytes=2 * fl + wl,
+                                 kernels=[k for k in ks if k in K])
     print(json.dumps(out, indent=1))
 
 
