@@ -791,6 +791,25 @@ __global__ __launch_bounds__(TLADDER_WG) __attribute__((amdgpu_waves_per_eu(BCC_
     twist_g_part<false>(w, lane_table(qtab, t), gcomb, st);
 }
 
+// BIP340 in two launches too (BCC_SCHNORR_SPLIT): the prep formed every scalar, so the G half
+// only runs the comb, the combine and the parity quantities; each half gets its own registers
+// (the fused BIP340 ladder spills).
+__global__ __launch_bounds__(TLADDER_WG) __attribute__((amdgpu_waves_per_eu(BCC_LADDERG_WAVES, BCC_LADDERG_WAVES))) void twist_ladder_g340_kernel(
+    u32* __restrict__ state, u32* __restrict__ qtab, const u32* __restrict__ gcomb, size_t cnt) {
+    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= cnt) return;
+    u32* w = lane_words(state, t, TSTATE_WORDS);
+    TwistStateView st;
+    st.p = w;
+    st.flags = w[T_FLAGS * LANE_STRIDE];
+    if (!(st.flags & LS_VALID)) {
+        w[T_STAT * LANE_STRIDE] = TW_REJECT;
+        return;
+    }
+    tw_load(st.sigma.v, w, T_SIGMA);
+    twist_g_part<true>(w, lane_table(qtab, t), gcomb, st);
+}
+
 // beta^-1 for every normal lane of a chunk by Montgomery's trick over the strided sub-chunk
 // {t, t+T, ...} (3 mults per lane + one Fermat inversion per thread), then the verdicts; the
 // exceptional lanes (adversarial only) run the exact fallback here, divergently.
@@ -808,7 +827,8 @@ template <bool BIP340>
 __global__ __launch_bounds__(256) void twist_fin_kernel(u32* __restrict__ state,
                                                         const u32* __restrict__ qtab,
                                                         uint8_t* __restrict__ verdict,
-                                                        size_t base, size_t cnt, size_t T) {
+                                                        size_t base, size_t cnt, size_t T,
+                                                        int and_mode) {
     const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= cnt || t >= T) return;
     fe acc = fe_one();
@@ -871,7 +891,8 @@ __global__ __launch_bounds__(256) void twist_fin_kernel(u32* __restrict__ state,
                 }
             }
         }
-        verdict[base + i] = (uint8_t)ok;
+        if (!and_mode) verdict[base + i] = (uint8_t)ok;
+        else if (!ok) verdict[base + i] = 0;  // the caller preset the row to 1 (verdict_and)
     }
 }
 
@@ -899,6 +920,17 @@ static bool ecdsa_twist() {
     static const bool on = [] {
         const char* e = getenv("BCC_ECDSA_PATH");
         return !(e && std::string(e) == "legacy");
+    }();
+    return on;
+}
+
+bool ecdsa_fin_clears() { return ecdsa_twist(); }
+
+// BCC_SCHNORR_SPLIT=1: the BIP340 ladder as a Q launch and a G launch (A/B runs)
+static bool schnorr_split() {
+    static const bool on = [] {
+        const char* e = getenv("BCC_SCHNORR_SPLIT");
+        return e && atoi(e) != 0;
     }();
     return on;
 }
@@ -1079,7 +1111,8 @@ int ecdsa_launch(SigScratch& sc, const uint8_t* d_tag, const uint8_t* d_x, const
 int ecdsa_launch_after_pre(SigScratch& sc, const uint8_t* d_tag, const uint8_t* d_x,
                            const uint8_t* d_y, const uint8_t* d_r, const uint8_t* d_s,
                            const uint8_t* d_m, uint8_t* d_verdict, size_t n, void* stream,
-                           void* ev_rows_read) {
+                           void* ev_rows_read, bool verdict_and) {
+    const int and_mode = verdict_and && ecdsa_twist() ? 1 : 0;
     if (n == 0) return 0;
     int dev = 0, cus = 0;
     fe* gtab = nullptr;
@@ -1103,7 +1136,7 @@ int ecdsa_launch_after_pre(SigScratch& sc, const uint8_t* d_tag, const uint8_t* 
             if (ev_rows_read) BCC_HIP_TRY(hipEventRecord((hipEvent_t)ev_rows_read, sm));
             const size_t T = std::max<size_t>((n + FIN_PER_THREAD - 1) / FIN_PER_THREAD, std::min<size_t>(n, (size_t)cus * 256));
             hipLaunchKernelGGL(twist_fin_kernel<false>, dim3((unsigned)((T + 255) / 256)), dim3(256), 0,
-                               sm, state, qtab, d_verdict, 0, n, T);
+                               sm, state, qtab, d_verdict, 0, n, T, and_mode);
             BCC_HIP_TRY(hipGetLastError());
             return 0;
         }
@@ -1127,7 +1160,7 @@ int ecdsa_launch_after_pre(SigScratch& sc, const uint8_t* d_tag, const uint8_t* 
             // the batched beta inversion: sub-chunks of <= 16 lanes, at least one wave per SIMD
             const size_t T = std::max<size_t>((cnt + FIN_PER_THREAD - 1) / FIN_PER_THREAD, std::min<size_t>(cnt, (size_t)cus * 256));
             hipLaunchKernelGGL(twist_fin_kernel<false>, dim3((unsigned)((T + 255) / 256)), dim3(256), 0,
-                               sm, state, qtab, d_verdict, base, cnt, T);
+                               sm, state, qtab, d_verdict, base, cnt, T, and_mode);
             BCC_HIP_TRY(hipGetLastError());
         }
         return 0;
@@ -1168,13 +1201,23 @@ int schnorr_launch(SigScratch& sc, const uint8_t* d_sig64, const uint8_t* d_msg3
             hipLaunchKernelGGL(schnorr_tprep_kernel, dim3((unsigned)((cnt + 255) / 256)), dim3(256),
                                0, sm, d_sig64, d_msg32, d_xonly32, base, cnt, qtab, state);
             BCC_HIP_TRY(hipGetLastError());
-            hipLaunchKernelGGL(twist_ladder_kernel<true>,
-                               dim3((unsigned)((cnt + TLADDER_WG - 1) / TLADDER_WG)),
-                               dim3(TLADDER_WG), 0, sm, state, qtab, gcomb, cnt);
+            if (schnorr_split()) {
+                hipLaunchKernelGGL(twist_ladder_q_kernel,
+                                   dim3((unsigned)((cnt + TLADDER_WG - 1) / TLADDER_WG)),
+                                   dim3(TLADDER_WG), 0, sm, state, qtab, cnt);
+                BCC_HIP_TRY(hipGetLastError());
+                hipLaunchKernelGGL(twist_ladder_g340_kernel,
+                                   dim3((unsigned)((cnt + TLADDER_WG - 1) / TLADDER_WG)),
+                                   dim3(TLADDER_WG), 0, sm, state, qtab, gcomb, cnt);
+            } else {
+                hipLaunchKernelGGL(twist_ladder_kernel<true>,
+                                   dim3((unsigned)((cnt + TLADDER_WG - 1) / TLADDER_WG)),
+                                   dim3(TLADDER_WG), 0, sm, state, qtab, gcomb, cnt);
+            }
             BCC_HIP_TRY(hipGetLastError());
             const size_t T = std::max<size_t>((cnt + FIN_PER_THREAD - 1) / FIN_PER_THREAD, std::min<size_t>(cnt, (size_t)cus * 256));
             hipLaunchKernelGGL(twist_fin_kernel<true>, dim3((unsigned)((T + 255) / 256)), dim3(256), 0,
-                               sm, state, qtab, d_verdict, base, cnt, T);
+                               sm, state, qtab, d_verdict, base, cnt, T, 0);
             BCC_HIP_TRY(hipGetLastError());
         }
         return 0;

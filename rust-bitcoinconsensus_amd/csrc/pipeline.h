@@ -365,10 +365,14 @@ int ecdsa_launch_q(SigScratch& sc, const uint8_t* d_r, const uint8_t* d_s, size_
 // ev_rows_read (optional hipEvent_t) is recorded on `stream` once the last kernel that reads the
 // s / m / key rows and the s^-1 rows has been launched (the prep kernel): later writers of those
 // rows (the next run's front kernels) need only wait for it, not for the ladder.
+// verdict_and: the caller has set d_verdict[0, n) to 1 (and may already have cleared rows, e.g.
+// the key-hash conditions); K_tfin then only clears the rows that fail.  Only on the twist path
+// (ecdsa_fin_clears()).
 int ecdsa_launch_after_pre(SigScratch& sc, const uint8_t* d_tag, const uint8_t* d_x,
                            const uint8_t* d_y, const uint8_t* d_r, const uint8_t* d_s,
                            const uint8_t* d_m, uint8_t* d_verdict, size_t n, void* stream,
-                           void* ev_rows_read = nullptr);
+                           void* ev_rows_read = nullptr, bool verdict_and = false);
+bool ecdsa_fin_clears();
 int schnorr_launch(SigScratch& sc, const uint8_t* d_sig64, const uint8_t* d_msg32,
                    const uint8_t* d_xonly32, uint8_t* d_verdict, size_t n, void* stream);
 
@@ -415,7 +419,8 @@ private:
     size_t up_rows_ = 0, up_total_ = 0;
     int launch_after_front(struct ihipStream_t* st);  // K_win, K2, K3
     int launch_key_hash(struct ihipStream_t* st);     // K_h160: key-hash conditions into the verdicts
-    int run_stages(void* stream);                     // run() up to K_tfin
+    int run_stages(void* stream);
+    bool kh_done_ = false;  // run_stages ran K_h160 already (ahead of the ladder, verdict_and)                     // run() up to K_tfin
     int dev_;
     void* own_stream_ = nullptr;   // hipStream_t, created on first use
     void* last_stream_ = nullptr;  // stream of the last run

@@ -1233,6 +1233,15 @@ static bool overlap_runs() {
     return on;
 }
 
+// K_h160 beside the Q ladder instead of after K_tfin (default); BCC_KEY_HASH_EARLY=0 reverts
+static bool key_hash_early() {
+    static const bool on = [] {
+        const char* e = getenv("BCC_KEY_HASH_EARLY");
+        return !(e && atoi(e) == 0);
+    }();
+    return on;
+}
+
 // K_inv on the main stream beside K_tkey (default since round 3: C2 +0.9..1.2 % in an interleaved
 // A/B, profiles/r03/ab/inv_main); BCC_INV_MAIN=0 puts it back ahead of K_tkey on the side stream
 static bool inv_on_main() {
@@ -1254,11 +1263,13 @@ int DeviceBatch::run(void* stream) {
         return run_ecdsa(st);  // K_h160 included
     }
     if (int e = run_stages(st)) return e;
+    if (kh_done_) return 0;  // K_h160 ran ahead of the ladder (run_stages)
     return launch_key_hash(st);
 }
 
 int DeviceBatch::run_stages(void* stream) {
     hipStream_t st = (hipStream_t)stream;
+    kh_done_ = false;
     if (!side_stream_) {
         hipStream_t s = nullptr, s2 = nullptr;
         hipEvent_t a = nullptr, b = nullptr, c = nullptr;
@@ -1347,8 +1358,19 @@ int DeviceBatch::run_stages(void* stream) {
     if (int e = ecdsa_launch_q(scratch_, d_r, d_s, n_rows_, side)) return e;
     BCC_HIP_TRY(hipEventRecord((hipEvent_t)ev_join_, side));
     if (int e = launch_front(st)) return e;
+    // K_h160 needs only the key rows and the programs: on the main stream it runs beside the Q
+    // ladder into verdicts preset to 1, and K_tfin then only clears failing rows (verdict_and),
+    // instead of running after K_tfin at the end of the critical path.  The key rows arrive on the
+    // side stream: the main stream waited for them before K_inv (inv_on_main).
+    const bool kh_early = n_hash_ && inv_on_main() && key_hash_early() && ecdsa_fin_clears();
+    if (kh_early) {
+        BCC_HIP_TRY(hipMemsetAsync(d_v, 1, n_rows_, st));
+        if (int e = launch_key_hash(st)) return e;
+        kh_done_ = true;
+    }
     BCC_HIP_TRY(hipStreamWaitEvent(st, (hipEvent_t)ev_join_, 0));
-    return ecdsa_launch_after_pre(scratch_, d_tag, d_x, d_y, d_r, d_s, d_m, d_v, n_rows_, st);
+    return ecdsa_launch_after_pre(scratch_, d_tag, d_x, d_y, d_r, d_s, d_m, d_v, n_rows_, st,
+                                  nullptr, kh_early);
 }
 
 // Verdicts come back through a pinned buffer of the batch (an asynchronous copy on the run's stream,

@@ -2,8 +2,8 @@
 
     python3 tools/update_traffic.py profiles/r03/r03y/c2/summary.json c2 1000000
 
-traffic = HBM bytes per signature stage (FETCH_SIZE x 2 + WRITE_SIZE per launch, summed over the
-stage's kernels; bench.py --no-extra runs, so every launch is a full-size one), the form bench.py
+traffic = HBM bytes per signature stage (FETCH_SIZE x 2 + WRITE_SIZE of the stage's kernels over
+the run / the stage executions; bench.py --no-extra runs, so there are no other launches), the form bench.py
 reads into roofline.traffic (it checks units and the kernel description)."""
 import json
 import os
@@ -20,11 +20,13 @@ def main(summary, config, units):
     path = os.path.join(ROOT, "profiles", "traffic.json")
     tj = json.load(open(path))
     e = tj.get(config, {})
-    e.update(units=units, traffic_bytes=st["per_launch_traffic_bytes"],
-             fetch_bytes_x2=st["per_launch_fetch_bytes_x2"], write_bytes=st["per_launch_write_bytes"],
-             source=f"{os.path.relpath(summary, ROOT)} (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, "
-                    f"per launch summed over {', '.join(st['kernels'])}; FETCH doubled per "
-                    "MI355X_MICROARCH.md)",
+    # per stage = all launches of the stage's kernels / the stage executions of the run (a stage
+    # launches its kernels once per lane chunk: C4's 8M tuples are two 4M chunks)
+    e.update(units=units, traffic_bytes=st["traffic_bytes"],
+             fetch_bytes_x2=st["fetch_bytes_x2"], write_bytes=st["write_bytes"],
+             source=f"{os.path.relpath(summary, ROOT)} (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes "
+                    f"over bench.py --no-extra, {st['executions']} stage executions of "
+                    f"{', '.join(st['kernels'])}; FETCH doubled per MI355X_MICROARCH.md)",
              kernel=bench.ECDSA_KERNELS if config in ("c2", "c3", "c4") else bench.SCHNORR_KERNELS)
     e.pop("instruction_mix", None)
     tj[config] = e
