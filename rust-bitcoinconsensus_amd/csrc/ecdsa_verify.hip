@@ -14,7 +14,7 @@
 // (G tables in LDS), and for BIP340 schnorr_{prep,ladder,parity}_kernel.
 // K_inv needs only the s rows: DeviceBatch::run launches it on a side stream beside the sighash
 // kernels.  Prep and ladder are separate launches so that each gets its own register allocation
-// (ladder: 4 waves per SIMD).  Tuples are processed in chunks of up to 4M lanes so the per-tuple
+// (ladder: 4 waves per SIMD).  Tuples are processed in chunks of up to 16M lanes so the per-tuple
 // scratch (Q table + ladder state, ~1.4 KB) stays bounded.
 //
 // HBM layout (all device-resident):
@@ -945,12 +945,14 @@ static const std::vector<fe>& host_gtab() {
     return t;
 }
 
-// Lanes per prep/ladder launch pair.  Larger chunks leave fewer kernel tails (measured on
-// MI355X, C2 1M: 256k lanes 65.8M/s, 1M lanes 71.0M/s; C4 8M: 2M 75.6M/s, 4M 76.8M/s); 4M lanes
-// cost at most 3.6 GiB of scratch per caller, allocated only up to the batch size.
+// Lanes per prep/ladder launch pair.  Larger chunks leave fewer kernel tails and fewer latency-
+// bound K_tfin passes (measured on MI355X, C2 1M: 256k lanes 65.8M/s, 1M lanes 71.0M/s; C4 8M:
+// 2M 75.6M/s, 4M 76.8M/s; round 3, C5 16M rows: 4M 100.1 / 100.5, 16M 107.4 / 106.7 M/s, C4 8M
+// equal at 4M and 8M, profiles/r03/ab/chunk); 16M lanes cost at most ≈22 GiB of scratch per
+// caller on a 288 GB device, allocated only up to the batch size.
 static size_t default_chunk_lanes() {
     const char* e = getenv("BCC_CHUNK");
-    return e ? (size_t)atol(e) : ((size_t)4 << 20);
+    return e ? (size_t)atol(e) : ((size_t)16 << 20);
 }
 static std::atomic<size_t> g_chunk_lanes{0};
 
