@@ -1455,6 +1455,8 @@ namespace {
 struct TaprootCtx {
     int dev = -1;
     hipStream_t stream = nullptr;
+    hipStream_t side = nullptr;  // the signature / key rows' upload beside the SigMsg kernels
+    hipEvent_t side_done = nullptr;
     SigScratch sc;
     void* arena = nullptr;
     size_t cap = 0;
@@ -1463,12 +1465,24 @@ struct TaprootCtx {
     ~TaprootCtx() {
         if (dev >= 0) (void)hipSetDevice(dev);
         if (stream) (void)hipStreamDestroy(stream);
+        if (side) (void)hipStreamDestroy(side);
+        if (side_done) (void)hipEventDestroy(side_done);
         if (arena) (void)hipFree(arena);
         if (image) (void)hipHostFree(image);
     }
 };
 
 }  // namespace
+
+// BCC_TAPROOT_SPLIT_UPLOAD=1: upload the signature / key rows on a side stream beside the SigMsg
+// kernels (A/B runs)
+static bool taproot_split_upload() {
+    static const bool on = [] {
+        const char* e = getenv("BCC_TAPROOT_SPLIT_UPLOAD");
+        return e && atoi(e) != 0;
+    }();
+    return on;
+}
 
 int gpu_taproot_verify(int device, const TaprootJobs& J, uint8_t* verdict, uint8_t* msg32_out) {
     const TaprootJobs* p = &J;
@@ -1607,7 +1621,21 @@ int gpu_taproot_verify_parts(int device, const TaprootJobs* const* Jp, size_t P,
     hipStream_t st = c.stream;
     ShaMid mid;
     tapsighash_midstate(mid.s);
-    BCC_HIP_TRY(hipMemcpyAsync(a, h, upload, hipMemcpyHostToDevice, st));
+    const bool split_up = taproot_split_upload();
+    if (split_up) {
+        // the tx bytes and jobs first on the main stream (the SigMsg kernels need them), the
+        // 96-byte signature / key rows on a side stream beside those kernels; the BIP340 kernels
+        // wait for both
+        if (!c.side) {
+            BCC_HIP_TRY(hipStreamCreateWithFlags(&c.side, hipStreamNonBlocking));
+            BCC_HIP_TRY(hipEventCreateWithFlags(&c.side_done, hipEventDisableTiming));
+        }
+        BCC_HIP_TRY(hipMemcpyAsync(a + off[MSG], h + off[MSG], upload - off[MSG], hipMemcpyHostToDevice, st));
+        BCC_HIP_TRY(hipMemcpyAsync(a, h, off[MSG], hipMemcpyHostToDevice, c.side));
+        BCC_HIP_TRY(hipEventRecord(c.side_done, c.side));
+    } else {
+        BCC_HIP_TRY(hipMemcpyAsync(a, h, upload, hipMemcpyHostToDevice, st));
+    }
     if (nttx) {  // KT_tx, then KT_msg: the SigMsgs from the tx bytes
         hipLaunchKernelGGL(taproot_tx_kernel, dim3((unsigned)((5 * nttx + XS_WG - 1) / XS_WG)),
                            dim3(XS_WG), 0, st, a + off[TXRAW], (const TtxRec*)(a + off[TTX]),
@@ -1641,6 +1669,7 @@ int gpu_taproot_verify_parts(int device, const TaprootJobs* const* Jp, size_t P,
                            (const uint32_t*)(a + off[MSG_ROW]), mid);
         BCC_HIP_TRY(hipGetLastError());
     }
+    if (split_up) BCC_HIP_TRY(hipStreamWaitEvent(st, c.side_done, 0));
     if (int e = schnorr_launch(c.sc, a + off[0], a + off[2], a + off[1], a + off[3], n, st)) {
         ctxs[device].reset();
         return e;
