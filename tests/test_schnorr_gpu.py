@@ -70,7 +70,7 @@ def test_schnorr_kernel_multi_chunk_property():
     import bitcoinconsensus_amd as B
     n = 600_000
     sig, msg, pk = _gen(n, 12)
-    B.set_chunk_lanes(262_144)  # 3 launches of the kernel pair (the default chunk holds 4M)
+    B.set_chunk_lanes(262_144)  # 3 launches of the kernel pair (the default chunk holds 16M)
     try:
         v = np.frombuffer(B.schnorr_verify_tuples(sig.tobytes(), msg.tobytes(), pk.tobytes()), np.uint8)
         assert v.all()
