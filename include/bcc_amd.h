@@ -227,6 +227,10 @@ int bcc_host_verify_tuples(const uint8_t* pub65, const uint8_t* msg32, const uin
  * (e.g. 719, hipErrorLaunchFailure: sticky, never retried). */
 void bcc_debug_fail_device_rounds(int rounds);
 void bcc_debug_fail_device_rounds_code(int rounds, int hip_error);
+/* Test hook: signature-kernel scratch requests above `lanes` lanes fail as out of memory (0: no
+ * cap).  The kernels then run in the largest chunk that fits (halving from the request, at least
+ * 64k lanes) instead of failing the round. */
+void bcc_debug_scratch_cap_lanes(size_t lanes);
 
 #ifdef __cplusplus
 }

@@ -74,6 +74,7 @@ def lib():
         L.bcc_taproot_verify_batch.argtypes = [ctypes.POINTER(TaprootCheck), sz,
                                                ctypes.POINTER(ctypes.c_int),
                                                ctypes.POINTER(ctypes.c_int), vp, ctypes.c_int]
+        L.bcc_debug_scratch_cap_lanes.argtypes = [sz]
         _bind_consensus(L)
         L.bcc_source_hash.restype = ctypes.c_char_p
         _lib = L
@@ -741,6 +742,17 @@ def gen_schnorr_sign(d32, m32, k32, device=0):
     if rc != 0:
         raise RuntimeError(f"mi_gen_schnorr_sign failed: hip error {rc}")
     return sig.raw[: 64 * n], xo.raw[: 32 * n], ok.raw[:n]
+
+
+def release_thread_state():
+    """Frees the calling thread's cached host / device state (bcc_release_thread_state)."""
+    lib().bcc_release_thread_state()
+
+
+def debug_scratch_cap_lanes(lanes):
+    """Test hook: signature-kernel scratch requests above `lanes` lanes fail as out of memory
+    (0: no cap); the library then halves its chunk until it fits (bcc_amd.h)."""
+    lib().bcc_debug_scratch_cap_lanes(lanes)
 
 
 def set_chunk_lanes(lanes):

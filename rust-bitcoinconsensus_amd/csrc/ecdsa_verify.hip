@@ -28,6 +28,7 @@
 // Row loads are two 16-byte loads per lane (a wave covers one contiguous 2 KiB span); every
 // scratch access of a wave is one 256-byte span.
 #include <atomic>
+#include <cstdio>
 #include <cstdlib>
 #include <memory>
 #include <string>
@@ -996,18 +997,46 @@ SigScratch::~SigScratch() {
     }
 }
 
+// Debug cap on the chunk scratch (tests, bcc_debug_scratch_cap_lanes): a larger request fails as
+// out of memory without touching the device.
+static std::atomic<size_t> g_scratch_cap{0};
+
+static hipError_t chunk_malloc(void** p, size_t lanes) {
+    const size_t cap = g_scratch_cap.load(std::memory_order_relaxed);
+    if (cap && lanes > cap) return hipErrorOutOfMemory;
+    return hipMalloc(p, lanes * (QTABLE_WORDS + TSTATE_WORDS) * sizeof(u32));
+}
+
 // Grows sc to n tuples (sinv rows when with_sinv) and min(n, chunk) lanes of chunk scratch;
-// returns the chunk stride C.
+// returns the chunk stride C.  When the device cannot hold the chunk (other callers' scratch, a
+// smaller GPU) the request is halved until it fits (at least 64k lanes): the launches then loop
+// over more, smaller chunks instead of failing the round.  The shortfall is remembered, so the
+// calls of one round agree on C.
 static int ensure_scratch(SigScratch& sc, int dev, size_t n, bool with_sinv, size_t* C) {
     if (sc.dev >= 0 && sc.dev != dev) return (int)hipErrorInvalidDevice;
     sc.dev = dev;
     const size_t want = std::min(chunk_lanes(), (n + 255) & ~(size_t)255);
-    if (want > sc.chunk_cap) {
+    if (want > sc.chunk_cap && want != sc.chunk_short) {
         if (sc.chunk) BCC_HIP_TRY(hipFree(sc.chunk));
         sc.chunk = nullptr;
         sc.chunk_cap = 0;
-        BCC_HIP_TRY(hipMalloc(&sc.chunk, want * (QTABLE_WORDS + TSTATE_WORDS) * sizeof(u32)));
-        sc.chunk_cap = want;
+        sc.chunk_short = 0;
+        constexpr size_t MIN_LANES = (size_t)1 << 16;
+        size_t lanes = want;
+        for (;;) {
+            const hipError_t e = chunk_malloc(&sc.chunk, lanes);
+            if (e == hipSuccess) break;
+            (void)hipGetLastError();
+            sc.chunk = nullptr;
+            if (e != hipErrorOutOfMemory || lanes <= MIN_LANES) return (int)e;
+            lanes = std::max(MIN_LANES, (lanes / 2 + 255) & ~(size_t)255);
+        }
+        if (lanes < want) {
+            fprintf(stderr, "[bcc] signature scratch: %zu lanes do not fit on device %d, using "
+                            "chunks of %zu\n", want, dev, lanes);
+            sc.chunk_short = want;
+        }
+        sc.chunk_cap = lanes;
     }
     if (with_sinv && n > sc.sinv_cap) {
         if (sc.sinv) BCC_HIP_TRY(hipFree(sc.sinv));
@@ -1018,7 +1047,7 @@ static int ensure_scratch(SigScratch& sc, int dev, size_t n, bool with_sinv, siz
         BCC_HIP_TRY(hipMalloc(&sc.sinv, cap * PRE_WORDS * sizeof(u32)));
         sc.sinv_cap = cap;
     }
-    *C = want;
+    *C = std::min(want, sc.chunk_cap);
     return 0;
 }
 
@@ -1057,6 +1086,7 @@ int ecdsa_launch_key(SigScratch& sc, const uint8_t* d_tag, const uint8_t* d_x,
     size_t C = 0;
     if (int e = device_tables(&dev, &gtab, &cus)) return e;
     if (int e = ensure_scratch(sc, dev, n, true, &C)) return e;
+    if (n > C) return 0;  // chunked: the whole prep runs per chunk after K_inv
     u32* qtab = (u32*)sc.chunk;
     u32* state = qtab + C * QTABLE_WORDS;
     hipLaunchKernelGGL(ecdsa_tkey_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
@@ -1415,3 +1445,7 @@ int mi_ecdsa_verify_tuples(const uint8_t* pub65, const uint8_t* msg32, const uin
 }
 
 }  // extern "C"
+
+extern "C" void bcc_debug_scratch_cap_lanes(size_t lanes) {
+    g_scratch_cap.store(lanes, std::memory_order_relaxed);
+}

@@ -143,6 +143,21 @@ void run_on_all_workers(const std::function<void()>& f) {
     for (auto& x : fut) x.get();
 }
 
+namespace {
+std::atomic<size_t> g_active_callers{0};
+thread_local size_t tl_active_depth = 0;
+}  // namespace
+
+ActiveCaller::ActiveCaller() {
+    if (tl_active_depth++ == 0) g_active_callers.fetch_add(1);
+}
+ActiveCaller::~ActiveCaller() {
+    if (--tl_active_depth == 0) g_active_callers.fetch_sub(1);
+}
+size_t other_active_callers() {
+    return g_active_callers.load() - (tl_active_depth ? 1 : 0);
+}
+
 std::future<int> run_async(std::function<int()> job) {
     return worker(-1).submit(std::move(job));  // key -1: the pipeline worker (no device of its own)
 }

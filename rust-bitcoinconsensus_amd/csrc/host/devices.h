@@ -27,6 +27,18 @@ std::future<int> run_async(std::function<int()> job);
 // worker) and waits: releases the state those threads keep for themselves.
 void run_on_all_workers(const std::function<void()>& f);
 
+// Marks a caller inside a batch entry point (verify_batch, the tuple and Taproot batches) for its
+// lifetime.  bcc_release_thread_state releases the shared workers' state only while no caller is
+// active: their device batches and scratch serve every caller's rounds.
+struct ActiveCaller {
+    ActiveCaller();
+    ~ActiveCaller();
+    ActiveCaller(const ActiveCaller&) = delete;
+    ActiveCaller& operator=(const ActiveCaller&) = delete;
+};
+// Callers inside an entry point other than the calling thread's own (0 for a lone caller).
+size_t other_active_callers();
+
 // Contiguous split of `weights` (in order) into k groups of about equal total weight; returns the
 // k + 1 group boundaries (indices into weights).
 std::vector<size_t> split_balanced(const std::vector<size_t>& weights, size_t k);

@@ -731,6 +731,35 @@ int device_round(int dev, const SighashJobs* const* pj, const TupleRows* const* 
     return gpu_verify_parts(dev, pj, pr, P, verdict, stage_s);
 }
 
+}  // namespace
+
+int resilient_round(int dev, const SighashJobs* const* pj, const TupleRows* const* pr, size_t P,
+                    uint8_t* verdict, double* stage_s, size_t* retries, size_t* host_rounds,
+                    const char* who) {
+    int e = device_round(dev, pj, pr, P, verdict, stage_s);
+    if (e != 0 && retryable(e)) {
+        fprintf(stderr, "[bcc] %s: device %d round failed (hip error %d), retrying\n", who, dev, e);
+        (*retries)++;
+        e = device_round(dev, pj, pr, P, verdict, stage_s);
+    }
+    if (e == 0) return 0;
+    if (!host_fallback_enabled()) {
+        fprintf(stderr, "[bcc] %s: device %d round failed (hip error %d), no verdict "
+                        "(BCC_DEVICE_FAILURE_ERROR)\n", who, dev, e);
+        return e;
+    }
+    size_t n = 0;
+    for (size_t p = 0; p < P; p++) n += pr[p]->size();
+    fprintf(stderr, "[bcc] %s: device %d round failed (hip error %d): verifying its %zu checks on "
+                    "the host CPU\n", who, dev, e, n);
+    host_verify_parts(pj, pr, P, verdict, host_threads());
+    note_host_fallback();
+    (*host_rounds)++;
+    return 0;
+}
+
+namespace {
+
 // Shards [t0, t1) of the round on device `dev`, as device batches whose blobs stay under
 // ROUND_BLOB_LIMIT (the device job records use 32-bit byte offsets): consecutive shards are
 // grouped greedily; a single shard above the limit is an error (reported, never silently
@@ -767,26 +796,19 @@ int run_device_group(int dev, const std::vector<Round>& rds, unsigned t0, unsign
             pr.push_back(&rds[t].rows);
         }
         double st = 0;
-        int e = too_big ? 1 : device_round(dev, pj.data(), pr.data(), pj.size(), verdict + row0[g0], &st);
-        if (e != 0 && retryable(e) && !too_big) {
-            fprintf(stderr, "[bcc] verify_batch: device %d round failed (hip error %d), retrying\n",
-                    dev, e);
-            (*retries)++;
-            e = device_round(dev, pj.data(), pr.data(), pj.size(), verdict + row0[g0], &st);
-        }
-        if (e != 0) {
-            if (!host_fallback_enabled()) {
-                fprintf(stderr, "[bcc] verify_batch: device %d round failed (hip error %d), no "
-                                "verdict (BCC_DEVICE_FAILURE_ERROR)\n", dev, e);
-                return e;
+        int e = 1;
+        if (too_big) {
+            if (host_fallback_enabled()) {
+                host_verify_parts(pj.data(), pr.data(), pj.size(), verdict + row0[g0], host_threads());
+                note_host_fallback();
+                (*host_rounds)++;
+                e = 0;
             }
-            fprintf(stderr, "[bcc] verify_batch: device %d round failed (hip error %d): verifying "
-                            "its %zu checks on the host CPU\n",
-                    dev, e, row0[g1] - row0[g0]);
-            host_verify_parts(pj.data(), pr.data(), pj.size(), verdict + row0[g0], host_threads());
-            note_host_fallback();
-            (*host_rounds)++;
+        } else {
+            e = resilient_round(dev, pj.data(), pr.data(), pj.size(), verdict + row0[g0], &st,
+                                retries, host_rounds, "verify_batch");
         }
+        if (e != 0) return e;
         *stage_total += st;
         g0 = g1;
     }
@@ -1262,6 +1284,7 @@ unsigned int bitcoinconsensus_version(void) { return BITCOINCONSENSUS_API_VER; }
 
 long bitcoinconsensus_verify_batch(const bcc_batch_item* items, size_t n, unsigned int flags,
                                    int* ret_out, bitcoinconsensus_error* err_out) {
+    bcc::host::ActiveCaller active;
     try {
         auto t0 = std::chrono::steady_clock::now();
         long r = run_batch(items, n, flags, ret_out, err_out);
@@ -1309,14 +1332,17 @@ void bcc_release_thread_state(void) {
     bcc::release_tuple_thread_state();
     bcc::host::release_pubkey_rows();
     bcc::host::release_team();
-    // the state the per-GPU and pipeline workers keep for the rounds they ran for callers
-    bcc::host::run_on_all_workers([] {
-        bcc::host::taproot_release_thread_state();
-        bcc::release_device_thread_state();
-        bcc::release_tuple_thread_state();
-        bcc::host::release_pubkey_rows();
-        bcc::host::release_team();
-    });
+    // the state the per-GPU and pipeline workers keep for the rounds they ran for callers: only
+    // when no other caller is inside an entry point (their rounds use it)
+    if (bcc::host::other_active_callers() == 0) {
+        bcc::host::run_on_all_workers([] {
+            bcc::host::taproot_release_thread_state();
+            bcc::release_device_thread_state();
+            bcc::release_tuple_thread_state();
+            bcc::host::release_pubkey_rows();
+            bcc::host::release_team();
+        });
+    }
 }
 
 int bcc_set_device(int device) {

@@ -41,6 +41,14 @@ size_t build_sighash_checks(const SighashCheck* checks, size_t n, SighashJobs& j
 void append_round(SighashJobs& dst, TupleRows& dst_rows, const SighashJobs& src,
                   const TupleRows& src_rows);
 
+// One device round of P parts on `dev` with the engine's failure handling: one retry on a fresh
+// device batch for a transient HIP error (*retries), then the device failure policy: the parts are
+// verified on the host CPU (*host_rounds, bcc_host_fallback_rounds) or the error is returned.
+// `who` names the entry point in the stderr log.
+int resilient_round(int dev, const SighashJobs* const* pj, const TupleRows* const* pr, size_t P,
+                    uint8_t* verdict, double* stage_s, size_t* retries, size_t* host_rounds,
+                    const char* who);
+
 // Frees the calling thread's Taproot job buffers (host/taproot.cpp).
 void taproot_release_thread_state();
 

@@ -164,8 +164,11 @@ void apply_key_hashes(const TupleRows& R, uint8_t* verdict) {
         key[0] = R.tag[row];
         memcpy(key + 1, &R.x[32 * (size_t)row], 32);
         size_t n = 33;
-        if (key[0] != 2 && key[0] != 3) {
-            memcpy(key + 33, &R.y[32 * (size_t)row], 32);
+        if (key[0] != 2 && key[0] != 3) {  // a 65-byte key (add_lazy stores its y; else zero)
+            if (R.y.size() >= 32 * ((size_t)row + 1))
+                memcpy(key + 33, &R.y[32 * (size_t)row], 32);
+            else
+                memset(key + 33, 0, 32);
             n = 65;
         }
         hash160(key, n, h);

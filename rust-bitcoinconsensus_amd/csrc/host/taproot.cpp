@@ -432,6 +432,7 @@ extern "C" int bcc_taproot_verify_batch(const bcc_taproot_check* items, size_t n
                                         int* serror_out, unsigned char* sighash_out, int device) {
     if (n == 0) return 0;
     if (!items || !ret_out || !serror_out) return -1;
+    bcc::host::ActiveCaller active;
     std::vector<int> devs = device < 0 ? bcc::host::device_list() : std::vector<int>{device};
     const size_t D = std::max<size_t>(1, std::min<size_t>(devs.size(), (n + 4095) / 4096));
     // contiguous item ranges per device, cut only between runs of the same tx

@@ -3,6 +3,7 @@
 
 #include <cstdlib>
 #include <condition_variable>
+#include <exception>
 #include <memory>
 #include <mutex>
 #include <thread>
@@ -27,10 +28,20 @@ public:
             gen_++;
         }
         cv_.notify_all();
-        f(0);
+        std::exception_ptr err;
+        try {
+            f(0);
+        } catch (...) {
+            err = std::current_exception();
+        }
+        // every worker must be done with f before it goes out of scope, even when f(0) threw
         std::unique_lock<std::mutex> lk(mu_);
         done_.wait(lk, [this] { return pending_ == 0; });
         job_ = nullptr;
+        if (!err) err = worker_err_;
+        worker_err_ = nullptr;
+        lk.unlock();
+        if (err) std::rethrow_exception(err);
     }
 
     void stop() {
@@ -66,8 +77,14 @@ private:
             if (id >= T_) continue;  // this pass needs fewer workers
             const std::function<void(unsigned)>* f = job_;
             lk.unlock();
-            (*f)(id);
+            std::exception_ptr err;
+            try {
+                (*f)(id);
+            } catch (...) {
+                err = std::current_exception();
+            }
             lk.lock();
+            if (err && !worker_err_) worker_err_ = err;  // rethrown by run() on the caller
             if (--pending_ == 0) done_.notify_one();
         }
     }
@@ -76,6 +93,7 @@ private:
     std::condition_variable cv_, done_;
     std::vector<std::thread> th_;
     const std::function<void(unsigned)>* job_ = nullptr;
+    std::exception_ptr worker_err_;
     unsigned T_ = 0, pending_ = 0;
     uint64_t gen_ = 0;
     bool stop_ = false;
@@ -101,16 +119,28 @@ void run_team(unsigned T, const std::function<void(unsigned)>& f) {
         return;
     }
     if (tl_in_team_run || !teams_on()) {
+        std::vector<std::exception_ptr> errs(T);
+        auto guarded = [&](unsigned t) {
+            try {
+                f(t);
+            } catch (...) {
+                errs[t] = std::current_exception();
+            }
+        };
         std::vector<std::thread> th;
-        for (unsigned t = 1; t < T; t++) th.emplace_back(f, t);
-        f(0);
+        for (unsigned t = 1; t < T; t++) th.emplace_back(guarded, t);
+        guarded(0);
         for (auto& x : th) x.join();
+        for (auto& e : errs)
+            if (e) std::rethrow_exception(e);
         return;
     }
     if (!tl_team) tl_team.reset(new Team());
-    tl_in_team_run = true;
+    struct InRun {  // cleared however run() leaves
+        InRun() { tl_in_team_run = true; }
+        ~InRun() { tl_in_team_run = false; }
+    } in_run;
     tl_team->run(T, f);
-    tl_in_team_run = false;
 }
 
 void release_team() { tl_team.reset(); }

@@ -12,6 +12,8 @@
 
 #include "bcc_amd.h"
 #include "devices.h"
+#include "engine.h"
+#include "host_verify.h"
 #include "sighash.h"
 
 namespace bcc {
@@ -84,6 +86,7 @@ extern "C" int bcc_pubkey_verify_batch(const uint8_t* pub_blob, const uint64_t* 
                                        int device) {
     if (n == 0) return 0;
     if (!pub_off || !sig_off || !msg32 || !verdict) return -1;
+    bcc::host::ActiveCaller active;
     std::vector<int> devs = device < 0 ? bcc::host::device_list() : std::vector<int>{device};
     const size_t D = std::min<size_t>(devs.size(), (n + 4095) / 4096);
     std::vector<std::function<int()>> jobs;
@@ -94,7 +97,17 @@ extern "C" int bcc_pubkey_verify_batch(const uint8_t* pub_blob, const uint64_t* 
             bcc::host::parse_rows(pub_blob, pub_off + lo, msg32 + 32 * lo, sig_blob, sig_off + lo,
                                   hi - lo, rows);
             bcc::SighashJobs none;
-            return bcc::gpu_verify_batch(devs[d], none, rows, verdict + lo);
+            if (hi - lo <= bcc::host::host_small_round()) {  // latency: the host lane code
+                bcc::host::host_verify_rows(rows, rows.msg.data(), verdict + lo,
+                                            bcc::host::host_threads());
+                return 0;
+            }
+            const bcc::SighashJobs* jp = &none;
+            const bcc::TupleRows* rp = &rows;
+            size_t retries = 0, host_rounds = 0;
+            double st = 0;
+            return bcc::host::resilient_round(devs[d], &jp, &rp, 1, verdict + lo, &st, &retries,
+                                              &host_rounds, "pubkey_verify_batch");
         });
     }
     devs.resize(D);

@@ -331,6 +331,7 @@ struct SigScratch {
     size_t sinv_cap = 0;   // tuples
     void* chunk = nullptr;
     size_t chunk_cap = 0;  // lanes
+    size_t chunk_short = 0;  // a chunk request the device could not hold (served by chunk_cap)
     size_t key_ready = 0;  // tuples whose key half of the prep ran ahead (ecdsa_launch_key)
     size_t q_ready = 0;    // tuples whose Q ladder ran ahead (ecdsa_launch_q)
     SigScratch() = default;

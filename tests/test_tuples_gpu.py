@@ -96,3 +96,25 @@ def test_c4_chunking_invariance(c4):
         assert c4.verdicts() == one
     finally:
         B.set_chunk_lanes(0)
+
+
+def test_scratch_oom_halves_the_chunk(c4):
+    """when the device cannot hold the default 16M-lane chunk scratch (other callers'
+    scratch, a smaller GPU), the round runs in halved chunks on the GPU -- same verdicts, no host
+    fallback (the autouse fixture checks bcc_host_fallback_rounds) and no error."""
+    import bitcoinconsensus_amd as B
+    B.release_thread_state()  # drop this thread's cached scratch so the next round reallocates
+    B.debug_scratch_cap_lanes(100_000)  # 120,064 lanes wanted: 65,536-lane chunks fit
+    try:
+        h = c4.host()
+        n = 120_000
+        po, so = h["pub_off"][: n + 1], h["sig_off"][: n + 1]
+        tuples = [(h["pub_blob"][po[i]:po[i + 1]].tobytes(), h["msg32"][32 * i:32 * i + 32].tobytes(),
+                   h["sig_blob"][so[i]:so[i + 1]].tobytes()) for i in range(n)]
+        v = B.pubkey_verify_batch(tuples)
+    finally:
+        B.debug_scratch_cap_lanes(0)
+        B.release_thread_state()
+    want = np.frombuffer(c4.verdicts(), np.uint8)[:n]
+    got = np.frombuffer(v, np.uint8)
+    assert (got == want).all(), np.nonzero(got != want)[0][:20]

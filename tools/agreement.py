@@ -14,7 +14,14 @@ err) must agree on every item.  Most chunks use VERIFY_ALL, two use P2SH|DERSIG 
 C4: the adversarial ECDSA tuple set (90 % valid + 18 classes, include/bcc_amd.h bcc_tupleset_c4)
 verified on the GPU, then every tuple re-verified by the REFERENCE (oracle/_ref: CPubKey::Verify of
 Bitcoin Core v0.21 + libsecp256k1, 16 host threads).  C5: the BIP340 set likewise against
-secp256k1_schnorrsig_verify.  Writes per-class counts and mismatches as JSON."""
+secp256k1_schnorrsig_verify.  Writes per-class counts and mismatches as JSON.
+
+--host-c4 / --host-scripts: the same checks with bcc_set_host_small_round(huge), i.e. every round
+verified by the engine's HOST lane code (4x64 limbs, safegcd inverses, wNAF-5 Q half,
+csrc/host/host_verify.cpp) -- the path that answers every lone verify() by default (rounds of <= 16
+checks).  The C4 leg goes through bcc_pubkey_verify_batch (host length filter + lax DER, then the
+host lane code), the script leg through bitcoinconsensus_verify_batch.  Every record carries the
+library's source_hash, so a run can be tied to the tree it tested."""
 import argparse
 import json
 import os
@@ -28,6 +35,48 @@ sys.path[:0] = [os.path.join(ROOT, "rust-bitcoinconsensus_amd"), os.path.join(RO
 import bitcoinconsensus_amd as B  # noqa: E402
 from fixtures import bip340_vectors  # noqa: E402
 from oracle_ctypes import Reference  # noqa: E402
+
+
+def check_host_c4(n, R, threads):
+    """C4 through bcc_pubkey_verify_batch with every round on the host lane code."""
+    import ctypes
+    t0 = time.time()
+    ts = B.TupleSet(n, kind="c4")
+    h = ts.host()
+    t1 = time.time()
+    u8p, u64p = ctypes.c_char_p, ctypes.POINTER(ctypes.c_uint64)
+    out = np.zeros(n, np.uint8)
+    B.set_host_small_round(1 << 62)
+    try:
+        rc = B.lib().bcc_pubkey_verify_batch(h["pub_blob"].ctypes.data_as(u8p),
+                                             h["pub_off"].ctypes.data_as(u64p),
+                                             h["msg32"].ctypes.data_as(u8p),
+                                             h["sig_blob"].ctypes.data_as(u8p),
+                                             h["sig_off"].ctypes.data_as(u64p),
+                                             out.ctypes.data_as(u8p), n, 0)
+    finally:
+        B.set_host_small_round(16)
+    t2 = time.time()
+    assert rc == 0, rc
+    ref, secs = R.pubkey_verify_blob(h["pub_blob"], h["pub_off"], h["msg32"], h["sig_blob"],
+                                     h["sig_off"], threads=threads)
+    cls = h["cls"]
+    mism = np.nonzero(out != ref)[0]
+    per = {}
+    for c in range(int(cls.max()) + 1):
+        m = cls == c
+        per[B.TupleSet.C4_CLASSES[c]] = dict(n=int(m.sum()), host_valid=int(out[m].sum()),
+                                             ref_valid=int(ref[m].sum()),
+                                             mismatches=int((out[m] != ref[m]).sum()))
+    res = dict(config="host_c4", path="host lane code (bcc_pubkey_verify_batch, host small round)",
+               n=n, host_valid=int(out.sum()), ref_valid=int(ref.sum()),
+               mismatches=int(len(mism)), first_mismatches=[int(i) for i in mism[:20]],
+               host_threads=B.host_threads(), generate_s=round(t1 - t0, 2),
+               host_verify_s=round(t2 - t1, 2), reference_s=round(secs, 2),
+               reference_threads=threads, classes=per)
+    ts.free()
+    print(json.dumps({k: res[k] for k in res if k != "classes"}), flush=True)
+    return res
 
 
 def check(kind, n, R, threads):
@@ -64,7 +113,7 @@ def check(kind, n, R, threads):
     return out
 
 
-def check_scripts(total, R, threads):
+def check_scripts(total, R, threads, host=False):
     import ctypes
     L, BL = B.lib(), B.blib()
     BL.bcc_workload_mutate.argtypes = [ctypes.c_void_p, ctypes.c_double, ctypes.c_uint64,
@@ -103,8 +152,14 @@ def check_scripts(total, R, threads):
         ret = np.zeros(n, np.int32)
         err = np.zeros(n, np.int32)
         g0 = time.time()
-        rc = L.bitcoinconsensus_verify_batch(items, n, flags, ret.ctypes.data, err.ctypes.data)
+        if host:
+            B.set_host_small_round(1 << 62)
+        try:
+            rc = L.bitcoinconsensus_verify_batch(items, n, flags, ret.ctypes.data, err.ctypes.data)
+        finally:
+            B.set_host_small_round(16)
         g1 = time.time()
+        st = B.last_batch_stats()
         rret = np.zeros(n, np.int32)
         rerr = np.zeros(n, np.int32)
         rs = R.L.ref_bulk_verify_items(threads, n, items, flags, rret.ctypes.data,
@@ -117,6 +172,7 @@ def check_scripts(total, R, threads):
             e["ref_valid"] += int(rret[m].sum())
             e["mismatches"] += int(((ret != rret) | (err != rerr))[m].sum())
         rec = dict(chunk=chunk, workload=kind, flags=flags, items=n, rc=int(rc),
+                   host_rounds=int(st["host_rounds"]), rounds=int(st["rounds"]),
                    gpu_valid=int(ret.sum()), ref_valid=int(rret.sum()), mismatches=int(len(bad)),
                    first_mismatches=[int(i) for i in bad[:10]],
                    verify_batch_s=round(g1 - g0, 2), reference_s=round(rs, 2),
@@ -130,7 +186,10 @@ def check_scripts(total, R, threads):
         wl.free()
         done += n
         chunk += 1
-    out.update(config="scripts", reference_threads=threads, mutated_rate=0.12)
+    out.update(config="host_scripts" if host else "scripts", reference_threads=threads,
+               mutated_rate=0.12,
+               path=("every round on the host lane code (host small round)" if host else
+                     "device rounds (GPU sighash + ECDSA kernels)"))
     return out
 
 
@@ -139,6 +198,8 @@ def main():
     ap.add_argument("--c4", type=int, default=10_000_000)
     ap.add_argument("--c5", type=int, default=4_000_000)
     ap.add_argument("--scripts", type=int, default=0)
+    ap.add_argument("--host-c4", type=int, default=0)
+    ap.add_argument("--host-scripts", type=int, default=0)
     ap.add_argument("--threads", type=int, default=16)
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "agreement.json"))
     a = ap.parse_args()
@@ -150,6 +211,13 @@ def main():
         res.append(check("c5", a.c5, R, a.threads))
     if a.scripts:
         res.append(check_scripts(a.scripts, R, a.threads))
+    if a.host_c4:
+        res.append(check_host_c4(a.host_c4, R, a.threads))
+    if a.host_scripts:
+        res.append(check_scripts(a.host_scripts, R, a.threads, host=True))
+    for r in res:
+        r["source_hash"] = B.source_hash()
+        r["host_fallback_rounds"] = B.host_fallback_rounds()
     json.dump(res, open(a.out, "w"), indent=1)
     assert all(r["mismatches"] == 0 for r in res), "GPU / reference verdicts differ"
 
