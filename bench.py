@@ -47,12 +47,9 @@ DEFAULT_N = {"c2": 1_000_000, "c3": 4000, "c4": 8_000_000, "c5": 16_000_000, "c5
 SEEDS = {"c2": 0x5EED0001, "c3": 0x5EED0003, "c4": 0x5EED0004, "c5": 0x5EED0005,
          "c5t": 0x5EED0006}
 # the ECDSA stage's kernels: the square-root-free path (default) or the round-1 path
-_LEGACY = os.environ.get("BCC_ECDSA_PATH") == "legacy"
-ECDSA_KERNELS = ("ecdsa (batch_sinv + ecdsa_key + ecdsa_prep + ecdsa_ladder)" if _LEGACY else
-                 "ecdsa (batch_sinv + ecdsa_tkey + ecdsa_tscal_q + twist_ladder_q + twist_ladder_g + "
+ECDSA_KERNELS = ("ecdsa (batch_sinv + ecdsa_tkey + ecdsa_tscal_q + twist_ladder_q + twist_ladder_g + "
                  "twist_fin<ecdsa>; no key square root)")
-SCHNORR_KERNELS = ("schnorr (prep + ladder + y-parity batch inversion)" if _LEGACY else
-                   "schnorr (schnorr_tprep + twist_ladder<bip340> + twist_fin<bip340>; "
+SCHNORR_KERNELS = ("schnorr (schnorr_tprep + twist_ladder<bip340> + twist_fin<bip340>; "
                    "no lift_x square root)")
 CPU_PASSES = 3                    # timed passes of the CPU baseline (median), after 1 warm-up
 
@@ -722,6 +719,9 @@ def main():
     ap.add_argument("--no-extra", action="store_true",
                     help="skip the drop-in / single-call / host-buffer extras (profiling runs: "
                          "every launch is then a full-size one)")
+    ap.add_argument("--sustain-s", type=float, default=3.0,
+                    help="after the timed steps, keep stepping for this long (HIP-event timed, "
+                         "reported as `sustained`; gives a GPU-busy sampler a multi-second window)")
     ap.add_argument("--traffic", type=float, default=None,
                     help="HBM bytes per ECDSA launch from a rocprofv3 --pmc run (profiles/)")
     args = ap.parse_args()
@@ -778,6 +778,42 @@ def main():
     barrier()
     elapsed = time.perf_counter() - ts
     elapsed, n_valid_all = aggregate(elapsed, n_valid, world)
+
+    # sustained window: the same step back to back for >= --sustain-s seconds on every rank
+    # (outside the K timed steps; a driver-side GPU-busy sampler sees a multi-second busy run)
+    sustained = None
+    if args.sustain_s > 0:
+        per = elapsed / max(1, args.steps)
+        k = max(1, int(args.sustain_s / max(per, 1e-4)))
+        barrier()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(k):
+            job.step(sp)
+        torch.cuda.synchronize()
+        barrier()
+        sus, _ = aggregate(time.perf_counter() - t1, 0, world)
+        sustained = dict(steps=k, seconds=sus, value=job.units * world * k / sus,
+                         ms_per_step=sus / k * 1e3)
+
+    # the drop-in per rank (north star: the per-input verify_batch API at 1..8 GPUs): every rank
+    # calls bitcoinconsensus_verify_batch on its own slice from host buffers at the same time,
+    # barrier-bracketed, max over ranks; reported beside value (host pass + H2D included)
+    per_rank = None
+    if args.config == "c2" and not args.no_extra:
+        job.wl.verify_batch()  # warm this rank's host / device state
+        best = None
+        for _ in range(2):
+            barrier()
+            t1 = time.perf_counter()
+            job.wl.verify_batch()
+            dt, _ = aggregate(time.perf_counter() - t1, 0, world)
+            best = dt if best is None else min(best, dt)
+        per_rank = dict(inputs_per_s=job.n * world / best, ms=best * 1e3, ranks=world,
+                        inputs_per_rank=job.n, host_threads_per_rank=B.host_threads(),
+                        cpu_share_per_rank=B.cpu_share(),
+                        note="one bitcoinconsensus_verify_batch caller per GPU on its own slice, "
+                             "all ranks at once, max wall time over ranks (best of 2)")
     # the global validity bitmap (RCCL all-gather, outside the timed loop)
     gathered = gather_verdicts(bytearray(job.item_verdicts()), world)
     bitmap = dict(units=int(len(gathered)), valid=int(gathered.sum()),
@@ -849,6 +885,10 @@ def main():
         }
         if not args.no_extra:
             out.update(job.extra(sighash_ms))
+        if sustained:
+            out["sustained"] = sustained
+        if per_rank:
+            out["drop_in_per_rank"] = per_rank
         out["source_hash"] = B.source_hash()
         out["verdicts_valid"] = n_valid_all
         out["validity_bitmap"] = bitmap

@@ -124,9 +124,8 @@ int bcc_set_chunk_lanes(size_t lanes);
 
 /* bitcoinconsensus_verify_batch pipelines a batch of at least two chunks: it is cut into chunks of
  * about `items` inputs (whole transactions), and each chunk's device round runs on a worker thread
- * while the host deserializes and interprets the next chunk.  0 disables it (the default, or the
- * BCC_PIPELINE_CHUNK environment variable; measured slower end to end on one MI355X box, see
- * DESIGN.md).  Results never depend on it. */
+ * while the host deserializes and interprets the next chunk.  Default 500000 (or the
+ * BCC_PIPELINE_CHUNK environment variable); 0 disables it.  Results never depend on it. */
 int bcc_set_pipeline_chunk(size_t items);
 
 /* Signature checks whose serial SHA-256 chain is longer than `blocks` 64-byte blocks (the legacy

@@ -1,16 +1,13 @@
-// Per-lane signature verification: one lane = one (pubkey, msg32, r, s) tuple.
-//
-// ECDSA restates secp256k1_ecdsa_verify semantics (secp256k1.c:423-438 + ecdsa_impl.h:207-275 +
-// eckey_impl.h:17-35); BIP340 restates secp256k1_schnorrsig_verify (modules/schnorrsig/
-// main_impl.h:190-237) with the x-only lift of modules/extrakeys/main_impl.h:21-39.  Both share
-// one SIMT-friendly multi-scalar ladder:
-//   R = u1*G + u2*Q,  u2 = k1 + lambda*k2 (GLV),  u1 = lo + 2^128*hi
-//   four 128-bit scalars, each recoded into SIGNED ODD fixed windows (every digit nonzero, so
-//   every lane of a wave adds at the same bit positions: no wNAF divergence);
-//   Q table {1,3,..,15}Q on an isomorphic curve (shared Z, no inversion), G tables in LDS;
-//   inversion-free final test r*Z^2 == X (ECDSA also (r+n)*Z^2 == X when r < p-n).
-// Verdicts are a pure function of the group arithmetic, so they equal the reference's on every
-// input, including the exceptional additions (P == +-Q) that adversarial inputs can reach.
+// Per-lane building blocks of the signature ladders (one lane = one tuple), shared by the
+// verification path (ecdsa_twist.h: ECDSA per secp256k1_ecdsa_verify, secp256k1.c:423-438 +
+// ecdsa_impl.h:207-275; BIP340 per secp256k1_schnorrsig_verify, modules/schnorrsig/
+// main_impl.h:190-237) and the synthetic-input generators (keygen and signing below):
+//   signed odd fixed-window recoding (every digit nonzero, so every lane of a wave adds at the
+//   same bit positions: no wNAF divergence), the shared-Z odd-multiples table of Q on an
+//   isomorphic curve (no inversion), the mixed addition into an accumulator, the BIP340
+//   challenge, and the affine G tables of the generators' fixed-base ladder.
+// (The round-1 verify lanes -- key decompression by a square root, G tables in LDS -- were retired
+// with their kernels in round 4; ecdsa_twist.h is the verification path.)
 #pragma once
 #include "secp256k1_device.h"
 #include "sha256_device.h"
@@ -105,106 +102,17 @@ BCC_HD void acc_add(gej& acc, bool& inf, const fe& px, const fe& py, const fe& s
     inf = rinf;
 }
 
-// Everything the ladder needs after the prep phase (the Q table lives in the QT store).
-struct LadderState {
-    u32 k[4][4];   // the four odd 128-bit scalars: k1 (Q), k2 (lambda Q), u1 lo (G), u1 hi (2^128 G)
-    u32 flags;     // bit0 valid, bit1 neg(k1), bit2 neg(k2), bits 3..6 odd-corrections of k[0..3]
-    fe sigma;      // E' = E scaled by sigma: a point (x, y) of E is (x sigma^2, y sigma^3) on E'
-    sc r;          // x-coordinate to test against: ECDSA r, or BIP340 r.x (< p)
-    // the ladder reads the state through these (the device view loads k and r at use)
-    BCC_HD u32 kword(int s, int w) const { return k[s][w]; }
-    BCC_HD void get_r(sc& o) const { o = r; }
-};
-
+// TwistState::flags bits (ecdsa_twist.h): valid, negated GLV halves, odd-fix corrections
 enum : u32 {
     LS_VALID = 1u, LS_NEG0 = 2u, LS_NEG1 = 4u, LS_CORR0 = 8u,  // LS_CORR0 << slot
 };
 
-// The ladder's scalars: u2 (for Q) split by GLV into k1 + lambda k2, u1 (for G) split at bit
-// 128 (ecmult_impl.h:446-559 splits the same way); every half made odd.  Sets st.k, st.flags.
-BCC_HD void set_ladder_scalars(LadderState& st, const sc& u1, const sc& u2) {
-    sc k1, k2;
-    sc_split_lambda(k1, k2, u2);
-    // |k| < 2^128: a split half whose upper 128 bits are nonzero is negative (n - |k|)
-    u32 flags = LS_VALID;
-    if ((k1.v[4] | k1.v[5] | k1.v[6] | k1.v[7]) != 0) {
-        sc_neg(k1, k1);
-        flags |= LS_NEG0;
-    }
-    if ((k2.v[4] | k2.v[5] | k2.v[6] | k2.v[7]) != 0) {
-        sc_neg(k2, k2);
-        flags |= LS_NEG1;
-    }
-    for (int i = 0; i < 4; i++) {
-        st.k[0][i] = k1.v[i];
-        st.k[1][i] = k2.v[i];
-        st.k[2][i] = u1.v[i];
-        st.k[3][i] = u1.v[4 + i];
-    }
-    // make each scalar odd: k even -> use k+1 (never carries), subtract the base point at the end
-    for (int s = 0; s < 4; s++) {
-        if ((st.k[s][0] & 1u) == 0) flags |= LS_CORR0 << s;
-        st.k[s][0] |= 1u;
-    }
-    st.flags = flags;
-}
-
 // Q table: odd multiples {1,3,..,15}Q on E' with one shared Z (ecmult_odd_multiples_table +
-// ge_globalz_set_table_gej restated, ecmult_impl.h:85-143), plus the lambda images beta*x.
-// Returns sigma, the scale of E' (total Z of the table).
-template <class QT>
-BCC_HD void build_q_table(const fe& qx, const fe& qy, QT& qt, fe& sigma) {
-    gej q1, d;
-    q1.x = qx; q1.y = qy; q1.z = fe_one();
-    gej_double(d, q1);                           // D = 2Q (Jacobian on E)
-    fe zd2, zd3, one = fe_one();
-    fe_sqr(zd2, d.z);
-    fe_mul(zd3, zd2, d.z);
-    gej cur;                                     // on E_{Zd}, D is affine (d.x, d.y)
-    fe_mul(cur.x, qx, zd2);
-    fe_mul(cur.y, qy, zd3);
-    cur.z = one;
-    qt.put(0, 0, cur.x);
-    qt.put(0, 2, cur.y);
-    for (int i = 1; i < QTAB; i++) {             // T_i = T_{i-1} + D, Z_i = Z_{i-1} * H_i
-        bool inf_unused;
-        gej nxt;
-        fe h;
-        gej_add_zinv(nxt, inf_unused, cur, d.x, d.y, one, false, &h);
-        cur = nxt;
-        qt.put(i, 0, cur.x);
-        qt.put(i, 2, cur.y);
-        qt.put(i, 1, h);                         // slot 1 holds H_i until the rescale pass
-    }
-    // rescale to the common Z_last: f_i = prod_{j>i} H_j
-    fe f = one, f2, f3, beta;
-    {
-        const u32 bl[8] = BCC_BETA_LIMBS;
-        fe_set(beta, bl);
-    }
-    for (int i = QTAB - 1; i >= 0; i--) {
-        fe ex, ey, h;
-        qt.get(i, 0, ex);
-        qt.get(i, 2, ey);
-        if (i > 0) qt.get(i, 1, h);
-        fe_sqr(f2, f);
-        fe_mul(f3, f2, f);
-        fe_mul(ex, ex, f2);
-        fe_mul(ey, ey, f3);
-        fe bx;
-        fe_mul(bx, ex, beta);
-        qt.put(i, 0, ex);
-        qt.put(i, 1, bx);
-        qt.put(i, 2, ey);
-        if (i > 0) fe_mul(f, f, h);
-    }
-    fe_mul(sigma, d.z, cur.z);                   // total scale Zd * Z_last
-}
-
-// The same table by co-Z arithmetic (Meloni's ZADDU; DBLU for the first doubling): every
-// T_i = T_{i-1} + 2Q is one co-Z addition that also re-expresses 2Q with T_i's Z (4M + 2S instead
-// of a mixed addition's 8M + 3S); the Z ratios h_i = X_{2Q} - X_{T_{i-1}} feed the same backward
-// rescale to the common Z as build_q_table.  Same output (entries up to the curve scale sigma).
+// ge_globalz_set_table_gej restated, ecmult_impl.h:85-143), plus the lambda images beta*x; returns
+// sigma, the scale of E' (total Z of the table).  Built by co-Z arithmetic (Meloni's ZADDU; DBLU
+// for the first doubling): every T_i = T_{i-1} + 2Q is one co-Z addition that also re-expresses
+// 2Q with T_i's Z (4M + 2S instead of a mixed addition's 8M + 3S); the Z ratios
+// h_i = X_{2Q} - X_{T_{i-1}} then rescale every entry to the common Z by a backward H-product.
 template <class QT>
 BCC_HD void build_q_table_coz(const fe& qx, const fe& qy, QT& qt, fe& sigma) {
     fe dx, dy, tx, ty;
@@ -288,171 +196,6 @@ BCC_HD void curve_rhs(fe& r, const fe& x) {
     fe_add(r, r, seven);
 }
 
-// Prep phase: pubkey parse/decompression (stage b), scalar checks, u1/u2, GLV split, odd fix-ups
-// and the Q table.  Returns false (and st.flags = 0) when the tuple is rejected outright.
-// tag = pubkey header byte (0 for "length invalid"), px/py as parsed from the big-endian bytes
-// (py ignored for compressed keys), r/s/m as raw integers from big-endian bytes.
-// sinv_pre: s^-1 mod n from the batched-inversion kernel (nullptr: invert here).
-// Pubkey parse (eckey_impl.h:17-35, ge_set_xo_var / ge_is_valid_var): tag = header byte (0 for
-// "length invalid"), px/py as parsed from the big-endian bytes (py ignored for compressed keys).
-// On success qy is the affine y (normalized for compressed keys).
-BCC_HD bool pubkey_load(u32 tag, const fe& px, const fe& py_in, fe& qy) {
-    bool compressed = (tag == 2u || tag == 3u);
-    bool full = (tag == 4u || tag == 6u || tag == 7u);
-    if (!compressed && !full) return false;
-    if (!fe_lt_p(px)) return false;
-    qy = py_in;
-    fe x3, t;
-    curve_rhs(x3, px);                       // x^3 + 7
-    if (compressed) {
-        if (!fe_sqrt(qy, x3)) return false;  // ge_set_xo_var: no square root
-        fe_normalize(qy);
-        if ((qy.v[0] & 1u) != (tag == 3u ? 1u : 0u)) fe_neg(qy, qy);
-        return true;
-    }
-    if (!fe_lt_p(qy)) return false;
-    if (tag != 4u && (qy.v[0] & 1u) != (tag == 7u ? 1u : 0u)) return false;  // hybrid parity
-    fe_sqr(t, qy);
-    return fe_equal(t, x3);                  // ge_is_valid_var
-}
-
-// Prep after the pubkey parse: scalar checks, u1/u2, GLV split, odd fix-ups and the Q table for
-// an already loaded key (qx, qy).
-template <class QT>
-BCC_HD bool ecdsa_prep_loaded(const fe& qx, const fe& qy, const sc& r_in, const sc& s_in,
-                              const sc& m_in, const sc* sinv_pre, QT& qt, LadderState& st);
-
-template <class QT>
-BCC_HD bool ecdsa_prep_lane(u32 tag, const fe& px_in, const fe& py_in, const sc& r_in,
-                            const sc& s_in, const sc& m_in, const sc* sinv_pre, QT& qt,
-                            LadderState& st) {
-    st.flags = 0;
-    fe qy;
-    if (!pubkey_load(tag, px_in, py_in, qy)) return false;
-    return ecdsa_prep_loaded(px_in, qy, r_in, s_in, m_in, sinv_pre, qt, st);
-}
-
-template <class QT>
-BCC_HD bool ecdsa_prep_loaded(const fe& qx, const fe& qy, const sc& r_in, const sc& s_in,
-                              const sc& m_in, const sc* sinv_pre, QT& qt, LadderState& st) {
-    const u32 N[8] = BCC_N_LIMBS;
-    st.flags = 0;
-    // ---- scalars (ecdsa_impl.h:216-222) ----
-    if (u256_is_zero(r_in.v) || u256_is_zero(s_in.v)) return false;
-    if (!u256_lt(r_in.v, N) || !u256_lt(s_in.v, N)) return false;
-    sc m = m_in;
-    if (!u256_lt(m.v, N)) {                      // scalar_set_b32 reduction
-        u32 tmp[8];
-        u256_sub(tmp, m.v, N);
-        for (int i = 0; i < 8; i++) m.v[i] = tmp[i];
-    }
-    sc sinv, u1, u2;
-    if (sinv_pre) sinv = *sinv_pre;
-    else sc_inv(sinv, s_in);
-    sc_mul(u1, m, sinv);
-    sc_mul(u2, r_in, sinv);
-    set_ladder_scalars(st, u1, u2);
-    st.r = r_in;
-    build_q_table(qx, qy, qt, st.sigma);
-    return true;
-}
-
-// Strauss over bit positions TOPQ..0 with shared doublings and the odd-fix corrections.
-// acc receives R on E' (Jacobian); returns true when R is the point at infinity.
-template <class ST, class QT, class GT>
-BCC_HD bool ladder_accumulate(const ST& st, const QT& qt, const GT& gt, gej& acc) {
-    const bool neg0 = (st.flags & LS_NEG0) != 0, neg1 = (st.flags & LS_NEG1) != 0;
-    bool inf = false;
-    {
-        bool ng;
-        u32 idx = digit_index(st.kword(0, 0), st.kword(0, 1), st.kword(0, 2), st.kword(0, 3), TOPQ, WQ,
-                              TOPQ, ng);
-        qt.get((int)idx, 0, acc.x);
-        qt.get((int)idx, 2, acc.y);
-        if (neg0) fe_neg(acc.y, acc.y);
-        acc.z = fe_one();
-    }
-    // One loop, one call site of the doubling and of the addition: the body is compiled once
-    // (a few thousand instructions) and stays resident in the instruction cache.  pos == -1 is
-    // the odd-fix step: for every scalar that was made odd, add the negated base point.
-#pragma unroll 1
-    for (int pos = TOPQ; pos >= -1; pos--) {
-        if (pos >= 0 && pos != TOPQ && !inf) {
-            gej t;
-            gej_double(t, acc);
-            acc = t;
-        }
-#pragma unroll 1
-        for (int slot = 0; slot < 4; slot++) {
-            const bool isg = slot >= 2;
-            const bool kneg = slot == 0 ? neg0 : slot == 1 ? neg1 : false;
-            u32 idx;
-            bool sneg;
-            if (pos >= 0) {
-                bool active = isg ? ((pos % WG) == 0 && pos <= TOPG) : ((pos % WQ) == 0);
-                if (slot == 0 && pos == TOPQ) active = false;  // initial value
-                if (!active) continue;
-                bool dneg;
-                idx = digit_index(st.kword(slot, 0), st.kword(slot, 1), st.kword(slot, 2),
-                                  st.kword(slot, 3), pos, isg ? WG : WQ, isg ? TOPG : TOPQ, dneg);
-                sneg = dneg ^ kneg;
-            } else {
-                if (!(st.flags & (LS_CORR0 << slot))) continue;  // per lane
-                idx = 0;
-                sneg = !kneg;
-            }
-            fe px, py;
-            if (isg) {
-                gt.get(slot - 2, (int)idx, px, py);
-            } else {
-                qt.get_pair((int)idx, slot == 0 ? 0 : 1, px, py);  // (x or beta*x, y)
-            }
-            if (sneg) fe_neg(py, py);
-            acc_add(acc, inf, px, py, st.sigma, isg);
-        }
-    }
-    return inf;
-}
-
-// ECDSA ladder phase: R = u1 G + u2 Q, then the inversion-free x-coordinate test.  Returns the
-// verdict.
-template <class ST, class QT, class GT>
-BCC_HD int ecdsa_ladder_lane(const ST& st, const QT& qt, const GT& gt) {
-    const u32 N[8] = BCC_N_LIMBS;
-    if (!(st.flags & LS_VALID)) return 0;
-    gej acc;
-    if (ladder_accumulate(st, qt, gt, acc)) return 0;  // R = infinity (ecdsa_impl.h:225-227)
-    // ---- x-coordinate test (ecdsa_impl.h:241-273): back on E, Z_E = Z * sigma ----
-    fe ze, z2, lhs, xr;
-    sc sr;
-    st.get_r(sr);
-    fe_mul(ze, acc.z, st.sigma);
-    fe_sqr(z2, ze);
-    for (int i = 0; i < 8; i++) xr.v[i] = sr.v[i];  // r < n < p
-    fe_mul(lhs, xr, z2);
-    if (fe_equal(lhs, acc.x)) return 1;
-    {
-        const u32 PMN[8] = BCC_PMN_LIMBS;
-        if (!u256_lt(sr.v, PMN)) return 0;       // xr + n >= p
-        u32 xn[8];
-        u256_add(xn, sr.v, N);
-        for (int i = 0; i < 8; i++) xr.v[i] = xn[i];
-        fe_mul(lhs, xr, z2);
-        if (fe_equal(lhs, acc.x)) return 1;
-    }
-    return 0;
-}
-
-// Both phases back to back (host tests, small batches).
-template <class QT, class GT>
-BCC_HD int ecdsa_verify_lane(u32 tag, const fe& px_in, const fe& py_in, const sc& r_in,
-                             const sc& s_in, const sc& m_in, QT& qt, const GT& gt,
-                             const sc* sinv_pre = nullptr) {
-    LadderState st;
-    if (!ecdsa_prep_lane(tag, px_in, py_in, r_in, s_in, m_in, sinv_pre, qt, st)) return 0;
-    return ecdsa_ladder_lane(st, qt, gt);
-}
-
 // ------------------------------------------------------------------------------------------
 // BIP340 (config C5): secp256k1_schnorrsig_verify, modules/schnorrsig/main_impl.h:190-237
 // ------------------------------------------------------------------------------------------
@@ -489,55 +232,6 @@ BCC_HD void schnorr_challenge(sc& e, const fe& rx, const fe& px, const sc& m) {
     }
 }
 
-// Prep phase of a BIP340 verify: rx < p (main_impl.h:207), s < n (:211-214), x-only lift of
-// the key with even y (extrakeys/main_impl.h:21-39: x < p and x^3 + 7 a square), challenge e,
-// then the ladder scalars for R = s G + (-e) P (main_impl.h:224-227).
-template <class QT>
-BCC_HD bool schnorr_prep_lane(const fe& px, const fe& rx, const sc& s_in, const sc& m, QT& qt,
-                              LadderState& st) {
-    const u32 N[8] = BCC_N_LIMBS;
-    st.flags = 0;
-    if (!fe_lt_p(rx)) return false;
-    if (!u256_lt(s_in.v, N)) return false;
-    if (!fe_lt_p(px)) return false;
-    fe py, x3;
-    curve_rhs(x3, px);
-    if (!fe_sqrt(py, x3)) return false;
-    fe_normalize(py);
-    if (py.v[0] & 1u) fe_neg(py, py);            // the even-y lift
-    sc e, ne;
-    schnorr_challenge(e, rx, px, m);
-    sc_neg(ne, e);
-    set_ladder_scalars(st, s_in, ne);
-#pragma unroll
-    for (int i = 0; i < 8; i++) st.r.v[i] = rx.v[i];
-    build_q_table(px, py, qt, st.sigma);
-    return true;
-}
-
-// Ladder phase of a BIP340 verify.  Returns 1 when R != infinity and x(R) == rx (tested
-// inversion-free as rx * Z_E^2 == X); ye / ze then hold Y and Z_E with y(R) = ye / ze^3, whose
-// parity (main_impl.h:234-236) needs one field inversion: batched across lanes on the device
-// (schnorr_parity_kernel), per lane in schnorr_verify_lane.
-template <class ST, class QT, class GT>
-BCC_HD int schnorr_ladder_lane(const ST& st, const QT& qt, const GT& gt, fe& ye, fe& ze) {
-    if (!(st.flags & LS_VALID)) return 0;
-    gej acc;
-    if (ladder_accumulate(st, qt, gt, acc)) return 0;  // ge_set_gej_var(inf) -> reject (:229-232)
-    fe z2, lhs, xr;
-    sc sr;
-    st.get_r(sr);
-    fe_mul(ze, acc.z, st.sigma);
-    if (fe_is_zero(ze)) return 0;                // unreachable for a finite R; keeps the batch
-                                                 // inversion well-defined regardless
-    fe_sqr(z2, ze);
-    for (int i = 0; i < 8; i++) xr.v[i] = sr.v[i];
-    fe_mul(lhs, xr, z2);
-    if (!fe_equal(lhs, acc.x)) return 0;
-    ye = acc.y;
-    return 1;
-}
-
 // y = ye * zinv^3 normalised; true when even (!secp256k1_fe_is_odd).
 BCC_HD bool schnorr_y_even(const fe& ye, const fe& zinv) {
     fe z2, z3, y;
@@ -546,18 +240,6 @@ BCC_HD bool schnorr_y_even(const fe& ye, const fe& zinv) {
     fe_mul(y, ye, z3);
     fe_normalize(y);
     return (y.v[0] & 1u) == 0;
-}
-
-// Whole BIP340 verify on one lane (host tests, small batches).
-template <class QT, class GT>
-BCC_HD int schnorr_verify_lane(const fe& px, const fe& rx, const sc& s, const sc& m, QT& qt,
-                               const GT& gt) {
-    LadderState st;
-    if (!schnorr_prep_lane(px, rx, s, m, qt, st)) return 0;
-    fe ye, ze, zi;
-    if (!schnorr_ladder_lane(st, qt, gt, ye, ze)) return 0;
-    fe_inv(zi, ze);
-    return schnorr_y_even(ye, zi) ? 1 : 0;
 }
 
 // k*G -> affine (x, y), normalized.  Used by the synthetic-workload generator (keygen, signing),

@@ -36,9 +36,6 @@ namespace bcc {
 #ifndef BCC_COMB_BITS
 #define BCC_COMB_BITS 16  // 16 windows x 32768 points = 32 MiB of tables (MALL-resident); 15 additions
 #endif
-#ifndef BCC_QTAB_COZ
-#define BCC_QTAB_COZ 1  // the Q_w table by co-Z additions (build_q_table_coz)
-#endif
 constexpr int WC = BCC_COMB_BITS;                 // comb window: 2^(WC-1) odd multiples per window
 constexpr int CTAB = 1 << (WC - 1);
 constexpr int CTOP = (256 + WC - 1) / WC - 1;     // top window index (19 for WC = 13)
@@ -129,11 +126,7 @@ BCC_HD bool twist_prep_key(u32 tag, const fe& px, const fe& py, QT& qt, TwistSta
     fe qx, qy;
     fe_mul(qx, px, v);
     fe_sqr(qy, v);
-#if BCC_QTAB_COZ
     build_q_table_coz(qx, qy, qt, st.sigma);
-#else
-    build_q_table(qx, qy, qt, st.sigma);
-#endif
     st.flags = flags;
     return true;
 }
@@ -612,11 +605,7 @@ BCC_HD bool schnorr_twist_prep(const fe& px, const fe& rx, const sc& s_in, const
     fe qx, qy;
     fe_mul(qx, px, v);
     fe_sqr(qy, v);
-#if BCC_QTAB_COZ
     build_q_table_coz(qx, qy, qt, st.sigma);
-#else
-    build_q_table(qx, qy, qt, st.sigma);
-#endif
     return true;
 }
 

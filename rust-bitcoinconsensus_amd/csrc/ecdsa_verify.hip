@@ -9,9 +9,8 @@
 //                                   comb from HBM tables), alpha / beta / K of the x-test
 //   K_tfin    twist_fin_kernel      batched beta^-1, "gamma = -alpha / beta is the key's y",
 //                                   exact fallback for the exceptional lanes
-// BIP340 runs the same three kernels (schnorr_tprep_kernel, twist_*_kernel<true>).
-// Round-1 path (BCC_ECDSA_PATH=legacy): K_inv, K_key (pubkey decompression), K_prep, K_ladder
-// (G tables in LDS), and for BIP340 schnorr_{prep,ladder,parity}_kernel.
+// BIP340 runs the same three kernels (schnorr_tprep_kernel, twist_*_kernel<true>).  (The round-1
+// path -- key decompression by a square root, G tables in LDS -- was retired in round 4.)
 // K_inv needs only the s rows: DeviceBatch::run launches it on a side stream beside the sighash
 // kernels.  Prep and ladder are separate launches so that each gets its own register allocation
 // (ladder: 4 waves per SIMD).  Tuples are processed in chunks of up to 16M lanes so the per-tuple
@@ -92,23 +91,7 @@ struct QTableGlobal {
 __device__ __forceinline__ u32* lane_table(u32* qtab, size_t t);
 constexpr int QTABLE_WORDS = QTAB * 32;     // 256 words = 1 KiB per lane
 __device__ __forceinline__ u32* lane_table(u32* qtab, size_t t) { return qtab + t * QTABLE_WORDS; }
-constexpr int STATE_WORDS = 16 + 1 + 8 + 8;  // LadderState
-constexpr int PRE_WORDS = 8 + 8 + 1;          // per tuple: s^-1, key y, key status
-
-// G tables staged in LDS (64 KiB per workgroup).
-struct GTableLDS {
-    const fe* xy;
-    __device__ void get(int tab, int i, fe& x, fe& y) const {
-        // LDS address space explicitly: ds_read instead of flat loads
-        const __attribute__((address_space(3))) u32* l = (const __attribute__((address_space(3))) u32*)xy;
-        const int b = (tab * GTAB + i) * 16;
-#pragma unroll
-        for (int j = 0; j < 8; j++) {
-            x.v[j] = l[b + j];
-            y.v[j] = l[b + 8 + j];
-        }
-    }
-};
+constexpr int PRE_WORDS = 8;  // per tuple: s^-1
 
 __device__ __forceinline__ void load_be32(fe& r, const uint8_t* p) {
     const uint4* q = reinterpret_cast<const uint4*>(p);
@@ -188,262 +171,9 @@ __global__ __launch_bounds__(256) void batch_sinv_kernel(const uint8_t* __restri
     store_limbs(sinv + 8 * t, inv);
 }
 
-__device__ __forceinline__ void store_state(u32* st, size_t C, const LadderState& s) {
-    int w = 0;
-#pragma unroll
-    for (int a = 0; a < 4; a++)
-#pragma unroll
-        for (int b = 0; b < 4; b++) st[(size_t)(w++) * C] = s.k[a][b];
-    st[(size_t)(w++) * C] = s.flags;
-#pragma unroll
-    for (int j = 0; j < 8; j++) st[(size_t)(w++) * C] = s.sigma.v[j];
-#pragma unroll
-    for (int j = 0; j < 8; j++) st[(size_t)(w++) * C] = s.r.v[j];
-}
-
-__device__ __forceinline__ void load_state(LadderState& s, const u32* st, size_t C) {
-    int w = 0;
-#pragma unroll
-    for (int a = 0; a < 4; a++)
-#pragma unroll
-        for (int b = 0; b < 4; b++) s.k[a][b] = st[(size_t)(w++) * C];
-    s.flags = st[(size_t)(w++) * C];
-#pragma unroll
-    for (int j = 0; j < 8; j++) s.sigma.v[j] = st[(size_t)(w++) * C];
-#pragma unroll
-    for (int j = 0; j < 8; j++) s.r.v[j] = st[(size_t)(w++) * C];
-}
-
-// The ladder's view of its state: flags and sigma live in registers; the scalar words and r
-// are loaded where they are used (store_state layout), which keeps 24 VGPRs free across the
-// loop.  The empty asm hides the address from LICM so the loads stay at their use.
-// Ladder workgroups are 512 lanes (8 waves), two per CU (4 waves per SIMD), each with its own
-// copy of the 64 KiB w = 10 G tables (128 of 160 KiB).  Measured on MI355X, C2 1M, ECDSA stage
-// (variants built by tools/variants/build.sh): w = 8 / 256-lane groups 77.3 M/s; w = 10 /
-// 512-lane groups 78.9 M/s (13 instead of 16 G additions per 128-bit half); w = 10 / 1024-lane
-// groups (one per CU, one shared table) 72.5 M/s and w = 8 / 1024 71.3 M/s: a CU whose only
-// workgroup has stragglers idles until the whole group retires.  The scalar words can also be
-// staged in LDS (BCC_K_IN_LDS: 16 words per lane, word w of lane l at w * LADDER_WG + l); at
-// w = 8 that measured the same as reading them from the wave-blocked scratch (77.3 vs 77.5 M/s),
-// and at w = 10 it would leave room for one workgroup per CU only, so it is off.  Five waves per
-// SIMD (640-lane groups, BCC_LADDER_WAVES=5) caps the ladder at 96 VGPRs and spills 25 of them:
-// 67.4 M/s (C2) and 77.7 M/s (C5) against 79.3 / 87.2 M/s at four waves.
-#ifndef BCC_LADDER_WG
-#define BCC_LADDER_WG 512
-#endif
-constexpr int LADDER_WG = BCC_LADDER_WG;
 #ifndef BCC_LADDER_WAVES
 #define BCC_LADDER_WAVES 4  // waves per SIMD the ladder kernels are register-allocated for
 #endif
-#ifndef BCC_K_IN_LDS
-#define BCC_K_IN_LDS 0
-#endif
-[[maybe_unused]] constexpr int KLDS_STRIDE = BCC_K_IN_LDS ? LADDER_WG : 1;
-
-struct LadderStateView {
-    const u32* p;
-    size_t C;
-    u32 flags;
-    fe sigma;
-    const u32* klds;  // this lane's 16 scalar words in LDS, stride KLDS_STRIDE
-    __device__ __forceinline__ u32 kword(int s, int w) const {
-#if BCC_K_IN_LDS
-        const u32* q = klds;
-        asm volatile("" : "+v"(q));
-        // the asm hides the address space too: restore it so this is an LDS (not flat) read
-        const __attribute__((address_space(3))) u32* l = (const __attribute__((address_space(3))) u32*)q;
-        return l[(s * 4 + w) * KLDS_STRIDE];
-#else
-        const u32* q = p;
-        asm volatile("" : "+v"(q));
-        const __attribute__((address_space(1))) u32* g = (const __attribute__((address_space(1))) u32*)q;
-        return g[(size_t)(s * 4 + w) * C];
-#endif
-    }
-    __device__ __forceinline__ void get_r(sc& o) const {
-#pragma unroll
-        for (int j = 0; j < 8; j++) o.v[j] = p[(25 + j) * C];
-    }
-};
-
-// Stage b (pubkey parse + decompression, eckey_impl.h:17-35) for every tuple, before and apart
-// from the prep kernel: the square root (266 of prep's ~420 modmuls) needs few registers, so it
-// runs at high occupancy here, and it reads only the key rows, so it runs on the side stream
-// beside the sighash kernels.  Writes y (8 limbs) and the parse status per tuple.
-__global__ __launch_bounds__(256) void ecdsa_key_kernel(const uint8_t* __restrict__ tag,
-                                                        const uint8_t* __restrict__ px,
-                                                        const uint8_t* __restrict__ py, size_t n,
-                                                        u32* __restrict__ keyy,
-                                                        u32* __restrict__ kok) {
-    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    fe x, y, qy;
-    load_be32(x, px + 32 * i);
-    load_be32(y, py + 32 * i);
-    const bool ok = pubkey_load(tag[i], x, y, qy);
-    sc o;
-#pragma unroll
-    for (int k = 0; k < 8; k++) o.v[k] = ok ? qy.v[k] : 0u;
-    store_limbs(keyy + 8 * i, o);
-    kok[i] = ok ? 1u : 0u;
-}
-
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void ecdsa_prep_kernel(
-    const uint8_t* __restrict__ px, const uint8_t* __restrict__ pr, const uint8_t* __restrict__ ps,
-    const uint8_t* __restrict__ pm, const u32* __restrict__ psinv, const u32* __restrict__ keyy,
-    const u32* __restrict__ kok, size_t base, size_t cnt, u32* __restrict__ qtab,
-    u32* __restrict__ state) {
-    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= cnt) return;
-    const size_t i = base + t;
-    LadderState st;
-    st.flags = 0;
-    QTableGlobal qt{lane_table(qtab, t)};
-    if (kok[i]) {
-        fe x, y;
-        sc r, s, m, si, yl;
-        load_be32(x, px + 32 * i);
-        load_limbs(yl, keyy + 8 * i);
-#pragma unroll
-        for (int k = 0; k < 8; k++) y.v[k] = yl.v[k];
-        load_be32(r, pr + 32 * i);
-        load_be32(s, ps + 32 * i);
-        load_be32(m, pm + 32 * i);
-        load_limbs(si, psinv + 8 * i);
-        ecdsa_prep_loaded(x, y, r, s, m, &si, qt, st);
-    }
-    store_state(lane_words(state, t, STATE_WORDS), LANE_STRIDE, st);
-}
-
-__global__ __launch_bounds__(LADDER_WG) __attribute__((amdgpu_waves_per_eu(BCC_LADDER_WAVES, BCC_LADDER_WAVES))) void ecdsa_ladder_kernel(const u32* __restrict__ state,
-                                                           const u32* __restrict__ qtab,
-                                                           const fe* __restrict__ gtab,
-                                                           uint8_t* __restrict__ verdict,
-                                                           size_t base, size_t cnt, size_t C) {
-    __shared__ fe g_lds[2 * GTAB * 2];
-#if BCC_K_IN_LDS
-    __shared__ u32 k_lds[16 * KLDS_STRIDE];
-#endif
-    for (int i = threadIdx.x; i < 2 * GTAB * 2; i += blockDim.x) g_lds[i] = gtab[i];
-    __syncthreads();
-    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= cnt) return;
-    LadderStateView st;
-    st.p = lane_words(state, t, STATE_WORDS);
-    st.C = LANE_STRIDE;
-    st.flags = st.p[16 * LANE_STRIDE];
-#pragma unroll
-    for (int j = 0; j < 8; j++) st.sigma.v[j] = st.p[(17 + j) * LANE_STRIDE];
-#if BCC_K_IN_LDS
-#pragma unroll
-    for (int w = 0; w < 16; w++) k_lds[w * KLDS_STRIDE + threadIdx.x] = st.p[w * LANE_STRIDE];
-    st.klds = k_lds + threadIdx.x;  // each lane reads only its own words: no barrier
-#endif
-    QTableGlobal qt{lane_table(const_cast<u32*>(qtab), t)};
-    GTableLDS gt{g_lds};
-    verdict[base + t] = (uint8_t)ecdsa_ladder_lane(st, qt, gt);
-}
-
-// ------------------------------------------------------------------------------------------
-// BIP340 (config C5).  Rows: sig[n][64] = r.x || s, msg[n][32], xonly[n][32] (the argument
-// order of secp256k1_schnorrsig_verify).  Same prep / ladder split and scratch layout as ECDSA;
-// the even-y test needs y(R) = Y / Z_E^3, so the ladder parks (Y, Z_E) in its lane's own Q-table
-// words 0..15 and schnorr_parity_kernel inverts all Z_E of a chunk by Montgomery's trick.
-// ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void schnorr_prep_kernel(
-    const uint8_t* __restrict__ psig, const uint8_t* __restrict__ pm,
-    const uint8_t* __restrict__ ppk, size_t base, size_t cnt, size_t C, u32* __restrict__ qtab,
-    u32* __restrict__ state) {
-    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= cnt) return;
-    const size_t i = base + t;
-    fe px, rx;
-    sc s, m;
-    load_be32(rx, psig + 64 * i);
-    load_be32(s, psig + 64 * i + 32);
-    load_be32(m, pm + 32 * i);
-    load_be32(px, ppk + 32 * i);
-    QTableGlobal qt{lane_table(qtab, t)};
-    LadderState st;
-    schnorr_prep_lane(px, rx, s, m, qt, st);
-    store_state(lane_words(state, t, STATE_WORDS), LANE_STRIDE, st);
-}
-
-__global__ __launch_bounds__(LADDER_WG) __attribute__((amdgpu_waves_per_eu(BCC_LADDER_WAVES, BCC_LADDER_WAVES))) void schnorr_ladder_kernel(
-    const u32* __restrict__ state, u32* __restrict__ qtab, const fe* __restrict__ gtab,
-    uint8_t* __restrict__ verdict, size_t base, size_t cnt, size_t C) {
-    __shared__ fe g_lds[2 * GTAB * 2];
-#if BCC_K_IN_LDS
-    __shared__ u32 k_lds[16 * KLDS_STRIDE];
-#endif
-    for (int i = threadIdx.x; i < 2 * GTAB * 2; i += blockDim.x) g_lds[i] = gtab[i];
-    __syncthreads();
-    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= cnt) return;
-    LadderStateView st;
-    st.p = lane_words(state, t, STATE_WORDS);
-    st.C = LANE_STRIDE;
-    st.flags = st.p[16 * LANE_STRIDE];
-#pragma unroll
-    for (int j = 0; j < 8; j++) st.sigma.v[j] = st.p[(17 + j) * LANE_STRIDE];
-#if BCC_K_IN_LDS
-#pragma unroll
-    for (int w = 0; w < 16; w++) k_lds[w * KLDS_STRIDE + threadIdx.x] = st.p[w * LANE_STRIDE];
-    st.klds = k_lds + threadIdx.x;  // each lane reads only its own words: no barrier
-#endif
-    QTableGlobal qt{lane_table(qtab, t)};
-    GTableLDS gt{g_lds};
-    fe ye, ze;
-    int ok = schnorr_ladder_lane(st, qt, gt, ye, ze);
-    if (!ok) {  // neutral element for the batch inversion
-        ye = fe_zero();
-        ze = fe_one();
-    }
-    qt.put(0, 0, ye);  // the lane's own table column; the ladder no longer reads it
-    qt.put(0, 1, ze);
-    verdict[base + t] = (uint8_t)ok;
-}
-
-// y-parity of R for every lane of a chunk: Z_E^-1 by Montgomery's trick over the strided
-// sub-chunk {t, t+T, ...} (3 mults per lane + one Fermat inversion per thread), prefix products
-// in Q-table words 16..23.  verdict &= (y even).
-__global__ __launch_bounds__(256) void schnorr_parity_kernel(u32* __restrict__ qtab,
-                                                             uint8_t* __restrict__ verdict,
-                                                             size_t base, size_t cnt, size_t C,
-                                                             size_t T) {
-    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= cnt || t >= T) return;
-    fe acc, z, ye;
-    QTableGlobal q0{lane_table(qtab, t)};
-    q0.get(0, 1, acc);
-    q0.put(0, 2, acc);
-    size_t last = t;
-    for (size_t i = t + T; i < cnt; i += T) {
-        QTableGlobal qi{lane_table(qtab, i)};
-        qi.get(0, 1, z);
-        fe_mul(acc, acc, z);
-        qi.put(0, 2, acc);  // Z_t * ... * Z_i
-        last = i;
-    }
-    fe inv;
-    fe_inv(inv, acc);
-    for (size_t i = last; i >= t + T; i -= T) {
-        QTableGlobal qi{lane_table(qtab, i)}, qp{lane_table(qtab, i - T)};
-        fe prev, zi;
-        qp.get(0, 2, prev);
-        fe_mul(zi, inv, prev);  // Z_i^-1
-        qi.get(0, 1, z);
-        fe_mul(inv, inv, z);    // (Z_t ... Z_{i-1})^-1
-        if (verdict[base + i]) {
-            qi.get(0, 0, ye);
-            verdict[base + i] = (uint8_t)schnorr_y_even(ye, zi);
-        }
-    }
-    if (verdict[base + t]) {
-        q0.get(0, 0, ye);
-        verdict[base + t] = (uint8_t)schnorr_y_even(ye, inv);
-    }
-}
 
 // ------------------------------------------------------------------------------------------
 // ECDSA, square-root-free path (ecdsa_twist.h): K_tprep -> K_tladder -> K_tfin.  The key is never
@@ -898,10 +628,9 @@ __global__ __launch_bounds__(256) void twist_fin_kernel(u32* __restrict__ state,
 }
 
 // ------------------------------------------------------------------------------------------
-// G tables (one read-only copy per device) and caller-owned scratch
+// Comb tables (one read-only copy per device) and caller-owned scratch
 // ------------------------------------------------------------------------------------------
 static std::mutex g_gtab_mu;
-static fe* g_gtab[64];
 static u32* g_gcomb[64];
 static int g_cus[64];
 
@@ -915,18 +644,6 @@ static const std::vector<fe>& host_gcomb() {
     return t;
 }
 
-// Signature path: the square-root-free twist path (default; ECDSA and BIP340) or the round-1 path
-// with the key square root (BCC_ECDSA_PATH=legacy), for A/B runs on one build.
-static bool ecdsa_twist() {
-    static const bool on = [] {
-        const char* e = getenv("BCC_ECDSA_PATH");
-        return !(e && std::string(e) == "legacy");
-    }();
-    return on;
-}
-
-bool ecdsa_fin_clears() { return ecdsa_twist(); }
-
 // BCC_SCHNORR_SPLIT=1: the BIP340 ladder as a Q launch and a G launch (A/B runs)
 static bool schnorr_split() {
     static const bool on = [] {
@@ -934,16 +651,6 @@ static bool schnorr_split() {
         return e && atoi(e) != 0;
     }();
     return on;
-}
-
-static const std::vector<fe>& host_gtab() {
-    static std::vector<fe> t;
-    static std::once_flag once;
-    std::call_once(once, [] {
-        t.resize(2 * GTAB * 2);
-        build_g_tables(t.data());
-    });
-    return t;
 }
 
 // Lanes per prep/ladder launch pair.  Larger chunks leave fewer kernel tails and fewer latency-
@@ -963,25 +670,20 @@ static size_t chunk_lanes() {
     return std::max<size_t>(256, (v + 255) & ~(size_t)255);
 }
 
-// Current device, its G tables and CU count.
-static int device_tables(int* dev, fe** gtab, int* cus) {
+// Current device, its comb tables and CU count.
+static int device_tables(int* dev, const u32** gcomb, int* cus) {
     BCC_HIP_TRY(hipGetDevice(dev));
     if (*dev < 0 || *dev >= 64) return (int)hipErrorInvalidDevice;
     std::lock_guard<std::mutex> lk(g_gtab_mu);
-    if (!g_gtab[*dev]) {
-        const auto& h = host_gtab();
-        fe* d = nullptr;
-        BCC_HIP_TRY(hipMalloc(&d, h.size() * sizeof(fe)));
-        BCC_HIP_TRY(hipMemcpy(d, h.data(), h.size() * sizeof(fe), hipMemcpyHostToDevice));
+    if (!g_gcomb[*dev]) {
         BCC_HIP_TRY(hipDeviceGetAttribute(&g_cus[*dev], hipDeviceAttributeMultiprocessorCount, *dev));
         const auto& hc = host_gcomb();
         fe* dc = nullptr;
         BCC_HIP_TRY(hipMalloc(&dc, hc.size() * sizeof(fe)));
         BCC_HIP_TRY(hipMemcpy(dc, hc.data(), hc.size() * sizeof(fe), hipMemcpyHostToDevice));
         g_gcomb[*dev] = reinterpret_cast<u32*>(dc);
-        g_gtab[*dev] = d;
     }
-    *gtab = g_gtab[*dev];
+    *gcomb = g_gcomb[*dev];
     *cus = g_cus[*dev];
     return 0;
 }
@@ -1053,38 +755,31 @@ static int ensure_scratch(SigScratch& sc, int dev, size_t n, bool with_sinv, siz
 
 int ecdsa_launch_pre(SigScratch& sc, const uint8_t* d_tag, const uint8_t* d_x,
                      const uint8_t* d_y, const uint8_t* d_s, size_t n, void* stream) {
+    (void)d_tag;
+    (void)d_x;
+    (void)d_y;
     if (n == 0) return 0;
     int dev = 0, cus = 0;
-    fe* gtab = nullptr;
+    const u32* gcomb = nullptr;
     size_t C = 0;
-    if (int e = device_tables(&dev, &gtab, &cus)) return e;
+    if (int e = device_tables(&dev, &gcomb, &cus)) return e;
     if (int e = ensure_scratch(sc, dev, n, true, &C)) return e;
-    u32* sinv = (u32*)sc.sinv;
     // K_inv: chunks of <= 16 tuples, but at least one wave per SIMD
     size_t T = std::max<size_t>((n + INV_PER_THREAD - 1) / INV_PER_THREAD, std::min<size_t>(n, (size_t)cus * 256));
     hipLaunchKernelGGL(batch_sinv_kernel, dim3((unsigned)((T + 255) / 256)), dim3(256), 0,
-                       (hipStream_t)stream, d_s, sinv, n, T);
-    BCC_HIP_TRY(hipGetLastError());
-    if (ecdsa_twist()) return 0;  // no key decompression on the twist path
-    hipLaunchKernelGGL(ecdsa_key_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
-                       (hipStream_t)stream, d_tag, d_x, d_y, n, sinv + 8 * sc.sinv_cap,
-                       sinv + 16 * sc.sinv_cap);
+                       (hipStream_t)stream, d_s, (u32*)sc.sinv, n, T);
     BCC_HIP_TRY(hipGetLastError());
     return 0;
 }
 
 int ecdsa_launch_key(SigScratch& sc, const uint8_t* d_tag, const uint8_t* d_x,
                      const uint8_t* d_y, size_t n, void* stream) {
-    static const bool off = [] {  // BCC_KEY_AHEAD=0: the whole prep after K_inv (A/B runs)
-        const char* e = getenv("BCC_KEY_AHEAD");
-        return e && atoi(e) == 0;
-    }();
     sc.key_ready = 0;
-    if (n == 0 || off || !ecdsa_twist() || n > chunk_lanes()) return 0;
+    if (n == 0 || n > chunk_lanes()) return 0;
     int dev = 0, cus = 0;
-    fe* gtab = nullptr;
+    const u32* gcomb = nullptr;
     size_t C = 0;
-    if (int e = device_tables(&dev, &gtab, &cus)) return e;
+    if (int e = device_tables(&dev, &gcomb, &cus)) return e;
     if (int e = ensure_scratch(sc, dev, n, true, &C)) return e;
     if (n > C) return 0;  // chunked: the whole prep runs per chunk after K_inv
     u32* qtab = (u32*)sc.chunk;
@@ -1096,22 +791,13 @@ int ecdsa_launch_key(SigScratch& sc, const uint8_t* d_tag, const uint8_t* d_x,
     return 0;
 }
 
-// BCC_LADDER_SPLIT=0: the fused ladder after the sighash kernels (A/B runs)
-static bool ladder_split() {
-    static const bool on = [] {
-        const char* e = getenv("BCC_LADDER_SPLIT");
-        return !(e && atoi(e) == 0);
-    }();
-    return on;
-}
-
 int ecdsa_launch_q(SigScratch& sc, const uint8_t* d_r, const uint8_t* d_s, size_t n, void* stream) {
     sc.q_ready = 0;
-    if (n == 0 || !ladder_split() || sc.key_ready != n || n > chunk_lanes()) return 0;
+    if (n == 0 || sc.key_ready != n || n > chunk_lanes()) return 0;
     int dev = 0, cus = 0;
-    fe* gtab = nullptr;
+    const u32* gcomb = nullptr;
     size_t C = 0;
-    if (int e = device_tables(&dev, &gtab, &cus)) return e;
+    if (int e = device_tables(&dev, &gcomb, &cus)) return e;
     if (int e = ensure_scratch(sc, dev, n, true, &C)) return e;
     if (n > C) return 0;
     u32* qtab = (u32*)sc.chunk;
@@ -1133,10 +819,9 @@ int ecdsa_launch(SigScratch& sc, const uint8_t* d_tag, const uint8_t* d_x, const
     sc.key_ready = 0;
     sc.q_ready = 0;
     if (int e = ecdsa_launch_pre(sc, d_tag, d_x, d_y, d_s, n, stream)) return e;
-    if (ladder_split()) {  // the same split kernels as DeviceBatch::run, on one stream
-        if (int e = ecdsa_launch_key(sc, d_tag, d_x, d_y, n, stream)) return e;
-        if (int e = ecdsa_launch_q(sc, d_r, d_s, n, stream)) return e;
-    }
+    // the same split kernels as DeviceBatch::run, on one stream
+    if (int e = ecdsa_launch_key(sc, d_tag, d_x, d_y, n, stream)) return e;
+    if (int e = ecdsa_launch_q(sc, d_r, d_s, n, stream)) return e;
     return ecdsa_launch_after_pre(sc, d_tag, d_x, d_y, d_r, d_s, d_m, d_verdict, n, stream);
 }
 
@@ -1144,72 +829,54 @@ int ecdsa_launch_after_pre(SigScratch& sc, const uint8_t* d_tag, const uint8_t* 
                            const uint8_t* d_y, const uint8_t* d_r, const uint8_t* d_s,
                            const uint8_t* d_m, uint8_t* d_verdict, size_t n, void* stream,
                            void* ev_rows_read, bool verdict_and) {
-    const int and_mode = verdict_and && ecdsa_twist() ? 1 : 0;
+    const int and_mode = verdict_and ? 1 : 0;
     if (n == 0) return 0;
     int dev = 0, cus = 0;
-    fe* gtab = nullptr;
+    const u32* gcomb = nullptr;
     size_t C = 0;
-    if (int e = device_tables(&dev, &gtab, &cus)) return e;
+    if (int e = device_tables(&dev, &gcomb, &cus)) return e;
     if (int e = ensure_scratch(sc, dev, n, true, &C)) return e;  // sized by ecdsa_launch_pre
     hipStream_t sm = (hipStream_t)stream;
     u32* sinv = (u32*)sc.sinv;
-    if (ecdsa_twist()) {
-        u32* qtab = (u32*)sc.chunk;
-        u32* state = qtab + C * QTABLE_WORDS;
-        const u32* gcomb = g_gcomb[dev];
-        const bool key_ahead = sc.key_ready == n && n <= C;
-        const bool q_ahead = sc.q_ready == n && n <= C;
-        sc.key_ready = 0;
-        sc.q_ready = 0;
-        if (q_ahead) {  // K_tkey, K_tscal_q and K_tladder_q ran ahead (ecdsa_launch_q)
-            hipLaunchKernelGGL(twist_ladder_g_kernel, dim3((unsigned)((n + TLADDER_WG - 1) / TLADDER_WG)),
-                               dim3(TLADDER_WG), 0, sm, state, qtab, gcomb, d_m, sinv, n);
-            BCC_HIP_TRY(hipGetLastError());
-            if (ev_rows_read) BCC_HIP_TRY(hipEventRecord((hipEvent_t)ev_rows_read, sm));
-            const size_t T = std::max<size_t>((n + FIN_PER_THREAD - 1) / FIN_PER_THREAD, std::min<size_t>(n, (size_t)cus * 256));
-            hipLaunchKernelGGL(twist_fin_kernel<false>, dim3((unsigned)((T + 255) / 256)), dim3(256), 0,
-                               sm, state, qtab, d_verdict, 0, n, T, and_mode);
-            BCC_HIP_TRY(hipGetLastError());
-            return 0;
-        }
-        for (size_t base = 0; base < n; base += C) {
-            const size_t cnt = std::min(C, n - base);
-            if (key_ahead) {
-                hipLaunchKernelGGL(ecdsa_tscal_kernel, dim3((unsigned)((cnt + 255) / 256)),
-                                   dim3(256), 0, sm, d_r, d_s, d_m, sinv, cnt, state);
-            } else {
-                hipLaunchKernelGGL(ecdsa_tprep_kernel, dim3((unsigned)((cnt + 255) / 256)),
-                                   dim3(256), 0, sm, d_tag, d_x, d_y, d_r, d_s, d_m, sinv, base,
-                                   cnt, qtab, state);
-            }
-            BCC_HIP_TRY(hipGetLastError());
-            if (ev_rows_read && base + cnt >= n)
-                BCC_HIP_TRY(hipEventRecord((hipEvent_t)ev_rows_read, sm));
-            hipLaunchKernelGGL(twist_ladder_kernel<false>,
-                               dim3((unsigned)((cnt + TLADDER_WG - 1) / TLADDER_WG)),
-                               dim3(TLADDER_WG), 0, sm, state, qtab, gcomb, cnt);
-            BCC_HIP_TRY(hipGetLastError());
-            // the batched beta inversion: sub-chunks of <= 16 lanes, at least one wave per SIMD
-            const size_t T = std::max<size_t>((cnt + FIN_PER_THREAD - 1) / FIN_PER_THREAD, std::min<size_t>(cnt, (size_t)cus * 256));
-            hipLaunchKernelGGL(twist_fin_kernel<false>, dim3((unsigned)((T + 255) / 256)), dim3(256), 0,
-                               sm, state, qtab, d_verdict, base, cnt, T, and_mode);
-            BCC_HIP_TRY(hipGetLastError());
-        }
-        return 0;
-    }
-    const u32* keyy = sinv + 8 * sc.sinv_cap;
-    const u32* kok = sinv + 16 * sc.sinv_cap;
     u32* qtab = (u32*)sc.chunk;
     u32* state = qtab + C * QTABLE_WORDS;
-    for (size_t base = 0; base < n; base += C) {
-        size_t cnt = std::min(C, n - base);
-        unsigned blocks = (unsigned)((cnt + 255) / 256);
-        hipLaunchKernelGGL(ecdsa_prep_kernel, dim3(blocks), dim3(256), 0, sm, d_x, d_r, d_s, d_m,
-                           sinv, keyy, kok, base, cnt, qtab, state);
+    const bool key_ahead = sc.key_ready == n && n <= C;
+    const bool q_ahead = sc.q_ready == n && n <= C;
+    sc.key_ready = 0;
+    sc.q_ready = 0;
+    if (q_ahead) {  // K_tkey, K_tscal_q and K_tladder_q ran ahead (ecdsa_launch_q)
+        hipLaunchKernelGGL(twist_ladder_g_kernel, dim3((unsigned)((n + TLADDER_WG - 1) / TLADDER_WG)),
+                           dim3(TLADDER_WG), 0, sm, state, qtab, gcomb, d_m, sinv, n);
         BCC_HIP_TRY(hipGetLastError());
-        hipLaunchKernelGGL(ecdsa_ladder_kernel, dim3((unsigned)((cnt + LADDER_WG - 1) / LADDER_WG)),
-                           dim3(LADDER_WG), 0, sm, state, qtab, gtab,
-                           d_verdict, base, cnt, C);
+        if (ev_rows_read) BCC_HIP_TRY(hipEventRecord((hipEvent_t)ev_rows_read, sm));
+        const size_t T = std::max<size_t>((n + FIN_PER_THREAD - 1) / FIN_PER_THREAD, std::min<size_t>(n, (size_t)cus * 256));
+        hipLaunchKernelGGL(twist_fin_kernel<false>, dim3((unsigned)((T + 255) / 256)), dim3(256), 0,
+                           sm, state, qtab, d_verdict, 0, n, T, and_mode);
+        BCC_HIP_TRY(hipGetLastError());
+        return 0;
+    }
+    // chunked (n above the scratch chunk): the whole prep, the fused ladder and K_tfin per chunk
+    for (size_t base = 0; base < n; base += C) {
+        const size_t cnt = std::min(C, n - base);
+        if (key_ahead) {
+            hipLaunchKernelGGL(ecdsa_tscal_kernel, dim3((unsigned)((cnt + 255) / 256)),
+                               dim3(256), 0, sm, d_r, d_s, d_m, sinv, cnt, state);
+        } else {
+            hipLaunchKernelGGL(ecdsa_tprep_kernel, dim3((unsigned)((cnt + 255) / 256)),
+                               dim3(256), 0, sm, d_tag, d_x, d_y, d_r, d_s, d_m, sinv, base,
+                               cnt, qtab, state);
+        }
+        BCC_HIP_TRY(hipGetLastError());
+        if (ev_rows_read && base + cnt >= n)
+            BCC_HIP_TRY(hipEventRecord((hipEvent_t)ev_rows_read, sm));
+        hipLaunchKernelGGL(twist_ladder_kernel<false>,
+                           dim3((unsigned)((cnt + TLADDER_WG - 1) / TLADDER_WG)),
+                           dim3(TLADDER_WG), 0, sm, state, qtab, gcomb, cnt);
+        BCC_HIP_TRY(hipGetLastError());
+        // the batched beta inversion: sub-chunks of <= 16 lanes, at least one wave per SIMD
+        const size_t T = std::max<size_t>((cnt + FIN_PER_THREAD - 1) / FIN_PER_THREAD, std::min<size_t>(cnt, (size_t)cus * 256));
+        hipLaunchKernelGGL(twist_fin_kernel<false>, dim3((unsigned)((T + 255) / 256)), dim3(256), 0,
+                           sm, state, qtab, d_verdict, base, cnt, T, and_mode);
         BCC_HIP_TRY(hipGetLastError());
     }
     return 0;
@@ -1219,55 +886,35 @@ int schnorr_launch(SigScratch& sc, const uint8_t* d_sig64, const uint8_t* d_msg3
                    const uint8_t* d_xonly32, uint8_t* d_verdict, size_t n, void* stream) {
     if (n == 0) return 0;
     int dev = 0, cus = 0;
-    fe* gtab = nullptr;
+    const u32* gcomb = nullptr;
     size_t C = 0;
-    if (int e = device_tables(&dev, &gtab, &cus)) return e;
+    if (int e = device_tables(&dev, &gcomb, &cus)) return e;
     if (int e = ensure_scratch(sc, dev, n, false, &C)) return e;
     hipStream_t sm = (hipStream_t)stream;
     u32* qtab = (u32*)sc.chunk;
     u32* state = qtab + C * QTABLE_WORDS;
-    if (ecdsa_twist()) {  // BIP340 on the square-root-free path
-        const u32* gcomb = g_gcomb[dev];
-        for (size_t base = 0; base < n; base += C) {
-            const size_t cnt = std::min(C, n - base);
-            hipLaunchKernelGGL(schnorr_tprep_kernel, dim3((unsigned)((cnt + 255) / 256)), dim3(256),
-                               0, sm, d_sig64, d_msg32, d_xonly32, base, cnt, qtab, state);
-            BCC_HIP_TRY(hipGetLastError());
-            if (schnorr_split()) {
-                hipLaunchKernelGGL(twist_ladder_q_kernel,
-                                   dim3((unsigned)((cnt + TLADDER_WG - 1) / TLADDER_WG)),
-                                   dim3(TLADDER_WG), 0, sm, state, qtab, cnt);
-                BCC_HIP_TRY(hipGetLastError());
-                hipLaunchKernelGGL(twist_ladder_g340_kernel,
-                                   dim3((unsigned)((cnt + TLADDER_WG - 1) / TLADDER_WG)),
-                                   dim3(TLADDER_WG), 0, sm, state, qtab, gcomb, cnt);
-            } else {
-                hipLaunchKernelGGL(twist_ladder_kernel<true>,
-                                   dim3((unsigned)((cnt + TLADDER_WG - 1) / TLADDER_WG)),
-                                   dim3(TLADDER_WG), 0, sm, state, qtab, gcomb, cnt);
-            }
-            BCC_HIP_TRY(hipGetLastError());
-            const size_t T = std::max<size_t>((cnt + FIN_PER_THREAD - 1) / FIN_PER_THREAD, std::min<size_t>(cnt, (size_t)cus * 256));
-            hipLaunchKernelGGL(twist_fin_kernel<true>, dim3((unsigned)((T + 255) / 256)), dim3(256), 0,
-                               sm, state, qtab, d_verdict, base, cnt, T, 0);
-            BCC_HIP_TRY(hipGetLastError());
-        }
-        return 0;
-    }
     for (size_t base = 0; base < n; base += C) {
-        size_t cnt = std::min(C, n - base);
-        unsigned blocks = (unsigned)((cnt + 255) / 256);
-        hipLaunchKernelGGL(schnorr_prep_kernel, dim3(blocks), dim3(256), 0, sm, d_sig64, d_msg32,
-                           d_xonly32, base, cnt, C, qtab, state);
+        const size_t cnt = std::min(C, n - base);
+        hipLaunchKernelGGL(schnorr_tprep_kernel, dim3((unsigned)((cnt + 255) / 256)), dim3(256),
+                           0, sm, d_sig64, d_msg32, d_xonly32, base, cnt, qtab, state);
         BCC_HIP_TRY(hipGetLastError());
-        hipLaunchKernelGGL(schnorr_ladder_kernel, dim3((unsigned)((cnt + LADDER_WG - 1) / LADDER_WG)),
-                           dim3(LADDER_WG), 0, sm, state, qtab, gtab,
-                           d_verdict, base, cnt, C);
+        if (schnorr_split()) {
+            hipLaunchKernelGGL(twist_ladder_q_kernel,
+                               dim3((unsigned)((cnt + TLADDER_WG - 1) / TLADDER_WG)),
+                               dim3(TLADDER_WG), 0, sm, state, qtab, cnt);
+            BCC_HIP_TRY(hipGetLastError());
+            hipLaunchKernelGGL(twist_ladder_g340_kernel,
+                               dim3((unsigned)((cnt + TLADDER_WG - 1) / TLADDER_WG)),
+                               dim3(TLADDER_WG), 0, sm, state, qtab, gcomb, cnt);
+        } else {
+            hipLaunchKernelGGL(twist_ladder_kernel<true>,
+                               dim3((unsigned)((cnt + TLADDER_WG - 1) / TLADDER_WG)),
+                               dim3(TLADDER_WG), 0, sm, state, qtab, gcomb, cnt);
+        }
         BCC_HIP_TRY(hipGetLastError());
-        // parity: sub-chunks of <= 16 lanes, at least one wave per SIMD
-        size_t T = std::max<size_t>((cnt + FIN_PER_THREAD - 1) / FIN_PER_THREAD, std::min<size_t>(cnt, (size_t)cus * 256));
-        hipLaunchKernelGGL(schnorr_parity_kernel, dim3((unsigned)((T + 255) / 256)), dim3(256), 0,
-                           sm, qtab, d_verdict, base, cnt, C, T);
+        const size_t T = std::max<size_t>((cnt + FIN_PER_THREAD - 1) / FIN_PER_THREAD, std::min<size_t>(cnt, (size_t)cus * 256));
+        hipLaunchKernelGGL(twist_fin_kernel<true>, dim3((unsigned)((T + 255) / 256)), dim3(256), 0,
+                           sm, state, qtab, d_verdict, base, cnt, T, 0);
         BCC_HIP_TRY(hipGetLastError());
     }
     return 0;

@@ -12,55 +12,6 @@ namespace bcc {
 
 #if defined(__HIP_DEVICE_COMPILE__)
 
-__device__ __forceinline__ void mad_cc(uint64_t& acc, uint32_t& hi, uint32_t x, uint32_t y) {
-    asm("v_mad_u64_u32 %0, vcc, %2, %3, %0\n\t"
-        "v_addc_co_u32_e32 %1, vcc, 0, %1, vcc"
-        : "+v"(acc), "+v"(hi)
-        : "v"(x), "v"(y)
-        : "vcc");
-}
-
-// 256x256 -> 512, columns 0..15
-__device__ __forceinline__ void mul_256x256_asm(uint32_t (&t)[16], const uint32_t (&a)[8],
-                                                const uint32_t (&b)[8]) {
-    uint64_t acc = (uint64_t)a[0] * b[0];
-    uint32_t hi = 0;
-    t[0] = (uint32_t)acc;
-    acc >>= 32;
-#pragma unroll
-    for (int k = 1; k < 15; k++) {
-#pragma unroll
-        for (int i = (k > 7 ? k - 7 : 0); i <= (k < 7 ? k : 7); i++) mad_cc(acc, hi, a[i], b[k - i]);
-        t[k] = (uint32_t)acc;
-        acc = (acc >> 32) | ((uint64_t)hi << 32);
-        hi = 0;
-    }
-    t[15] = (uint32_t)acc;  // column 15 holds only the final carry
-    (void)hi;
-}
-
-// squaring: per column the cross products once, the 96-bit column doubled, plus the square term
-__device__ __forceinline__ void sqr_256_asm(uint32_t (&t)[16], const uint32_t (&a)[8]) {
-    uint64_t carry = 0;  // carry into the current column (< 2^38)
-#pragma unroll
-    for (int k = 0; k < 15; k++) {
-        uint64_t acc = 0;
-        uint32_t hi = 0;
-        // cross products i < j, i + j == k
-#pragma unroll
-        for (int i = (k > 7 ? k - 7 : 0); i < (k + 1) / 2; i++) mad_cc(acc, hi, a[i], a[k - i]);
-        // double the 96-bit column sum
-        hi = (hi << 1) | (uint32_t)(acc >> 63);
-        acc <<= 1;
-        if ((k & 1) == 0) mad_cc(acc, hi, a[k / 2], a[k / 2]);
-        uint64_t s = acc + carry;  // add the incoming carry
-        hi += (s < acc ? 1u : 0u);
-        t[k] = (uint32_t)s;
-        carry = (s >> 32) | ((uint64_t)hi << 32);
-    }
-    t[15] = (uint32_t)carry;
-}
-
 // ---- 256-bit add / sub / shift mod p as single asm statements ----
 // The common path is one 8-limb carry chain plus a two-limb fold of the wrap-around
 // (2^256 == 2^32 + 977); the fold's carry into limb 2 (probability ~2^-64 per lane) and a
@@ -81,20 +32,11 @@ __device__ __forceinline__ void sqr_256_asm(uint32_t (&t)[16], const uint32_t (&
     OPC " %[r6], vcc, 0, %[r6], vcc\n\t" OPC " %[r7], vcc, 0, %[r7], vcc\n"       \
     ".Ldone%=:"
 
-// The carry (borrow) of limb 7, in VCC, as t1 = c and t0 = 977 c: two selects (default), or
-// (BCC_ADD_NOCND) one add-with-carry of zeros plus a 24-bit multiply, no v_cndmask.
-#ifndef BCC_ADD_NOCND
-#define BCC_ADD_NOCND 0
-#endif
-#if BCC_ADD_NOCND
-#define BCC_CARRY_TO_T01                                                           \
-    "v_addc_co_u32_e64 %[t1], %[tmp], 0, 0, vcc\n\t"                               \
-    "v_mul_u32_u24_e32 %[t0], %[k977], %[t1]\n\t"
-#else
+// The carry (borrow) of limb 7, in VCC, as t1 = c and t0 = 977 c (two selects; an add-with-carry
+// plus a 24-bit multiply instead measured neutral, profiles/r02tw4).
 #define BCC_CARRY_TO_T01                                                           \
     "v_cndmask_b32_e64 %[t0], 0, %[k977], vcc\n\t"                                 \
     "v_cndmask_b32_e64 %[t1], 0, 1, vcc\n\t"
-#endif
 
 #define BCC_R_OUT                                                                  \
     [r0] "=&v"(r[0]), [r1] "=&v"(r[1]), [r2] "=&v"(r[2]), [r3] "=&v"(r[3]),      \
@@ -187,49 +129,12 @@ __device__ __forceinline__ uint32_t addc(uint32_t x, uint32_t y, uint32_t cin, u
     return __builtin_addc(x, y, cin, &cout);
 }
 
-// t (512 bits) mod p, weakly reduced (< 2^256): t_lo + t_hi * (2^32 + 977)
-__device__ __forceinline__ void fe_reduce512_asm(uint32_t (&r)[8], const uint32_t (&t)[16]) {
-    // u = t_lo + (t_hi << 32): nine limbs via one carry chain
-    uint32_t u[9], c;
-    u[0] = t[0];
-    u[1] = addc(t[1], t[8], 0, c);
-#pragma unroll
-    for (int i = 2; i < 8; i++) u[i] = addc(t[i], t[7 + i], c, c);
-    u[8] = t[15] + c;  // t[15] + carry cannot overflow past 2^32 here? keep the carry below
-    uint32_t u8c = (u[8] < t[15]) ? 1u : 0u;
-    // r = u + 977 * t_hi, column by column; each column < 2^43
-    uint64_t acc = (uint64_t)t[8] * 977u + u[0];
-    r[0] = (uint32_t)acc;
-#pragma unroll
-    for (int i = 1; i < 8; i++) {
-        acc = (uint64_t)t[8 + i] * 977u + (acc >> 32) + u[i];
-        r[i] = (uint32_t)acc;
-    }
-    // coefficient of 2^256: u8 (+ its carry) + column carry, < 2^33 + 2^11
-    uint64_t top = (acc >> 32) + u[8] + ((uint64_t)u8c << 32);
-    // fold top * (2^32 + 977)
-    uint64_t f = top * 977u + r[0];
-    r[0] = (uint32_t)f;
-    uint32_t c2;
-    uint64_t f1 = (uint64_t)r[1] + (uint32_t)top + (f >> 32);  // < 2^34
-    r[1] = (uint32_t)f1;
-    uint32_t carry = (uint32_t)(f1 >> 32) + (uint32_t)(top >> 32);  // into limb 2, <= 3
-    r[2] = addc(r[2], carry, 0, c2);
-#pragma unroll
-    for (int i = 3; i < 8; i++) r[i] = addc(r[i], 0, c2, c2);
-    if (c2) {  // wrapped past 2^256 (rare): add 2^32 + 977 once more, cannot carry again
-        uint32_t c3;
-        r[0] = addc(r[0], 977u, 0, c3);
-        r[1] = addc(r[1], 1u, c3, c3);
-#pragma unroll
-        for (int i = 2; i < 8; i++) r[i] = addc(r[i], 0, c3, c3);
-    }
-}
-
-// r = t mod p (weak), third formulation: s = t_hi * 977 as a chain of v_mad_u64_u32 whose 64-bit
-// addend is the previous product's high word (p >> 32: one move into a zero-high pair, no 64-bit
-// add), then x = t_lo + s + (t_hi << 32) as two carry chains, then the top fold as in
-// fe_reduce512_asm.  Fewer moves and no v_lshl_add_u64 per limb.
+// r = t mod p (weak, < 2^256) with 2^256 == 2^32 + 977: s = t_hi * 977 as a chain of
+// v_mad_u64_u32 whose 64-bit addend is the previous product's high word (p >> 32: one move into a
+// zero-high pair, no 64-bit add), then x = t_lo + s + (t_hi << 32) as two carry chains, then the
+// top (< 2^34) folded once more; the rare wrap past 2^256 runs behind a branch.  (A per-limb asm
+// carry-chain reduction with SGPR carries measured 4-6 % slower in the ladder: profiles/r02/
+// ab_field_reduction_sqrtail.txt.)
 __device__ __forceinline__ void fe_reduce512_v3(uint32_t (&r)[8], const uint32_t (&t)[16]) {
     uint32_t s[9];
     uint64_t p = (uint64_t)t[8] * 977u;
@@ -264,88 +169,6 @@ __device__ __forceinline__ void fe_reduce512_v3(uint32_t (&r)[8], const uint32_t
 #pragma unroll
     for (int i = 3; i < 8; i++) r[i] = addc(x[i], 0, c2, c2);
     if (c2) {  // wrapped past 2^256 (rare): add 2^32 + 977 once more, cannot carry again
-        uint32_t c3;
-        r[0] = addc(r[0], 977u, 0, c3);
-        r[1] = addc(r[1], 1u, c3, c3);
-#pragma unroll
-        for (int i = 2; i < 8; i++) r[i] = addc(r[i], 0, c3, c3);
-    }
-}
-
-// r = t mod p (weak, r < 2^256), in carry chains of inline asm (no 64-bit adds, no zero-extension
-// moves).  With 2^256 == 2^32 + 977 (mod p) and p_i = t[8+i] * 977 (64-bit, v_mad_u64_u32):
-//   x = sum_i t[i] 2^32i + sum_i t[8+i] 2^32(i+1) + sum_i lo(p_i) 2^32i + sum_i hi(p_i) 2^32(i+1)
-// as three carry chains over ten limbs (A: t_lo + lo(p) on VCC, B: + t_hi << 32, C: + hi(p) << 32,
-// on SGPR pairs, skewed so that neighbouring instructions are independent), then top = x8 + x9 2^32
-// (< 2^34) folded once more as top * 977 + top << 32 (chains D, E); that cannot wrap past 2^256
-// more than once, and the rare wrap adds 2^32 + 977 (a wave-uniform branch).
-// gfx950 resolves VCC / SGPR carry dependencies between back-to-back VALU instructions in
-// hardware (tools/hazard/carry_hazard.hip: 3 x 4M biased chains per form, 0 mismatches), so the
-// chains carry no s_nop pads.
-__device__ __forceinline__ void fe_reduce512_chain(uint32_t (&r)[8], const uint32_t (&t)[16]) {
-    // one statement per limb; the three carries travel between statements in SGPR pairs, and
-    // each product p_i = t[8+i] * 977 is formed just ahead of its limb (few live registers)
-    uint32_t x[10];
-    uint64_t ca, cb, cc;
-    uint64_t p = (uint64_t)t[8] * 977u, q;
-    x[0] = t[0];
-    asm("v_add_co_u32_e64 %0, %1, %0, %2" : "+v"(x[0]), "=s"(ca) : "v"((uint32_t)p));
-    q = (uint64_t)t[9] * 977u;
-    x[1] = t[1];
-    asm("v_addc_co_u32_e64 %0, %1, %0, %4, %1\n\t"
-        "v_add_co_u32_e64 %0, %2, %0, %5\n\t"
-        "v_add_co_u32_e64 %0, %3, %0, %6"
-        : "+v"(x[1]), "+s"(ca), "=s"(cb), "=s"(cc)
-        : "v"((uint32_t)q), "v"(t[8]), "v"((uint32_t)(p >> 32)));
-#pragma unroll
-    for (int i = 2; i < 8; i++) {
-        p = q;
-        q = (uint64_t)t[8 + i] * 977u;
-        x[i] = t[i];
-        asm("v_addc_co_u32_e64 %0, %1, %0, %4, %1\n\t"
-            "v_addc_co_u32_e64 %0, %2, %0, %5, %2\n\t"
-            "v_addc_co_u32_e64 %0, %3, %0, %6, %3"
-            : "+v"(x[i]), "+s"(ca), "+s"(cb), "+s"(cc)
-            : "v"((uint32_t)q), "v"(t[7 + i]), "v"((uint32_t)(p >> 32)));
-    }
-    asm("v_addc_co_u32_e64 %0, %2, 0, 0, %2\n\t"
-        "v_addc_co_u32_e64 %0, %3, %0, %5, %3\n\t"
-        "v_addc_co_u32_e64 %0, %4, %0, %6, %4\n\t"
-        "v_addc_co_u32_e64 %1, %3, 0, 0, %3\n\t"
-        "v_addc_co_u32_e64 %1, %4, %1, 0, %4"
-        : "=&v"(x[8]), "=&v"(x[9]), "+s"(ca), "+s"(cb), "+s"(cc)
-        : "v"(t[15]), "v"((uint32_t)(q >> 32)));
-    const uint32_t x0 = x[0], x1 = x[1], x2 = x[2], x3 = x[3], x4 = x[4], x5 = x[5], x6 = x[6],
-                   x7 = x[7], x8 = x[8], x9 = x[9];
-    // fold top = x8 + x9 * 2^32 (< 2^34): + top * 977 (f) at limb 0, + top at limb 1
-    const uint64_t f = (uint64_t)x8 * 977u;
-    const uint32_t flo = (uint32_t)f, fhi = (uint32_t)(f >> 32) + x9 * 977u;
-    uint32_t w;
-    uint64_t ce;
-    asm("v_add_co_u32_e64 %[r0], vcc, %[x0], %[flo]\n\t"
-        "v_addc_co_u32_e64 %[r1], vcc, %[x1], %[fhi], vcc\n\t"
-        "v_addc_co_u32_e64 %[r2], vcc, %[x2], %[x9], vcc\n\t"
-        "v_add_co_u32_e64 %[r1], %[ce], %[r1], %[x8]\n\t"
-        "v_addc_co_u32_e64 %[r3], vcc, %[x3], 0, vcc\n\t"
-        "v_addc_co_u32_e64 %[r2], %[ce], %[r2], 0, %[ce]\n\t"
-        "v_addc_co_u32_e64 %[r4], vcc, %[x4], 0, vcc\n\t"
-        "v_addc_co_u32_e64 %[r3], %[ce], %[r3], 0, %[ce]\n\t"
-        "v_addc_co_u32_e64 %[r5], vcc, %[x5], 0, vcc\n\t"
-        "v_addc_co_u32_e64 %[r4], %[ce], %[r4], 0, %[ce]\n\t"
-        "v_addc_co_u32_e64 %[r6], vcc, %[x6], 0, vcc\n\t"
-        "v_addc_co_u32_e64 %[r5], %[ce], %[r5], 0, %[ce]\n\t"
-        "v_addc_co_u32_e64 %[r7], vcc, %[x7], 0, vcc\n\t"
-        "v_addc_co_u32_e64 %[r6], %[ce], %[r6], 0, %[ce]\n\t"
-        "v_addc_co_u32_e64 %[w], vcc, 0, 0, vcc\n\t"
-        "v_addc_co_u32_e64 %[r7], %[ce], %[r7], 0, %[ce]\n\t"
-        "v_addc_co_u32_e64 %[w], %[ce], %[w], 0, %[ce]"
-        : [r0] "=&v"(r[0]), [r1] "=&v"(r[1]), [r2] "=&v"(r[2]), [r3] "=&v"(r[3]),
-          [r4] "=&v"(r[4]), [r5] "=&v"(r[5]), [r6] "=&v"(r[6]), [r7] "=&v"(r[7]), [w] "=&v"(w),
-          [ce] "=&s"(ce)
-        : [x0] "v"(x0), [x1] "v"(x1), [x2] "v"(x2), [x3] "v"(x3), [x4] "v"(x4), [x5] "v"(x5),
-          [x6] "v"(x6), [x7] "v"(x7), [x8] "v"(x8), [x9] "v"(x9), [flo] "v"(flo), [fhi] "v"(fhi)
-        : "vcc");
-    if (w) {  // wrapped past 2^256 (rare): add 2^32 + 977 once more; cannot carry again
         uint32_t c3;
         r[0] = addc(r[0], 977u, 0, c3);
         r[1] = addc(r[1], 1u, c3, c3);

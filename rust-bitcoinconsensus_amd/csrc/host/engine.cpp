@@ -536,6 +536,8 @@ struct BatchState {
     std::vector<uint32_t> tx_first;  // first item of each entry
     std::vector<std::vector<uint32_t>> tx_slices;  // per-thread scans building tx_first
     unsigned flags = 0;
+    size_t n = 0;  // items of the current call: st / txs only grow (a shrink would free every
+                   // dropped Item's / TxEntry's buffers, and the next larger call re-allocate them)
 };
 
 // Runs f(t) for t in [0, T) on the calling thread's persistent team (inline when T == 1).
@@ -551,7 +553,7 @@ inline size_t share_lo(size_t n, unsigned t, unsigned T) { return n * t / T; }
 // whose BIP143 aux slots and legacy template the shard's Round owns), balanced by count: shard t
 // is items [bound[t], bound[t + 1]).
 std::vector<size_t> shard_bounds(const BatchState& b, unsigned T) {
-    const size_t n = b.st.size(), E = b.tx_first.size();
+    const size_t n = b.n, E = b.tx_first.size();
     std::vector<size_t> bound(T + 1, n);
     bound[0] = 0;
     for (unsigned t = 0; t + 1 < T; t++) {  // the first tx starting at or after the even split
@@ -570,7 +572,8 @@ std::vector<size_t> shard_bounds(const BatchState& b, unsigned T) {
 void prepare(BatchState& b, const bcc_batch_item* items, size_t n, unsigned flags, unsigned T,
              std::vector<std::vector<uint32_t>>* shards = nullptr,
              std::vector<std::vector<uint32_t>>* runs = nullptr) {
-    b.st.resize(n);  // the state is reused across calls: every field is (re)set below
+    if (b.st.size() < n) b.st.resize(n);  // reused across calls: every field is (re)set below
+    b.n = n;
     b.flags = flags;
     auto& st = b.st;
     const bool flags_ok = (flags & ~(unsigned)FLAGS_VERIFY_ALL) == 0;
@@ -600,7 +603,7 @@ void prepare(BatchState& b, const bcc_batch_item* items, size_t n, unsigned flag
         }
     }
     const size_t E = b.tx_first.size();
-    b.txs.resize(E);
+    if (b.txs.size() < E) b.txs.resize(E);  // grow only, like st
     // per-thread timing (bcc_batch_stats prepare_*): dispatch -> start lag, parse, batched HASH160
     using pclk = std::chrono::steady_clock;
     std::vector<double> lag(T, 0), tparse(T, 0), thash(T, 0);
@@ -627,9 +630,11 @@ void prepare(BatchState& b, const bcc_batch_item* items, size_t n, unsigned flag
         for (size_t k = klo; k < khi; k++) {
             const bcc_batch_item* in = &items[b.tx_first[k]];
             TxEntry& e = b.txs[k];
-            e.aux[0] = e.aux[1] = e.aux[2] = -1;
+            e.aux[0] = e.aux[1] = e.aux[2] = -1;  // every per-round slot (Round::reset's set)
             e.tpl = -1;
             e.wtx = -1;
+            e.htpl = -1;
+            e.hdig = -1;
             e.ok = flags_ok && in->tx_to != nullptr && parse_tx(in->tx_to, in->tx_to_len, e.tx);
             const size_t end = k + 1 < E ? b.tx_first[k + 1] : n;
             for (size_t i = b.tx_first[k]; i < end; i++) {
@@ -1012,7 +1017,9 @@ long chunk_finish(ChunkRun& c, int* ret_out, bitcoinconsensus_error* err_out, bo
         auto s1 = clk::now();
         chunk_stitch(c);
         t_stats.stitch_seconds += since(s1);
-        chunk_interpret(c);
+        bool rerun = false;  // every speculation held (the common case): no further pass at all
+        for (unsigned t = 0; t < c.T; t++) rerun |= !c.run_list[t].empty();
+        if (rerun) chunk_interpret(c);
     }
     for (unsigned t = 0; t < c.T; t++) {
         t_stats.host_rejected += c.rds[t].host_rejected;
@@ -1049,7 +1056,7 @@ void chunk_release_if_large(ChunkRun& c) {
             std::vector<uint32_t>().swap(st[i].pending);
         }
         c.rds[t] = Round();
-        const size_t E = c.b.txs.size();
+        const size_t E = c.b.txs.size();  // every entry, not only this call's
         for (size_t k = share_lo(E, t, c.T); k < share_lo(E, t + 1, c.T); k++) c.b.txs[k].tx = Tx();
     });
     c.b = BatchState();
@@ -1057,23 +1064,23 @@ void chunk_release_if_large(ChunkRun& c) {
 }
 
 // Items per pipelined chunk (bcc_set_pipeline_chunk, BCC_PIPELINE_CHUNK; 0 disables pipelining).
-// Off by default: measured on the GPU box, the overlap hides the chunk's device round but the
-// next chunk's deserialization pass runs 6-7x slower beside it (prepare 13-16 -> 95-106 ms for
-// 1M inputs in 262k chunks; profiles/r02/e2e_pipeline_ab.txt), a net loss.
+// Round 4: chunk k's device round on the pipeline worker beside chunk k + 1's host pass, default
+// 500000 items: 1M C2 inputs 24.9-25.2 -> 28.1-28.5 M inputs/s sustained over 10-call runs on the
+// GPU box (profiles/r04/pipeline).  Rounds 2-3 measured pipelining as a loss; the cause was two
+// per-chunk costs of the host pass, not interference from the device thread (a CPU-only probe
+// with a sleeping device stub reproduced it, tools/pipe_probe): an interpreter pass over every
+// shard after each device round even when no item needed a re-run (Round::reset walks every
+// touched tx), and the per-item state shrinking and re-growing between chunks of different
+// sizes (every Item's / TxEntry's buffers freed and re-allocated).  Both are gone.
 std::atomic<size_t> g_pipeline_chunk{[] {
     const char* e = getenv("BCC_PIPELINE_CHUNK");
-    return e ? (size_t)atoll(e) : (size_t)0;
+    return e ? (size_t)atoll(e) : (size_t)500000;
 }()};
 size_t pipeline_chunk() { return g_pipeline_chunk.load(std::memory_order_relaxed); }
 
-// Staging threads of a pipelined device round (BCC_PIPELINE_STAGE_THREADS, default 4).
-unsigned pipeline_stage_threads() {
-    static const unsigned v = [] {
-        const char* e = getenv("BCC_PIPELINE_STAGE_THREADS");
-        return e ? (unsigned)atoi(e) : 4u;
-    }();
-    return v;
-}
+// Staging threads of a pipelined device round: it fills its pinned image beside the next chunk's
+// host pass, which has the CPU share.
+constexpr unsigned PIPELINE_STAGE_THREADS = 4;
 
 // Runs the batch; fills ret/err per item.  Returns -1 if the device pipeline failed twice in a
 // row for some round: the items that round left unfinished get ret 0 and BCC_ERR_DEVICE_FAILURE
@@ -1119,7 +1126,7 @@ long run_batch(const bcc_batch_item* items, size_t n, unsigned flags, int* ret_o
             }
             if (c.pending_round)
                 c.fut = run_async([&c] {
-                    set_stage_threads(pipeline_stage_threads());  // beside the host pass
+                    set_stage_threads(PIPELINE_STAGE_THREADS);  // beside the host pass
                     return chunk_device_round(c);
                 });
             prev = &c;

@@ -102,15 +102,6 @@ private:
 thread_local std::unique_ptr<Team> tl_team;
 thread_local bool tl_in_team_run = false;  // a nested pass from f(0) gets plain threads
 
-// BCC_HOST_TEAM=0: a fresh std::thread per share and pass (the round-2 behaviour, for A/B runs)
-bool teams_on() {
-    static const bool on = [] {
-        const char* e = getenv("BCC_HOST_TEAM");
-        return !(e && atoi(e) == 0);
-    }();
-    return on;
-}
-
 }  // namespace
 
 void run_team(unsigned T, const std::function<void(unsigned)>& f) {
@@ -118,7 +109,7 @@ void run_team(unsigned T, const std::function<void(unsigned)>& f) {
         f(0);
         return;
     }
-    if (tl_in_team_run || !teams_on()) {
+    if (tl_in_team_run) {
         std::vector<std::exception_ptr> errs(T);
         auto guarded = [&](unsigned t) {
             try {

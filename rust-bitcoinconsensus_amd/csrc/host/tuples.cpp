@@ -77,6 +77,22 @@ thread_local bcc::TupleRows tl_pubkey_rows;
 
 void release_pubkey_rows() { tl_pubkey_rows = bcc::TupleRows(); }
 
+// One device round of rows (the tuple-level entry point's): the host lane code for a small round,
+// else the device with the engine's failure handling.
+int tuple_round(int dev, const bcc::TupleRows& rows, uint8_t* verdict) {
+    if (rows.size() <= host_small_round()) {  // latency: the host lane code
+        host_verify_rows(rows, rows.msg.data(), verdict, host_threads());
+        return 0;
+    }
+    const bcc::SighashJobs none;
+    const bcc::SighashJobs* jp = &none;
+    const bcc::TupleRows* rp = &rows;
+    size_t retries = 0, host_rounds = 0;
+    double st = 0;
+    return resilient_round(dev, &jp, &rp, 1, verdict, &st, &retries, &host_rounds,
+                           "pubkey_verify_batch");
+}
+
 }  // namespace host
 }  // namespace bcc
 
@@ -96,18 +112,7 @@ extern "C" int bcc_pubkey_verify_batch(const uint8_t* pub_blob, const uint64_t* 
             bcc::TupleRows& rows = bcc::host::tl_pubkey_rows;
             bcc::host::parse_rows(pub_blob, pub_off + lo, msg32 + 32 * lo, sig_blob, sig_off + lo,
                                   hi - lo, rows);
-            bcc::SighashJobs none;
-            if (hi - lo <= bcc::host::host_small_round()) {  // latency: the host lane code
-                bcc::host::host_verify_rows(rows, rows.msg.data(), verdict + lo,
-                                            bcc::host::host_threads());
-                return 0;
-            }
-            const bcc::SighashJobs* jp = &none;
-            const bcc::TupleRows* rp = &rows;
-            size_t retries = 0, host_rounds = 0;
-            double st = 0;
-            return bcc::host::resilient_round(devs[d], &jp, &rp, 1, verdict + lo, &st, &retries,
-                                              &host_rounds, "pubkey_verify_batch");
+            return bcc::host::tuple_round(devs[d], rows, verdict + lo);
         });
     }
     devs.resize(D);

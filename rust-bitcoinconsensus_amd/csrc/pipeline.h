@@ -212,17 +212,20 @@ struct TupleRows {
         y.resize(32 * size(), 0);
         pad_msg(size());
     }
-    void copy_y(uint8_t* out) const {  // 32 * size() bytes
-        const size_t n = std::min(y.size(), 32 * size());
-        if (n) memcpy(out, y.data(), n);
-        memset(out + n, 0, 32 * size() - n);
+    void copy_y(uint8_t* out) const { copy_y(out, 0, size()); }  // 32 * size() bytes
+    void copy_msg(uint8_t* out) const { copy_msg(out, 0, size()); }
+    // rows [lo, hi) only, into out (= row lo's slot)
+    void copy_y(uint8_t* out, size_t lo, size_t hi) const {
+        const size_t have = std::min(std::max(y.size() / 32, lo), hi);  // stored rows in range end
+        if (have > lo) memcpy(out, &y[32 * lo], 32 * (have - lo));
+        if (hi > have) memset(out + 32 * (have - lo), 0, 32 * (hi - have));
     }
-    void copy_msg(uint8_t* out) const {  // 32 * size() bytes
-        const size_t n = std::min(msg.size(), 32 * size());
-        if (n) memcpy(out, msg.data(), n);
-        for (size_t k = n / 32; k < size(); k++) {
-            memset(out + 32 * k, 0, 32);
-            out[32 * k] = 1;
+    void copy_msg(uint8_t* out, size_t lo, size_t hi) const {
+        const size_t have = std::min(std::max(msg.size() / 32, lo), hi);
+        if (have > lo) memcpy(out, &msg[32 * lo], 32 * (have - lo));
+        for (size_t k = have; k < hi; k++) {
+            memset(out + 32 * (k - lo), 0, 32);
+            out[32 * (k - lo)] = 1;
         }
     }
     void add_key_hash(uint32_t row, const uint8_t* prog20) {
@@ -361,19 +364,17 @@ int ecdsa_launch_key(SigScratch& sc, const uint8_t* d_tag, const uint8_t* d_x, c
 // (ecdsa_launch_pre / ecdsa_launch_key for the same n, ordered before it); the next
 // ecdsa_launch_after_pre for the same n then forms u1 from the sighash rows and runs only the G
 // ladder, the combine and K_tfin.  A no-op (returns 0) unless the key half ran ahead and n fits one
-// scratch chunk, or with BCC_LADDER_SPLIT=0.
+// scratch chunk.
 int ecdsa_launch_q(SigScratch& sc, const uint8_t* d_r, const uint8_t* d_s, size_t n, void* stream);
 // ev_rows_read (optional hipEvent_t) is recorded on `stream` once the last kernel that reads the
 // s / m / key rows and the s^-1 rows has been launched (the prep kernel): later writers of those
 // rows (the next run's front kernels) need only wait for it, not for the ladder.
 // verdict_and: the caller has set d_verdict[0, n) to 1 (and may already have cleared rows, e.g.
-// the key-hash conditions); K_tfin then only clears the rows that fail.  Only on the twist path
-// (ecdsa_fin_clears()).
+// the key-hash conditions); K_tfin then only clears the rows that fail.
 int ecdsa_launch_after_pre(SigScratch& sc, const uint8_t* d_tag, const uint8_t* d_x,
                            const uint8_t* d_y, const uint8_t* d_r, const uint8_t* d_s,
                            const uint8_t* d_m, uint8_t* d_verdict, size_t n, void* stream,
                            void* ev_rows_read = nullptr, bool verdict_and = false);
-bool ecdsa_fin_clears();
 int schnorr_launch(SigScratch& sc, const uint8_t* d_sig64, const uint8_t* d_msg32,
                    const uint8_t* d_xonly32, uint8_t* d_verdict, size_t n, void* stream);
 
@@ -411,34 +412,24 @@ public:
 private:
     int sync();
     void* pick(void* stream);
-    int launch_wtx(void* stream);
-    int launch_sighash(struct ihipStream_t* st, void* ev_wtx);
     int launch_front(struct ihipStream_t* st);        // K_wtx + K3' + K1 fused, then the rest
-    static bool async_upload();
     int upload_on(struct ihipStream_t* rows_stream, struct ihipStream_t* rest_stream);
-    bool up_pending_ = false;      // the staged image is not on the device yet (async_upload)
+    bool up_pending_ = false;      // the staged image is not on the device yet (issued by run)
     size_t up_rows_ = 0, up_total_ = 0;
     int launch_after_front(struct ihipStream_t* st);  // K_win, K2, K3
     int launch_key_hash(struct ihipStream_t* st);     // K_h160: key-hash conditions into the verdicts
     int run_stages(void* stream);
-    bool kh_done_ = false;  // run_stages ran K_h160 already (ahead of the ladder, verdict_and)                     // run() up to K_tfin
+    bool kh_done_ = false;  // run_stages ran K_h160 already (ahead of the ladder, verdict_and)
     int dev_;
     void* own_stream_ = nullptr;   // hipStream_t, created on first use
     void* last_stream_ = nullptr;  // stream of the last run
-    void* side_stream_ = nullptr;  // K_inv beside the sighash kernels (run())
-    void* wtx_stream_ = nullptr;   // K_wtx beside both (run())
-    void* sh_stream_ = nullptr;    // the other sighash kernels (run(), overlap mode)
+    void* side_stream_ = nullptr;  // the key / Q-ladder chain beside the sighash kernels (run())
     void* ev_fork_ = nullptr;      // hipEvent_t: run() start on the main stream
-    void* ev_join_ = nullptr;      // hipEvent_t: K_inv done on the side stream
-    void* ev_wtx_ = nullptr;       // hipEvent_t: K_wtx done on the side stream
-    void* ev_rows_ = nullptr;      // hipEvent_t: the last run's prep kernel (rows read)
+    void* ev_join_ = nullptr;      // hipEvent_t: the Q ladder done on the side stream
     void* ev_block_ = nullptr;     // hipEvent_t (blocking sync): host waits sleep, not spin
     int wait(void* stream);
-    void* ev_front_ = nullptr;     // hipEvent_t: this run's sighash kernels done (overlap mode)
     void* ev_up_ = nullptr;        // hipEvent_t: the tuple rows uploaded (K_inv on the main stream)
     void* ev_inv_ = nullptr;       // hipEvent_t: K_inv done on the main stream
-    bool rows_pending_ = false;    // ev_rows_ recorded by an earlier run (on rows_stream_)
-    void* rows_stream_ = nullptr;
     SigScratch scratch_;
     void* arena_ = nullptr;
     size_t cap_ = 0;

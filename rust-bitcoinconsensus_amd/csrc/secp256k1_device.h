@@ -179,21 +179,11 @@ BCC_HD void fe_reduce512(fe& r, const u32 (&t)[16]) {
     }
 }
 
-// Device builds use the inline-asm carry-chain product / reduction (fe_asm.h); host builds
-// (tests/native) use the portable formulation above.  Both compute the same weak residue class.
-// Device reduction: the C formulation (fe_reduce512_asm, default) or the carry-chain asm
-// (fe_asm.h fe_reduce512_chain: ~30 % fewer instructions per reduction, but 4-6 % SLOWER in the
-// ladder, its VALU -> SGPR carry round trips being longer than the moves it saves; interleaved A/B
-// in profiles/r02/ab_field_reduction_sqrtail.txt).  A compile-time switch for A/B builds.
-#ifndef BCC_RED_CHAIN
-#define BCC_RED_CHAIN 0
-#endif
-// fe_reduce512_v3 (default): the 977-products chained through their high words, two carry chains
-// for the rest: 4.4 % fewer VALU instructions in the ladder's doubling / addition and +2.4 % on
-// C2 (interleaved A/B, profiles/r02tw4/ab_summary.txt).
-#ifndef BCC_RED_V3
-#define BCC_RED_V3 1
-#endif
+// Device builds use the inline-asm column products (fe_asm_gen.h) and fe_reduce512_v3 (fe_asm.h:
+// the 977-products chained through their high words, two carry chains for the rest; 4.4 % fewer
+// VALU instructions in the ladder than the round-1 reduction, profiles/r02tw4/ab_summary.txt);
+// host builds use 4 x 64-bit limbs (below) or the portable formulation above.  All compute the
+// same weak residue class.
 
 #if !defined(__HIP_DEVICE_COMPILE__) && defined(__SIZEOF_INT128__)
 // Host builds (the engine's host verification, host_verify.cpp, and tests/native): 4 x 64-bit limbs
@@ -260,13 +250,7 @@ BCC_HD void fe_mul(fe& r, const fe& a, const fe& b) {
     u32 t[16];
 #if defined(__HIP_DEVICE_COMPILE__)
     mul_256x256_col(t, a.v, b.v);
-#if BCC_RED_CHAIN
-    fe_reduce512_chain(r.v, t);
-#elif BCC_RED_V3
     fe_reduce512_v3(r.v, t);
-#else
-    fe_reduce512_asm(r.v, t);
-#endif
 #else
     mul_256x256(t, a.v, b.v);
     fe_reduce512(r, t);
@@ -281,13 +265,7 @@ BCC_HD void fe_sqr(fe& r, const fe& a) {
     u32 t[16];
 #if defined(__HIP_DEVICE_COMPILE__)
     sqr_256_col(t, a.v);
-#if BCC_RED_CHAIN
-    fe_reduce512_chain(r.v, t);
-#elif BCC_RED_V3
     fe_reduce512_v3(r.v, t);
-#else
-    fe_reduce512_asm(r.v, t);
-#endif
 #else
     sqr_256(t, a.v);
     fe_reduce512(r, t);

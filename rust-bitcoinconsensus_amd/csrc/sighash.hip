@@ -814,16 +814,11 @@ DeviceBatch::~DeviceBatch() {
     (void)hipSetDevice(dev_);
     if (own_stream_) (void)hipStreamDestroy((hipStream_t)own_stream_);
     if (side_stream_) (void)hipStreamDestroy((hipStream_t)side_stream_);
-    if (sh_stream_) (void)hipStreamDestroy((hipStream_t)sh_stream_);
-    if (wtx_stream_) (void)hipStreamDestroy((hipStream_t)wtx_stream_);
     if (ev_fork_) (void)hipEventDestroy((hipEvent_t)ev_fork_);
     if (ev_join_) (void)hipEventDestroy((hipEvent_t)ev_join_);
-    if (ev_wtx_) (void)hipEventDestroy((hipEvent_t)ev_wtx_);
     if (ev_up_) (void)hipEventDestroy((hipEvent_t)ev_up_);
     if (ev_inv_) (void)hipEventDestroy((hipEvent_t)ev_inv_);
-    if (ev_rows_) (void)hipEventDestroy((hipEvent_t)ev_rows_);
     if (ev_block_) (void)hipEventDestroy((hipEvent_t)ev_block_);
-    if (ev_front_) (void)hipEventDestroy((hipEvent_t)ev_front_);
     if (arena_) (void)hipFree(arena_);
     if (host_image_) (void)hipHostFree(host_image_);
     if (vbuf_) (void)hipHostFree(vbuf_);
@@ -878,7 +873,6 @@ int DeviceBatch::stage(const SighashJobs& j, const TupleRows& rows) {
 // jobs and no pageable-memory staging.
 int DeviceBatch::stage_parts(const SighashJobs* const* J, const TupleRows* const* Rw, size_t P) {
     if (int e = sync()) return e;  // the previous run may still read the arena / the image
-    rows_pending_ = false;
     std::vector<size_t> row0(P + 1, 0), auxb0(P + 1, 0), preb0(P + 1, 0), auxi0(P + 1, 0),
         prei0(P + 1, 0), pat0(P + 1, 0), tpl0(P + 1, 0), code0(P + 1, 0), tj0(P + 1, 0),
         raw0(P + 1, 0), wtx0(P + 1, 0), wj0(P + 1, 0), win0(P + 1, 0), h0(P + 1, 0);
@@ -979,19 +973,28 @@ int DeviceBatch::stage_parts(const SighashJobs* const* J, const TupleRows* const
     d_zeros_ = a + off[ZEROS]; d_intab_ = (uint32_t*)(a + off[INTAB]); d_txd_ = a + off[TXD];
     uint8_t* h = (uint8_t*)host_image_;
     memset(h + off[ZEROS], 0, 64);
-    auto fill = [&](size_t p) {
-        const SighashJobs& j = *J[p];
+    // the rows of part p in [lo, hi): the bulk of a tuple batch, copied in blocks by the team
+    auto fill_rows = [&](size_t p, size_t lo, size_t hi) {
         const TupleRows& rw = *Rw[p];
-        const size_t nr = rw.size(), r0 = row0[p];
+        const size_t r0 = row0[p] + lo, nr = hi - lo;
         auto cp = [&](int b, size_t at, const void* src, size_t len) {
             if (len) memcpy(h + off[b] + at, src, len);
         };
-        cp(TAG, r0, rw.tag.data(), nr);
-        cp(X, 32 * r0, rw.x.data(), 32 * nr);
-        if (need_y && nr) rw.copy_y(h + off[Y] + 32 * r0);  // rows past the stored prefix: zero
-        cp(RR, 32 * r0, rw.r.data(), 32 * nr);
-        cp(S, 32 * r0, rw.s.data(), 32 * nr);
-        if (need_m && nr) rw.copy_msg(h + off[M] + 32 * r0);  // rows past the stored prefix: ONE
+        cp(TAG, r0, rw.tag.data() + lo, nr);
+        cp(X, 32 * r0, rw.x.data() + 32 * lo, 32 * nr);
+        if (need_y && nr) rw.copy_y(h + off[Y] + 32 * r0, lo, hi);  // past the stored prefix: zero
+        cp(RR, 32 * r0, rw.r.data() + 32 * lo, 32 * nr);
+        cp(S, 32 * r0, rw.s.data() + 32 * lo, 32 * nr);
+        if (need_m && nr) rw.copy_msg(h + off[M] + 32 * r0, lo, hi);  // past the stored prefix: ONE
+    };
+    // part p's jobs and key-hash records (offsets fixed up for the concatenation)
+    auto fill = [&](size_t p) {
+        const SighashJobs& j = *J[p];
+        const TupleRows& rw = *Rw[p];
+        const size_t r0 = row0[p];
+        auto cp = [&](int b, size_t at, const void* src, size_t len) {
+            if (len) memcpy(h + off[b] + at, src, len);
+        };
         cp(AUX, auxb0[p], j.aux.data(), j.aux.size());
         cp(PRE, preb0[p], j.pre.data(), j.pre.size());
         const uint32_t ablk = (uint32_t)(auxb0[p] / 64), pblk = (uint32_t)(preb0[p] / 64);
@@ -1038,25 +1041,36 @@ int DeviceBatch::stage_parts(const SighashJobs* const* J, const TupleRows* const
         for (size_t k = 0; k < rw.hrow.size(); k++) hr[k] = rw.hrow[k] + (uint32_t)r0;
         cp(HPROG, 20 * h0[p], rw.hprog.data(), rw.hprog.size());
     };
-    const size_t nth = std::min<size_t>(P, tl_stage_threads ? tl_stage_threads : P);
+    // work items: blocks of <= 64k rows of every part, then every part's jobs
+    struct Work {
+        size_t p, lo, hi;  // hi == 0: part p's jobs
+    };
+    std::vector<Work> work;
+    constexpr size_t RB = (size_t)1 << 16;
+    for (size_t p = 0; p < P; p++)
+        for (size_t lo = 0, nr = Rw[p]->size(); lo < nr; lo += RB)
+            work.push_back(Work{p, lo, std::min(nr, lo + RB)});
+    for (size_t p = 0; p < P; p++) work.push_back(Work{p, 0, 0});
+    auto run_work = [&](const Work& w) {
+        if (w.hi) fill_rows(w.p, w.lo, w.hi);
+        else fill(w.p);
+    };
+    const size_t want = tl_stage_threads ? tl_stage_threads : std::max<size_t>(P, 16);
+    const size_t nth = std::min(work.size(), want);
     if (nth <= 1 || upload < ((size_t)1 << 20)) {
-        for (size_t p = 0; p < P; p++) fill(p);
+        for (const Work& w : work) run_work(w);
     } else {
         host::run_team((unsigned)nth, [&](unsigned t) {
-            for (size_t p = t; p < P; p += nth) fill(p);
+            for (size_t k = t; k < work.size(); k += nth) run_work(work[k]);
         });
     }
     BCC_HIP_TRY(hipSetDevice(dev_));
-    if (async_upload()) {
-        // the copy is issued by the next run, in two parts on the two streams that need them
-        // first (upload_on): the tuple rows on the side stream ahead of K_inv / K_tkey / the Q
-        // ladder, the sighash inputs on the main stream ahead of the front kernel
-        up_pending_ = true;
-        up_rows_ = off[AUX];
-        up_total_ = upload;
-    } else {
-        BCC_HIP_TRY(hipMemcpy(arena_, host_image_, upload, hipMemcpyHostToDevice));
-    }
+    // the copy is issued by the next run, in two parts on the two streams that need them first
+    // (upload_on): the tuple rows on the side stream ahead of K_inv / K_tkey / the Q ladder, the
+    // sighash inputs on the main stream ahead of the front kernel
+    up_pending_ = true;
+    up_rows_ = off[AUX];
+    up_total_ = upload;
     if (need_y) BCC_HIP_TRY(hipMemcpy(a + off[Y], h + off[Y], 32 * R, hipMemcpyHostToDevice));
     if (need_m) {
         BCC_HIP_TRY(hipMemcpy(a + off[M], h + off[M], 32 * R, hipMemcpyHostToDevice));
@@ -1068,15 +1082,6 @@ int DeviceBatch::stage_parts(const SighashJobs* const* J, const TupleRows* const
         BCC_HIP_TRY(hipStreamSynchronize(nullptr));
     }
     return 0;
-}
-
-// BCC_ASYNC_UPLOAD=0: stage_parts copies the whole image synchronously (the round-2 way; A/B).
-bool DeviceBatch::async_upload() {
-    static const bool on = [] {
-        const char* e = getenv("BCC_ASYNC_UPLOAD");
-        return !(e && atoi(e) == 0);
-    }();
-    return on;
 }
 
 // The staged image's pending upload: all of it on `rows_stream` when `rest_stream` is null, else
@@ -1096,34 +1101,6 @@ int DeviceBatch::upload_on(hipStream_t rows_stream, hipStream_t rest_stream) {
         BCC_HIP_TRY(hipMemcpyAsync(a + up_rows_, h + up_rows_, up_total_ - up_rows_,
                                    hipMemcpyHostToDevice, rest_stream));
     return 0;
-}
-
-int DeviceBatch::launch_wtx(void* stream) {
-    if (n_wtx_) {  // K_wtx: device-side deserialization + BIP143 per-tx hashes
-        hipLaunchKernelGGL(bip143_tx_kernel, dim3((unsigned)((3 * n_wtx_ + XS_WG - 1) / XS_WG)),
-                           dim3(XS_WG), 0, (hipStream_t)stream, d_txraw_, d_wtx_, (uint32_t)n_wtx_,
-                           d_intab_, d_txd_);
-        BCC_HIP_TRY(hipGetLastError());
-    }
-    return 0;
-}
-
-// The sighash kernels on `st`; K_wtx too unless run() already launched it on the side stream
-// (then K_win waits for `ev_wtx`).
-int DeviceBatch::launch_sighash(hipStream_t st, void* ev_wtx) {
-    if (n_aux_ + n_tjob_) {  // K1 + K3' in one launch
-        const size_t lanes = n_aux_ + n_tjob_;
-        hipLaunchKernelGGL(sha256d_aux_tpl_kernel, dim3((unsigned)((lanes + 63) / 64)), dim3(64), 0, st,
-                           d_aux_, d_aux_off_, d_aux_nblk_, (uint32_t)n_aux_, d_auxd_, d_tpl_, d_code_,
-                           d_tjob_, (uint32_t)n_tjob_, d_m);
-        BCC_HIP_TRY(hipGetLastError());
-    }
-    if (ev_wtx) {
-        if (n_wtx_) BCC_HIP_TRY(hipStreamWaitEvent(st, (hipEvent_t)ev_wtx, 0));
-    } else if (int e = launch_wtx(st)) {
-        return e;
-    }
-    return launch_after_front(st);
 }
 
 // K_win, K2, K3: everything of the sighash stage after K_wtx / K1 / K3'.
@@ -1221,37 +1198,6 @@ int DeviceBatch::launch_key_hash(hipStream_t st) {
     return 0;
 }
 
-// Consecutive run()s of a resident batch may overlap (BCC_OVERLAP_RUNS=1): see DeviceBatch::run.
-// Off by default: +1.5 % on the staged C2 loop (84.2-85.6 -> 86.2-86.5 M verifies/s,
-// profiles/r02tw3) but -15 % on C3's verify_batch calls (1.78-1.80 -> 1.43-1.61 M inputs/s,
-// profiles/r02tw7): its fourth stream exceeds the box's 4 hardware queues per process.
-static bool overlap_runs() {
-    static const bool on = [] {
-        const char* e = getenv("BCC_OVERLAP_RUNS");
-        return e && atoi(e) != 0;
-    }();
-    return on;
-}
-
-// K_h160 beside the Q ladder instead of after K_tfin (default); BCC_KEY_HASH_EARLY=0 reverts
-static bool key_hash_early() {
-    static const bool on = [] {
-        const char* e = getenv("BCC_KEY_HASH_EARLY");
-        return !(e && atoi(e) == 0);
-    }();
-    return on;
-}
-
-// K_inv on the main stream beside K_tkey (default since round 3: C2 +0.9..1.2 % in an interleaved
-// A/B, profiles/r03/ab/inv_main); BCC_INV_MAIN=0 puts it back ahead of K_tkey on the side stream
-static bool inv_on_main() {
-    static const bool on = [] {
-        const char* e = getenv("BCC_INV_MAIN");
-        return !(e && atoi(e) == 0);
-    }();
-    return on;
-}
-
 // K_inv and K_key read only the s and key rows, so they run on a side stream beside the sighash
 // kernels (fork / join by events: graph-capturable); prep + ladder wait for both.
 int DeviceBatch::run(void* stream) {
@@ -1267,110 +1213,53 @@ int DeviceBatch::run(void* stream) {
     return launch_key_hash(st);
 }
 
+// Two streams: the sighash stage on the main stream (K_wtx + K3' + K1 fused into one front launch,
+// then K_win / K2 / K3), and on the side stream the key half of the prep (K_tkey) and everything
+// the message does not enter -- the signature half of the prep and the Q ladder
+// (ecdsa_launch_q); the G ladder and K_tfin wait for both.  K_inv (one latency-bound wave per
+// SIMD) runs on the main stream beside K_tkey, so the side stream's chain to the Q ladder does not
+// include it (C2 +0.9..1.2 % in an interleaved A/B, profiles/r03/ab/inv_main).  K_h160 needs only
+// the key rows and the programs: it runs on the main stream beside the Q ladder into verdicts
+// preset to 1, and K_tfin then only clears failing rows (verdict_and), instead of running after
+// K_tfin at the end of the critical path.
 int DeviceBatch::run_stages(void* stream) {
     hipStream_t st = (hipStream_t)stream;
     kh_done_ = false;
     if (!side_stream_) {
-        hipStream_t s = nullptr, s2 = nullptr;
-        hipEvent_t a = nullptr, b = nullptr, c = nullptr;
+        hipStream_t s = nullptr;
+        hipEvent_t a = nullptr, b = nullptr, c = nullptr, d = nullptr;
         BCC_HIP_TRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-        // a third stream only for the overlap mode: every stream beyond two shares a hardware queue
-        if (overlap_runs()) BCC_HIP_TRY(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
         BCC_HIP_TRY(hipEventCreateWithFlags(&a, hipEventDisableTiming));
         BCC_HIP_TRY(hipEventCreateWithFlags(&b, hipEventDisableTiming));
         BCC_HIP_TRY(hipEventCreateWithFlags(&c, hipEventDisableTiming));
+        BCC_HIP_TRY(hipEventCreateWithFlags(&d, hipEventDisableTiming));
         side_stream_ = s;
-        wtx_stream_ = s2;
         ev_fork_ = a;
         ev_join_ = b;
-        ev_wtx_ = c;
+        ev_up_ = c;
+        ev_inv_ = d;
     }
-    hipStream_t side = (hipStream_t)side_stream_, ws = (hipStream_t)wtx_stream_;
-    if (overlap_runs()) {
-        if (int e = upload_on(st, nullptr)) return e;
-        // Run-to-run overlap: this run's front (K_inv; K_wtx then the other sighash kernels) waits
-        // only for the previous run's prep kernel -- the last reader of the rows it rewrites --
-        // not for that run's ladder, so it fills the ladder's tail.  Prep waits for the front.
-        if (!ev_rows_) {
-            hipEvent_t a = nullptr, b = nullptr;
-            BCC_HIP_TRY(hipEventCreateWithFlags(&a, hipEventDisableTiming));
-            BCC_HIP_TRY(hipEventCreateWithFlags(&b, hipEventDisableTiming));
-            ev_rows_ = a;
-            ev_front_ = b;
-        }
-        if (!sh_stream_) {
-            hipStream_t s3 = nullptr;
-            BCC_HIP_TRY(hipStreamCreateWithFlags(&s3, hipStreamNonBlocking));
-            sh_stream_ = s3;
-        }
-        hipStream_t ss = (hipStream_t)sh_stream_;
-        BCC_HIP_TRY(hipEventRecord((hipEvent_t)ev_fork_, st));  // staging / earlier work on st
-        hipEvent_t gate = rows_pending_ && rows_stream_ == st ? (hipEvent_t)ev_rows_
-                                                              : (hipEvent_t)ev_fork_;
-        BCC_HIP_TRY(hipStreamWaitEvent(side, gate, 0));
-        BCC_HIP_TRY(hipStreamWaitEvent(ws, gate, 0));
-        BCC_HIP_TRY(hipStreamWaitEvent(ss, gate, 0));
-        if (int e = ecdsa_launch_pre(scratch_, d_tag, d_x, d_y, d_s, n_rows_, side)) return e;
-        BCC_HIP_TRY(hipEventRecord((hipEvent_t)ev_join_, side));
-        // K_wtx on ws beside K1 + K3' on ss (a block's long legacy chains and its BIP143 per-tx
-        // chains overlap), K_win on ss after both
-        if (n_wtx_) {
-            if (int e = launch_wtx(ws)) return e;
-            BCC_HIP_TRY(hipEventRecord((hipEvent_t)ev_wtx_, ws));
-        }
-        if (int e = launch_sighash(ss, ev_wtx_)) return e;
-        BCC_HIP_TRY(hipEventRecord((hipEvent_t)ev_front_, ss));
-        BCC_HIP_TRY(hipStreamWaitEvent(st, (hipEvent_t)ev_join_, 0));
-        BCC_HIP_TRY(hipStreamWaitEvent(st, (hipEvent_t)ev_front_, 0));
-        rows_pending_ = true;
-        rows_stream_ = st;
-        return ecdsa_launch_after_pre(scratch_, d_tag, d_x, d_y, d_r, d_s, d_m, d_v, n_rows_, st,
-                                      ev_rows_);
-    }
+    hipStream_t side = (hipStream_t)side_stream_;
     BCC_HIP_TRY(hipEventRecord((hipEvent_t)ev_fork_, st));
     BCC_HIP_TRY(hipStreamWaitEvent(side, (hipEvent_t)ev_fork_, 0));
-    // two streams: the sighash stage on the main stream (K_wtx + K3' + K1 fused into one front
-    // launch, then K_win / K2 / K3), and on the side stream K_inv, the key half of the prep
-    // (K_tkey) and everything the message does not enter -- the signature half of the prep and
-    // the Q ladder (ecdsa_launch_q); the G ladder and K_tfin wait for both
-    (void)ws;
     if (int e = upload_on(side, st)) return e;
-    if (inv_on_main()) {
-        // K_inv (one latency-bound wave per SIMD) on the main stream, beside K_tkey on the side
-        // stream, instead of ahead of it: the side stream's chain to the Q ladder loses K_inv
-        if (!ev_up_) {
-            hipEvent_t a = nullptr, b = nullptr;
-            BCC_HIP_TRY(hipEventCreateWithFlags(&a, hipEventDisableTiming));
-            BCC_HIP_TRY(hipEventCreateWithFlags(&b, hipEventDisableTiming));
-            ev_up_ = a;
-            ev_inv_ = b;
-        }
-        BCC_HIP_TRY(hipEventRecord((hipEvent_t)ev_up_, side));  // the s rows are on the device
-        BCC_HIP_TRY(hipStreamWaitEvent(st, (hipEvent_t)ev_up_, 0));
-        if (int e = ecdsa_launch_pre(scratch_, d_tag, d_x, d_y, d_s, n_rows_, st)) return e;
-        BCC_HIP_TRY(hipEventRecord((hipEvent_t)ev_inv_, st));
-        if (int e = ecdsa_launch_key(scratch_, d_tag, d_x, d_y, n_rows_, side)) return e;
-        BCC_HIP_TRY(hipStreamWaitEvent(side, (hipEvent_t)ev_inv_, 0));  // K_tscal_q reads s^-1
-    } else {
-        if (int e = ecdsa_launch_pre(scratch_, d_tag, d_x, d_y, d_s, n_rows_, side)) return e;
-        if (int e = ecdsa_launch_key(scratch_, d_tag, d_x, d_y, n_rows_, side)) return e;
-    }
+    BCC_HIP_TRY(hipEventRecord((hipEvent_t)ev_up_, side));  // the s / key rows are on the device
+    BCC_HIP_TRY(hipStreamWaitEvent(st, (hipEvent_t)ev_up_, 0));
+    if (int e = ecdsa_launch_pre(scratch_, d_tag, d_x, d_y, d_s, n_rows_, st)) return e;
+    BCC_HIP_TRY(hipEventRecord((hipEvent_t)ev_inv_, st));
+    if (int e = ecdsa_launch_key(scratch_, d_tag, d_x, d_y, n_rows_, side)) return e;
+    BCC_HIP_TRY(hipStreamWaitEvent(side, (hipEvent_t)ev_inv_, 0));  // K_tscal_q reads s^-1
     if (int e = ecdsa_launch_q(scratch_, d_r, d_s, n_rows_, side)) return e;
     BCC_HIP_TRY(hipEventRecord((hipEvent_t)ev_join_, side));
     if (int e = launch_front(st)) return e;
-    // K_h160 needs only the key rows and the programs: on the main stream it runs beside the Q
-    // ladder into verdicts preset to 1, and K_tfin then only clears failing rows (verdict_and),
-    // instead of running after K_tfin at the end of the critical path.  The key rows arrive on the
-    // side stream: the main stream waited for them before K_inv (inv_on_main).
-    const bool kh_early = n_hash_ && inv_on_main() && key_hash_early() && ecdsa_fin_clears();
-    if (kh_early) {
+    if (n_hash_) {
         BCC_HIP_TRY(hipMemsetAsync(d_v, 1, n_rows_, st));
         if (int e = launch_key_hash(st)) return e;
         kh_done_ = true;
     }
     BCC_HIP_TRY(hipStreamWaitEvent(st, (hipEvent_t)ev_join_, 0));
     return ecdsa_launch_after_pre(scratch_, d_tag, d_x, d_y, d_r, d_s, d_m, d_v, n_rows_, st,
-                                  nullptr, kh_early);
+                                  nullptr, kh_done_);
 }
 
 // Verdicts come back through a pinned buffer of the batch (an asynchronous copy on the run's stream,

@@ -1,5 +1,5 @@
-// tests/native/lane_host.cpp — TEST ONLY. Runs the product's per-lane ECDSA code
-// (rust-bitcoinconsensus_amd/csrc/ecdsa_lane.h) on the CPU, so the exact arithmetic the HIP kernel
+// tests/native/lane_host.cpp — TEST ONLY. Runs the product's per-lane signature code
+// (rust-bitcoinconsensus_amd/csrc/ecdsa_twist.h + ecdsa_lane.h) on the CPU, so the exact arithmetic the HIP kernel
 // executes can be checked against the oracle without a GPU. Never linked into the product.
 #include "../../rust-bitcoinconsensus_amd/csrc/ecdsa_lane.h"
 #include "../../rust-bitcoinconsensus_amd/csrc/ecdsa_twist.h"
@@ -18,25 +18,6 @@ static std::vector<fe>& gtab() {
     return t;
 }
 
-extern "C" int lane_verify(unsigned tag, const unsigned char* x32, const unsigned char* y32,
-                           const unsigned char* r32, const unsigned char* s32,
-                           const unsigned char* m32) {
-    fe px, py;
-    sc r, s, m;
-    fe_from_be_bytes(px, x32);
-    fe_from_be_bytes(py, y32);
-    fe t;
-    fe_from_be_bytes(t, r32);
-    memcpy(r.v, t.v, 32);
-    fe_from_be_bytes(t, s32);
-    memcpy(s.v, t.v, 32);
-    fe_from_be_bytes(t, m32);
-    memcpy(m.v, t.v, 32);
-    QTableArray qt;
-    GTableArray gt{gtab().data()};
-    return ecdsa_verify_lane(tag, px, py, r, s, m, qt, gt);
-}
-
 static std::vector<fe>& gcomb() {
     static std::vector<fe> t;
     if (t.empty()) {
@@ -46,7 +27,8 @@ static std::vector<fe>& gcomb() {
     return t;
 }
 
-// the square-root-free ECDSA path (ecdsa_twist.h), same arguments as lane_verify
+// the square-root-free ECDSA path (ecdsa_twist.h): the key header byte, x, y (ignored for 02/03),
+// r, s and the message as 32-byte big-endian strings
 extern "C" int lane_verify_twist(unsigned tag, const unsigned char* x32, const unsigned char* y32,
                                  const unsigned char* r32, const unsigned char* s32,
                                  const unsigned char* m32) {
@@ -99,22 +81,6 @@ extern "C" int lane_schnorr_verify_twist(const unsigned char* sig64, const unsig
     QTableArray qt;
     GCombArray gc{gcomb().data()};
     return schnorr_verify_twist_lane(px, rx, s, m, qt, gc);
-}
-
-// BIP340: sig64 = r.x || s, msg32, x-only key (secp256k1_schnorrsig_verify argument order)
-extern "C" int lane_schnorr_verify(const unsigned char* sig64, const unsigned char* msg32,
-                                   const unsigned char* xonly32) {
-    fe px, rx, t;
-    sc s, m;
-    fe_from_be_bytes(rx, sig64);
-    fe_from_be_bytes(t, sig64 + 32);
-    memcpy(s.v, t.v, 32);
-    fe_from_be_bytes(t, msg32);
-    memcpy(m.v, t.v, 32);
-    fe_from_be_bytes(px, xonly32);
-    QTableArray qt;
-    GTableArray gt{gtab().data()};
-    return schnorr_verify_lane(px, rx, s, m, qt, gt);
 }
 
 // the generator's BIP340 signer (nonce supplied): returns 0 for d or k == 0

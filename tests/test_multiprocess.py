@@ -1,9 +1,10 @@
-"""CPU, world_size 2 over gloo: the multi-GPU bench path's aggregation (max wall time over ranks,
-sum of valid verdicts) and per-rank shard seeding, exercised without a GPU."""
+"""CPU, world_size 2 and 4 over gloo: the multi-GPU bench path's aggregation (max wall time over
+ranks, sum of valid verdicts) and per-rank shard seeding, exercised without a GPU."""
 import os
 import socket
 import sys
 
+import pytest
 import torch.multiprocessing as mp
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -28,18 +29,21 @@ def _worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def test_aggregate_world2_gloo():
+@pytest.mark.parametrize("world", [2, 4])
+def test_aggregate_gloo(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    ps = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in ps:
         p.start()
     for p in ps:
         p.join(120)
         assert p.exitcode == 0
-    res = sorted(q.get() for _ in range(2))
-    assert res == [(0, 2.0, 201), (1, 2.0, 201)]
+    res = sorted(q.get() for _ in range(world))
+    want_t = float(world)  # max over ranks of 1 + rank
+    want_v = sum(100 + r for r in range(world))
+    assert res == [(r, want_t, want_v) for r in range(world)]
 
 
 def _shard_worker(rank, world, port, q):
@@ -63,9 +67,10 @@ def _shard_worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def test_sharded_tuple_set_gather_world2_gloo():
-    """§8e: two ranks each verify their half of one tuple set; the gathered validity bitmap equals
-    the single-process verdicts (and the reference's labels)."""
+@pytest.mark.parametrize("world", [2, 4])
+def test_sharded_tuple_set_gather_gloo(world):
+    """§8e: `world` ranks each verify their contiguous range of one tuple set; the gathered validity
+    bitmap equals the single-process verdicts (and the reference's labels)."""
     sys.path[:0] = [os.path.join(ROOT, "tests")]
     import engine_stub
     from fixtures import ecdsa_tuples
@@ -73,16 +78,16 @@ def test_sharded_tuple_set_gather_world2_gloo():
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_shard_worker, args=(r, 2, port, q)) for r in range(2)]
+    ps = [ctx.Process(target=_shard_worker, args=(r, world, port, q)) for r in range(world)]
     for p in ps:
         p.start()
     for p in ps:
         p.join(300)
         assert p.exitcode == 0
-    res = dict(q.get() for _ in range(2))
+    res = dict(q.get() for _ in range(world))
     ts = ecdsa_tuples() * 3
     single = engine_stub.pubkey_verify(engine_stub.load(), ts)
-    assert res[0] == res[1] == single
+    assert all(res[r] == single for r in range(world))
     assert list(single) == [t["verdict"] for t in ts]
 
 

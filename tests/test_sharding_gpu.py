@@ -89,3 +89,35 @@ def test_rank_partition_of_one_global_set():
         t.run()
     assert t_full.verdicts() == b"".join(t.verdicts() for t in t_parts)
     assert t_full.verdicts() == bytes(hf["expect"])
+
+
+def test_eight_entry_device_list():
+    """The node shape: an 8-entry device list, here device 0 eight times, so eight
+    persistent per-GPU workers with their own streams, arenas and scratch split each round of
+    verify_batch (cut at transaction boundaries) and each tuple batch (equal ranges) -- the same
+    code path an 8 x MI355X node runs.  Verdicts equal the single-device engine's and the
+    reference labels."""
+    import json
+    import os
+    import bitcoinconsensus_amd as B
+    from fixtures import ecdsa_tuples
+    shape = [tuple(t) for t in json.load(open(os.path.join(
+        os.path.dirname(os.path.abspath(__file__)), "golden", "block413567_shape.json")))["txs"]]
+    wl = B.Workload(kind="block", shape=shape[:800], seed=0x5EED0013)
+    items = [wl.item(i) for i in range(wl.n)]
+    ts = ecdsa_tuples() * 16
+    tuples = [(t["pub"], t["hash"], t["sig"]) for t in ts]
+    B.set_devices([])
+    single = B.verify_batch(items)
+    one = B.pubkey_verify_batch(tuples, device=0)
+    try:
+        B.set_devices([0] * 8)
+        assert B.get_devices() == [0] * 8
+        multi = B.verify_batch(items)
+        st = B.last_batch_stats()
+        many = B.pubkey_verify_batch(tuples, device=-1)
+    finally:
+        B.set_devices([])
+    assert st["devices"] == 8
+    assert multi == single and all(r == 1 for r, _ in multi)
+    assert many == one and list(one) == [t["verdict"] for t in ts]
