@@ -149,7 +149,8 @@ int mi_primbench(int prim, int iters, int warm, double* cycles, double* ms);
 
 /* ---- field self-test (tests only): one device Fp operation over n operand pairs ------------
  * a, b, out: n x 8 little-endian u32 limbs.  op: 0 add, 1 sub, 2 mul, 3 sqr, 4/5/6 shift by
- * 1/2/3, 7 neg, 8 is_zero (out[0]), 9 normalize.  Results are weak (< 2^256) except 8, 9. */
+ * 1/2/3, 7 neg, 8 is_zero (out[0]), 9 normalize, 10 fe_inv (mod p), 11 sc_inv (mod n, a < n).
+ * Results are weak (< 2^256) except 8-11. */
 int mi_fe_selftest(int op, const uint32_t* a, const uint32_t* b, uint32_t* out, size_t n);
 
 #ifdef __cplusplus

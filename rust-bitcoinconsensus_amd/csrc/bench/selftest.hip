@@ -29,6 +29,16 @@ __global__ __launch_bounds__(256) void fe_selftest_kernel(int op, const u32* __r
         case 7: fe_neg(r, x); break;
         case 8: r.v[0] = fe_is_zero(x) ? 1u : 0u; break;
         case 9: r = x; fe_normalize(r); break;
+        case 10: fe_inv(r, x); break;  // weak input, normalized inverse
+        case 11: {                     // scalar inverse of x < n
+            sc xs, rs;
+#pragma unroll
+            for (int j = 0; j < 8; j++) xs.v[j] = x.v[j];
+            sc_inv(rs, xs);
+#pragma unroll
+            for (int j = 0; j < 8; j++) r.v[j] = rs.v[j];
+            break;
+        }
         default: break;
     }
 #pragma unroll
@@ -40,7 +50,8 @@ __global__ __launch_bounds__(256) void fe_selftest_kernel(int op, const u32* __r
 extern "C" {
 
 // a, b, out: n x 8 little-endian u32 limbs (host memory).  op: 0 add, 1 sub, 2 mul, 3 sqr,
-// 4/5/6 shift left by 1/2/3, 7 neg, 8 is_zero (out[0]), 9 normalize.  0 on success.
+// 4/5/6 shift left by 1/2/3, 7 neg, 8 is_zero (out[0]), 9 normalize, 10 fe_inv, 11 sc_inv (a < n).
+// 0 on success.
 int mi_fe_selftest(int op, const uint32_t* a, const uint32_t* b, uint32_t* out, size_t n) {
     using namespace bcc;
     if (n == 0) return 0;

@@ -30,6 +30,8 @@
 #define BCC_HD_NOINLINE
 #endif
 
+#include "modinv_device.h"  // the lanes' safegcd inverse (fe_inv, sc_inv)
+
 namespace bcc {
 
 typedef uint32_t u32;
@@ -495,11 +497,23 @@ BCC_HD bool fe_sqrt(fe& r, const fe& a) {
     return fe_equal(t, a);
 }
 
-// r = a^(p-2) (host builds: the variable-time safegcd inverse, modinv_host.h)
+// r = a^-1 mod p (0 for a == 0): the safegcd inverse, 30-bit divstep batches on the device
+// (modinv_device.h), 62-bit variable-time batches on the host (modinv_host.h).  Round 4 replaced
+// the Fermat chain below (kept for BCC_INV_SAFEGCD=0 builds, the A/B baseline): C2 ECDSA stage
+// 10.36-10.40 -> 9.99-10.01 ms, C3 staged ECDSA stage 1.41 -> 1.09 ms (profiles/r04/ab_safegcd).
+#ifndef BCC_INV_SAFEGCD
+#define BCC_INV_SAFEGCD 1
+#endif
 BCC_HD void fe_inv(fe& r, const fe& a) {
 #if defined(BCC_FE_HOST64)
     const u32 P[8] = BCC_P_LIMBS;
     modinv::inverse_var(r.v, a.v, P);
+    return;
+#elif BCC_INV_SAFEGCD
+    const u32 P[8] = BCC_P_LIMBS;
+    fe an = a;
+    fe_normalize(an);  // weak input: the inverse wants a < p
+    mi30::inverse(r.v, an.v, P, 0x2ddacacfu);
     return;
 #endif
     fe x223, x22, x2, t;
@@ -773,6 +787,10 @@ BCC_HD void sc_inv(sc& r, const sc& a) {
 #if defined(BCC_FE_HOST64)  // host builds: the variable-time safegcd inverse (modinv_host.h)
     const u32 N[8] = BCC_N_LIMBS;
     modinv::inverse_var(r.v, a.v, N);
+    return;
+#elif BCC_INV_SAFEGCD  // device: the 30-bit safegcd (modinv_device.h); a < n
+    const u32 N[8] = BCC_N_LIMBS;
+    mi30::inverse(r.v, a.v, N, 0x2a774ec1u);
     return;
 #endif
     // n - 2 = FFFFFFFF FFFFFFFF FFFFFFFF FFFFFFFE BAAEDCE6 AF48A03B BFD25E8C D036413F

@@ -163,3 +163,14 @@ extern "C" void lane_split(const unsigned char* k32, unsigned char* k1, unsigned
     memcpy(t.v, b.v, 32);
     fe_to_be_bytes(k2, t);
 }
+
+// the GPU lanes' safegcd inverse (csrc/modinv_device.h) on the CPU: r = a^-1 mod m, little-endian
+// 32-bit limbs, minv30 = m^-1 mod 2^30
+extern "C" void lane_mi30_inverse(const uint32_t* a, const uint32_t* m, uint32_t minv30,
+                                  uint32_t* r) {
+    uint32_t aa[8], mm[8], rr[8];
+    memcpy(aa, a, 32);
+    memcpy(mm, m, 32);
+    bcc::mi30::inverse(rr, aa, mm, minv30);
+    memcpy(r, rr, 32);
+}

@@ -82,3 +82,27 @@ def test_field_is_zero_and_normalize():
     assert [g & 1 for g in z] == [1 if v % P == 0 else 0 for v in vals]
     nrm = run(9, pairs)
     assert nrm == [v % P for v in vals]
+
+
+N = 0xFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFEBAAEDCE6AF48A03BBFD25E8CD0364141
+
+
+@pytest.mark.gpu
+def test_safegcd_inverses_match_integers():
+    """The lanes' safegcd inverse (csrc/modinv_device.h: 30-bit branchless divstep batches, wave-
+    uniform early exit) behind fe_inv (K_tfin) and sc_inv (K_inv): weak field operands (>= p
+    included) and scalars < n, edge values and random lanes mixed in the same waves, against
+    pow(a, -1, m); zero maps to zero as with the Fermat chains."""
+    rng = random.Random(0x1417)
+    fvals = EDGES + [rng.getrandbits(256) for _ in range(6000)]
+    rng.shuffle(fvals)
+    got = run(10, [(v, 0) for v in fvals])
+    bad = [(v, g) for v, g in zip(fvals, got)
+           if g != (pow(v % P, -1, P) if v % P else 0)]
+    assert not bad, f"fe_inv: {len(bad)} mismatches, first {bad[0]}"
+    svals = [0, 1, 2, N - 1, N - 2, (N + 1) // 2, 2**255 % N, 2**128] + \
+        [rng.randrange(N) for _ in range(6000)]
+    rng.shuffle(svals)
+    got = run(11, [(v, 0) for v in svals])
+    bad = [(v, g) for v, g in zip(svals, got) if g != (pow(v, -1, N) if v else 0)]
+    assert not bad, f"sc_inv: {len(bad)} mismatches, first {bad[0]}"

@@ -22,7 +22,7 @@ def lane():
     src = os.path.join(HERE, "native", "lane_host.cpp")
     deps = [src] + [os.path.join(HERE, "..", "rust-bitcoinconsensus_amd", "csrc", f)
                     for f in ("ecdsa_lane.h", "ecdsa_twist.h", "secp256k1_device.h", "modinv_host.h",
-                              "sha256_device.h")]
+                              "modinv_device.h", "sha256_device.h")]
     if not os.path.exists(SO) or any(os.path.getmtime(d) > os.path.getmtime(SO) for d in deps):
         os.makedirs(os.path.dirname(SO), exist_ok=True)
         subprocess.check_call(["g++", "-O2", "-std=c++17", "-shared", "-fPIC", "-o", SO, src])
@@ -184,3 +184,22 @@ def test_lane_scalar_mul_inv_mod_n(lane):
         a = rnd.randrange(1, N)
         lane.lane_sc_inv(a.to_bytes(32, "big"), out)
         assert int.from_bytes(out.raw, "big") == pow(a, -1, N)
+
+
+def test_mi30_safegcd_inverse_host(lane):
+    """The GPU lanes' inverse (csrc/modinv_device.h, compiled here for the CPU) against
+    pow(a, -1, m) for p and n: edge and random operands (the device run is in test_field_gpu)."""
+    P = 2**256 - 2**32 - 977
+    rng = random.Random(0x30)
+    arr = ctypes.c_uint32 * 8
+    for m in (P, N):
+        minv = pow(m, -1, 2**30)
+        vals = [0, 1, 2, 3, m - 1, m - 2, (m + 1) // 2, 2**255 % m, 2**128] + \
+            [rng.randrange(m) for _ in range(3000)]
+        for a in vals:
+            out = arr()
+            lane.lane_mi30_inverse(arr(*[(a >> (32 * i)) & 0xFFFFFFFF for i in range(8)]),
+                                   arr(*[(m >> (32 * i)) & 0xFFFFFFFF for i in range(8)]),
+                                   ctypes.c_uint32(minv), out)
+            got = sum(out[i] << (32 * i) for i in range(8))
+            assert got == (pow(a, -1, m) if a else 0), (hex(m), hex(a))
