@@ -293,82 +293,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
     tw_store(w, T_Y, st.ychk.v);
 }
 
-// The same prep in two halves (ecdsa_launch_key): K_tkey reads only the tag and key rows (it may
-// run beside the sighash kernels and K_inv), K_tscal the r / s / m / s^-1 rows after them.
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void ecdsa_tkey_kernel(
-    const uint8_t* __restrict__ tag, const uint8_t* __restrict__ px,
-    const uint8_t* __restrict__ py, size_t cnt, u32* __restrict__ qtab, u32* __restrict__ state) {
-    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= cnt) return;
-    fe x, y;
-    load_be32(x, px + 32 * t);
-    load_be32(y, py + 32 * t);
-    QTableGlobal qt{lane_table(qtab, t)};
-    TwistState st;
-    const bool ok = twist_prep_key(tag[t], x, y, qt, st);
-    u32* w = lane_words(state, t, TSTATE_WORDS);
-    w[T_FLAGS * LANE_STRIDE] = ok ? st.flags : 0u;
-    if (!ok) return;
-    tw_store(w, T_SIGMA, st.sigma.v);
-    tw_store(w, T_V, st.v.v);
-    tw_store(w, T_Y, st.ychk.v);
-}
-
-__global__ __launch_bounds__(256) void ecdsa_tscal_kernel(
-    const uint8_t* __restrict__ pr, const uint8_t* __restrict__ ps,
-    const uint8_t* __restrict__ pm, const u32* __restrict__ psinv, size_t cnt,
-    u32* __restrict__ state) {
-    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= cnt) return;
-    u32* w = lane_words(state, t, TSTATE_WORDS);
-    const u32 kflags = w[T_FLAGS * LANE_STRIDE];
-    if (!(kflags & LS_VALID)) return;  // K_tkey rejected the key (flags 0)
-    sc r, s, m, si;
-    load_be32(r, pr + 32 * t);
-    load_be32(s, ps + 32 * t);
-    load_be32(m, pm + 32 * t);
-    load_limbs(si, psinv + 8 * t);
-    TwistState st;
-    if (!twist_prep_scalars(kflags, r, s, m, &si, st)) {
-        w[T_FLAGS * LANE_STRIDE] = 0u;
-        return;
-    }
-#pragma unroll
-    for (int a = 0; a < 4; a++)
-#pragma unroll
-        for (int b = 0; b < 4; b++) w[(T_K + a * 4 + b) * LANE_STRIDE] = st.k[a][b];
-    w[T_FLAGS * LANE_STRIDE] = st.flags;
-    tw_store(w, T_R, st.r.v);
-}
-
-// The signature half of K_tscal alone (K_tscal_q): r / s checks, u2 and its GLV split -- no
-// message, so it and the Q ladder after it run beside the sighash kernels; u1 is formed by the G
-// ladder kernel once the sighashes exist.
-__global__ __launch_bounds__(256) void ecdsa_tscal_q_kernel(
-    const uint8_t* __restrict__ pr, const uint8_t* __restrict__ ps,
-    const u32* __restrict__ psinv, size_t cnt, u32* __restrict__ state) {
-    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= cnt) return;
-    u32* w = lane_words(state, t, TSTATE_WORDS);
-    const u32 kflags = w[T_FLAGS * LANE_STRIDE];
-    if (!(kflags & LS_VALID)) return;  // K_tkey rejected the key (flags 0)
-    sc r, s, si;
-    load_be32(r, pr + 32 * t);
-    load_be32(s, ps + 32 * t);
-    load_limbs(si, psinv + 8 * t);
-    TwistState st;
-    if (!twist_prep_u2(kflags, r, s, &si, st)) {
-        w[T_FLAGS * LANE_STRIDE] = 0u;
-        return;
-    }
-#pragma unroll
-    for (int a = 0; a < 2; a++)
-#pragma unroll
-        for (int b = 0; b < 4; b++) w[(T_K + a * 4 + b) * LANE_STRIDE] = st.k[a][b];
-    w[T_FLAGS * LANE_STRIDE] = st.flags;
-    tw_store(w, T_R, st.r.v);
-}
-
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void schnorr_tprep_kernel(
     const uint8_t* __restrict__ psig, const uint8_t* __restrict__ pm,
     const uint8_t* __restrict__ ppk, size_t base, size_t cnt, u32* __restrict__ qtab,
@@ -467,23 +391,58 @@ __global__ __launch_bounds__(TLADDER_WG) __attribute__((amdgpu_waves_per_eu(BCC_
     twist_g_part<BIP340>(w, lt, gcomb, st);
 }
 
-// The ECDSA ladder in two launches (ecdsa_launch_q / ecdsa_launch_after_pre): K_tladder_q needs
+// The ECDSA ladder in two launches (ecdsa_launch_q / ecdsa_launch_after_pre): the Q half needs
 // only the key and u2, so it runs on the side stream beside the sighash kernels; K_tladder_g
 // forms u1 = m s^-1 from the sighash row (twist_prep_u1) and finishes the lane.
 #ifndef BCC_LADDERQ_WAVES
 #define BCC_LADDERQ_WAVES BCC_LADDER_WAVES
 #endif
-__global__ __launch_bounds__(TLADDER_WG) __attribute__((amdgpu_waves_per_eu(BCC_LADDERQ_WAVES, BCC_LADDERQ_WAVES))) void twist_ladder_q_kernel(
-    u32* __restrict__ state, u32* __restrict__ qtab, size_t cnt) {
+// The Q half, K_keyq (round 4: the former K_tkey + K_tscal_q + K_tladder_q in one launch, for
+// rounds that fit one scratch chunk): key parse without a square root and the co-Z Q_w table, the r / s checks, u2 = r s^-1
+// and its GLV split, then B = u2 Q_w.  The table build alone ran at about 60 % of the ladder's
+// issue rate as its own launch (its 1 KiB lane-major table writes); fused, its instructions fill
+// the same waves as the ladder's (108 VGPRs, 4 waves per SIMD, no spill).
+__global__ __launch_bounds__(TLADDER_WG) __attribute__((amdgpu_waves_per_eu(BCC_LADDERQ_WAVES, BCC_LADDERQ_WAVES))) void twist_keyq_kernel(
+    const uint8_t* __restrict__ tag, const uint8_t* __restrict__ px, const uint8_t* __restrict__ py,
+    const uint8_t* __restrict__ pr, const uint8_t* __restrict__ ps, const u32* __restrict__ psinv,
+    size_t cnt, u32* __restrict__ qtab, u32* __restrict__ state) {
     const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= cnt) return;
     u32* w = lane_words(state, t, TSTATE_WORDS);
-    TwistStateView st;
-    st.p = w;
-    st.flags = w[T_FLAGS * LANE_STRIDE];
-    if (!(st.flags & LS_VALID)) return;  // K_tladder_g writes the status
-    tw_load(st.sigma.v, w, T_SIGMA);
-    twist_q_part(lane_table(qtab, t), st);
+    u32* lt = lane_table(qtab, t);
+    {
+        fe x, y;
+        load_be32(x, px + 32 * t);
+        load_be32(y, py + 32 * t);
+        TwistState st;
+        QTableGlobal qt{lt};
+        bool ok = twist_prep_key(tag[t], x, y, qt, st);
+        if (ok) {
+            tw_store(w, T_SIGMA, st.sigma.v);
+            tw_store(w, T_V, st.v.v);
+            tw_store(w, T_Y, st.ychk.v);
+            sc r, s, si;
+            load_be32(r, pr + 32 * t);
+            load_be32(s, ps + 32 * t);
+            load_limbs(si, psinv + 8 * t);
+            ok = twist_prep_u2(st.flags, r, s, &si, st);
+        }
+        if (!ok) {
+            w[T_FLAGS * LANE_STRIDE] = 0u;  // K_tladder_g writes the status
+            return;
+        }
+#pragma unroll
+        for (int a = 0; a < 2; a++)
+#pragma unroll
+            for (int b = 0; b < 4; b++) w[(T_K + a * 4 + b) * LANE_STRIDE] = st.k[a][b];
+        w[T_FLAGS * LANE_STRIDE] = st.flags;
+        tw_store(w, T_R, st.r.v);
+    }
+    TwistStateView sv;
+    sv.p = w;
+    sv.flags = w[T_FLAGS * LANE_STRIDE];
+    tw_load(sv.sigma.v, w, T_SIGMA);
+    twist_q_part(lt, sv);
 }
 
 // The G half keeps the combine's temporaries live beside the comb accumulator: at four waves
@@ -520,25 +479,6 @@ __global__ __launch_bounds__(TLADDER_WG) __attribute__((amdgpu_waves_per_eu(BCC_
     st.flags = flags;
     tw_load(st.sigma.v, w, T_SIGMA);
     twist_g_part<false>(w, lane_table(qtab, t), gcomb, st);
-}
-
-// BIP340 in two launches too (BCC_SCHNORR_SPLIT): the prep formed every scalar, so the G half
-// only runs the comb, the combine and the parity quantities; each half gets its own registers
-// (the fused BIP340 ladder spills).
-__global__ __launch_bounds__(TLADDER_WG) __attribute__((amdgpu_waves_per_eu(BCC_LADDERG_WAVES, BCC_LADDERG_WAVES))) void twist_ladder_g340_kernel(
-    u32* __restrict__ state, u32* __restrict__ qtab, const u32* __restrict__ gcomb, size_t cnt) {
-    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= cnt) return;
-    u32* w = lane_words(state, t, TSTATE_WORDS);
-    TwistStateView st;
-    st.p = w;
-    st.flags = w[T_FLAGS * LANE_STRIDE];
-    if (!(st.flags & LS_VALID)) {
-        w[T_STAT * LANE_STRIDE] = TW_REJECT;
-        return;
-    }
-    tw_load(st.sigma.v, w, T_SIGMA);
-    twist_g_part<true>(w, lane_table(qtab, t), gcomb, st);
 }
 
 // beta^-1 for every normal lane of a chunk by Montgomery's trick over the strided sub-chunk
@@ -642,15 +582,6 @@ static const std::vector<fe>& host_gcomb() {
         build_g_comb(t.data());
     });
     return t;
-}
-
-// BCC_SCHNORR_SPLIT=1: the BIP340 ladder as a Q launch and a G launch (A/B runs)
-static bool schnorr_split() {
-    static const bool on = [] {
-        const char* e = getenv("BCC_SCHNORR_SPLIT");
-        return e && atoi(e) != 0;
-    }();
-    return on;
 }
 
 // Lanes per prep/ladder launch pair.  Larger chunks leave fewer kernel tails and fewer latency-
@@ -772,8 +703,14 @@ int ecdsa_launch_pre(SigScratch& sc, const uint8_t* d_tag, const uint8_t* d_x,
     return 0;
 }
 
+// The key half runs inside the fused Q launch (twist_keyq_kernel, ecdsa_launch_q): this only
+// marks the round's keys as handled there when the round fits one scratch chunk.
 int ecdsa_launch_key(SigScratch& sc, const uint8_t* d_tag, const uint8_t* d_x,
                      const uint8_t* d_y, size_t n, void* stream) {
+    (void)d_tag;
+    (void)d_x;
+    (void)d_y;
+    (void)stream;
     sc.key_ready = 0;
     if (n == 0 || n > chunk_lanes()) return 0;
     int dev = 0, cus = 0;
@@ -782,16 +719,12 @@ int ecdsa_launch_key(SigScratch& sc, const uint8_t* d_tag, const uint8_t* d_x,
     if (int e = device_tables(&dev, &gcomb, &cus)) return e;
     if (int e = ensure_scratch(sc, dev, n, true, &C)) return e;
     if (n > C) return 0;  // chunked: the whole prep runs per chunk after K_inv
-    u32* qtab = (u32*)sc.chunk;
-    u32* state = qtab + C * QTABLE_WORDS;
-    hipLaunchKernelGGL(ecdsa_tkey_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
-                       (hipStream_t)stream, d_tag, d_x, d_y, n, qtab, state);
-    BCC_HIP_TRY(hipGetLastError());
     sc.key_ready = n;
     return 0;
 }
 
-int ecdsa_launch_q(SigScratch& sc, const uint8_t* d_r, const uint8_t* d_s, size_t n, void* stream) {
+int ecdsa_launch_q(SigScratch& sc, const uint8_t* d_tag, const uint8_t* d_x, const uint8_t* d_y,
+                   const uint8_t* d_r, const uint8_t* d_s, size_t n, void* stream) {
     sc.q_ready = 0;
     if (n == 0 || sc.key_ready != n || n > chunk_lanes()) return 0;
     int dev = 0, cus = 0;
@@ -802,12 +735,9 @@ int ecdsa_launch_q(SigScratch& sc, const uint8_t* d_r, const uint8_t* d_s, size_
     if (n > C) return 0;
     u32* qtab = (u32*)sc.chunk;
     u32* state = qtab + C * QTABLE_WORDS;
-    hipStream_t st = (hipStream_t)stream;
-    hipLaunchKernelGGL(ecdsa_tscal_q_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
-                       d_r, d_s, (const u32*)sc.sinv, n, state);
-    BCC_HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(twist_ladder_q_kernel, dim3((unsigned)((n + TLADDER_WG - 1) / TLADDER_WG)),
-                       dim3(TLADDER_WG), 0, st, state, qtab, n);
+    hipLaunchKernelGGL(twist_keyq_kernel, dim3((unsigned)((n + TLADDER_WG - 1) / TLADDER_WG)),
+                       dim3(TLADDER_WG), 0, (hipStream_t)stream, d_tag, d_x, d_y, d_r, d_s,
+                       (const u32*)sc.sinv, n, qtab, state);
     BCC_HIP_TRY(hipGetLastError());
     sc.q_ready = n;
     return 0;
@@ -821,7 +751,7 @@ int ecdsa_launch(SigScratch& sc, const uint8_t* d_tag, const uint8_t* d_x, const
     if (int e = ecdsa_launch_pre(sc, d_tag, d_x, d_y, d_s, n, stream)) return e;
     // the same split kernels as DeviceBatch::run, on one stream
     if (int e = ecdsa_launch_key(sc, d_tag, d_x, d_y, n, stream)) return e;
-    if (int e = ecdsa_launch_q(sc, d_r, d_s, n, stream)) return e;
+    if (int e = ecdsa_launch_q(sc, d_tag, d_x, d_y, d_r, d_s, n, stream)) return e;
     return ecdsa_launch_after_pre(sc, d_tag, d_x, d_y, d_r, d_s, d_m, d_verdict, n, stream);
 }
 
@@ -840,11 +770,10 @@ int ecdsa_launch_after_pre(SigScratch& sc, const uint8_t* d_tag, const uint8_t* 
     u32* sinv = (u32*)sc.sinv;
     u32* qtab = (u32*)sc.chunk;
     u32* state = qtab + C * QTABLE_WORDS;
-    const bool key_ahead = sc.key_ready == n && n <= C;
     const bool q_ahead = sc.q_ready == n && n <= C;
     sc.key_ready = 0;
     sc.q_ready = 0;
-    if (q_ahead) {  // K_tkey, K_tscal_q and K_tladder_q ran ahead (ecdsa_launch_q)
+    if (q_ahead) {  // the key half, u2 and the Q ladder ran ahead (ecdsa_launch_q)
         hipLaunchKernelGGL(twist_ladder_g_kernel, dim3((unsigned)((n + TLADDER_WG - 1) / TLADDER_WG)),
                            dim3(TLADDER_WG), 0, sm, state, qtab, gcomb, d_m, sinv, n);
         BCC_HIP_TRY(hipGetLastError());
@@ -858,14 +787,9 @@ int ecdsa_launch_after_pre(SigScratch& sc, const uint8_t* d_tag, const uint8_t* 
     // chunked (n above the scratch chunk): the whole prep, the fused ladder and K_tfin per chunk
     for (size_t base = 0; base < n; base += C) {
         const size_t cnt = std::min(C, n - base);
-        if (key_ahead) {
-            hipLaunchKernelGGL(ecdsa_tscal_kernel, dim3((unsigned)((cnt + 255) / 256)),
-                               dim3(256), 0, sm, d_r, d_s, d_m, sinv, cnt, state);
-        } else {
-            hipLaunchKernelGGL(ecdsa_tprep_kernel, dim3((unsigned)((cnt + 255) / 256)),
-                               dim3(256), 0, sm, d_tag, d_x, d_y, d_r, d_s, d_m, sinv, base,
-                               cnt, qtab, state);
-        }
+        hipLaunchKernelGGL(ecdsa_tprep_kernel, dim3((unsigned)((cnt + 255) / 256)),
+                           dim3(256), 0, sm, d_tag, d_x, d_y, d_r, d_s, d_m, sinv, base,
+                           cnt, qtab, state);
         BCC_HIP_TRY(hipGetLastError());
         if (ev_rows_read && base + cnt >= n)
             BCC_HIP_TRY(hipEventRecord((hipEvent_t)ev_rows_read, sm));
@@ -898,19 +822,9 @@ int schnorr_launch(SigScratch& sc, const uint8_t* d_sig64, const uint8_t* d_msg3
         hipLaunchKernelGGL(schnorr_tprep_kernel, dim3((unsigned)((cnt + 255) / 256)), dim3(256),
                            0, sm, d_sig64, d_msg32, d_xonly32, base, cnt, qtab, state);
         BCC_HIP_TRY(hipGetLastError());
-        if (schnorr_split()) {
-            hipLaunchKernelGGL(twist_ladder_q_kernel,
-                               dim3((unsigned)((cnt + TLADDER_WG - 1) / TLADDER_WG)),
-                               dim3(TLADDER_WG), 0, sm, state, qtab, cnt);
-            BCC_HIP_TRY(hipGetLastError());
-            hipLaunchKernelGGL(twist_ladder_g340_kernel,
-                               dim3((unsigned)((cnt + TLADDER_WG - 1) / TLADDER_WG)),
-                               dim3(TLADDER_WG), 0, sm, state, qtab, gcomb, cnt);
-        } else {
-            hipLaunchKernelGGL(twist_ladder_kernel<true>,
-                               dim3((unsigned)((cnt + TLADDER_WG - 1) / TLADDER_WG)),
-                               dim3(TLADDER_WG), 0, sm, state, qtab, gcomb, cnt);
-        }
+        hipLaunchKernelGGL(twist_ladder_kernel<true>,
+                           dim3((unsigned)((cnt + TLADDER_WG - 1) / TLADDER_WG)),
+                           dim3(TLADDER_WG), 0, sm, state, qtab, gcomb, cnt);
         BCC_HIP_TRY(hipGetLastError());
         const size_t T = std::max<size_t>((cnt + FIN_PER_THREAD - 1) / FIN_PER_THREAD, std::min<size_t>(cnt, (size_t)cus * 256));
         hipLaunchKernelGGL(twist_fin_kernel<true>, dim3((unsigned)((T + 255) / 256)), dim3(256), 0,

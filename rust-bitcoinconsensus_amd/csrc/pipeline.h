@@ -353,19 +353,17 @@ int ecdsa_launch(SigScratch& sc, const uint8_t* d_tag, const uint8_t* d_x, const
 // after them (must be ordered after both, and after the sighash kernels that write m).
 int ecdsa_launch_pre(SigScratch& sc, const uint8_t* d_tag, const uint8_t* d_x,
                      const uint8_t* d_y, const uint8_t* d_s, size_t n, void* stream);
-// The key half of the twist-path prep (K_tkey: key parse and Q_w table, which read only the tag and
-// key rows) launched ahead on `stream`, e.g. beside the sighash kernels; the next
-// ecdsa_launch_after_pre for the same n (ordered after it) then runs only the scalar half.  A no-op
-// (returns 0) on the legacy path or when n needs more than one scratch chunk.
+// The message-free part of the ECDSA lane ahead of the sighash kernels, in one launch
+// (twist_keyq_kernel): the key half of the prep (key parse without a square root, the co-Z Q_w
+// table), the r / s half (u2 = r s^-1, GLV split) and the Q ladder B = u2 Q_w, on `stream` after
+// K_inv (ecdsa_launch_pre for the same n, ordered before it).  ecdsa_launch_key marks the round
+// (no launch; it may be called from any stream); the next ecdsa_launch_after_pre for the same n
+// then forms u1 from the sighash rows and runs only the G ladder, the combine and K_tfin.  Both
+// are no-ops (return 0) when n does not fit one scratch chunk (the chunked path preps per chunk).
 int ecdsa_launch_key(SigScratch& sc, const uint8_t* d_tag, const uint8_t* d_x, const uint8_t* d_y,
                      size_t n, void* stream);
-// The message-free part of the ECDSA lane ahead of the sighash kernels: the r / s half of the
-// prep (u2 = r s^-1, GLV split) and the Q ladder B = u2 Q_w, on `stream` after K_inv and K_tkey
-// (ecdsa_launch_pre / ecdsa_launch_key for the same n, ordered before it); the next
-// ecdsa_launch_after_pre for the same n then forms u1 from the sighash rows and runs only the G
-// ladder, the combine and K_tfin.  A no-op (returns 0) unless the key half ran ahead and n fits one
-// scratch chunk.
-int ecdsa_launch_q(SigScratch& sc, const uint8_t* d_r, const uint8_t* d_s, size_t n, void* stream);
+int ecdsa_launch_q(SigScratch& sc, const uint8_t* d_tag, const uint8_t* d_x, const uint8_t* d_y,
+                   const uint8_t* d_r, const uint8_t* d_s, size_t n, void* stream);
 // ev_rows_read (optional hipEvent_t) is recorded on `stream` once the last kernel that reads the
 // s / m / key rows and the s^-1 rows has been launched (the prep kernel): later writers of those
 // rows (the next run's front kernels) need only wait for it, not for the ladder.
@@ -426,10 +424,9 @@ private:
     void* side_stream_ = nullptr;  // the key / Q-ladder chain beside the sighash kernels (run())
     void* ev_fork_ = nullptr;      // hipEvent_t: run() start on the main stream
     void* ev_join_ = nullptr;      // hipEvent_t: the Q ladder done on the side stream
+    void* ev_up_ = nullptr;        // hipEvent_t: the tuple rows uploaded (side stream)
     void* ev_block_ = nullptr;     // hipEvent_t (blocking sync): host waits sleep, not spin
     int wait(void* stream);
-    void* ev_up_ = nullptr;        // hipEvent_t: the tuple rows uploaded (K_inv on the main stream)
-    void* ev_inv_ = nullptr;       // hipEvent_t: K_inv done on the main stream
     SigScratch scratch_;
     void* arena_ = nullptr;
     size_t cap_ = 0;

@@ -817,7 +817,6 @@ DeviceBatch::~DeviceBatch() {
     if (ev_fork_) (void)hipEventDestroy((hipEvent_t)ev_fork_);
     if (ev_join_) (void)hipEventDestroy((hipEvent_t)ev_join_);
     if (ev_up_) (void)hipEventDestroy((hipEvent_t)ev_up_);
-    if (ev_inv_) (void)hipEventDestroy((hipEvent_t)ev_inv_);
     if (ev_block_) (void)hipEventDestroy((hipEvent_t)ev_block_);
     if (arena_) (void)hipFree(arena_);
     if (host_image_) (void)hipHostFree(host_image_);
@@ -1214,46 +1213,39 @@ int DeviceBatch::run(void* stream) {
 }
 
 // Two streams: the sighash stage on the main stream (K_wtx + K3' + K1 fused into one front launch,
-// then K_win / K2 / K3), and on the side stream the key half of the prep (K_tkey) and everything
-// the message does not enter -- the signature half of the prep and the Q ladder
-// (ecdsa_launch_q); the G ladder and K_tfin wait for both.  K_inv (one latency-bound wave per
-// SIMD) runs on the main stream beside K_tkey, so the side stream's chain to the Q ladder does not
-// include it (C2 +0.9..1.2 % in an interleaved A/B, profiles/r03/ab/inv_main).  K_h160 needs only
-// the key rows and the programs: it runs on the main stream beside the Q ladder into verdicts
-// preset to 1, and K_tfin then only clears failing rows (verdict_and), instead of running after
-// K_tfin at the end of the critical path.
+// then K_win / K2 / K3), and on the side stream everything the message does not enter: K_inv,
+// then one launch with the key half of the prep, u2 and the Q ladder (ecdsa_launch_q); the G
+// ladder and K_tfin wait for both.  K_h160 needs only the key rows and the programs: it runs on the
+// main stream beside the Q ladder into verdicts preset to 1, and K_tfin then only clears failing
+// rows (verdict_and), instead of running after K_tfin at the end of the critical path.
 int DeviceBatch::run_stages(void* stream) {
     hipStream_t st = (hipStream_t)stream;
     kh_done_ = false;
     if (!side_stream_) {
         hipStream_t s = nullptr;
-        hipEvent_t a = nullptr, b = nullptr, c = nullptr, d = nullptr;
+        hipEvent_t a = nullptr, b = nullptr, c = nullptr;
         BCC_HIP_TRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
         BCC_HIP_TRY(hipEventCreateWithFlags(&a, hipEventDisableTiming));
         BCC_HIP_TRY(hipEventCreateWithFlags(&b, hipEventDisableTiming));
         BCC_HIP_TRY(hipEventCreateWithFlags(&c, hipEventDisableTiming));
-        BCC_HIP_TRY(hipEventCreateWithFlags(&d, hipEventDisableTiming));
         side_stream_ = s;
         ev_fork_ = a;
         ev_join_ = b;
         ev_up_ = c;
-        ev_inv_ = d;
     }
     hipStream_t side = (hipStream_t)side_stream_;
     BCC_HIP_TRY(hipEventRecord((hipEvent_t)ev_fork_, st));
     BCC_HIP_TRY(hipStreamWaitEvent(side, (hipEvent_t)ev_fork_, 0));
     if (int e = upload_on(side, st)) return e;
-    BCC_HIP_TRY(hipEventRecord((hipEvent_t)ev_up_, side));  // the s / key rows are on the device
-    BCC_HIP_TRY(hipStreamWaitEvent(st, (hipEvent_t)ev_up_, 0));
-    if (int e = ecdsa_launch_pre(scratch_, d_tag, d_x, d_y, d_s, n_rows_, st)) return e;
-    BCC_HIP_TRY(hipEventRecord((hipEvent_t)ev_inv_, st));
+    BCC_HIP_TRY(hipEventRecord((hipEvent_t)ev_up_, side));  // the tuple rows are on the device
+    if (int e = ecdsa_launch_pre(scratch_, d_tag, d_x, d_y, d_s, n_rows_, side)) return e;
     if (int e = ecdsa_launch_key(scratch_, d_tag, d_x, d_y, n_rows_, side)) return e;
-    BCC_HIP_TRY(hipStreamWaitEvent(side, (hipEvent_t)ev_inv_, 0));  // K_tscal_q reads s^-1
-    if (int e = ecdsa_launch_q(scratch_, d_r, d_s, n_rows_, side)) return e;
+    if (int e = ecdsa_launch_q(scratch_, d_tag, d_x, d_y, d_r, d_s, n_rows_, side)) return e;
     BCC_HIP_TRY(hipEventRecord((hipEvent_t)ev_join_, side));
     if (int e = launch_front(st)) return e;
     if (n_hash_) {
         BCC_HIP_TRY(hipMemsetAsync(d_v, 1, n_rows_, st));
+        BCC_HIP_TRY(hipStreamWaitEvent(st, (hipEvent_t)ev_up_, 0));  // K_h160 reads the key rows
         if (int e = launch_key_hash(st)) return e;
         kh_done_ = true;
     }
