@@ -46,9 +46,9 @@ METRIC = "ECDSA verifies/sec (node) at 1/2/4/8 MI355X; % of int-ALU roofline"
 DEFAULT_N = {"c2": 1_000_000, "c3": 4000, "c4": 8_000_000, "c5": 16_000_000, "c5t": 1_000_000}
 SEEDS = {"c2": 0x5EED0001, "c3": 0x5EED0003, "c4": 0x5EED0004, "c5": 0x5EED0005,
          "c5t": 0x5EED0006}
-# the ECDSA stage's kernels: the square-root-free path (default) or the round-1 path
-ECDSA_KERNELS = ("ecdsa (batch_sinv + ecdsa_tkey + ecdsa_tscal_q + twist_ladder_q + twist_ladder_g + "
-                 "twist_fin<ecdsa>; no key square root)")
+# the ECDSA stage's kernels (the square-root-free twist path)
+ECDSA_KERNELS = ("ecdsa (batch_sinv + twist_keyq + twist_ladder_g + twist_fin<ecdsa>; "
+                 "no key square root)")
 SCHNORR_KERNELS = ("schnorr (schnorr_tprep + twist_ladder<bip340> + twist_fin<bip340>; "
                    "no lift_x square root)")
 CPU_PASSES = 3                    # timed passes of the CPU baseline (median), after 1 warm-up
@@ -853,12 +853,14 @@ def main():
                                               "own SGPR carries per asm block, 8 waves/SIMD)"),
                     per_launch=dict(verifies=sig_units, mads=sig_units * job.mads, avg_ms=sig_ms,
                                     verifies_per_s=sig_units / (sig_ms * 1e-3)))
-        cm = os.path.join(ROOT, "profiles", "r03", "ladder_cost_model.json")
+        cm = next((c for c in (os.path.join(ROOT, "profiles", r, "ladder_cost_model.json")
+                               for r in ("r04", "r03")) if os.path.exists(c)), "")
         if args.config == "c2" and os.path.exists(cm):
             # why frac stops where it does (committed PMC passes + microbenchmark): the ladder is
             # VALU-issue-bound; its cycles split by instruction class at the measured issue costs
             d = json.load(open(cm))
-            kname = next((n for n in ("twist_ladder_q_kernel", "twist_ladder_kernel<false>")
+            kname = next((n for n in ("twist_keyq_kernel", "twist_ladder_q_kernel",
+                                    "twist_ladder_kernel<false>")
                           if "bench:" + n in d["kernels"]), None)
             k = d["kernels"].get("bench:" + kname) if kname else None
             if k:
@@ -867,7 +869,7 @@ def main():
                     valu_per_verify=k["valu_per_wave"],
                     issue_cost_cycles=d["issue_cost_cycles_per_wave_instr"],
                     predicted_over_measured_cycles=k["predicted_over_measured"],
-                    source="profiles/r03/ladder_cost_model.json (tools/isa/cost_model.py)")
+                    source=os.path.relpath(cm, ROOT) + " (tools/isa/cost_model.py)")
         cpu = None
         if world == 1 and not args.no_cpu:
             default_sample = {"c2": 200_000, "c3": 100_000, "c4": 400_000, "c5": 400_000,

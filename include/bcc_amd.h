@@ -128,10 +128,15 @@ int bcc_set_chunk_lanes(size_t lanes);
  * BCC_PIPELINE_CHUNK environment variable); 0 disables it.  Results never depend on it. */
 int bcc_set_pipeline_chunk(size_t items);
 
-/* Signature checks whose serial SHA-256 chain is longer than `blocks` 64-byte blocks (the legacy
- * preimages and BIP143 per-tx hashes of many-input transactions) are hashed on the host CPU
- * instead of in one GPU lane each (BCC_HOST_CHAIN_BLOCKS; default 0: every chain on the GPU).  Results never depend on it. */
+/* Legacy signature checks whose serial SHA-256 chain is longer than `blocks` 64-byte blocks (the
+ * preimages of many-input transactions) are hashed on the host CPU instead of in one GPU lane each
+ * (BCC_HOST_CHAIN_BLOCKS; default 0: every legacy chain on the GPU).  On one GPU the host hashes
+ * them while the device round's message-independent kernels run.  BIP143 checks of a tx whose
+ * per-tx chains (hashPrevouts / hashSequence / hashOutputs) exceed BCC_HOST_BIP143_BLOCKS (default
+ * 32) blocks are hashed on the host (linear in the tx).  Results never depend on either. */
 int bcc_set_host_chain_blocks(unsigned blocks);
+/* The BIP143 threshold above (BCC_HOST_BIP143_BLOCKS; default 32; 0: every BIP143 chain on the GPU). */
+int bcc_set_host_bip143_blocks(unsigned blocks);
 
 /* Key-hash spends (P2WPKH, and P2PKH scriptPubKeys): on an input's first interpreter run the
  * HASH160(pubkey) == program comparison of OP_EQUALVERIFY is checked on the device beside the

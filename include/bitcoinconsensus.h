@@ -16,7 +16,12 @@
  *
  * Return convention: 1 = valid, 0 = invalid or error; *err is written only when err != NULL.
  * Check order: flags -> deserialize -> nIn -> size -> (ERR_OK) -> script.
- * Every signature check runs on the GPU (HIP, gfx950); there is no CPU verification fallback.
+ * Where signature checks run: a round of more than BCC_HOST_SMALL_ROUND_DEFAULT (16) checks is
+ * verified on the GPU (HIP, gfx950).  Smaller rounds (a lone call of ..._with_amount, tiny batches)
+ * run on the host CPU with the kernels' own lane arithmetic compiled for the host, because one GPU
+ * lane's ladder latency exceeds the whole host check (bcc_amd.h: bcc_set_host_small_round; 0 puts
+ * every round on the GPU).  Rounds the GPU could not deliver go to the host as described under
+ * "Device failure" below.  Either way the verdicts are the reference's.
  * Thread safety: reentrant.  Each calling thread gets its own HIP stream, device arena, pinned
  * staging buffer and kernel scratch per device (created on its first call, reused afterwards), so
  * concurrent callers never share mutable device state; the only shared state is the read-only

@@ -459,11 +459,19 @@ def cpu_share():
 
 
 def set_host_chain_blocks(blocks):
-    """bcc_set_host_chain_blocks: checks whose SHA-256 chain exceeds `blocks` blocks are hashed on
-    the host CPU (0: every chain on the GPU)."""
+    """bcc_set_host_chain_blocks: legacy checks whose SHA-256 chain exceeds `blocks` blocks are
+    hashed on the host CPU (0, the default: every legacy chain on the GPU)."""
     L = lib()
     L.bcc_set_host_chain_blocks.argtypes = [ctypes.c_uint]
     L.bcc_set_host_chain_blocks(blocks)
+
+
+def set_host_bip143_blocks(blocks):
+    """bcc_set_host_bip143_blocks: BIP143 checks of a tx whose per-tx hash chains exceed `blocks`
+    blocks are hashed on the host CPU (default 32; 0: every chain on the GPU)."""
+    L = lib()
+    L.bcc_set_host_bip143_blocks.argtypes = [ctypes.c_uint]
+    L.bcc_set_host_bip143_blocks(blocks)
 
 
 def set_device_key_hash(on):

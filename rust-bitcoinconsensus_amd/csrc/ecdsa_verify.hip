@@ -723,6 +723,27 @@ int ecdsa_launch_key(SigScratch& sc, const uint8_t* d_tag, const uint8_t* d_x,
     return 0;
 }
 
+// Small rounds are latency-bound: at most one TLADDER_WG group per CU, every wave alone on its
+// SIMD -- unless a workgroup of the sighash kernels running beside K_keyq on the other stream
+// lands on the same CU and halves that SIMD's issue rate for the whole front (C3: K_keyq 0.85 ms
+// alone, 1.7 ms beside the sighash front).  Such a launch therefore reserves nearly all of its
+// CU's 160 KiB LDS (unused): the sighash kernels' groups (8.4 KB of LDS each) go to other CUs.
+constexpr size_t KEYQ_EXCLUSIVE_LDS = 152 * 1024;
+
+static size_t keyq_lds(size_t groups, int cus) {
+    static const bool ok = [] {
+        if (hipFuncSetAttribute((const void*)&twist_keyq_kernel,
+                                hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)KEYQ_EXCLUSIVE_LDS) == hipSuccess)
+            return true;
+        (void)hipGetLastError();
+        fprintf(stderr, "[bcc] K_keyq: no %zu-byte LDS reservation on this device; small rounds "
+                        "share CUs with the sighash kernels\n", KEYQ_EXCLUSIVE_LDS);
+        return false;
+    }();
+    return ok && groups <= (size_t)cus ? KEYQ_EXCLUSIVE_LDS : 0;
+}
+
 int ecdsa_launch_q(SigScratch& sc, const uint8_t* d_tag, const uint8_t* d_x, const uint8_t* d_y,
                    const uint8_t* d_r, const uint8_t* d_s, size_t n, void* stream) {
     sc.q_ready = 0;
@@ -735,9 +756,10 @@ int ecdsa_launch_q(SigScratch& sc, const uint8_t* d_tag, const uint8_t* d_x, con
     if (n > C) return 0;
     u32* qtab = (u32*)sc.chunk;
     u32* state = qtab + C * QTABLE_WORDS;
-    hipLaunchKernelGGL(twist_keyq_kernel, dim3((unsigned)((n + TLADDER_WG - 1) / TLADDER_WG)),
-                       dim3(TLADDER_WG), 0, (hipStream_t)stream, d_tag, d_x, d_y, d_r, d_s,
-                       (const u32*)sc.sinv, n, qtab, state);
+    const size_t groups = (n + TLADDER_WG - 1) / TLADDER_WG;
+    hipLaunchKernelGGL(twist_keyq_kernel, dim3((unsigned)groups), dim3(TLADDER_WG),
+                       (unsigned)keyq_lds(groups, cus), (hipStream_t)stream, d_tag, d_x, d_y, d_r,
+                       d_s, (const u32*)sc.sinv, n, qtab, state);
     BCC_HIP_TRY(hipGetLastError());
     sc.q_ready = n;
     return 0;

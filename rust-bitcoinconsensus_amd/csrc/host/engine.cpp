@@ -93,10 +93,13 @@ struct TxEntry {
 // the round's thousands of short chains finish in microseconds.  A check whose chain exceeds
 // host_chain_blocks() blocks is therefore hashed on the host: BIP143 checks of such a tx inline
 // (the per-tx digests once, then a ~4-block preimage each), legacy template / host-preimage jobs in
-// a parallel pass over all shards after the interpreter pass (run_host_jobs).  Their tuple rows
-// then carry the sighash in msg (uploaded); everything else is unchanged.
+// a parallel pass over all shards (hash_host_jobs).  On one GPU that pass runs while the device
+// round's message-independent kernels (K_inv, the key / Q-ladder launch, the sighash front) run,
+// and its digests reach the message rows just before the G ladder (LateHost, DeviceBatch::put_late);
+// on several GPUs it runs before the round.  Everything else is unchanged.
 struct HostJobs {
-    uint32_t chain_blocks = 0;       // offload threshold in 64-byte blocks (0: never)
+    uint32_t chain_blocks = 0;       // legacy offload threshold in 64-byte blocks (0: never)
+    uint32_t bip143_blocks = 0;      // BIP143 per-tx chain threshold (0: never)
     std::vector<uint8_t> tpl, code;  // templates / code fields of offloaded legacy ALL jobs
     std::vector<TplJob> tjobs;       // offsets into tpl / code, row = the tuple row
     std::vector<uint8_t> pre;        // offloaded host preimages (NONE / SINGLE / ACP), unpadded
@@ -114,6 +117,15 @@ struct HostJobs {
 std::atomic<uint32_t> g_host_chain_blocks{[] {
     const char* e = getenv("BCC_HOST_CHAIN_BLOCKS");
     return e ? (uint32_t)atoi(e) : 0u;
+}()};
+
+// BIP143 checks of a tx whose hashPrevouts / hashSequence / hashOutputs chains exceed this many
+// blocks are hashed on the host: the three per-tx digests once (one ~250-block chain for a
+// 442-input tx: ~10 us on the host's SHA extensions, ~1.6 ms in one GPU lane), then a ~4-block
+// preimage per check.  Unlike legacy preimages (O(inputs^2) bytes per tx) this is linear in the tx.
+std::atomic<uint32_t> g_host_bip143_blocks{[] {
+    const char* e = getenv("BCC_HOST_BIP143_BLOCKS");
+    return e ? (uint32_t)atoi(e) : 32u;
 }()};
 
 // Key-hash spends (P2WPKH, P2PKH): the first run leaves HASH160(key) == program to the device,
@@ -227,15 +239,21 @@ void host_bip143_sighash(HostJobs& host, TxEntry& te, unsigned nin, const Bytes&
     host.inline_rows++;
 }
 
-// `host` (optional): checks whose SHA chain exceeds host->chain_blocks are hashed on the host
-// (HostJobs); `msg_row` = the tuple row's msg (BIP143 offloads write it at once).
+// `host` (optional): legacy checks whose SHA chain exceeds host->chain_blocks, and every BIP143
+// check of a tx whose per-tx chains exceed host->bip143_blocks, are hashed on the host (HostJobs);
+// their msg rows in `rows` are materialized (the other rows stay lazy ONE).
 void add_sighash_job(SighashJobs& jobs, TxEntry& te, const bcc_batch_item& in, const Bytes& code,
                      SigVersion sv, int hashtype, uint32_t row, std::vector<uint8_t>& scratch,
                      Bip143Job& bip143, std::vector<TxEntry*>& touched, HostJobs* host = nullptr,
-                     uint8_t* msg_row = nullptr) {
+                     TupleRows* rows = nullptr) {
     const Tx& tx = te.tx;
     const unsigned nin = in.n_in;
-    const uint32_t hb = host && msg_row ? host->chain_blocks : 0;
+    const uint32_t hb = host && rows ? host->chain_blocks : 0;
+    const uint32_t hb143 = host && rows ? host->bip143_blocks : 0;
+    auto msg_row = [&]() {
+        rows->pad_msg(row + 1);
+        return &rows->msg[32 * (size_t)row];
+    };
     if (sv == SIGVERSION_BASE && legacy_all_type(hashtype)) {
         // device-assembled from the tx template (pipeline.h TplJob), or a host job (long template)
         if (te.tpl < 0 && te.htpl < 0) {
@@ -258,6 +276,7 @@ void add_sighash_job(SighashJobs& jobs, TxEntry& te, const bcc_batch_item& in, c
         tj.row = row;
         tj.nblk = SighashJobs::tpl_nblk(tj.tpl_len, tj.code_len);
         if (te.htpl >= 0) {
+            msg_row();  // hash_host_jobs writes the row
             tj.tpl_off = (uint32_t)te.htpl;
             tj.code_off = (uint32_t)host->code.size();
             host->code.insert(host->code.end(), scratch.begin(), scratch.end());
@@ -270,6 +289,7 @@ void add_sighash_job(SighashJobs& jobs, TxEntry& te, const bcc_batch_item& in, c
     } else if (sv == SIGVERSION_BASE) {
         if (build_legacy_preimage(tx, nin, code, hashtype, scratch)) {
             if (hb && sha_padded_len(scratch.size()) / 64 > hb) {
+                msg_row();
                 host->pre.insert(host->pre.end(), scratch.begin(), scratch.end());
                 host->pre_off.push_back(host->pre.size());
                 host->pre_row.push_back(row);
@@ -278,10 +298,10 @@ void add_sighash_job(SighashJobs& jobs, TxEntry& te, const bcc_batch_item& in, c
             }
         }
         // else: SIGHASH_SINGLE bug, msg stays ONE
-    } else if (hb && (te.hdig >= 0 || (te.wtx < 0 && bip143_tx_chain_blocks(tx) > hb))) {
+    } else if (hb143 && (te.hdig >= 0 || (te.wtx < 0 && bip143_tx_chain_blocks(tx) > hb143))) {
         // a long BIP143 tx: every check of it on the host, at once
         host_bip143_sighash(*host, te, nin, code, hashtype, in.amount, scratch, bip143, touched,
-                            msg_row);
+                            msg_row());
     } else if ((hashtype & 0x1f) != 3) {
         // BIP143 assembled on the device from the raw tx bytes (pipeline.h WinJob): the
         // host appends the tx once per round and a record per check
@@ -422,13 +442,11 @@ public:
             return false;
         }
         const int hashtype = sig.back();
-        uint8_t one[32] = {0};
-        one[0] = 1;  // uint256::ONE as raw bytes: the SIGHASH_SINGLE-bug message
-        // y only for a 65-byte key, msg only when the host may write it (long chains on the host):
-        // the device initialises every msg row to ONE itself (TupleRows::add_lazy)
+        // y only for a 65-byte key; msg rows stay lazy (uint256 ONE, the SIGHASH_SINGLE-bug
+        // message, initialised by the device) unless add_sighash_job hashes the row on the host
         const bool key65 = pub.size() == 65;
         const uint32_t row = rows.add_lazy(pub[0], pub.data() + 1, r, s, key65 ? pub.data() + 33 : nullptr,
-                                           host.chain_blocks ? one : nullptr);
+                                           nullptr);
         if (key65) rows.y_unused = false;
         if (key_prog) {
             rows.add_key_hash(row, key_prog);
@@ -436,7 +454,7 @@ public:
             key_hashes++;
         }
         add_sighash_job(jobs, *it.tx, *it.in, code, sv, hashtype, row, scratch, bip143, touched,
-                        &host, host.chain_blocks ? &rows.msg[32 * (size_t)row] : nullptr);
+                        &host, &rows);
         it.cache.push_back(Item::Check{koff, klen, -2 - (int32_t)pending.size()});
         if (consult) it.pending.push_back((uint32_t)pending.size());
         pending.push_back(Pending{item_idx, (uint32_t)(it.cache.size() - 1)});
@@ -451,6 +469,7 @@ public:
         pending.clear();
         host.clear();
         host.chain_blocks = g_host_chain_blocks.load(std::memory_order_relaxed);
+        host.bip143_blocks = g_host_bip143_blocks.load(std::memory_order_relaxed);
         for (auto* t : touched) {
             t->aux[0] = t->aux[1] = t->aux[2] = -1;
             t->tpl = -1;
@@ -462,19 +481,27 @@ public:
     }
 };
 
-// The offloaded legacy jobs of every shard, hashed in parallel on the calling thread's team (their
-// rows' msg receive the sighash).  Marks the rows of every shard with host-written messages for
-// upload.
-void run_host_jobs(std::vector<Round>& rds, unsigned T) {
-    std::vector<std::pair<uint32_t, uint32_t>> work;  // (shard, job): tjobs first, then pre
+// Marks the rows of every shard with host-written messages for upload (inline BIP143 rows now,
+// offloaded jobs' rows before or during the device round).  Returns whether any job is pending.
+bool mark_host_rows(std::vector<Round>& rds, unsigned T) {
+    bool any = false;
     for (unsigned t = 0; t < T; t++) {
         HostJobs& h = rds[t].host;
         if (h.pending() || h.inline_rows) {
             rds[t].rows.msg_one = false;
             rds[t].rows.pad_msg(rds[t].rows.size());
         }
-        for (uint32_t k = 0; k < h.pending(); k++) work.emplace_back(t, k);
+        any |= h.pending() != 0;
     }
+    return any;
+}
+
+// The offloaded legacy jobs of every shard, hashed in parallel on the calling thread's team (their
+// rows' msg receive the sighash).
+void hash_host_jobs(std::vector<Round>& rds, unsigned T) {
+    std::vector<std::pair<uint32_t, uint32_t>> work;  // (shard, job): tjobs first, then pre
+    for (unsigned t = 0; t < T; t++)
+        for (uint32_t k = 0; k < rds[t].host.pending(); k++) work.emplace_back(t, k);
     if (work.empty()) return;
     size_t blocks = 0;
     for (const auto& w : work) {
@@ -509,6 +536,23 @@ void run_host_jobs(std::vector<Round>& rds, unsigned T) {
         }
     });
 }
+
+// A round's offloaded jobs hashed while the device runs (single-GPU rounds): the device round
+// calls ensure() through its LateMsgFill once the message-independent kernels are queued; every
+// host path that needs the messages calls it first.  Hashes once per interpreter pass.
+struct LateHost {
+    std::vector<Round>* rds = nullptr;
+    unsigned T = 0;
+    bool done = false;
+    void ensure() {
+        if (done) return;
+        auto h0 = std::chrono::steady_clock::now();
+        hash_host_jobs(*rds, T);
+        t_stats.host_jobs_seconds +=
+            std::chrono::duration<double>(std::chrono::steady_clock::now() - h0).count();
+        done = true;
+    }
+};
 
 bool DeferringChecker::check_ecdsa(const Bytes& sig, const Bytes& pub, const Bytes& code,
                                    SigVersion sv) {
@@ -730,22 +774,22 @@ bool interpret_shard(BatchState& b, const std::vector<uint32_t>& idx, Round& rd)
 
 // One device round over the parts [p0, p1): fault injection first, then the device pipeline.
 int device_round(int dev, const SighashJobs* const* pj, const TupleRows* const* pr, size_t P,
-                 uint8_t* verdict, double* stage_s) {
+                 uint8_t* verdict, double* stage_s, const LateMsgFill* late) {
     for (int f = g_fail_rounds.load(); f > 0;)
         if (g_fail_rounds.compare_exchange_weak(f, f - 1)) return g_fail_code.load();
-    return gpu_verify_parts(dev, pj, pr, P, verdict, stage_s);
+    return gpu_verify_parts(dev, pj, pr, P, verdict, stage_s, late);
 }
 
 }  // namespace
 
 int resilient_round(int dev, const SighashJobs* const* pj, const TupleRows* const* pr, size_t P,
                     uint8_t* verdict, double* stage_s, size_t* retries, size_t* host_rounds,
-                    const char* who) {
-    int e = device_round(dev, pj, pr, P, verdict, stage_s);
+                    const char* who, const LateMsgFill* late) {
+    int e = device_round(dev, pj, pr, P, verdict, stage_s, late);
     if (e != 0 && retryable(e)) {
         fprintf(stderr, "[bcc] %s: device %d round failed (hip error %d), retrying\n", who, dev, e);
         (*retries)++;
-        e = device_round(dev, pj, pr, P, verdict, stage_s);
+        e = device_round(dev, pj, pr, P, verdict, stage_s, late);
     }
     if (e == 0) return 0;
     if (!host_fallback_enabled()) {
@@ -757,6 +801,11 @@ int resilient_round(int dev, const SighashJobs* const* pj, const TupleRows* cons
     for (size_t p = 0; p < P; p++) n += pr[p]->size();
     fprintf(stderr, "[bcc] %s: device %d round failed (hip error %d): verifying its %zu checks on "
                     "the host CPU\n", who, dev, e, n);
+    if (late) {  // the late rows' messages into the host rows
+        std::vector<uint32_t> lr;
+        std::vector<uint8_t> ld;
+        (*late)(lr, ld);
+    }
     host_verify_parts(pj, pr, P, verdict, host_threads());
     note_host_fallback();
     (*host_rounds)++;
@@ -772,9 +821,11 @@ namespace {
 // (gpu_verify_parts drops the failed one); *retries counts those.  If the device still cannot
 // deliver, the failure policy decides: the batch is verified on the host (*host_rounds counts
 // those) or the error is returned.  Returns 0 or the error.
+// `late` (optional): the group's offloaded host jobs are hashed during each device batch and their
+// rows' messages delivered through LateMsgFill.
 int run_device_group(int dev, const std::vector<Round>& rds, unsigned t0, unsigned t1,
                      const std::vector<size_t>& row0, uint8_t* verdict, double* stage_total,
-                     size_t* retries, size_t* host_rounds) {
+                     size_t* retries, size_t* host_rounds, LateHost* late) {
     unsigned g0 = t0;
     while (g0 < t1) {
         size_t sz[5] = {0, 0, 0, 0, 0};
@@ -800,9 +851,25 @@ int run_device_group(int dev, const std::vector<Round>& rds, unsigned t0, unsign
             pj.push_back(&rds[t].jobs);
             pr.push_back(&rds[t].rows);
         }
+        // the late rows of shards [g0, g1), batch-local
+        const LateMsgFill fill = [&, g0, g1](std::vector<uint32_t>& rows, std::vector<uint8_t>& digs) {
+            late->ensure();
+            for (unsigned t = g0; t < g1; t++) {
+                const Round& rd = rds[t];
+                const uint32_t base = (uint32_t)(row0[t] - row0[g0]);
+                auto put = [&](uint32_t r) {
+                    rows.push_back(base + r);
+                    const uint8_t* m = &rd.rows.msg[32 * (size_t)r];
+                    digs.insert(digs.end(), m, m + 32);
+                };
+                for (const TplJob& tj : rd.host.tjobs) put(tj.row);
+                for (uint32_t r : rd.host.pre_row) put(r);
+            }
+        };
         double st = 0;
         int e = 1;
         if (too_big) {
+            if (late) late->ensure();
             if (host_fallback_enabled()) {
                 host_verify_parts(pj.data(), pr.data(), pj.size(), verdict + row0[g0], host_threads());
                 note_host_fallback();
@@ -811,7 +878,7 @@ int run_device_group(int dev, const std::vector<Round>& rds, unsigned t0, unsign
             }
         } else {
             e = resilient_round(dev, pj.data(), pr.data(), pj.size(), verdict + row0[g0], &st,
-                                retries, host_rounds, "verify_batch");
+                                retries, host_rounds, "verify_batch", late ? &fill : nullptr);
         }
         if (e != 0) return e;
         *stage_total += st;
@@ -826,8 +893,9 @@ int run_device_group(int dev, const std::vector<Round>& rds, unsigned t0, unsign
 // the GPUs' worker threads and write their verdicts at their row offsets.
 int run_device_round(const std::vector<Round>& rds, unsigned T, const std::vector<size_t>& row0,
                      uint8_t* verdict, double* stage_total, size_t* devices_used,
-                     size_t* retries, size_t* host_rounds) {
+                     size_t* retries, size_t* host_rounds, LateHost* late) {
     if (row0[T] <= host_small_round()) {  // a small round: lower latency on the host CPU
+        if (late) late->ensure();
         std::vector<const SighashJobs*> pj;
         std::vector<const TupleRows*> pr;
         for (unsigned t = 0; t < T; t++) {
@@ -838,6 +906,10 @@ int run_device_round(const std::vector<Round>& rds, unsigned T, const std::vecto
         return host_verify_parts(pj.data(), pr.data(), T, verdict, host_threads());
     }
     const std::vector<int> devs = device_list();
+    if (late && devs.size() != 1) {  // the late hook is for single-GPU rounds (chunk_interpret)
+        late->ensure();
+        late = nullptr;
+    }
     std::vector<size_t> w(T);
     for (unsigned t = 0; t < T; t++) w[t] = rds[t].pending.size();
     const size_t D = std::min<size_t>(devs.size(), T);
@@ -851,7 +923,7 @@ int run_device_round(const std::vector<Round>& rds, unsigned T, const std::vecto
         jd.push_back(devs[d]);
         jobs.push_back([&, d] {
             return run_device_group(devs[d], rds, (unsigned)cut[d], (unsigned)cut[d + 1], row0,
-                                    verdict, &st[d], &rt[d], &hr[d]);
+                                    verdict, &st[d], &rt[d], &hr[d], late);
         });
     }
     const int e = jobs.empty() ? 0 : run_on_devices(jd, jobs);
@@ -879,6 +951,8 @@ struct ChunkRun {
     int sync_rc = 0;             // result of a synchronous device round
     double stage_s = 0;
     size_t devices_used = 0, retries = 0, host_rounds = 0;
+    LateHost late;               // offloaded host jobs of the current pass (hashed during the round)
+    bool late_pending = false;
 };
 
 // Host state of bitcoinconsensus_verify_batch, per calling thread, reused across its calls: two
@@ -897,9 +971,14 @@ void chunk_interpret(ChunkRun& c) {
         ran[t] = interpret_shard(c.b, c.run_list[t], c.rds[t]);
     });
     t_stats.interpret_seconds += since(i0);
-    auto h0 = clk::now();
-    run_host_jobs(c.rds, c.T);
-    t_stats.host_jobs_seconds += since(h0);
+    // the offloaded jobs' rows are marked now; single-GPU rounds hash the jobs themselves while the
+    // device runs the message-independent kernels (LateHost), multi-GPU rounds before the round
+    c.late = LateHost{&c.rds, c.T, false};
+    c.late_pending = mark_host_rows(c.rds, c.T);
+    if (c.late_pending && device_list().size() != 1) {
+        c.late.ensure();
+        c.late_pending = false;
+    }
     size_t npend = 0;
     bool any = false;
     for (unsigned t = 0; t < c.T; t++) {
@@ -949,7 +1028,7 @@ void chunk_start(ChunkRun& c, const bcc_batch_item* items, size_t n, unsigned fl
 // The chunk's pending device round (its arguments stay valid until the chunk's next pass).
 int chunk_device_round(ChunkRun& c) {
     return run_device_round(c.rds, c.T, c.row0, c.verdict.data(), &c.stage_s, &c.devices_used,
-                            &c.retries, &c.host_rounds);
+                            &c.retries, &c.host_rounds, c.late_pending ? &c.late : nullptr);
 }
 
 // Stitches a device round's verdicts into the items; the items whose speculation failed get
@@ -1148,10 +1227,13 @@ size_t build_first_round(const bcc_batch_item* items, size_t n, unsigned flags, 
                          TupleRows& rows, std::vector<uint32_t>* tuple_item) {
     BatchState b;
     prepare(b, items, n, flags, 1);
-    Round rd;
+    std::vector<Round> rds(1);
+    Round& rd = rds[0];
+    rd.reset();  // the engine's thresholds: long chains hashed on the host as in a live round
     std::vector<uint32_t> all(n);
     for (size_t i = 0; i < n; i++) all[i] = (uint32_t)i;
     interpret_shard(b, all, rd);
+    if (mark_host_rows(rds, 1)) hash_host_jobs(rds, 1);
     if (tuple_item) {
         tuple_item->clear();
         for (const auto& p : rd.pending) tuple_item->push_back(p.item);
@@ -1324,6 +1406,11 @@ int bcc_set_device_key_hash(int on) {
 
 int bcc_set_host_chain_blocks(unsigned blocks) {
     bcc::host::g_host_chain_blocks.store(blocks, std::memory_order_relaxed);
+    return 0;
+}
+
+int bcc_set_host_bip143_blocks(unsigned blocks) {
+    bcc::host::g_host_bip143_blocks.store(blocks, std::memory_order_relaxed);
     return 0;
 }
 

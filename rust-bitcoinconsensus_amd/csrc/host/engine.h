@@ -44,10 +44,12 @@ void append_round(SighashJobs& dst, TupleRows& dst_rows, const SighashJobs& src,
 // One device round of P parts on `dev` with the engine's failure handling: one retry on a fresh
 // device batch for a transient HIP error (*retries), then the device failure policy: the parts are
 // verified on the host CPU (*host_rounds, bcc_host_fallback_rounds) or the error is returned.
-// `who` names the entry point in the stderr log.
+// `who` names the entry point in the stderr log.  `late` (optional): rows whose message the host
+// delivers during the round (pipeline.h LateMsgFill); it is also called before a host fallback, so
+// those rows' host messages are complete before the host verifies them.
 int resilient_round(int dev, const SighashJobs* const* pj, const TupleRows* const* pr, size_t P,
                     uint8_t* verdict, double* stage_s, size_t* retries, size_t* host_rounds,
-                    const char* who);
+                    const char* who, const LateMsgFill* late = nullptr);
 
 // Frees the calling thread's Taproot job buffers (host/taproot.cpp).
 void taproot_release_thread_state();

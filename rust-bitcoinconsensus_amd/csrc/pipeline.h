@@ -11,6 +11,7 @@
 #include <algorithm>
 #include <cstring>
 #include <vector>
+#include <functional>
 
 namespace bcc {
 
@@ -137,10 +138,10 @@ struct SighashJobs {
         if (n) memcpy(o + h, m, n);
         return off;
     }
-    uint32_t add_code(const uint8_t* m, size_t n) {
+    uint32_t add_code(const uint8_t* m, size_t n) {  // + a zero dword (K3' funnel reads)
         uint32_t off = (uint32_t)code.size();
         code.insert(code.end(), m, m + n);
-        code.resize(off + ((n + 3) & ~(size_t)3), 0);
+        code.resize(off + ((n + 3) & ~(size_t)3) + 4, 0);
         return off;
     }
     static uint32_t tpl_nblk(uint32_t tpl_len, uint32_t code_len) {
@@ -379,6 +380,12 @@ int schnorr_launch(SigScratch& sc, const uint8_t* d_sig64, const uint8_t* d_msg3
 // Device-resident batch (one per device / per caller thread).  stage() uploads, run() only
 // launches kernels (graph-capturable: no allocation, no synchronisation, once the scratch has
 // grown to the batch).  A null stream means the batch's own non-blocking stream.
+// Messages that are known only after a round's launches: the long SHA chains hashed on the host
+// while the device runs the message-independent kernels (engine.cpp, bcc_set_host_chain_blocks).
+// Called once those kernels are queued; appends batch-local rows and their 32-byte digests.  The
+// G ladder (the first kernel that reads a message) waits for them.
+using LateMsgFill = std::function<void(std::vector<uint32_t>& rows, std::vector<uint8_t>& digs)>;
+
 class DeviceBatch {
 public:
     explicit DeviceBatch(int device);
@@ -386,7 +393,7 @@ public:
     int stage(const SighashJobs& jobs, const TupleRows& rows);
     // the concatenation of P parts (row / message / job indices fixed up per part)
     int stage_parts(const SighashJobs* const* jobs, const TupleRows* const* rows, size_t P);
-    int run(void* stream);                       // K1..K4
+    int run(void* stream, const LateMsgFill* late = nullptr);  // K1..K4
     int run_sighash(void* stream);               // K1..K3 only
     int run_ecdsa(void* stream);                 // K4 only
     int fetch_verdicts(uint8_t* out);            // synchronous D2H (waits for the last run)
@@ -416,7 +423,13 @@ private:
     size_t up_rows_ = 0, up_total_ = 0;
     int launch_after_front(struct ihipStream_t* st);  // K_win, K2, K3
     int launch_key_hash(struct ihipStream_t* st);     // K_h160: key-hash conditions into the verdicts
-    int run_stages(void* stream);
+    int run_stages(void* stream, const LateMsgFill* late);
+    int put_late(struct ihipStream_t* st, const LateMsgFill* late);  // late rows -> d_m (K_late)
+    std::vector<uint32_t> late_rows_;
+    std::vector<uint8_t> late_digs_;
+    void* late_host_ = nullptr;  // pinned: rows then digests
+    uint8_t* late_dev_ = nullptr;
+    size_t late_cap_ = 0;        // entries of late_host_ / late_dev_
     bool kh_done_ = false;  // run_stages ran K_h160 already (ahead of the ladder, verdict_and)
     int dev_;
     void* own_stream_ = nullptr;   // hipStream_t, created on first use
@@ -468,7 +481,9 @@ void release_tuple_thread_state();
 int gpu_verify_batch(int device, const SighashJobs& jobs, const TupleRows& rows, uint8_t* verdict,
                      double* stage_seconds = nullptr);
 // The same over the concatenation of `parts` (jobs[p], rows[p]) pairs: verdict rows in order.
+// `late` (optional): rows whose message the host delivers after the launches (LateMsgFill).
 int gpu_verify_parts(int device, const SighashJobs* const* jobs, const TupleRows* const* rows,
-                     size_t parts, uint8_t* verdict, double* stage_seconds = nullptr);
+                     size_t parts, uint8_t* verdict, double* stage_seconds = nullptr,
+                     const LateMsgFill* late = nullptr);
 
 }  // namespace bcc

@@ -14,6 +14,15 @@ namespace bcc {
 
 SHA_HD uint32_t sha_rotr(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }
 
+// a ^ b ^ c in one gfx950 v_bitop3_b32 (truth table 0x96); the compiler pairs two v_xor_b32 instead
+SHA_HD uint32_t sha_xor3(uint32_t a, uint32_t b, uint32_t c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+#else
+    return a ^ b ^ c;
+#endif
+}
+
 SHA_HD void sha256_init_state(uint32_t s[8]) {
     s[0] = 0x6a09e667u; s[1] = 0xbb67ae85u; s[2] = 0x3c6ef372u; s[3] = 0xa54ff53au;
     s[4] = 0x510e527fu; s[5] = 0x9b05688cu; s[6] = 0x1f83d9abu; s[7] = 0x5be0cd19u;
@@ -38,13 +47,13 @@ SHA_HD void sha256_compress(uint32_t s[8], uint32_t w[16]) {
             wi = w[i];
         } else {
             uint32_t w15 = w[(i - 15) & 15], w2 = w[(i - 2) & 15];
-            uint32_t s0 = sha_rotr(w15, 7) ^ sha_rotr(w15, 18) ^ (w15 >> 3);
-            uint32_t s1 = sha_rotr(w2, 17) ^ sha_rotr(w2, 19) ^ (w2 >> 10);
+            uint32_t s0 = sha_xor3(sha_rotr(w15, 7), sha_rotr(w15, 18), w15 >> 3);
+            uint32_t s1 = sha_xor3(sha_rotr(w2, 17), sha_rotr(w2, 19), w2 >> 10);
             wi = w[i & 15] + s0 + w[(i - 7) & 15] + s1;
             w[i & 15] = wi;
         }
-        uint32_t t1 = h + (sha_rotr(e, 6) ^ sha_rotr(e, 11) ^ sha_rotr(e, 25)) + ((e & f) ^ (~e & g)) + K[i] + wi;
-        uint32_t t2 = (sha_rotr(a, 2) ^ sha_rotr(a, 13) ^ sha_rotr(a, 22)) + ((a & b) ^ (a & c) ^ (b & c));
+        uint32_t t1 = h + sha_xor3(sha_rotr(e, 6), sha_rotr(e, 11), sha_rotr(e, 25)) + ((e & f) ^ (~e & g)) + K[i] + wi;
+        uint32_t t2 = sha_xor3(sha_rotr(a, 2), sha_rotr(a, 13), sha_rotr(a, 22)) + ((a & b) ^ (a & c) ^ (b & c));
         h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
     }
     s[0] += a; s[1] += b; s[2] += c; s[3] += d; s[4] += e; s[5] += f; s[6] += g; s[7] += h;

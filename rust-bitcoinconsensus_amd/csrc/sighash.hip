@@ -157,6 +157,60 @@ __device__ __forceinline__ uint32_t tpl_word(const TplMsg& m, uint32_t q) {
            tpl_byte(m, q + 3);
 }
 
+// The 16 message words of a block that lies before the trailer (q0 + 64 <= e3), from three byte
+// sources -- A: T itself (g < pos), C: the code field (pos <= g < s3), B: T shifted by the code
+// (s3 <= g < e3) -- each read as 17 consecutive dwords and funnel-shifted to the block by one
+// v_perm per word (which also makes the word big-endian), then merged by per-byte masks.  The
+// lanes of a wave are consecutive inputs of one tx, so their splices fall in different blocks:
+// with masks every lane runs the same instructions (no divergent per-byte assembly), and the
+// dwords are fetched a block ahead of the compression.  Dword indices are clamped to the
+// template / code (both zero-padded past their end, SighashJobs::add_tpl / add_code); a clamped
+// dword only feeds bytes its mask discards.
+struct TplSrc {
+    uint32_t a[16], b[17], c[17];
+};
+
+struct TplGeom {
+    int32_t pos, s3, ob, oc;    // splice, end of the code field, B / C byte offsets at q = 0
+    uint32_t amax, cmax;        // last readable dword index of T / of the code field
+    uint32_t sel_b, sel_c;      // v_perm selectors: funnel by (offset & 3) + byte swap
+};
+
+__device__ __forceinline__ uint32_t tpl_clamp(int32_t i, uint32_t hi) {
+    return (uint32_t)min(max(i, 0), (int32_t)hi);
+}
+
+__device__ __forceinline__ void tpl_fetch(const TplMsg& m, const TplGeom& g, uint32_t q0, TplSrc& x) {
+    const uint32_t* T = reinterpret_cast<const uint32_t*>(m.T);
+    const uint32_t* C = reinterpret_cast<const uint32_t*>(m.C);
+    const int32_t ia = (int32_t)(q0 >> 2), ib = (g.ob + (int32_t)q0) >> 2, ic = (g.oc + (int32_t)q0) >> 2;
+#pragma unroll
+    for (int k = 0; k < 16; k++) x.a[k] = T[tpl_clamp(ia + k, g.amax)];
+#pragma unroll
+    for (int k = 0; k < 17; k++) x.b[k] = T[tpl_clamp(ib + k, g.amax)];
+#pragma unroll
+    for (int k = 0; k < 17; k++) x.c[k] = C[tpl_clamp(ic + k, g.cmax)];
+}
+
+// leading n of the 4 bytes of a big-endian word (n clamped to [0, 4])
+__device__ __forceinline__ uint32_t tpl_lead_mask(int32_t n) {
+    n = min(max(n, 0), 4);
+    return (uint32_t)(0xFFFFFFFF00000000ull >> (8 * n));
+}
+
+__device__ __forceinline__ void tpl_words(const TplGeom& g, uint32_t q0, const TplSrc& x,
+                                          uint32_t (&w)[16]) {
+#pragma unroll
+    for (int k = 0; k < 16; k++) {
+        const int32_t q = (int32_t)q0 + 4 * k;
+        const uint32_t wa = __builtin_amdgcn_perm(0u, x.a[k], 0x00010203u);
+        const uint32_t wb = __builtin_amdgcn_perm(x.b[k + 1], x.b[k], g.sel_b);
+        const uint32_t wc = __builtin_amdgcn_perm(x.c[k + 1], x.c[k], g.sel_c);
+        const uint32_t m1 = tpl_lead_mask(g.pos - q), m2 = tpl_lead_mask(g.s3 - q);
+        w[k] = (wa & m1) | (((wc & m2) | (wb & ~m2)) & ~m1);
+    }
+}
+
 __device__ __forceinline__ void sha256d_tpl_lane(const uint8_t* __restrict__ tpl,
                                                  const uint8_t* __restrict__ code,
                                                  const TplJob* __restrict__ jobs, uint32_t i,
@@ -171,19 +225,30 @@ __device__ __forceinline__ void sha256d_tpl_lane(const uint8_t* __restrict__ tpl
     m.e3 = m.L - 4;
     m.tail = j.nblk * 64 - 8;
     m.ht = j.hashtype;
+    TplGeom g;
+    g.pos = (int32_t)m.pos;
+    g.s3 = (int32_t)m.s3;
+    g.ob = 1 - (int32_t)j.code_len;  // B byte of message byte q: T[q - code_len + 1]
+    g.oc = -(int32_t)m.pos;          // C byte: code[q - pos]
+    g.amax = ((j.tpl_len + 3) >> 2) + 1;
+    g.cmax = (j.code_len + 3) >> 2;
+    g.sel_b = (uint32_t)(g.ob & 3) * 0x01010101u + 0x00010203u;
+    g.sel_c = (uint32_t)(g.oc & 3) * 0x01010101u + 0x00010203u;
+    const uint32_t fast_blocks = m.e3 / 64;  // blocks wholly before the hashtype trailer
     uint32_t st[8];
     sha256_init_state(st);
-    uint32_t nxt[16];
-#pragma unroll
-    for (int w = 0; w < 16; w++) nxt[w] = tpl_word(m, 4 * w);
-    for (uint32_t b = 0; b < j.nblk; b++) {
+    TplSrc nxt;
+    if (fast_blocks) tpl_fetch(m, g, 0, nxt);
+    for (uint32_t b = 0; b < fast_blocks; b++) {
+        uint32_t w[16];
+        tpl_words(g, 64 * b, nxt, w);
+        if (b + 1 < fast_blocks) tpl_fetch(m, g, 64 * (b + 1), nxt);
+        sha256_compress(st, w);
+    }
+    for (uint32_t b = fast_blocks; b < j.nblk; b++) {  // the trailer: byte by byte
         uint32_t w[16];
 #pragma unroll
-        for (int k = 0; k < 16; k++) w[k] = nxt[k];
-        if (b + 1 < j.nblk) {
-#pragma unroll
-            for (int k = 0; k < 16; k++) nxt[k] = tpl_word(m, 64 * (b + 1) + 4 * k);
-        }
+        for (int k = 0; k < 16; k++) w[k] = tpl_word(m, 64 * b + 4 * k);
         sha256_compress(st, w);
     }
     uint32_t d[8];
@@ -821,6 +886,8 @@ DeviceBatch::~DeviceBatch() {
     if (arena_) (void)hipFree(arena_);
     if (host_image_) (void)hipHostFree(host_image_);
     if (vbuf_) (void)hipHostFree(vbuf_);
+    if (late_host_) (void)hipHostFree(late_host_);
+    if (late_dev_) (void)hipFree(late_dev_);
 }
 
 void* DeviceBatch::pick(void* stream) {
@@ -1197,17 +1264,63 @@ int DeviceBatch::launch_key_hash(hipStream_t st) {
     return 0;
 }
 
+// K_late: the host-hashed messages (LateMsgFill) into their rows, one lane per row.
+__global__ void __launch_bounds__(256) late_msgs_kernel(const uint32_t* __restrict__ rows,
+                                                        const uint4* __restrict__ digs, uint32_t n,
+                                                        uint8_t* __restrict__ m) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    uint4* dst = (uint4*)(m + 32 * (size_t)rows[k]);
+    dst[0] = digs[2 * k];
+    dst[1] = digs[2 * k + 1];
+}
+
+// Calls the late fill on the host (the GPU meanwhile runs what is queued), then one H2D copy of
+// the rows + digests and K_late on `st`.  The rows were range-checked against the staged batch.
+int DeviceBatch::put_late(hipStream_t st, const LateMsgFill* late) {
+    late_rows_.clear();
+    late_digs_.clear();
+    (*late)(late_rows_, late_digs_);
+    const size_t k = late_rows_.size();
+    if (k == 0) return 0;
+    if (late_digs_.size() != 32 * k) return (int)hipErrorInvalidValue;
+    for (uint32_t r : late_rows_)
+        if (r >= n_rows_) return (int)hipErrorInvalidValue;
+    const size_t dig_off = align256(4 * k);
+    if (k > late_cap_) {
+        if (late_host_) BCC_HIP_TRY(hipHostFree(late_host_));
+        if (late_dev_) BCC_HIP_TRY(hipFree(late_dev_));
+        late_host_ = nullptr;
+        late_dev_ = nullptr;
+        late_cap_ = 0;
+        BCC_HIP_TRY(hipHostMalloc(&late_host_, dig_off + 32 * k, hipHostMallocDefault));
+        BCC_HIP_TRY(hipMalloc(&late_dev_, dig_off + 32 * k));
+        late_cap_ = k;
+    }
+    uint8_t* h = (uint8_t*)late_host_;
+    memcpy(h, late_rows_.data(), 4 * k);
+    memcpy(h + dig_off, late_digs_.data(), 32 * k);
+    BCC_HIP_TRY(hipMemcpyAsync(late_dev_, h, dig_off + 32 * k, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(late_msgs_kernel, dim3((unsigned)((k + 255) / 256)), dim3(256), 0, st,
+                       (const uint32_t*)late_dev_, (const uint4*)(late_dev_ + dig_off), (uint32_t)k,
+                       d_m);
+    BCC_HIP_TRY(hipGetLastError());
+    return 0;
+}
+
 // K_inv and K_key read only the s and key rows, so they run on a side stream beside the sighash
 // kernels (fork / join by events: graph-capturable); prep + ladder wait for both.
-int DeviceBatch::run(void* stream) {
+int DeviceBatch::run(void* stream, const LateMsgFill* late) {
     BCC_HIP_TRY(hipSetDevice(dev_));
     hipStream_t st = (hipStream_t)pick(stream);
     if (!st) return (int)hipErrorOutOfMemory;
     if (n_rows_ == 0 || n_aux_ + n_tjob_ + n_pre_ + n_wjob_ == 0) {
         if (int e = run_sighash(st)) return e;
+        if (late)
+            if (int e = put_late(st, late)) return e;
         return run_ecdsa(st);  // K_h160 included
     }
-    if (int e = run_stages(st)) return e;
+    if (int e = run_stages(st, late)) return e;
     if (kh_done_) return 0;  // K_h160 ran ahead of the ladder (run_stages)
     return launch_key_hash(st);
 }
@@ -1218,7 +1331,7 @@ int DeviceBatch::run(void* stream) {
 // ladder and K_tfin wait for both.  K_h160 needs only the key rows and the programs: it runs on the
 // main stream beside the Q ladder into verdicts preset to 1, and K_tfin then only clears failing
 // rows (verdict_and), instead of running after K_tfin at the end of the critical path.
-int DeviceBatch::run_stages(void* stream) {
+int DeviceBatch::run_stages(void* stream, const LateMsgFill* late) {
     hipStream_t st = (hipStream_t)stream;
     kh_done_ = false;
     if (!side_stream_) {
@@ -1248,6 +1361,10 @@ int DeviceBatch::run_stages(void* stream) {
         BCC_HIP_TRY(hipStreamWaitEvent(st, (hipEvent_t)ev_up_, 0));  // K_h160 reads the key rows
         if (int e = launch_key_hash(st)) return e;
         kh_done_ = true;
+    }
+    if (late) {  // host-hashed messages: the host works while the queued kernels run
+        if (!n_hash_) BCC_HIP_TRY(hipStreamWaitEvent(st, (hipEvent_t)ev_up_, 0));  // rows uploaded
+        if (int e = put_late(st, late)) return e;
     }
     BCC_HIP_TRY(hipStreamWaitEvent(st, (hipEvent_t)ev_join_, 0));
     return ecdsa_launch_after_pre(scratch_, d_tag, d_x, d_y, d_r, d_s, d_m, d_v, n_rows_, st,
@@ -1296,7 +1413,7 @@ int gpu_verify_batch(int device, const SighashJobs& jobs, const TupleRows& rows,
 thread_local std::vector<std::unique_ptr<DeviceBatch>> tl_batches;
 
 int gpu_verify_parts(int device, const SighashJobs* const* jobs, const TupleRows* const* rows,
-                     size_t parts, uint8_t* verdict, double* stage_seconds) {
+                     size_t parts, uint8_t* verdict, double* stage_seconds, const LateMsgFill* late) {
     size_t n = 0;
     for (size_t p = 0; p < parts; p++) n += rows[p]->size();
     if (n == 0) return 0;
@@ -1309,7 +1426,7 @@ int gpu_verify_parts(int device, const SighashJobs* const* jobs, const TupleRows
     int e = b.stage_parts(jobs, rows, parts);
     if (!e && stage_seconds)
         *stage_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-    if (!e) e = b.run(nullptr);
+    if (!e) e = b.run(nullptr, late);
     if (!e) e = b.fetch_verdicts(verdict);
     if (e) cache[device].reset();  // a retry starts from a fresh batch (streams, arena, scratch)
     return e;
@@ -1336,8 +1453,6 @@ namespace {
 struct TaprootCtx {
     int dev = -1;
     hipStream_t stream = nullptr;
-    hipStream_t side = nullptr;  // the signature / key rows' upload beside the SigMsg kernels
-    hipEvent_t side_done = nullptr;
     SigScratch sc;
     void* arena = nullptr;
     size_t cap = 0;
@@ -1346,24 +1461,12 @@ struct TaprootCtx {
     ~TaprootCtx() {
         if (dev >= 0) (void)hipSetDevice(dev);
         if (stream) (void)hipStreamDestroy(stream);
-        if (side) (void)hipStreamDestroy(side);
-        if (side_done) (void)hipEventDestroy(side_done);
         if (arena) (void)hipFree(arena);
         if (image) (void)hipHostFree(image);
     }
 };
 
 }  // namespace
-
-// BCC_TAPROOT_SPLIT_UPLOAD=1: upload the signature / key rows on a side stream beside the SigMsg
-// kernels (A/B runs)
-static bool taproot_split_upload() {
-    static const bool on = [] {
-        const char* e = getenv("BCC_TAPROOT_SPLIT_UPLOAD");
-        return e && atoi(e) != 0;
-    }();
-    return on;
-}
 
 int gpu_taproot_verify(int device, const TaprootJobs& J, uint8_t* verdict, uint8_t* msg32_out) {
     const TaprootJobs* p = &J;
@@ -1502,21 +1605,7 @@ int gpu_taproot_verify_parts(int device, const TaprootJobs* const* Jp, size_t P,
     hipStream_t st = c.stream;
     ShaMid mid;
     tapsighash_midstate(mid.s);
-    const bool split_up = taproot_split_upload();
-    if (split_up) {
-        // the tx bytes and jobs first on the main stream (the SigMsg kernels need them), the
-        // 96-byte signature / key rows on a side stream beside those kernels; the BIP340 kernels
-        // wait for both
-        if (!c.side) {
-            BCC_HIP_TRY(hipStreamCreateWithFlags(&c.side, hipStreamNonBlocking));
-            BCC_HIP_TRY(hipEventCreateWithFlags(&c.side_done, hipEventDisableTiming));
-        }
-        BCC_HIP_TRY(hipMemcpyAsync(a + off[MSG], h + off[MSG], upload - off[MSG], hipMemcpyHostToDevice, st));
-        BCC_HIP_TRY(hipMemcpyAsync(a, h, off[MSG], hipMemcpyHostToDevice, c.side));
-        BCC_HIP_TRY(hipEventRecord(c.side_done, c.side));
-    } else {
-        BCC_HIP_TRY(hipMemcpyAsync(a, h, upload, hipMemcpyHostToDevice, st));
-    }
+    BCC_HIP_TRY(hipMemcpyAsync(a, h, upload, hipMemcpyHostToDevice, st));
     if (nttx) {  // KT_tx, then KT_msg: the SigMsgs from the tx bytes
         hipLaunchKernelGGL(taproot_tx_kernel, dim3((unsigned)((5 * nttx + XS_WG - 1) / XS_WG)),
                            dim3(XS_WG), 0, st, a + off[TXRAW], (const TtxRec*)(a + off[TTX]),
@@ -1550,7 +1639,6 @@ int gpu_taproot_verify_parts(int device, const TaprootJobs* const* Jp, size_t P,
                            (const uint32_t*)(a + off[MSG_ROW]), mid);
         BCC_HIP_TRY(hipGetLastError());
     }
-    if (split_up) BCC_HIP_TRY(hipStreamWaitEvent(st, c.side_done, 0));
     if (int e = schnorr_launch(c.sc, a + off[0], a + off[2], a + off[1], a + off[3], n, st)) {
         ctxs[device].reset();
         return e;

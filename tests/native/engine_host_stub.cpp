@@ -21,16 +21,38 @@ static size_t unpadded_len(const uint8_t* m, size_t padded) {
     return (size_t)(bits / 8);
 }
 
-int gpu_verify_batch(int, const SighashJobs& j, const TupleRows& rows, uint8_t* verdict, double*);
+static void stub_sighash(const SighashJobs& j, std::vector<uint8_t>& msg);
+static void stub_ecdsa(const TupleRows& rows, const uint8_t* msg, uint8_t* verdict);
 void set_stage_threads(unsigned) {}  // the device batch is stubbed out
 void release_device_thread_state() {}
 void release_tuple_thread_state() {}
-int gpu_verify_parts(int dev, const SighashJobs* const* jobs, const TupleRows* const* rows, size_t parts,
-                     uint8_t* verdict, double*) {
+// As DeviceBatch: the rows are copied (staged) first, the sighash jobs hash into the copy, then the
+// late rows (host-hashed while the device runs) land in it (put_late), then the ECDSA stage.
+int gpu_verify_parts(int, const SighashJobs* const* jobs, const TupleRows* const* rows, size_t parts,
+                     uint8_t* verdict, double*, const LateMsgFill* late) {
+    std::vector<TupleRows> staged(parts);
+    std::vector<uint8_t> msg;
+    for (size_t p = 0; p < parts; p++) {
+        staged[p] = *rows[p];
+        staged[p].materialize();  // rows stored without y / msg (TupleRows::add_lazy): zero / ONE
+        std::vector<uint8_t> m = staged[p].msg;
+        stub_sighash(*jobs[p], m);
+        msg.insert(msg.end(), m.begin(), m.end());
+    }
+    if (late) {
+        std::vector<uint32_t> lr;
+        std::vector<uint8_t> ld;
+        (*late)(lr, ld);
+        if (ld.size() != 32 * lr.size()) return 1;
+        for (size_t k = 0; k < lr.size(); k++) {
+            if (32 * (size_t)lr[k] >= msg.size()) return 1;
+            memcpy(&msg[32 * (size_t)lr[k]], &ld[32 * k], 32);
+        }
+    }
     size_t r0 = 0;
     for (size_t p = 0; p < parts; p++) {
-        gpu_verify_batch(dev, *jobs[p], *rows[p], verdict + r0, nullptr);
-        r0 += rows[p]->size();
+        stub_ecdsa(staged[p], &msg[32 * r0], verdict + r0);
+        r0 += staged[p].size();
     }
     return 0;
 }
@@ -68,11 +90,13 @@ static void stub_sighash(const SighashJobs& j, std::vector<uint8_t>& msg) {
     }
 }
 
-int gpu_verify_batch(int, const SighashJobs& j, const TupleRows& rows_in, uint8_t* verdict, double*) {
-    TupleRows rows = rows_in;
-    rows.materialize();  // rows stored without y / msg (TupleRows::add_lazy): zero / ONE
-    std::vector<uint8_t> msg = rows.msg;
-    stub_sighash(j, msg);
+int gpu_verify_batch(int dev, const SighashJobs& j, const TupleRows& rows, uint8_t* verdict, double*) {
+    const SighashJobs* jp = &j;
+    const TupleRows* rp = &rows;
+    return gpu_verify_parts(dev, &jp, &rp, 1, verdict, nullptr, nullptr);
+}
+
+static void stub_ecdsa(const TupleRows& rows, const uint8_t* msg, uint8_t* verdict) {
     for (size_t i = 0; i < rows.size(); i++) {
         uint8_t pub[65];
         pub[0] = rows.tag[i];
@@ -88,7 +112,6 @@ int gpu_verify_batch(int, const SighashJobs& j, const TupleRows& rows_in, uint8_
                                                     &msg[32 * i]);
     }
     bcc::host::apply_key_hashes(rows, verdict);  // the device's key_hash_kernel
-    return 0;
 }
 
 // BIP341 jobs (host/taproot.cpp): aux messages single SHA-256, patch, TapSighash over the

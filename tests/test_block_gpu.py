@@ -28,18 +28,21 @@ def wl():
     return B.Workload(kind="block", shape=sub, seed=0x5EED0003)
 
 
-@pytest.mark.parametrize("chain_blocks", [32, 0])
-def test_block_workload_all_valid_and_matches_reference(wl, chain_blocks):
-    """chain_blocks 32: the big txs' long SHA chains hashed on the host; 0 (default): every
-    chain in a GPU lane."""
+@pytest.mark.parametrize("chain_blocks,bip143_blocks", [(32, 32), (0, 32), (0, 0)])
+def test_block_workload_all_valid_and_matches_reference(wl, chain_blocks, bip143_blocks):
+    """chain_blocks 32: the big txs' long legacy chains hashed on the host (during the device
+    round); bip143_blocks 32 (default): their BIP143 per-tx digests and preimages on the host;
+    (0, 0): every chain in a GPU lane."""
     import bitcoinconsensus_amd as B
     B.set_host_chain_blocks(chain_blocks)
+    B.set_host_bip143_blocks(bip143_blocks)
     try:
         n_valid, ret = wl.verify_batch()
         st = B.last_batch_stats()
     finally:
         B.set_host_chain_blocks(0)
-    assert (st["host_hashed"] > 0) == (chain_blocks > 0)
+        B.set_host_bip143_blocks(32)
+    assert (st["host_hashed"] > 0) == (chain_blocks + bip143_blocks > 0)
     assert n_valid == wl.n and all(r == 1 for r in ret)
     assert st["rounds"] == 1          # multisig candidate pairs are queued up front: no re-run
     assert st["tuples"] > wl.n        # multisig inputs verify 2-3 signatures
@@ -51,10 +54,23 @@ def test_block_workload_all_valid_and_matches_reference(wl, chain_blocks):
 
 
 @pytest.mark.skipif(not reference_available(), reason="oracle/_ref not built")
-def test_block_workload_mutations_match_reference(wl):
+@pytest.mark.parametrize("chain_blocks", [0, 16])
+def test_block_workload_mutations_match_reference(wl, chain_blocks):
     """Single-byte flips anywhere in a spending transaction (signatures, pubkeys, scripts,
-    outpoints, amounts, lengths) under three flag sets: per-item (ret, err) equals the reference."""
+    outpoints, amounts, lengths) under three flag sets: per-item (ret, err) equals the reference.
+    chain_blocks 16: the many-input txs' chains hashed on the host while the device round runs
+    (their digests reach the message rows before the G ladder)."""
     import bitcoinconsensus_amd as B
+    B.set_host_chain_blocks(chain_blocks)
+    try:
+        _mutations(B, wl)
+        if chain_blocks:
+            assert B.last_batch_stats()["host_hashed"] > 0
+    finally:
+        B.set_host_chain_blocks(0)
+
+
+def _mutations(B, wl):
     R = Reference()
     rng = random.Random(3)
     items = []

@@ -123,8 +123,10 @@ def test_script_cases_host_hashed_chains(eng, blocks):
     preimage jobs in the parallel pass, long-tx BIP143 checks inline): identical results, as
     batches and as single calls."""
     eng.bcc_set_host_chain_blocks.argtypes = [ctypes.c_uint]
+    eng.bcc_set_host_bip143_blocks.argtypes = [ctypes.c_uint]
     try:
         eng.bcc_set_host_chain_blocks(blocks)
+        eng.bcc_set_host_bip143_blocks(blocks)
         hashed = []
         test_script_cases_as_batches(eng, hashed)
         assert sum(hashed) > 0  # the offload ran
@@ -133,6 +135,7 @@ def test_script_cases_host_hashed_chains(eng, blocks):
             test_crate_vectors(eng)
     finally:
         eng.bcc_set_host_chain_blocks(0)
+        eng.bcc_set_host_bip143_blocks(32)
 
 
 @pytest.mark.parametrize("on", [0, 1])

@@ -7,8 +7,8 @@ import os
 import sys
 
 O = sys.argv[1]
-KEEP = ("twist_ladder", "prim_kernel", "ecdsa_tprep", "batch_sinv", "twist_fin", "ecdsa_tkey",
-        "ecdsa_tscal", "bip143")
+KEEP = ("twist_ladder", "twist_keyq", "prim_kernel", "ecdsa_tprep", "batch_sinv", "twist_fin",
+        "bip143")
 
 
 def main():
