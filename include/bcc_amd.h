@@ -129,9 +129,10 @@ int bcc_set_chunk_lanes(size_t lanes);
 int bcc_set_pipeline_chunk(size_t items);
 
 /* Legacy signature checks whose serial SHA-256 chain is longer than `blocks` 64-byte blocks (the
- * preimages of many-input transactions) are hashed on the host CPU instead of in one GPU lane each
- * (BCC_HOST_CHAIN_BLOCKS; default 0: every legacy chain on the GPU).  On one GPU the host hashes
- * them while the device round's message-independent kernels run.  BIP143 checks of a tx whose
+ * preimages of many-input transactions) are hashed on the host CPU instead of in one GPU lane each,
+ * while the device round's message-independent kernels run (BCC_HOST_CHAIN_BLOCKS; default 260,
+ * about the Q ladder's latency in GPU-lane blocks; 0: every legacy chain on the GPU).  Single-GPU
+ * rounds only, at most 2^19 blocks per interpreter pass.  BIP143 checks of a tx whose
  * per-tx chains (hashPrevouts / hashSequence / hashOutputs) exceed BCC_HOST_BIP143_BLOCKS (default
  * 32) blocks are hashed on the host (linear in the tx).  Results never depend on either. */
 int bcc_set_host_chain_blocks(unsigned blocks);
@@ -191,6 +192,9 @@ typedef struct bcc_batch_stats {
     /* key-hash conditions (HASH160(pubkey) == program) checked on the device beside their
      * signature (bcc_set_device_key_hash) */
     size_t device_key_hashes;
+    /* interpreter passes per shard: the slowest shard and the mean (summed over passes): their
+     * ratio is the passes' load imbalance */
+    double interpret_shard_max_seconds, interpret_shard_mean_seconds;
 } bcc_batch_stats;
 /* Statistics of the calling thread's last bitcoinconsensus_verify_batch / verify call. */
 void bcc_last_batch_stats(bcc_batch_stats* out);

@@ -211,7 +211,9 @@ class BatchStats(ctypes.Structure):
                 ("stitch_seconds", ctypes.c_double), ("finish_seconds", ctypes.c_double),
                 ("host_jobs_seconds", ctypes.c_double), ("prepare_lag_seconds", ctypes.c_double),
                 ("prepare_parse_seconds", ctypes.c_double), ("prepare_hash_seconds", ctypes.c_double),
-                ("device_key_hashes", ctypes.c_size_t)]
+                ("device_key_hashes", ctypes.c_size_t),
+                ("interpret_shard_max_seconds", ctypes.c_double),
+                ("interpret_shard_mean_seconds", ctypes.c_double)]
 
 
 def _bind_consensus(L):

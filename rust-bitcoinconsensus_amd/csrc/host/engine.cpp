@@ -86,20 +86,22 @@ struct TxEntry {
 };
 
 // Long serial SHA chains stay on the host.  One GPU lane compresses one block
-// in ~6.5 us (the SHA-256 rounds are a dependent chain; a lone wave cannot hide their latency), the
+// in ~4 us (a lone wave issues the ~2,100 instructions of a template block one after another), the
 // host's SHA extensions in ~35 ns.  A many-input transaction (block413567's 442-input tx) has
 // chains of ~250-290 blocks -- its legacy preimages (every input's template is ~18 KB) and its
 // BIP143 hashPrevouts -- which would set the whole device round's front at ~2 ms while the rest of
 // the round's thousands of short chains finish in microseconds.  A check whose chain exceeds
 // host_chain_blocks() blocks is therefore hashed on the host: BIP143 checks of such a tx inline
 // (the per-tx digests once, then a ~4-block preimage each), legacy template / host-preimage jobs in
-// a parallel pass over all shards (hash_host_jobs).  On one GPU that pass runs while the device
-// round's message-independent kernels (K_inv, the key / Q-ladder launch, the sighash front) run,
-// and its digests reach the message rows just before the G ladder (LateHost, DeviceBatch::put_late);
-// on several GPUs it runs before the round.  Everything else is unchanged.
+// a parallel pass over all shards (hash_host_jobs) that runs while the device round's
+// message-independent kernels (K_inv, the key / Q-ladder launch, the sighash front) run; its
+// digests reach the message rows just before the G ladder (LateHost, DeviceBatch::put_late).
+// Legacy offload is for single-GPU rounds only (on several GPUs the pass would run before the
+// round) and is capped per shard (HostJobs::BUDGET_BLOCKS).  Everything else is unchanged.
 struct HostJobs {
     uint32_t chain_blocks = 0;       // legacy offload threshold in 64-byte blocks (0: never)
     uint32_t bip143_blocks = 0;      // BIP143 per-tx chain threshold (0: never)
+    std::atomic<uint64_t>* planned = nullptr;  // legacy blocks sent to the host this pass, all shards
     std::vector<uint8_t> tpl, code;  // templates / code fields of offloaded legacy ALL jobs
     std::vector<TplJob> tjobs;       // offsets into tpl / code, row = the tuple row
     std::vector<uint8_t> pre;        // offloaded host preimages (NONE / SINGLE / ACP), unpadded
@@ -112,11 +114,26 @@ struct HostJobs {
         tpl.clear(); code.clear(); tjobs.clear(); pre.clear(); pre_off.assign(1, 0); pre_row.clear();
         dig.clear(); inline_rows = 0;
     }
+    // Legacy work an interpreter pass may send to the host, in blocks, over all shards: the jobs
+    // are hashed while the device round's message-independent kernels run (~1 ms), dealt over the
+    // host threads at ~35 ns a block (2^19 blocks: ~1.1 ms on 16 threads, though a round's
+    // chains above the default threshold are usually a fraction of it).  Beyond it the chains stay
+    // on the GPU, whose lanes hash thousands of them side by side.
+    static constexpr uint64_t BUDGET_BLOCKS = (uint64_t)1 << 19;
+    bool take(uint64_t blocks) {
+        if (!planned) return false;
+        if (planned->fetch_add(blocks, std::memory_order_relaxed) + blocks <= BUDGET_BLOCKS)
+            return true;
+        planned->fetch_sub(blocks, std::memory_order_relaxed);
+        return false;
+    }
 };
 
+// Default 260: a GPU lane hashes ~4 us a block, so a chain above ~250 blocks outlasts the device
+// round's Q ladder (~0.9 ms for a small round) and would set the round's length.
 std::atomic<uint32_t> g_host_chain_blocks{[] {
     const char* e = getenv("BCC_HOST_CHAIN_BLOCKS");
-    return e ? (uint32_t)atoi(e) : 0u;
+    return e ? (uint32_t)atoi(e) : 260u;
 }()};
 
 // BIP143 checks of a tx whose hashPrevouts / hashSequence / hashOutputs chains exceed this many
@@ -255,17 +272,23 @@ void add_sighash_job(SighashJobs& jobs, TxEntry& te, const bcc_batch_item& in, c
         return &rows->msg[32 * (size_t)row];
     };
     if (sv == SIGVERSION_BASE && legacy_all_type(hashtype)) {
-        // device-assembled from the tx template (pipeline.h TplJob), or a host job (long template)
-        if (te.tpl < 0 && te.htpl < 0) {
+        // device-assembled from the tx template (pipeline.h TplJob), or a host job (a long
+        // template, while the shard's host budget lasts; the tx's later checks then go to a device
+        // copy of the same template)
+        auto place_tpl = [&](bool on_host) {
             build_legacy_template(tx, scratch);
+            if (te.tpl < 0 && te.htpl < 0) touched.push_back(&te);
             te.tpl_len = (uint32_t)scratch.size();
-            if (hb && SighashJobs::tpl_nblk(te.tpl_len, 1) > hb) {
+            if (on_host) {
                 te.htpl = (int64_t)host->tpl.size();
                 host->tpl.insert(host->tpl.end(), scratch.begin(), scratch.end());
             } else {
                 te.tpl = jobs.add_tpl(scratch.data(), scratch.size());
             }
-            touched.push_back(&te);
+        };
+        if (te.tpl < 0 && te.htpl < 0) {
+            te.tpl_len = (uint32_t)legacy_template_len(tx);
+            place_tpl(hb && SighashJobs::tpl_nblk(te.tpl_len, 1) > hb);
         }
         build_script_code_field(code, scratch);
         TplJob tj;
@@ -275,7 +298,13 @@ void add_sighash_job(SighashJobs& jobs, TxEntry& te, const bcc_batch_item& in, c
         tj.hashtype = (uint32_t)hashtype;
         tj.row = row;
         tj.nblk = SighashJobs::tpl_nblk(tj.tpl_len, tj.code_len);
-        if (te.htpl >= 0) {
+        const bool on_host = te.htpl >= 0 && host->take(tj.nblk);
+        if (!on_host && te.tpl < 0) {  // budget spent: this tx's remaining checks on the device
+            std::vector<uint8_t> field(scratch);
+            place_tpl(false);
+            scratch.swap(field);
+        }
+        if (on_host) {
             msg_row();  // hash_host_jobs writes the row
             tj.tpl_off = (uint32_t)te.htpl;
             tj.code_off = (uint32_t)host->code.size();
@@ -288,7 +317,8 @@ void add_sighash_job(SighashJobs& jobs, TxEntry& te, const bcc_batch_item& in, c
         }
     } else if (sv == SIGVERSION_BASE) {
         if (build_legacy_preimage(tx, nin, code, hashtype, scratch)) {
-            if (hb && sha_padded_len(scratch.size()) / 64 > hb) {
+            const uint64_t nb = sha_padded_len(scratch.size()) / 64;
+            if (hb && nb > hb && host->take(nb)) {
                 msg_row();
                 host->pre.insert(host->pre.end(), scratch.begin(), scratch.end());
                 host->pre_off.push_back(host->pre.size());
@@ -461,14 +491,15 @@ public:
         return true;  // speculative
     }
 
-    void reset() {
+    // legacy_host: legacy chains may go to the host (single-GPU rounds, chunk_interpret)
+    void reset(bool legacy_host = true) {
         jobs.clear();
         rows.clear();
         rows.msg_one = true;   // every row enters with msg = ONE (defer)
         rows.y_unused = true;  // until a 65-byte key is deferred
         pending.clear();
         host.clear();
-        host.chain_blocks = g_host_chain_blocks.load(std::memory_order_relaxed);
+        host.chain_blocks = legacy_host ? g_host_chain_blocks.load(std::memory_order_relaxed) : 0;
         host.bip143_blocks = g_host_bip143_blocks.load(std::memory_order_relaxed);
         for (auto* t : touched) {
             t->aux[0] = t->aux[1] = t->aux[2] = -1;
@@ -593,9 +624,9 @@ void run_threads(unsigned T, F f) {
 // Contiguous [lo, hi) share t of T over n units.
 inline size_t share_lo(size_t n, unsigned t, unsigned T) { return n * t / T; }
 
-// Boundaries of T contiguous shards of whole transactions (items of one tx share its TxEntry,
-// whose BIP143 aux slots and legacy template the shard's Round owns), balanced by count: shard t
-// is items [bound[t], bound[t + 1]).
+// Boundaries of T contiguous shards of whole tx entries (items of one entry share its TxEntry,
+// whose BIP143 aux slots and legacy template the shard's Round owns; prepare cuts a many-input tx
+// into several entries), balanced by count: shard t is items [bound[t], bound[t + 1]).
 std::vector<size_t> shard_bounds(const BatchState& b, unsigned T) {
     const size_t n = b.n, E = b.tx_first.size();
     std::vector<size_t> bound(T + 1, n);
@@ -644,6 +675,25 @@ void prepare(BatchState& b, const bcc_batch_item* items, size_t n, unsigned flag
         for (unsigned t = 0; t < T; t++) {
             std::copy(b.tx_slices[t].begin(), b.tx_slices[t].end(), b.tx_first.begin() + at);
             at += b.tx_slices[t].size();
+        }
+    }
+    // A run longer than a quarter of a shard (a many-input tx) is cut into pieces of at most that
+    // many items, each its own TxEntry (the tx parsed once per piece, with its own per-round
+    // template / aux slots), so that shard_bounds can balance the interpreter passes: C3's
+    // 442-input txs made one shard 2.4x the mean (bcc_batch_stats interpret_shard_*).
+    if (T > 1) {
+        const size_t M = std::max<size_t>(32, n / (4 * (size_t)T));
+        bool longrun = false;
+        for (size_t k = 0; k < b.tx_first.size() && !longrun; k++)
+            longrun = (k + 1 < b.tx_first.size() ? b.tx_first[k + 1] : n) - b.tx_first[k] > M;
+        if (longrun) {
+            std::vector<uint32_t> cut;
+            cut.reserve(b.tx_first.size() + n / M + 1);
+            for (size_t k = 0; k < b.tx_first.size(); k++) {
+                const size_t end = k + 1 < b.tx_first.size() ? b.tx_first[k + 1] : n;
+                for (size_t i = b.tx_first[k]; i < end; i += M) cut.push_back((uint32_t)i);
+            }
+            b.tx_first.swap(cut);
         }
     }
     const size_t E = b.tx_first.size();
@@ -952,6 +1002,8 @@ struct ChunkRun {
     double stage_s = 0;
     size_t devices_used = 0, retries = 0, host_rounds = 0;
     LateHost late;               // offloaded host jobs of the current pass (hashed during the round)
+    // their blocks (HostJobs::take); held by pointer so that ChunkRun stays movable
+    std::unique_ptr<std::atomic<uint64_t>> host_planned = std::make_unique<std::atomic<uint64_t>>(0);
     bool late_pending = false;
 };
 
@@ -966,11 +1018,24 @@ inline double since(clk::time_point a) { return std::chrono::duration<double>(cl
 void chunk_interpret(ChunkRun& c) {
     std::vector<char> ran(c.T, 0);
     auto i0 = clk::now();
+    const bool one_gpu = device_list().size() == 1;
+    c.host_planned->store(0, std::memory_order_relaxed);
+    std::vector<double> ts(c.T, 0);
     run_threads(c.T, [&](unsigned t) {
-        c.rds[t].reset();
+        auto s0 = clk::now();
+        c.rds[t].reset(one_gpu);
+        c.rds[t].host.planned = c.host_planned.get();
         ran[t] = interpret_shard(c.b, c.run_list[t], c.rds[t]);
+        ts[t] = since(s0);
     });
     t_stats.interpret_seconds += since(i0);
+    double tmax = 0, tsum = 0;
+    for (double x : ts) {
+        tmax = std::max(tmax, x);
+        tsum += x;
+    }
+    t_stats.interpret_shard_max_seconds += tmax;
+    t_stats.interpret_shard_mean_seconds += tsum / c.T;
     // the offloaded jobs' rows are marked now; single-GPU rounds hash the jobs themselves while the
     // device runs the message-independent kernels (LateHost), multi-GPU rounds before the round
     c.late = LateHost{&c.rds, c.T, false};
@@ -1001,11 +1066,18 @@ void chunk_interpret(ChunkRun& c) {
     c.verdict.assign(npend, 0);
 }
 
+constexpr size_t SHORT_PASS_ITEMS = 65536;
+
 // prepare + shards + the first interpreter pass of items [0, n) of `items`.
 void chunk_start(ChunkRun& c, const bcc_batch_item* items, size_t n, unsigned flags) {
     auto t0 = clk::now();
     c.n = n;
-    c.T = n >= 256 ? std::min<unsigned>(host_threads(), (unsigned)(n / 64)) : 1u;
+    // A short host pass (a block-sized batch) on at most the CPU share: three times the quota
+    // pays off for long passes alternating with long device waits (host_threads()), but for a
+    // ~1 ms pass the extra threads only queue for the CPUs and their wake-ups
+    // (C3 at 48 threads vs 16: 2.9-3.0 vs 4.7-5.4 M inputs/s, profiles/r04/c3).
+    const unsigned cap = n < SHORT_PASS_ITEMS ? std::min(host_threads(), cpu_share()) : host_threads();
+    c.T = n >= 256 ? std::min<unsigned>(cap, (unsigned)(n / 64)) : 1u;
     const unsigned T = c.T;
     prepare(c.b, items, n, flags, T, &c.shards, &c.run_list);  // + the shard / run lists
     t_stats.prepare_seconds += since(t0);
@@ -1230,6 +1302,8 @@ size_t build_first_round(const bcc_batch_item* items, size_t n, unsigned flags, 
     std::vector<Round> rds(1);
     Round& rd = rds[0];
     rd.reset();  // the engine's thresholds: long chains hashed on the host as in a live round
+    std::atomic<uint64_t> planned{0};
+    rd.host.planned = &planned;
     std::vector<uint32_t> all(n);
     for (size_t i = 0; i < n; i++) all[i] = (uint32_t)i;
     interpret_shard(b, all, rd);

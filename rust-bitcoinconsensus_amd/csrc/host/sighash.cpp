@@ -122,6 +122,15 @@ void build_legacy_template(const Tx& tx, std::vector<uint8_t>& o) {
     put_le(o, tx.locktime, 4);
 }
 
+static size_t compact_size_len(size_t n) { return n < 0xfd ? 1 : n <= 0xffff ? 3 : n <= 0xffffffffu ? 5 : 9; }
+
+size_t legacy_template_len(const Tx& tx) {
+    size_t out = 0;
+    for (const auto& o : tx.vout) out += o.ser.n;
+    return 4 + compact_size_len(tx.vin.size()) + 41 * tx.vin.size() +
+           compact_size_len(tx.vout.size()) + out + 4;
+}
+
 size_t legacy_template_pos(const Tx& tx, unsigned nin) {
     const size_t n = tx.vin.size();
     const size_t cs = n < 0xfd ? 1 : n <= 0xffff ? 3 : n <= 0xffffffffu ? 5 : 9;

@@ -37,6 +37,7 @@ bool build_legacy_preimage(const Tx& tx, unsigned nin, const Bytes& script_code,
 // legacy_all_type: hashtypes whose preimage has that form (not NONE / SINGLE / ANYONECANPAY).
 void build_legacy_template(const Tx& tx, std::vector<uint8_t>& out);
 size_t legacy_template_pos(const Tx& tx, unsigned nin);
+size_t legacy_template_len(const Tx& tx);  // build_legacy_template's output size
 void build_script_code_field(const Bytes& script_code, std::vector<uint8_t>& out);
 inline bool legacy_all_type(int hashtype) {
     return (hashtype & 0x80) == 0 && (hashtype & 0x1f) != 2 && (hashtype & 0x1f) != 3;

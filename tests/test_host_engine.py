@@ -117,6 +117,33 @@ def test_script_cases_pipelined(eng):
         eng.bcc_set_pipeline_chunk(0)
 
 
+def test_long_tx_runs_cut_into_entries(eng):
+    """Items arriving as long runs on one tx buffer (the inputs of a many-input tx): prepare cuts
+    a run longer than a quarter of a shard into several TxEntry pieces (each parsed on its own,
+    with its own template / aux slots) so the interpreter shards balance.  Every item's result
+    equals the reference label, with the pieces in different shards."""
+    allc = cases()
+    flags = max({c["flags"] for c in allc}, key=lambda f: sum(c["flags"] == f for c in allc))
+    cs = [c for c in allc if c["flags"] == flags][:20]
+    R = 300
+    arr = (Item * (len(cs) * R))()
+    keep = []
+    for k, c in enumerate(cs):
+        spk, tx = bytes.fromhex(c["spk"]), bytes.fromhex(c["tx"])
+        bs = ctypes.create_string_buffer(spk, max(1, len(spk)))
+        bt = ctypes.create_string_buffer(tx, max(1, len(tx)))
+        keep += [bs, bt]
+        for r in range(R):
+            arr[k * R + r] = Item(ctypes.addressof(bs), len(spk), c["amount"], ctypes.addressof(bt),
+                                  len(tx), c["nin"])
+    ret = (ctypes.c_int * len(arr))()
+    err = (ctypes.c_int * len(arr))()
+    eng.bitcoinconsensus_verify_batch(arr, len(arr), flags, ret, err)
+    got = list(zip(ret, err))
+    exp = [(c["ret"], c["err"]) for c in cs for _ in range(R)]
+    assert got == exp
+
+
 @pytest.mark.parametrize("blocks", [1, 2, 5])
 def test_script_cases_host_hashed_chains(eng, blocks):
     """Checks whose SHA chain exceeds `blocks` blocks hashed on the host (legacy template and
@@ -134,7 +161,7 @@ def test_script_cases_host_hashed_chains(eng, blocks):
             test_script_cases_single_calls(eng)
             test_crate_vectors(eng)
     finally:
-        eng.bcc_set_host_chain_blocks(0)
+        eng.bcc_set_host_chain_blocks(260)
         eng.bcc_set_host_bip143_blocks(32)
 
 
@@ -216,19 +243,11 @@ def _batch(eng, vs, flags=None):
     return rc, list(zip(ret, err))
 
 
-class Stats(ctypes.Structure):
-    _fields_ = [(k, ctypes.c_size_t) for k in ("items", "tuples", "rounds", "preimages",
-                                                "aux_messages", "host_rejected")] + [
-        (k, ctypes.c_double) for k in ("host_seconds", "gpu_seconds", "prepare_seconds",
-                                       "interpret_seconds", "merge_seconds", "stage_seconds",
-                                       "total_seconds")] + [("device_retries", ctypes.c_size_t),
-                                                             ("devices", ctypes.c_size_t),
-                                                             ("host_rounds", ctypes.c_size_t),
-                                                             ("host_hashed", ctypes.c_size_t)] + [
-        (k, ctypes.c_double) for k in ("shard_seconds", "stitch_seconds", "finish_seconds",
-                                       "host_jobs_seconds", "prepare_lag_seconds",
-                                       "prepare_parse_seconds", "prepare_hash_seconds")] + [
-        ("device_key_hashes", ctypes.c_size_t)]
+def Stats():
+    """The package's mirror of bcc_batch_stats (checked against the C layout by
+    tests/test_abi_symbols.py), so the engine never writes past a stale copy."""
+    import bitcoinconsensus_amd as B
+    return B.BatchStats()
 
 
 def test_device_failure_retried_once(eng):
