@@ -15,9 +15,9 @@ P3="SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU2 SQ_INST_CYCLES_VMEM_RD SQ_BUSY_CY
 i=0
 for P in "$P1" "$P2" "$P3"; do
   i=$((i+1))
-  timeout -s KILL 120 rocprofv3 --pmc $P -d $O/bench_p$i -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --no-cpu --no-extra --steps 1 --warmup 0 > /dev/null 2> $O/bench_p$i.err || { tail -5 $O/bench_p$i.err; exit 2; }
+  timeout -s KILL 120 rocprofv3 --pmc $P -d $O/bench_p$i -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --no-cpu --no-extra --sustain-s 0 --steps 1 --warmup 0 > /dev/null 2> $O/bench_p$i.err || { tail -5 $O/bench_p$i.err; exit 2; }
   timeout -s KILL 120 rocprofv3 --pmc $P -d $O/prim_p$i -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/tools/isa/prim_table.py $O/prim_p$i.json > /dev/null 2> $O/prim_p$i.err || { tail -5 $O/prim_p$i.err; exit 3; }
 done
-timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $O/trace -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --no-cpu --no-extra --steps 3 --warmup 1 > $O/bench_trace.json 2> $O/trace.err || { tail -5 $O/trace.err; exit 4; }
+timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $O/trace -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --no-cpu --no-extra --sustain-s 0 --steps 3 --warmup 1 > $O/bench_trace.json 2> $O/trace.err || { tail -5 $O/trace.err; exit 4; }
 cd $GRAFT_REPO_ROOT
 python3 tools/isa/pmc_summary.py $O > $O/summary.txt && cat $O/summary.txt

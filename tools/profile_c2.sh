@@ -6,7 +6,7 @@ T=${1:-r02x}; shift
 O=$GRAFT_REPO_ROOT/gpurun_out/$T
 mkdir -p $O/c2
 cd /tmp
-B="python3 $GRAFT_REPO_ROOT/bench.py --no-cpu --no-extra $*"
+B="python3 $GRAFT_REPO_ROOT/bench.py --no-cpu --no-extra --sustain-s 0 $*"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/c2/trace -o run --output-format csv -- $B --steps 5 --warmup 2 > $O/c2/bench_under_rocprof.json 2> $O/c2_trace.err || exit 1
 timeout -s KILL 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_INSTS_SALU SQ_WAVES GRBM_GUI_ACTIVE -d $O/c2/pmc_sq -o run --output-format csv -- $B --steps 1 --warmup 0 > /dev/null 2> $O/c2_sq.err || exit 4
 if [ "$FULL" = 1 ]; then

@@ -70,10 +70,14 @@ def main(d):
             out["bench_under_rocprof"] = json.loads(open(bench).read().strip().splitlines()[-1])
         except (ValueError, IndexError):
             pass
-    n_stage = 7 if "drop_in_end_to_end" in out.get("bench_under_rocprof", {}) else 4
+    n_default = 7 if "drop_in_end_to_end" in out.get("bench_under_rocprof", {}) else 4
     for st, ks in stages.items():
         if not any("fetch_size_launches" in K.get(k, {}) for k in ks):
             continue
+        # one launch of each stage kernel per execution (one lane chunk): the launch count is
+        # the execution count, whatever else the run did (a bench.py sustained window)
+        nl = {K[k]["fetch_size_launches"] for k in ks if "fetch_size_launches" in K.get(k, {})}
+        n_stage = nl.pop() if len(nl) == 1 else n_default
         fb = sum(K[k].get("fetch_size_bytes_total", 0) for k in ks if k in K) / n_stage
         wb = sum(K[k].get("write_size_bytes_total", 0) for k in ks if k in K) / n_stage
         out.setdefault("stages", {})[st] = dict(executions=n_stage, fetch_bytes=fb, fetch_bytes_x2=2 * fb,
