@@ -118,3 +118,39 @@ def test_scratch_oom_halves_the_chunk(c4):
     want = np.frombuffer(c4.verdicts(), np.uint8)[:n]
     got = np.frombuffer(v, np.uint8)
     assert (got == want).all(), np.nonzero(got != want)[0][:20]
+
+
+def test_c4_c5_bench_sizes_match_labels():
+    """BASELINE.json's full sizes through the bench's own staged path (one 16M-lane chunk): every
+    one of C4's 8M tuples and C5's 16M rows gets its construction label (the labels themselves are
+    pinned against the reference at 300k / 100k above), and a 200k random sample of each is
+    re-checked against the reference directly."""
+    import bitcoinconsensus_amd as B
+    rng = np.random.default_rng(44)
+    vec = [(t["sig"], t["msg"], t["pub"], t["verdict"]) for t in bip340_vectors()]
+    for kind, n, seed in (("c4", 8_000_000, 0x5EED0004), ("c5", 16_000_000, 0x5EED0005)):
+        ts = B.TupleSet(n, kind=kind, seed=seed, vectors=vec if kind == "c5" else ())
+        ts.run()
+        v = np.frombuffer(ts.verdicts(), np.uint8)
+        h = ts.host()
+        bad = np.nonzero(v != h["expect"])[0]
+        assert len(bad) == 0, (kind, bad[:20])
+        if reference_available():
+            idx = np.sort(rng.choice(n, 200_000, replace=False))
+            rows = lambda a, w: np.ascontiguousarray(np.asarray(a).reshape(-1, w)[idx]).ravel()  # noqa: E731
+            if kind == "c4":
+                def sub_blob(blob, off):
+                    parts = [bytes(blob[off[i]:off[i + 1]]) for i in idx]
+                    o = np.zeros(len(parts) + 1, np.uint64)
+                    o[1:] = np.cumsum([len(p) for p in parts])
+                    return np.frombuffer(b"".join(parts) + b"\0", np.uint8), o
+                pb, po = sub_blob(h["pub_blob"], h["pub_off"])
+                sb, so = sub_blob(h["sig_blob"], h["sig_off"])
+                ref, _ = Reference().pubkey_verify_blob(pb, po, rows(h["msg32"], 32), sb, so,
+                                                        threads=THREADS)
+            else:
+                ref, _ = Reference().schnorr_verify_rows(rows(h["sig64"], 64), rows(h["msg32"], 32),
+                                                         rows(h["xonly32"], 32), threads=THREADS)
+            got = v[idx]
+            assert np.array_equal(got, ref), (kind, np.nonzero(got != ref)[0][:20])
+        del ts
