@@ -195,6 +195,9 @@ typedef struct bcc_batch_stats {
     /* interpreter passes per shard: the slowest shard and the mean (summed over passes): their
      * ratio is the passes' load imbalance */
     double interpret_shard_max_seconds, interpret_shard_mean_seconds;
+    /* CPU time of the whole process (every thread) during the call, and during the caller's waits
+     * for device rounds: under a CFS quota the first bounds back-to-back calls */
+    double process_cpu_seconds, process_cpu_in_gpu_wait_seconds;
 } bcc_batch_stats;
 /* Statistics of the calling thread's last bitcoinconsensus_verify_batch / verify call. */
 void bcc_last_batch_stats(bcc_batch_stats* out);

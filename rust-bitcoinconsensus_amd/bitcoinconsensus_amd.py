@@ -213,7 +213,9 @@ class BatchStats(ctypes.Structure):
                 ("prepare_parse_seconds", ctypes.c_double), ("prepare_hash_seconds", ctypes.c_double),
                 ("device_key_hashes", ctypes.c_size_t),
                 ("interpret_shard_max_seconds", ctypes.c_double),
-                ("interpret_shard_mean_seconds", ctypes.c_double)]
+                ("interpret_shard_mean_seconds", ctypes.c_double),
+                ("process_cpu_seconds", ctypes.c_double),
+                ("process_cpu_in_gpu_wait_seconds", ctypes.c_double)]
 
 
 def _bind_consensus(L):

@@ -823,10 +823,16 @@ bool interpret_shard(BatchState& b, const std::vector<uint32_t>& idx, Round& rd)
 }
 
 // One device round over the parts [p0, p1): fault injection first, then the device pipeline.
-int device_round(int dev, const SighashJobs* const* pj, const TupleRows* const* pr, size_t P,
-                 uint8_t* verdict, double* stage_s, const LateMsgFill* late) {
+// A pending injected fault (bcc_debug_fail_device_rounds): its code, consumed; else 0.
+int take_injected_fault() {
     for (int f = g_fail_rounds.load(); f > 0;)
         if (g_fail_rounds.compare_exchange_weak(f, f - 1)) return g_fail_code.load();
+    return 0;
+}
+
+int device_round(int dev, const SighashJobs* const* pj, const TupleRows* const* pr, size_t P,
+                 uint8_t* verdict, double* stage_s, const LateMsgFill* late) {
+    if (int e = take_injected_fault()) return e;
     return gpu_verify_parts(dev, pj, pr, P, verdict, stage_s, late);
 }
 
@@ -871,6 +877,22 @@ namespace {
 // (gpu_verify_parts drops the failed one); *retries counts those.  If the device still cannot
 // deliver, the failure policy decides: the batch is verified on the host (*host_rounds counts
 // those) or the error is returned.  Returns 0 or the error.
+// The late rows of shards [g0, g1) of `rds` (batch-local), after the host jobs are hashed.
+void late_rows(const std::vector<Round>& rds, const std::vector<size_t>& row0, unsigned g0,
+               unsigned g1, std::vector<uint32_t>& rows, std::vector<uint8_t>& digs) {
+    for (unsigned t = g0; t < g1; t++) {
+        const Round& rd = rds[t];
+        const uint32_t base = (uint32_t)(row0[t] - row0[g0]);
+        auto put = [&](uint32_t r) {
+            rows.push_back(base + r);
+            const uint8_t* m = &rd.rows.msg[32 * (size_t)r];
+            digs.insert(digs.end(), m, m + 32);
+        };
+        for (const TplJob& tj : rd.host.tjobs) put(tj.row);
+        for (uint32_t r : rd.host.pre_row) put(r);
+    }
+}
+
 // `late` (optional): the group's offloaded host jobs are hashed during each device batch and their
 // rows' messages delivered through LateMsgFill.
 int run_device_group(int dev, const std::vector<Round>& rds, unsigned t0, unsigned t1,
@@ -904,17 +926,7 @@ int run_device_group(int dev, const std::vector<Round>& rds, unsigned t0, unsign
         // the late rows of shards [g0, g1), batch-local
         const LateMsgFill fill = [&, g0, g1](std::vector<uint32_t>& rows, std::vector<uint8_t>& digs) {
             late->ensure();
-            for (unsigned t = g0; t < g1; t++) {
-                const Round& rd = rds[t];
-                const uint32_t base = (uint32_t)(row0[t] - row0[g0]);
-                auto put = [&](uint32_t r) {
-                    rows.push_back(base + r);
-                    const uint8_t* m = &rd.rows.msg[32 * (size_t)r];
-                    digs.insert(digs.end(), m, m + 32);
-                };
-                for (const TplJob& tj : rd.host.tjobs) put(tj.row);
-                for (uint32_t r : rd.host.pre_row) put(r);
-            }
+            late_rows(rds, row0, g0, g1, rows, digs);
         };
         double st = 0;
         int e = 1;
@@ -1001,6 +1013,9 @@ struct ChunkRun {
     int sync_rc = 0;             // result of a synchronous device round
     double stage_s = 0;
     size_t devices_used = 0, retries = 0, host_rounds = 0;
+    // the first device round of a pipelined chunk, staged by the caller (prestage_round)
+    std::unique_ptr<StagedRound, void (*)(StagedRound*)> staged{nullptr, gpu_staged_free};
+    bool prestaged = false;
     LateHost late;               // offloaded host jobs of the current pass (hashed during the round)
     // their blocks (HostJobs::take); held by pointer so that ChunkRun stays movable
     std::unique_ptr<std::atomic<uint64_t>> host_planned = std::make_unique<std::atomic<uint64_t>>(0);
@@ -1013,6 +1028,12 @@ thread_local ChunkRun tl_chunk[2];
 
 using clk = std::chrono::steady_clock;
 inline double since(clk::time_point a) { return std::chrono::duration<double>(clk::now() - a).count(); }
+
+// CPU time of every thread of the process so far (bcc_batch_stats process_cpu_*)
+inline double process_cpu() {
+    timespec ts;
+    return clock_gettime(CLOCK_PROCESS_CPUTIME_ID, &ts) == 0 ? ts.tv_sec + 1e-9 * ts.tv_nsec : 0.0;
+}
 
 // One interpreter pass over the chunk's run lists; sets up the device round it needs (if any).
 void chunk_interpret(ChunkRun& c) {
@@ -1097,10 +1118,60 @@ void chunk_start(ChunkRun& c, const bcc_batch_item* items, size_t n, unsigned fl
     chunk_interpret(c);
 }
 
+// Pipelined chunks: the caller stages the chunk's first device round into the chunk's own device
+// batch with its whole team (the pinned image fill), so the pipeline worker only uploads, launches
+// and waits.  Staged on the worker instead, the fill ran on a few threads beside the next chunk's
+// host pass, which holds the CPU quota (stage 4.3 -> 7.4-9 ms per 1M inputs, profiles/r04/pipeline).
+// Single-GPU rounds that go to the device as one batch only; anything else keeps the general path.
+void prestage_round(ChunkRun& c) {
+    c.prestaged = false;
+    const std::vector<int> devs = device_list();
+    if (devs.size() != 1 || c.row0[c.T] <= host_small_round()) return;
+    size_t sz[5] = {0, 0, 0, 0, 0};
+    std::vector<const SighashJobs*> pj;
+    std::vector<const TupleRows*> pr;
+    for (unsigned t = 0; t < c.T; t++) {
+        const SighashJobs& j = c.rds[t].jobs;
+        const size_t add[5] = {j.aux.size(), j.pre.size(), j.tpl.size(), j.code.size(), j.txraw.size()};
+        for (int k = 0; k < 5; k++) sz[k] += add[k];
+        pj.push_back(&j);
+        pr.push_back(&c.rds[t].rows);
+    }
+    for (int k = 0; k < 5; k++)
+        if (sz[k] > ROUND_BLOB_LIMIT) return;
+    if (!c.staged) c.staged.reset(gpu_staged_new(devs[0]));
+    double st = 0;
+    set_stage_threads(cpu_share());  // a memory-bound fill: more threads than CPUs only add CPU time
+    const int e = gpu_staged_stage(c.staged.get(), pj.data(), pr.data(), pj.size(), &st);
+    set_stage_threads(0);
+    if (e != 0) return;
+    t_stats.stage_seconds += st;
+    c.prestaged = true;
+}
+
 // The chunk's pending device round (its arguments stay valid until the chunk's next pass).
 int chunk_device_round(ChunkRun& c) {
+    LateHost* late = c.late_pending ? &c.late : nullptr;
+    if (c.prestaged) {
+        c.prestaged = false;
+        int e = take_injected_fault();
+        if (!e) {
+            const LateMsgFill fill = [&](std::vector<uint32_t>& rows, std::vector<uint8_t>& digs) {
+                late->ensure();
+                late_rows(c.rds, c.row0, 0, c.T, rows, digs);
+            };
+            e = gpu_staged_run(c.staged.get(), c.verdict.data(), late ? &fill : nullptr);
+        }
+        if (e == 0) {
+            c.devices_used = std::max<size_t>(c.devices_used, 1);
+            return 0;
+        }
+        fprintf(stderr, "[bcc] verify_batch: staged device round failed (hip error %d): running it "
+                        "again through the general path\n", e);
+        c.retries++;
+    }
     return run_device_round(c.rds, c.T, c.row0, c.verdict.data(), &c.stage_s, &c.devices_used,
-                            &c.retries, &c.host_rounds, c.late_pending ? &c.late : nullptr);
+                            &c.retries, &c.host_rounds, late);
 }
 
 // Stitches a device round's verdicts into the items; the items whose speculation failed get
@@ -1136,6 +1207,7 @@ long chunk_finish(ChunkRun& c, int* ret_out, bitcoinconsensus_error* err_out, bo
     long status = 0;
     while (c.pending_round) {
         auto g0 = clk::now();
+        const double p0 = process_cpu();
         int e;
         if (c.fut.valid()) {
             e = c.fut.get();
@@ -1145,6 +1217,7 @@ long chunk_finish(ChunkRun& c, int* ret_out, bitcoinconsensus_error* err_out, bo
             e = chunk_device_round(c);
         }
         *gpu_s += since(g0);
+        t_stats.process_cpu_in_gpu_wait_seconds += process_cpu() - p0;
         t_stats.stage_seconds += c.stage_s;
         t_stats.device_retries += c.retries;
         t_stats.host_rounds += c.host_rounds;
@@ -1247,6 +1320,7 @@ long run_batch(const bcc_batch_item* items, size_t n, unsigned flags, int* ret_o
     t_stats.items = n;
     double gpu_s = 0;
     auto t0 = clk::now();
+    const double cpu0 = process_cpu();
     const size_t chunk = pipeline_chunk();
     long status = 0, valid = 0;
     auto account = [&](long r) {
@@ -1275,11 +1349,13 @@ long run_batch(const bcc_batch_item* items, size_t n, unsigned flags, int* ret_o
                 account(chunk_finish(*prev, ret_out + prev_lo, err_out ? err_out + prev_lo : nullptr,
                                      true, &gpu_s));
             }
-            if (c.pending_round)
+            if (c.pending_round) {
+                prestage_round(c);  // the pinned image filled here, with the caller's team
                 c.fut = run_async([&c] {
-                    set_stage_threads(PIPELINE_STAGE_THREADS);  // beside the host pass
+                    set_stage_threads(PIPELINE_STAGE_THREADS);  // re-runs stage beside the host pass
                     return chunk_device_round(c);
                 });
+            }
             prev = &c;
             prev_lo = cut[k];
         }
@@ -1290,6 +1366,7 @@ long run_batch(const bcc_batch_item* items, size_t n, unsigned flags, int* ret_o
     }
     t_stats.host_seconds = since(t0) - gpu_s;
     t_stats.gpu_seconds = gpu_s;
+    t_stats.process_cpu_seconds = process_cpu() - cpu0;
     return status < 0 ? -1 : valid;
 }
 

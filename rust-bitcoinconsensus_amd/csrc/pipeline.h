@@ -481,6 +481,19 @@ void release_tuple_thread_state();
 int gpu_verify_batch(int device, const SighashJobs& jobs, const TupleRows& rows, uint8_t* verdict,
                      double* stage_seconds = nullptr);
 // The same over the concatenation of `parts` (jobs[p], rows[p]) pairs: verdict rows in order.
+// A device round staged by one thread and run by another (the pipelined verify_batch: the caller
+// fills the pinned image with its whole team, the pipeline worker uploads, launches and waits).
+// The object keeps its device batch (arena, pinned image, scratch, streams) for reuse.
+struct StagedRound;
+StagedRound* gpu_staged_new(int device);
+void gpu_staged_free(StagedRound* s);
+// Fills s's pinned image from the parts (which must stay unchanged until gpu_staged_run returns).
+int gpu_staged_stage(StagedRound* s, const SighashJobs* const* jobs, const TupleRows* const* rows,
+                     size_t parts, double* stage_seconds);
+// Runs the staged round on the calling thread (any thread): verdict rows in order.  On an error
+// the batch is dropped (the next stage starts from a fresh one).
+int gpu_staged_run(StagedRound* s, uint8_t* verdict, const LateMsgFill* late);
+
 // `late` (optional): rows whose message the host delivers after the launches (LateMsgFill).
 int gpu_verify_parts(int device, const SighashJobs* const* jobs, const TupleRows* const* rows,
                      size_t parts, uint8_t* verdict, double* stage_seconds = nullptr,

@@ -1432,6 +1432,35 @@ int gpu_verify_parts(int device, const SighashJobs* const* jobs, const TupleRows
     return e;
 }
 
+struct StagedRound {
+    int dev;
+    std::unique_ptr<DeviceBatch> b;
+};
+
+StagedRound* gpu_staged_new(int device) { return new StagedRound{device, nullptr}; }
+void gpu_staged_free(StagedRound* s) { delete s; }
+
+int gpu_staged_stage(StagedRound* s, const SighashJobs* const* jobs, const TupleRows* const* rows,
+                     size_t parts, double* stage_seconds) {
+    if (s->dev < 0) return (int)hipErrorInvalidDevice;
+    BCC_HIP_TRY(hipSetDevice(s->dev));
+    if (!s->b) s->b = std::make_unique<DeviceBatch>(s->dev);
+    auto t0 = std::chrono::steady_clock::now();
+    int e = s->b->stage_parts(jobs, rows, parts);
+    if (!e && stage_seconds)
+        *stage_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (e) s->b.reset();
+    return e;
+}
+
+int gpu_staged_run(StagedRound* s, uint8_t* verdict, const LateMsgFill* late) {
+    if (!s->b) return (int)hipErrorInvalidValue;
+    int e = s->b->run(nullptr, late);
+    if (!e) e = s->b->fetch_verdicts(verdict);
+    if (e) s->b.reset();
+    return e;
+}
+
 // ------------------------------------------------------------------------------------------
 // BIP341 / BIP342 batch (host/taproot.cpp builds the jobs).
 void tapsighash_midstate(uint32_t out[8]) {

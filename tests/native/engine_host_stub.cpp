@@ -57,6 +57,25 @@ int gpu_verify_parts(int, const SighashJobs* const* jobs, const TupleRows* const
     return 0;
 }
 
+// The staged round: the parts are kept and evaluated when it runs (like the device's upload).
+struct StagedRound {
+    int dev;
+    std::vector<const SighashJobs*> jobs;
+    std::vector<const TupleRows*> rows;
+};
+StagedRound* gpu_staged_new(int device) { return new StagedRound{device, {}, {}}; }
+void gpu_staged_free(StagedRound* s) { delete s; }
+int gpu_staged_stage(StagedRound* s, const SighashJobs* const* jobs, const TupleRows* const* rows,
+                     size_t parts, double*) {
+    s->jobs.assign(jobs, jobs + parts);
+    s->rows.assign(rows, rows + parts);
+    return 0;
+}
+int gpu_staged_run(StagedRound* s, uint8_t* verdict, const LateMsgFill* late) {
+    return gpu_verify_parts(s->dev, s->jobs.data(), s->rows.data(), s->jobs.size(), verdict,
+                            nullptr, late);
+}
+
 // The sighash stage: msg rows (entering as rows.msg) overwritten by every job's digest.
 static void stub_sighash(const SighashJobs& j, std::vector<uint8_t>& msg) {
     std::vector<uint8_t> auxd(32 * j.aux_off.size());

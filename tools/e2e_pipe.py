@@ -26,6 +26,7 @@ def main():
             B.set_pipeline_chunk(ch)
             wl.verify_batch()  # this setting's state
             ms, best = [], None
+            c0 = time.process_time()  # CPU time of every thread of the process
             t0 = time.perf_counter()
             for _ in range(k):
                 t1 = time.perf_counter()
@@ -36,13 +37,16 @@ def main():
                     best = (dt1, B.last_batch_stats())
                 assert nv == n
             dt = time.perf_counter() - t0
+            cpu = time.process_time() - c0
             st = best[1]
             rec = dict(chunk=ch, rep=rep, calls=k, sustained_inputs_per_s=round(k * n / dt),
                        best_inputs_per_s=round(n / best[0]), call_ms_min=round(min(ms), 1),
                        call_ms_median=round(sorted(ms)[k // 2], 1),
                        best_breakdown_ms={x: round(st[x + "_seconds"] * 1e3, 2) for x in
                                           ("prepare", "interpret", "stitch", "finish", "stage",
-                                           "gpu", "host", "prepare_parse", "prepare_lag")},
+                                           "gpu", "host", "prepare_parse", "prepare_lag",
+                                           "process_cpu", "process_cpu_in_gpu_wait")},
+                       cpu_ms_per_call=round(1e3 * cpu / k, 1),
                        host_threads=B.host_threads(), cpu_share=B.cpu_share())
             print(json.dumps(rec), flush=True)
     B.set_pipeline_chunk(0)

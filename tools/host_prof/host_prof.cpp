@@ -33,6 +33,19 @@ int gpu_verify_parts(int, const SighashJobs* const*, const TupleRows* const* row
     memset(verdict, 1, n);
     return 0;
 }
+struct StagedRound {
+    std::vector<const TupleRows*> rows;
+};
+StagedRound* gpu_staged_new(int) { return new StagedRound{}; }
+void gpu_staged_free(StagedRound* s) { delete s; }
+int gpu_staged_stage(StagedRound* s, const SighashJobs* const*, const TupleRows* const* rows,
+                     size_t parts, double*) {
+    s->rows.assign(rows, rows + parts);
+    return 0;
+}
+int gpu_staged_run(StagedRound* s, uint8_t* verdict, const LateMsgFill* late) {
+    return gpu_verify_parts(0, nullptr, s->rows.data(), s->rows.size(), verdict, nullptr, late);
+}
 namespace host {
 void taproot_release_thread_state() {}  // taproot.cpp is not linked here
 }  // namespace host

@@ -44,6 +44,19 @@ int gpu_verify_batch(int d, const SighashJobs& j, const TupleRows& r, uint8_t* v
     const TupleRows* rp = &r;
     return gpu_verify_parts(d, &jp, &rp, 1, v, s);
 }
+struct StagedRound {
+    std::vector<const TupleRows*> rows;
+};
+StagedRound* gpu_staged_new(int) { return new StagedRound{}; }
+void gpu_staged_free(StagedRound* s) { delete s; }
+int gpu_staged_stage(StagedRound* s, const SighashJobs* const*, const TupleRows* const* rows,
+                     size_t parts, double*) {
+    s->rows.assign(rows, rows + parts);
+    return 0;
+}
+int gpu_staged_run(StagedRound* s, uint8_t* verdict, const LateMsgFill* late) {
+    return gpu_verify_parts(0, nullptr, s->rows.data(), s->rows.size(), verdict, nullptr, late);
+}
 int gpu_taproot_verify_parts(int, const TaprootJobs* const*, size_t, uint8_t*, uint8_t*) { return -1; }
 }  // namespace bcc
 
