@@ -1141,10 +1141,11 @@ void prestage_round(ChunkRun& c) {
         if (sz[k] > ROUND_BLOB_LIMIT) return;
     if (!c.staged) c.staged.reset(gpu_staged_new(devs[0]));
     double st = 0;
-    set_stage_threads(cpu_share());  // a memory-bound fill: more threads than CPUs only add CPU time
-    const int e = gpu_staged_stage(c.staged.get(), pj.data(), pr.data(), pj.size(), &st);
-    set_stage_threads(0);
-    if (e != 0) return;
+    struct StageThreads {  // a memory-bound fill: more threads than CPUs only add CPU time
+        StageThreads() { set_stage_threads(cpu_share()); }
+        ~StageThreads() { set_stage_threads(0); }
+    } share_threads;
+    if (gpu_staged_stage(c.staged.get(), pj.data(), pr.data(), pj.size(), &st) != 0) return;
     t_stats.stage_seconds += st;
     c.prestaged = true;
 }
