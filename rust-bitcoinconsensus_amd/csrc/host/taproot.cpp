@@ -42,6 +42,13 @@ struct Part {
 // job parts of the calling thread (run_range; released by bcc_release_thread_state)
 thread_local std::vector<Part> tl_parts;
 
+// A launched round of the pipelined run_range: its rows' items and the verdict / sighash buffers.
+struct RoundOut {
+    std::vector<uint32_t> item_of_row;
+    std::vector<uint8_t> verdict, msg;
+};
+thread_local RoundOut tl_round_out[2];
+
 // The parsed tx (and spent outputs) an adjacent run of items shares, and its TtxRec in the
 // current part.
 struct TxState {
@@ -193,11 +200,10 @@ void build_part(const bcc_taproot_check* items, size_t lo, size_t hi, int* ret, 
     }
 }
 
-// Items [lo, hi) on `device`: host parts in parallel, one GPU round, verdicts scattered back.
-// A round whose message blobs would not fit the kernels' 32-bit offsets is split in two.
-int run_range(const bcc_taproot_check* items, size_t lo, size_t hi, int* ret, int* serr,
-              unsigned char* sighash_out, int device) {
-    if (lo >= hi) return 0;
+// Builds the parts of items [lo, hi) in parallel on the calling thread's team (tl_parts).
+// Returns the number of parts, or 0 when the round's message blobs would not fit the kernels'
+// 32-bit offsets (the caller splits it).
+size_t build_round(const bcc_taproot_check* items, size_t lo, size_t hi, int* ret, int* serr) {
     // parts: contiguous item ranges, cut only between runs of the same tx
     const unsigned T = pool_threads(hi - lo, 2048);
     std::vector<size_t> cut{lo};
@@ -220,38 +226,108 @@ int run_range(const bcc_taproot_check* items, size_t lo, size_t hi, int* ret, in
         aux_b += parts[p].jobs.aux.size() + parts[p].jobs.dev.ext.size();
         msg_b += parts[p].jobs.msg.size() + parts[p].jobs.dev.txraw.size();
     }
-    if ((aux_b >= ((size_t)1 << 32) || msg_b >= ((size_t)1 << 32)) && hi - lo > 1) {
+    if (aux_b >= ((size_t)1 << 32) || msg_b >= ((size_t)1 << 32)) return 0;
+    return NP;
+}
+
+// Launches the round built in tl_parts (NP parts) on `slot`; its row -> item map goes to out.
+int launch_round(size_t NP, int device, int slot, RoundOut& out) {
+    std::vector<const TaprootJobs*> pj;
+    out.item_of_row.clear();
+    for (size_t p = 0; p < NP; p++) {
+        const Part& q = tl_parts[p];
+        pj.push_back(&q.jobs);
+        out.item_of_row.insert(out.item_of_row.end(), q.item_of_row.begin(), q.item_of_row.end());
+    }
+    return gpu_taproot_begin(device, slot, pj.data(), pj.size());
+}
+
+// Waits for the round on `slot` and writes its verdicts (and sighashes) to the items.
+int finish_round(int device, int slot, RoundOut& out, int* ret, int* serr,
+                 unsigned char* sighash_out) {
+    const size_t n = out.item_of_row.size();
+    if (n == 0) return 0;
+    out.verdict.resize(n);
+    out.msg.resize(sighash_out ? 32 * n : 0);
+    if (int e = gpu_taproot_end(device, slot, out.verdict.data(), sighash_out ? out.msg.data() : nullptr))
+        return e;
+    for (size_t r = 0; r < n; r++) {
+        const uint32_t i = out.item_of_row[r];
+        ret[i] = out.verdict[r] ? 1 : 0;
+        serr[i] = out.verdict[r] ? 0 : BCC_SCRIPT_ERR_SCHNORR_SIG;
+        if (sighash_out) memcpy(sighash_out + 32 * (size_t)i, &out.msg[32 * r], 32);
+    }
+    out.item_of_row.clear();
+    return 0;
+}
+
+// Items [lo, hi) on `device` as one GPU round: host parts in parallel, verdicts scattered back.
+// A round whose message blobs would not fit the kernels' 32-bit offsets is split in two.
+int run_range(const bcc_taproot_check* items, size_t lo, size_t hi, int* ret, int* serr,
+              unsigned char* sighash_out, int device) {
+    if (lo >= hi) return 0;
+    if (sighash_out)
+        for (size_t i = lo; i < hi; i++) memset(sighash_out + 32 * i, 0, 32);
+    const size_t NP = build_round(items, lo, hi, ret, serr);
+    if (NP == 0 && hi - lo > 1) {
         const size_t mid = lo + (hi - lo) / 2;
         if (int e = run_range(items, lo, mid, ret, serr, sighash_out, device)) return e;
         return run_range(items, mid, hi, ret, serr, sighash_out, device);
     }
-    std::vector<const TaprootJobs*> pj;
-    std::vector<uint32_t> item_of_row;
-    for (size_t p = 0; p < NP; p++) {
-        const Part& q = parts[p];
-        pj.push_back(&q.jobs);
-        item_of_row.insert(item_of_row.end(), q.item_of_row.begin(), q.item_of_row.end());
-    }
-    const size_t n = item_of_row.size();
+    RoundOut& out = tl_round_out[0];
+    if (int e = launch_round(NP, device, 0, out)) return e;
+    return finish_round(device, 0, out, ret, serr, sighash_out);
+}
+
+// Rounds of about PIPE_ROUND checks, pipelined (a batch of at least two): round k's host parts
+// are built while round k - 1 runs on the GPU, and round k's upload (on the other context's
+// stream) runs beside round k - 1's kernels.  One C5T round of 1M checks spent ≈6 ms building
+// parts, ≈6 ms uploading and ≈12 ms in kernels, back to back; pipelined in 131,072-check rounds
+// 1M checks take 16-19 ms (262,144: 19.5-20; 500,000: 18.4-18.5; profiles/r04/c5t).
+#ifndef BCC_TAPROOT_PIPE_ROUND
+#define BCC_TAPROOT_PIPE_ROUND 131072
+#endif
+constexpr size_t PIPE_ROUND = BCC_TAPROOT_PIPE_ROUND;
+
+int run_pipelined(const bcc_taproot_check* items, size_t lo, size_t hi, int* ret, int* serr,
+                  unsigned char* sighash_out, int device) {
+    if (hi - lo < 2 * PIPE_ROUND) return run_range(items, lo, hi, ret, serr, sighash_out, device);
     if (sighash_out)
         for (size_t i = lo; i < hi; i++) memset(sighash_out + 32 * i, 0, 32);
-    if (n == 0) return 0;
-    std::vector<uint8_t> verdict(n), msg(sighash_out ? 32 * n : 0);
-    if (int e = gpu_taproot_verify_parts(device, pj.data(), pj.size(), verdict.data(),
-                                         sighash_out ? msg.data() : nullptr))
-        return e;
-    for (size_t r = 0; r < n; r++) {
-        const uint32_t i = item_of_row[r];
-        ret[i] = verdict[r] ? 1 : 0;
-        serr[i] = verdict[r] ? 0 : BCC_SCRIPT_ERR_SCHNORR_SIG;
-        if (sighash_out) memcpy(sighash_out + 32 * (size_t)i, &msg[32 * r], 32);
+    std::vector<size_t> cut{lo};
+    while (cut.back() < hi) {
+        size_t c = std::min(hi, cut.back() + PIPE_ROUND);
+        while (c < hi && items[c].tx == items[c - 1].tx) c++;
+        cut.push_back(c);
     }
-    return 0;
+    int prev = -1;  // slot of the round in flight
+    int err = 0;
+    for (size_t k = 0; k + 1 < cut.size() && !err; k++) {
+        const int slot = (int)(k & 1);
+        const size_t NP = build_round(items, cut[k], cut[k + 1], ret, serr);
+        if (NP == 0) {  // too large for one launch: this round alone, unpipelined
+            if (prev >= 0) err = finish_round(device, prev, tl_round_out[prev], ret, serr, sighash_out);
+            prev = -1;
+            if (!err) err = run_range(items, cut[k], cut[k + 1], ret, serr, sighash_out, device);
+            continue;
+        }
+        err = launch_round(NP, device, slot, tl_round_out[slot]);
+        if (prev >= 0) {
+            const int e = finish_round(device, prev, tl_round_out[prev], ret, serr, sighash_out);
+            if (!err) err = e;
+        }
+        prev = err ? -1 : slot;
+    }
+    if (prev >= 0 && !err) err = finish_round(device, prev, tl_round_out[prev], ret, serr, sighash_out);
+    return err;
 }
 
 }  // namespace
 
-void taproot_release_thread_state() { std::vector<Part>().swap(tl_parts); }
+void taproot_release_thread_state() {
+    std::vector<Part>().swap(tl_parts);
+    for (auto& o : tl_round_out) o = RoundOut();
+}
 
 void taproot_dev_sigmsg_host(const TaprootTxJobs& D, uint8_t* msg) {
     static const uint8_t tag[10] = {'T', 'a', 'p', 'S', 'i', 'g', 'h', 'a', 's', 'h'};
@@ -343,8 +419,8 @@ extern "C" int bcc_taproot_verify_batch(const bcc_taproot_check* items, size_t n
         const int dev = devs[d];
         jobs.push_back([=] {
             for (size_t r = lo; r < hi; r += ROUND)
-                if (int e = bcc::host::run_range(items, r, std::min(hi, r + ROUND), ret_out,
-                                                 serror_out, sighash_out, dev))
+                if (int e = bcc::host::run_pipelined(items, r, std::min(hi, r + ROUND), ret_out,
+                                                     serror_out, sighash_out, dev))
                     return e;
             return 0;
         });

@@ -324,6 +324,12 @@ int gpu_taproot_verify(int device, const TaprootJobs& jobs, uint8_t* verdict, ui
 // The same over the concatenation of P parts (rows in part order).
 int gpu_taproot_verify_parts(int device, const TaprootJobs* const* parts, size_t P,
                              uint8_t* verdict, uint8_t* msg32_out);
+// The same in two phases on one of two contexts per (thread, device): begin stages, uploads and
+// launches on `slot`'s stream and returns; end waits for it and copies the verdicts (and, with
+// msg32_out, the sighashes) back.  The pipelined bcc_taproot_verify_batch alternates the slots, so
+// a round's upload runs beside the previous round's kernels.  Each begin is matched by an end.
+int gpu_taproot_begin(int device, int slot, const TaprootJobs* const* parts, size_t P);
+int gpu_taproot_end(int device, int slot, uint8_t* verdict, uint8_t* msg32_out);
 
 // Device scratch of the signature kernels: s^-1 rows (ECDSA) and, for one chunk of lanes, the
 // Q tables + ladder states.  Every synchronous entry point owns one per (thread, device), so

@@ -1482,6 +1482,7 @@ namespace {
 struct TaprootCtx {
     int dev = -1;
     hipStream_t stream = nullptr;
+    size_t n = 0, off_verdict = 0, off_msg = 0;  // the round launched by gpu_taproot_begin
     SigScratch sc;
     void* arena = nullptr;
     size_t cap = 0;
@@ -1504,16 +1505,24 @@ int gpu_taproot_verify(int device, const TaprootJobs& J, uint8_t* verdict, uint8
 
 // The parts (one per host thread) are concatenated straight into the pinned image, each part by
 // its own thread with its index fix-ups (no merged host copy), then go to HBM in one DMA copy.
-thread_local std::unique_ptr<TaprootCtx> tl_taproot_ctxs[64];
+// Per (thread, device) two contexts: the pipelined rounds of bcc_taproot_verify_batch alternate
+// between them, so one round's upload runs beside the previous round's kernels.
+thread_local std::unique_ptr<TaprootCtx> tl_taproot_ctxs[64][2];
 
 // Frees the calling thread's device batches and Taproot contexts (bcc_release_thread_state).
 void release_device_thread_state() {
     tl_batches.clear();
-    for (auto& c : tl_taproot_ctxs) c.reset();
+    for (auto& d : tl_taproot_ctxs)
+        for (auto& c : d) c.reset();
 }
 
 int gpu_taproot_verify_parts(int device, const TaprootJobs* const* Jp, size_t P, uint8_t* verdict,
                              uint8_t* msg32_out) {
+    if (int e = gpu_taproot_begin(device, 0, Jp, P)) return e;
+    return gpu_taproot_end(device, 0, verdict, msg32_out);
+}
+
+int gpu_taproot_begin(int device, int slot, const TaprootJobs* const* Jp, size_t P) {
     std::vector<size_t> row0(P + 1, 0), aux0(P + 1, 0), msg0(P + 1, 0), auxi0(P + 1, 0),
         msgi0(P + 1, 0), pat0(P + 1, 0), raw0(P + 1, 0), ttx0(P + 1, 0), tj0(P + 1, 0),
         ext0(P + 1, 0), in0(P + 1, 0);
@@ -1532,22 +1541,31 @@ int gpu_taproot_verify_parts(int device, const TaprootJobs* const* Jp, size_t P,
         in0[q + 1] = in0[q] + J.dev.in_entries;
     }
     const size_t n = row0[P];
-    if (n == 0) return 0;
-    if (device < 0 || device >= 64) return (int)hipErrorInvalidDevice;
+    if (device < 0 || device >= 64 || slot < 0 || slot > 1) return (int)hipErrorInvalidDevice;
+    if (n == 0) {
+        if (tl_taproot_ctxs[device][slot]) tl_taproot_ctxs[device][slot]->n = 0;
+        return 0;
+    }
     if (aux0[P] >= ((size_t)1 << 32) || msg0[P] >= ((size_t)1 << 32) || raw0[P] >= ((size_t)1 << 32) ||
         ext0[P] >= ((size_t)1 << 32)) {
         fprintf(stderr, "[bcc] gpu_taproot_verify: a message blob exceeds 4 GiB; split the batch\n");
         return (int)hipErrorInvalidValue;
     }
-    auto& ctxs = tl_taproot_ctxs;
-    if (!ctxs[device]) {
+    auto& slot_ctx = tl_taproot_ctxs[device][slot];
+    if (!slot_ctx) {
         auto c = std::make_unique<TaprootCtx>();
         c->dev = device;
         BCC_HIP_TRY(hipSetDevice(device));
         BCC_HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-        ctxs[device] = std::move(c);
+        slot_ctx = std::move(c);
     }
-    TaprootCtx& c = *ctxs[device];
+    TaprootCtx& c = *slot_ctx;
+    c.n = 0;
+    // this slot's previous round must be done with the arena and the pinned image
+    if (hipStreamSynchronize(c.stream) != hipSuccess) {
+        slot_ctx.reset();
+        return (int)hipErrorLaunchFailure;
+    }
     BCC_HIP_TRY(hipSetDevice(device));
     const size_t naux = auxi0[P], nmsg = msgi0[P], npat = pat0[P], nttx = ttx0[P], ntj = tj0[P];
     // layout: sig64 | pk32 | msg32 | verdict | aux | msg | aux_off | aux_nblk | msg_off |
@@ -1669,16 +1687,31 @@ int gpu_taproot_verify_parts(int device, const TaprootJobs* const* Jp, size_t P,
         BCC_HIP_TRY(hipGetLastError());
     }
     if (int e = schnorr_launch(c.sc, a + off[0], a + off[2], a + off[1], a + off[3], n, st)) {
-        ctxs[device].reset();
+        slot_ctx.reset();
         return e;
     }
+    c.n = n;
+    c.off_verdict = off[3];
+    c.off_msg = off[2];
+    return 0;
+}
+
+int gpu_taproot_end(int device, int slot, uint8_t* verdict, uint8_t* msg32_out) {
+    if (device < 0 || device >= 64 || slot < 0 || slot > 1) return (int)hipErrorInvalidDevice;
+    auto& slot_ctx = tl_taproot_ctxs[device][slot];
+    if (!slot_ctx || slot_ctx->n == 0) return 0;
+    TaprootCtx& c = *slot_ctx;
+    BCC_HIP_TRY(hipSetDevice(device));
+    const uint8_t* a = (const uint8_t*)c.arena;
+    const size_t n = c.n;
+    c.n = 0;
     int rc = 0;
-    if ((rc = (int)hipMemcpyAsync(verdict, a + off[3], n, hipMemcpyDeviceToHost, st)) ||
-        (msg32_out &&
-         (rc = (int)hipMemcpyAsync(msg32_out, a + off[2], 32 * n, hipMemcpyDeviceToHost, st))) ||
-        (rc = (int)hipStreamSynchronize(st))) {
+    if ((rc = (int)hipMemcpyAsync(verdict, a + c.off_verdict, n, hipMemcpyDeviceToHost, c.stream)) ||
+        (msg32_out && (rc = (int)hipMemcpyAsync(msg32_out, a + c.off_msg, 32 * n,
+                                                hipMemcpyDeviceToHost, c.stream))) ||
+        (rc = (int)hipStreamSynchronize(c.stream))) {
         fprintf(stderr, "[bcc] gpu_taproot_verify failed: %d\n", rc);
-        ctxs[device].reset();  // a retry starts from a fresh stream / arena / scratch
+        slot_ctx.reset();  // a retry starts from a fresh stream / arena / scratch
         return rc;
     }
     return 0;

@@ -146,6 +146,23 @@ int gpu_taproot_verify_parts(int dev, const TaprootJobs* const* parts, size_t P,
     return 0;
 }
 
+// The two-phase form: begin evaluates at once (the parts are rebuilt after it returns), end copies.
+static thread_local std::vector<uint8_t> tl_tap_verdict[2], tl_tap_msg[2];
+int gpu_taproot_begin(int dev, int slot, const TaprootJobs* const* parts, size_t P) {
+    size_t n = 0;
+    for (size_t q = 0; q < P; q++) n += parts[q]->rows();
+    tl_tap_verdict[slot].assign(n, 0);
+    tl_tap_msg[slot].assign(32 * n, 0);
+    return gpu_taproot_verify_parts(dev, parts, P, tl_tap_verdict[slot].data(), tl_tap_msg[slot].data());
+}
+int gpu_taproot_end(int, int slot, uint8_t* verdict, uint8_t* msg32_out) {
+    const size_t n = tl_tap_verdict[slot].size();
+    if (n) memcpy(verdict, tl_tap_verdict[slot].data(), n);
+    if (msg32_out && n) memcpy(msg32_out, tl_tap_msg[slot].data(), 32 * n);
+    tl_tap_verdict[slot].clear();
+    return 0;
+}
+
 int gpu_taproot_verify(int, const TaprootJobs& j, uint8_t* verdict, uint8_t* msg32_out) {
     std::vector<uint8_t> auxd(32 * j.aux_off.size());
     for (size_t a = 0; a < j.aux_off.size(); a++) {

@@ -75,3 +75,41 @@ def test_taproot_random_batch_vs_reference():
             bad.append((i, out[i], ret, serr))
     assert not bad, bad[:10]
     assert sum(o[0] == 1 for o in out) > 2000
+
+
+def test_taproot_pipelined_rounds_equal_single_rounds():
+    """A batch of at least two pipeline rounds (2 x 131,072 checks) runs as rounds alternating
+    between two device contexts (one round's upload beside the previous round's kernels): every
+    ret / serror / sighash equals the same checks run in single-round calls, the corrupted 5 % are
+    exactly the invalid ones, and a sample matches the reference."""
+    import ctypes
+    import numpy as np
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    n = 600_000
+    job = bench.C5T(B, n, 0x5EED0106, 0)
+    L = B.lib()
+    ret = np.zeros(n, np.int32)
+    err = np.zeros(n, np.int32)
+    hs = np.zeros((n, 32), np.uint8)
+    p32 = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_int))  # noqa: E731
+    assert L.bcc_taproot_verify_batch(job.arr, n, p32(ret), p32(err), hs.ctypes.data, 0) == 0
+    ret1 = np.zeros(n, np.int32)
+    err1 = np.zeros(n, np.int32)
+    hs1 = np.zeros((n, 32), np.uint8)
+    T = B.TaprootCheck
+    step = 100_000  # each call below two pipeline rounds: a single round
+    for lo in range(0, n, step):
+        m = min(step, n - lo)
+        arr = ctypes.cast(ctypes.addressof(job.arr) + lo * ctypes.sizeof(T), ctypes.POINTER(T))
+        assert L.bcc_taproot_verify_batch(arr, m, p32(ret1[lo:]), p32(err1[lo:]),
+                                          hs1[lo:].ctypes.data, 0) == 0
+    assert np.array_equal(ret, ret1) and np.array_equal(err, err1) and np.array_equal(hs, hs1)
+    assert int((ret == 1).sum()) == job.expect
+    assert np.array_equal(hs, job.hs)  # the sighashes the signatures were made over
+    if reference_available():
+        R = Reference()
+        for i in np.random.default_rng(5).choice(n, 300, replace=False):
+            r, e, h = R.taproot_check(bytes(job.tx[i]), bytes(job.spent[i]), 0, bytes(job.sig[i]),
+                                      bytes(job.xo[i]), 0)
+            assert (r, e) == (int(ret[i]), int(err[i])) and h == bytes(hs[i]), i
