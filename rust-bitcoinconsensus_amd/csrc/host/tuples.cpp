@@ -8,6 +8,7 @@
 #include <algorithm>
 #include <cstring>
 #include <thread>
+#include <memory>
 #include <vector>
 
 #include "bcc_amd.h"
@@ -75,7 +76,20 @@ void parse_rows(const uint8_t* pub_blob, const uint64_t* pub_off, const uint8_t*
 // fresh vectors on one thread before the parallel parse, and unmaps them afterwards.
 thread_local bcc::TupleRows tl_pubkey_rows;
 
-void release_pubkey_rows() { tl_pubkey_rows = bcc::TupleRows(); }
+// The pipelined form (tuple_rounds): two row sets and two staged device rounds per thread.
+struct TupleSlot {
+    bcc::TupleRows rows;
+    std::unique_ptr<bcc::StagedRound, void (*)(bcc::StagedRound*)> staged{nullptr,
+                                                                         bcc::gpu_staged_free};
+    int dev = -1;
+    size_t lo = 0, n = 0;  // the rows' range in the caller's arrays (n == 0: nothing in flight)
+};
+thread_local TupleSlot tl_tuple_slots[2];
+
+void release_pubkey_rows() {
+    tl_pubkey_rows = bcc::TupleRows();
+    for (auto& s : tl_tuple_slots) s = TupleSlot();
+}
 
 // One device round of rows (the tuple-level entry point's): the host lane code for a small round,
 // else the device with the engine's failure handling.
@@ -91,6 +105,50 @@ int tuple_round(int dev, const bcc::TupleRows& rows, uint8_t* verdict) {
     double st = 0;
     return resilient_round(dev, &jp, &rp, 1, verdict, &st, &retries, &host_rounds,
                            "pubkey_verify_batch");
+}
+
+// Rounds of about TUPLE_ROUND tuples, pipelined: round k's rows are parsed and staged on the
+// calling thread's team while round k - 1 runs, and round k's upload (its own device batch and
+// streams) runs beside round k - 1's kernels.  A staging or device error sends the round through
+// tuple_round (retry on a fresh batch, then the failure policy).
+constexpr size_t TUPLE_ROUND = (size_t)1 << 20;
+
+int tuple_rounds(int dev, const uint8_t* pub_blob, const uint64_t* pub_off, const uint8_t* msg32,
+                 const uint8_t* sig_blob, const uint64_t* sig_off, size_t n, uint8_t* verdict) {
+    auto finish = [&](TupleSlot& s) -> int {
+        if (s.n == 0) return 0;
+        const size_t lo = s.lo;
+        s.n = 0;
+        if (bcc::gpu_staged_finish(s.staged.get(), verdict + lo) == 0) return 0;
+        return tuple_round(dev, s.rows, verdict + lo);
+    };
+    int err = 0;
+    size_t k = 0;
+    for (size_t lo = 0; lo < n && !err; lo += TUPLE_ROUND, k++) {
+        TupleSlot& s = tl_tuple_slots[k & 1];
+        const size_t m = std::min(TUPLE_ROUND, n - lo);
+        if (int e = finish(s)) err = e;  // (only after an error) this slot's last round
+        parse_rows(pub_blob, pub_off + lo, msg32 + 32 * lo, sig_blob, sig_off + lo, m, s.rows);
+        if (!s.staged || s.dev != dev) {
+            s.staged.reset(bcc::gpu_staged_new(dev));
+            s.dev = dev;
+        }
+        const bcc::SighashJobs none;
+        const bcc::SighashJobs* jp = &none;
+        const bcc::TupleRows* rp = &s.rows;
+        double st = 0;
+        s.lo = lo;
+        s.n = m;
+        if (bcc::gpu_staged_stage(s.staged.get(), &jp, &rp, 1, &st) != 0 ||
+            bcc::gpu_staged_launch(s.staged.get(), nullptr) != 0) {
+            s.n = 0;
+            if (int e = tuple_round(dev, s.rows, verdict + lo)) err = e;
+        }
+        if (int e = finish(tl_tuple_slots[(k + 1) & 1])) err = err ? err : e;  // round k - 1
+    }
+    for (auto& s : tl_tuple_slots)
+        if (int e = finish(s)) err = err ? err : e;
+    return err;
 }
 
 }  // namespace host
@@ -109,6 +167,9 @@ extern "C" int bcc_pubkey_verify_batch(const uint8_t* pub_blob, const uint64_t* 
     for (size_t d = 0; d < D; d++) {
         const size_t lo = n * d / D, hi = n * (d + 1) / D;
         jobs.push_back([=] {  // contiguous equal range on devs[d] (offsets stay absolute)
+            if (hi - lo >= 2 * bcc::host::TUPLE_ROUND)
+                return bcc::host::tuple_rounds(devs[d], pub_blob, pub_off + lo, msg32 + 32 * lo,
+                                               sig_blob, sig_off + lo, hi - lo, verdict + lo);
             bcc::TupleRows& rows = bcc::host::tl_pubkey_rows;
             bcc::host::parse_rows(pub_blob, pub_off + lo, msg32 + 32 * lo, sig_blob, sig_off + lo,
                                   hi - lo, rows);

@@ -499,6 +499,10 @@ int gpu_staged_stage(StagedRound* s, const SighashJobs* const* jobs, const Tuple
 // Runs the staged round on the calling thread (any thread): verdict rows in order.  On an error
 // the batch is dropped (the next stage starts from a fresh one).
 int gpu_staged_run(StagedRound* s, uint8_t* verdict, const LateMsgFill* late);
+// The same in two phases: launch uploads and queues the kernels and returns; finish waits and
+// copies the verdicts.  Two staged rounds in flight overlap one's upload with the other's kernels.
+int gpu_staged_launch(StagedRound* s, const LateMsgFill* late);
+int gpu_staged_finish(StagedRound* s, uint8_t* verdict);
 
 // `late` (optional): rows whose message the host delivers after the launches (LateMsgFill).
 int gpu_verify_parts(int device, const SighashJobs* const* jobs, const TupleRows* const* rows,

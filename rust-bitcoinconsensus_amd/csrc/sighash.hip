@@ -1453,12 +1453,23 @@ int gpu_staged_stage(StagedRound* s, const SighashJobs* const* jobs, const Tuple
     return e;
 }
 
-int gpu_staged_run(StagedRound* s, uint8_t* verdict, const LateMsgFill* late) {
+int gpu_staged_launch(StagedRound* s, const LateMsgFill* late) {
     if (!s->b) return (int)hipErrorInvalidValue;
     int e = s->b->run(nullptr, late);
-    if (!e) e = s->b->fetch_verdicts(verdict);
     if (e) s->b.reset();
     return e;
+}
+
+int gpu_staged_finish(StagedRound* s, uint8_t* verdict) {
+    if (!s->b) return (int)hipErrorInvalidValue;
+    int e = s->b->fetch_verdicts(verdict);
+    if (e) s->b.reset();
+    return e;
+}
+
+int gpu_staged_run(StagedRound* s, uint8_t* verdict, const LateMsgFill* late) {
+    if (int e = gpu_staged_launch(s, late)) return e;
+    return gpu_staged_finish(s, verdict);
 }
 
 // ------------------------------------------------------------------------------------------

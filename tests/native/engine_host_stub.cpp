@@ -62,8 +62,9 @@ struct StagedRound {
     int dev;
     std::vector<const SighashJobs*> jobs;
     std::vector<const TupleRows*> rows;
+    std::vector<uint8_t> verdicts;  // gpu_staged_launch's
 };
-StagedRound* gpu_staged_new(int device) { return new StagedRound{device, {}, {}}; }
+StagedRound* gpu_staged_new(int device) { return new StagedRound{device, {}, {}, {}}; }
 void gpu_staged_free(StagedRound* s) { delete s; }
 int gpu_staged_stage(StagedRound* s, const SighashJobs* const* jobs, const TupleRows* const* rows,
                      size_t parts, double*) {
@@ -74,6 +75,18 @@ int gpu_staged_stage(StagedRound* s, const SighashJobs* const* jobs, const Tuple
 int gpu_staged_run(StagedRound* s, uint8_t* verdict, const LateMsgFill* late) {
     return gpu_verify_parts(s->dev, s->jobs.data(), s->rows.data(), s->jobs.size(), verdict,
                             nullptr, late);
+}
+// launch evaluates at once (the caller may rebuild its rows afterwards), finish copies
+int gpu_staged_launch(StagedRound* s, const LateMsgFill* late) {
+    size_t n = 0;
+    for (const TupleRows* r : s->rows) n += r->size();
+    std::vector<uint8_t>& v = s->verdicts;
+    v.assign(n, 0);
+    return gpu_staged_run(s, v.data(), late);
+}
+int gpu_staged_finish(StagedRound* s, uint8_t* verdict) {
+    if (!s->verdicts.empty()) memcpy(verdict, s->verdicts.data(), s->verdicts.size());
+    return 0;
 }
 
 // The sighash stage: msg rows (entering as rows.msg) overwritten by every job's digest.

@@ -135,6 +135,17 @@ def test_c4_c5_bench_sizes_match_labels():
         h = ts.host()
         bad = np.nonzero(v != h["expect"])[0]
         assert len(bad) == 0, (kind, bad[:20])
+        if kind == "c4":  # the same 8M through the host-buffer entry point (pipelined rounds)
+            import ctypes
+            L = ctypes.CDLL(B.lib()._name)  # own handle: argtypes of its own
+            u64p, vp = ctypes.POINTER(ctypes.c_uint64), ctypes.c_void_p
+            f = L.bcc_pubkey_verify_batch
+            f.argtypes = [vp, u64p, vp, vp, u64p, vp, ctypes.c_size_t, ctypes.c_int]
+            out = np.zeros(n, np.uint8)
+            assert f(h["pub_blob"].ctypes.data, h["pub_off"].ctypes.data_as(u64p),
+                     h["msg32"].ctypes.data, h["sig_blob"].ctypes.data,
+                     h["sig_off"].ctypes.data_as(u64p), out.ctypes.data, n, 0) == 0
+            assert np.array_equal(out, v)
         if reference_available():
             idx = np.sort(rng.choice(n, 200_000, replace=False))
             rows = lambda a, w: np.ascontiguousarray(np.asarray(a).reshape(-1, w)[idx]).ravel()  # noqa: E731

@@ -57,6 +57,10 @@ int gpu_staged_stage(StagedRound* s, const SighashJobs* const*, const TupleRows*
 int gpu_staged_run(StagedRound* s, uint8_t* verdict, const LateMsgFill* late) {
     return gpu_verify_parts(0, nullptr, s->rows.data(), s->rows.size(), verdict, nullptr, late);
 }
+int gpu_staged_launch(StagedRound*, const LateMsgFill*) { return 0; }
+int gpu_staged_finish(StagedRound* s, uint8_t* verdict) {
+    return gpu_staged_run(s, verdict, nullptr);
+}
 int gpu_taproot_verify_parts(int, const TaprootJobs* const*, size_t, uint8_t*, uint8_t*) { return -1; }
 }  // namespace bcc
 
