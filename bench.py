@@ -49,7 +49,7 @@ SEEDS = {"c2": 0x5EED0001, "c3": 0x5EED0003, "c4": 0x5EED0004, "c5": 0x5EED0005,
 # the ECDSA stage's kernels (the square-root-free twist path)
 ECDSA_KERNELS = ("ecdsa (batch_sinv + twist_keyq + twist_ladder_g + twist_fin<ecdsa>; "
                  "no key square root)")
-SCHNORR_KERNELS = ("schnorr (schnorr_tprep + twist_ladder<bip340> + twist_fin<bip340>; "
+SCHNORR_KERNELS = ("schnorr (schnorr_tladder: prep + ladder fused, + twist_fin<bip340>; "
                    "no lift_x square root)")
 CPU_PASSES = 3                    # timed passes of the CPU baseline (median), after 1 warm-up
 

@@ -9,7 +9,8 @@
 //                                   comb from HBM tables), alpha / beta / K of the x-test
 //   K_tfin    twist_fin_kernel      batched beta^-1, "gamma = -alpha / beta is the key's y",
 //                                   exact fallback for the exceptional lanes
-// BIP340 runs the same three kernels (schnorr_tprep_kernel, twist_*_kernel<true>).  (The round-1
+// BIP340 runs one fused prep + ladder launch (schnorr_tladder_kernel, round 4) and
+// twist_fin_kernel<true>.  (The round-1
 // path -- key decompression by a square root, G tables in LDS -- was retired in round 4.)
 // K_inv needs only the s rows: DeviceBatch::run launches it on a side stream beside the sighash
 // kernels.  Prep and ladder are separate launches so that each gets its own register allocation
@@ -293,34 +294,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
     tw_store(w, T_Y, st.ychk.v);
 }
 
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void schnorr_tprep_kernel(
-    const uint8_t* __restrict__ psig, const uint8_t* __restrict__ pm,
-    const uint8_t* __restrict__ ppk, size_t base, size_t cnt, u32* __restrict__ qtab,
-    u32* __restrict__ state) {
-    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= cnt) return;
-    const size_t i = base + t;
-    fe px, rx;
-    sc s, m;
-    load_be32(rx, psig + 64 * i);
-    load_be32(s, psig + 64 * i + 32);
-    load_be32(m, pm + 32 * i);
-    load_be32(px, ppk + 32 * i);
-    QTableGlobal qt{lane_table(qtab, t)};
-    TwistState st;
-    schnorr_twist_prep(px, rx, s, m, qt, st);
-    u32* w = lane_words(state, t, TSTATE_WORDS);
-#pragma unroll
-    for (int a = 0; a < 4; a++)
-#pragma unroll
-        for (int b = 0; b < 4; b++) w[(T_K + a * 4 + b) * LANE_STRIDE] = st.k[a][b];
-    w[T_FLAGS * LANE_STRIDE] = st.flags;
-    tw_store(w, T_SIGMA, st.sigma.v);
-    tw_store(w, T_R, st.r.v);
-    tw_store(w, T_V, st.v.v);
-    tw_store(w, T_Y, st.ychk.v);
-}
-
 // Ladder workgroups of 256 lanes: no LDS (the comb tables are read from HBM / L2), so the only
 // occupancy limit is the register file (4 waves per SIMD at <= 128 VGPRs).
 #ifndef BCC_TLADDER_WG
@@ -389,6 +362,53 @@ __global__ __launch_bounds__(TLADDER_WG) __attribute__((amdgpu_waves_per_eu(BCC_
     u32* lt = lane_table(qtab, t);
     twist_q_part(lt, st);
     twist_g_part<BIP340>(w, lt, gcomb, st);
+}
+
+// BIP340 in one launch per chunk (round 4, as K_keyq fuses the ECDSA key half): each lane runs
+// the prep (key without a square root, e = H(r || P || m), the co-Z P_w table, the GLV split) and
+// then the ladder (twist_ladder_kernel<true>'s body) on its own table and state words, so the
+// prep's instructions fill the ladder's 4-wave SIMDs; as its own 3-wave launch (round 3's
+// schnorr_tprep_kernel) it cost 14.2 of 149.6 ms per 16M rows.  Fused: C5 106.1-106.4 ->
+// 110.9-111.8 M verifies/s in an interleaved A/B (profiles/r04/schnorr_fused).
+__global__ __launch_bounds__(TLADDER_WG) __attribute__((amdgpu_waves_per_eu(BCC_LADDER_WAVES, BCC_LADDER_WAVES))) void schnorr_tladder_kernel(
+    const uint8_t* __restrict__ psig, const uint8_t* __restrict__ pm,
+    const uint8_t* __restrict__ ppk, size_t base, size_t cnt, u32* __restrict__ qtab,
+    u32* __restrict__ state, const u32* __restrict__ gcomb) {
+    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= cnt) return;
+    const size_t i = base + t;
+    u32* w = lane_words(state, t, TSTATE_WORDS);
+    u32* lt = lane_table(qtab, t);
+    {
+        fe px, rx;
+        sc s, m;
+        load_be32(rx, psig + 64 * i);
+        load_be32(s, psig + 64 * i + 32);
+        load_be32(m, pm + 32 * i);
+        load_be32(px, ppk + 32 * i);
+        QTableGlobal qt{lt};
+        TwistState st;
+        schnorr_twist_prep(px, rx, s, m, qt, st);
+#pragma unroll
+        for (int a = 0; a < 4; a++)
+#pragma unroll
+            for (int b = 0; b < 4; b++) w[(T_K + a * 4 + b) * LANE_STRIDE] = st.k[a][b];
+        w[T_FLAGS * LANE_STRIDE] = st.flags;
+        tw_store(w, T_SIGMA, st.sigma.v);
+        tw_store(w, T_R, st.r.v);
+        tw_store(w, T_V, st.v.v);
+        tw_store(w, T_Y, st.ychk.v);
+    }
+    TwistStateView sv;
+    sv.p = w;
+    sv.flags = w[T_FLAGS * LANE_STRIDE];
+    if (!(sv.flags & LS_VALID)) {
+        w[T_STAT * LANE_STRIDE] = TW_REJECT;
+        return;
+    }
+    tw_load(sv.sigma.v, w, T_SIGMA);
+    twist_q_part(lt, sv);
+    twist_g_part<true>(w, lt, gcomb, sv);
 }
 
 // The ECDSA ladder in two launches (ecdsa_launch_q / ecdsa_launch_after_pre): the Q half needs
@@ -841,12 +861,9 @@ int schnorr_launch(SigScratch& sc, const uint8_t* d_sig64, const uint8_t* d_msg3
     u32* state = qtab + C * QTABLE_WORDS;
     for (size_t base = 0; base < n; base += C) {
         const size_t cnt = std::min(C, n - base);
-        hipLaunchKernelGGL(schnorr_tprep_kernel, dim3((unsigned)((cnt + 255) / 256)), dim3(256),
-                           0, sm, d_sig64, d_msg32, d_xonly32, base, cnt, qtab, state);
-        BCC_HIP_TRY(hipGetLastError());
-        hipLaunchKernelGGL(twist_ladder_kernel<true>,
-                           dim3((unsigned)((cnt + TLADDER_WG - 1) / TLADDER_WG)),
-                           dim3(TLADDER_WG), 0, sm, state, qtab, gcomb, cnt);
+        hipLaunchKernelGGL(schnorr_tladder_kernel,
+                           dim3((unsigned)((cnt + TLADDER_WG - 1) / TLADDER_WG)), dim3(TLADDER_WG),
+                           0, sm, d_sig64, d_msg32, d_xonly32, base, cnt, qtab, state, gcomb);
         BCC_HIP_TRY(hipGetLastError());
         const size_t T = std::max<size_t>((cnt + FIN_PER_THREAD - 1) / FIN_PER_THREAD, std::min<size_t>(cnt, (size_t)cus * 256));
         hipLaunchKernelGGL(twist_fin_kernel<true>, dim3((unsigned)((T + 255) / 256)), dim3(256), 0,

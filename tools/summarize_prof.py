@@ -61,7 +61,7 @@ def main(d):
     stages = {"ecdsa": ["batch_sinv_kernel", "ecdsa_tprep_kernel", "twist_keyq_kernel",
                         "twist_ladder_g_kernel", "void twist_ladder_kernel<false>",
                         "void twist_fin_kernel<false>"],
-              "schnorr": ["schnorr_tprep_kernel", "void twist_ladder_kernel<true>",
+              "schnorr": ["schnorr_tladder_kernel", "schnorr_tprep_kernel", "void twist_ladder_kernel<true>",
                           "void twist_fin_kernel<true>"]}
     K = out["kernels"]
     bench = os.path.join(d, "bench_under_rocprof.json")
