@@ -838,6 +838,8 @@ int device_round(int dev, const SighashJobs* const* pj, const TupleRows* const* 
 
 }  // namespace
 
+int injected_device_fault() { return take_injected_fault(); }
+
 int resilient_round(int dev, const SighashJobs* const* pj, const TupleRows* const* pr, size_t P,
                     uint8_t* verdict, double* stage_s, size_t* retries, size_t* host_rounds,
                     const char* who, const LateMsgFill* late) {

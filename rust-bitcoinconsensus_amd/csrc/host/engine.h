@@ -41,6 +41,10 @@ size_t build_sighash_checks(const SighashCheck* checks, size_t n, SighashJobs& j
 void append_round(SighashJobs& dst, TupleRows& dst_rows, const SighashJobs& src,
                   const TupleRows& src_rows);
 
+// A pending bcc_debug_fail_device_rounds fault, consumed (its HIP error code), else 0: the staged
+// rounds (tuples.cpp) take it as a failed staging, as device_round does for a failed round.
+int injected_device_fault();
+
 // One device round of P parts on `dev` with the engine's failure handling: one retry on a fresh
 // device batch for a transient HIP error (*retries), then the device failure policy: the parts are
 // verified on the host CPU (*host_rounds, bcc_host_fallback_rounds) or the error is returned.

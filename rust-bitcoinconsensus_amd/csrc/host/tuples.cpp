@@ -139,7 +139,8 @@ int tuple_rounds(int dev, const uint8_t* pub_blob, const uint64_t* pub_off, cons
         double st = 0;
         s.lo = lo;
         s.n = m;
-        if (bcc::gpu_staged_stage(s.staged.get(), &jp, &rp, 1, &st) != 0 ||
+        if (injected_device_fault() != 0 ||
+            bcc::gpu_staged_stage(s.staged.get(), &jp, &rp, 1, &st) != 0 ||
             bcc::gpu_staged_launch(s.staged.get(), nullptr) != 0) {
             s.n = 0;
             if (int e = tuple_round(dev, s.rows, verdict + lo)) err = e;

@@ -120,6 +120,48 @@ def test_scratch_oom_halves_the_chunk(c4):
     assert (got == want).all(), np.nonzero(got != want)[0][:20]
 
 
+def test_pipelined_tuple_round_failure():
+    """bcc_pubkey_verify_batch's pipelined rounds (at least 2M tuples, tuples.cpp tuple_rounds): a
+    staged round that fails (an injected transient device fault) is re-run through the
+    single-round path on a fresh batch -- same verdicts, rc 0, no host fallback (the autouse
+    fixture); under BCC_DEVICE_FAILURE_ERROR three faults (the staged round, its re-run and the
+    retry) make the call return the error instead of a verdict."""
+    import ctypes
+    import bitcoinconsensus_amd as B
+    n = 2_300_000
+    ts = B.TupleSet(n, kind="c4", seed=0x5EED0014)
+    h = ts.host()
+    L = ctypes.CDLL(B.lib()._name)  # own handle: argtypes of its own
+    u64p, vp = ctypes.POINTER(ctypes.c_uint64), ctypes.c_void_p
+    f = L.bcc_pubkey_verify_batch
+    f.argtypes = [vp, u64p, vp, vp, u64p, vp, ctypes.c_size_t, ctypes.c_int]
+
+    def call():
+        out = np.zeros(n, np.uint8)
+        rc = f(h["pub_blob"].ctypes.data, h["pub_off"].ctypes.data_as(u64p), h["msg32"].ctypes.data,
+               h["sig_blob"].ctypes.data, h["sig_off"].ctypes.data_as(u64p), out.ctypes.data, n, 0)
+        return rc, out
+
+    B.debug_fail_device_rounds(1)
+    try:
+        rc, out = call()
+    finally:
+        B.debug_fail_device_rounds(0)
+    assert rc == 0
+    bad = np.nonzero(out != h["expect"])[0]
+    assert len(bad) == 0, bad[:20]
+    B.set_device_failure_policy(B.DEVICE_FAILURE_ERROR)
+    B.debug_fail_device_rounds(3)
+    try:
+        rc, _ = call()
+    finally:
+        B.debug_fail_device_rounds(0)
+        B.set_device_failure_policy(B.DEVICE_FAILURE_HOST)
+    assert rc != 0
+    rc, out = call()  # and the next call is whole again
+    assert rc == 0 and np.array_equal(out, h["expect"])
+
+
 def test_c4_c5_bench_sizes_match_labels():
     """BASELINE.json's full sizes through the bench's own staged path (one 16M-lane chunk): every
     one of C4's 8M tuples and C5's 16M rows gets its construction label (the labels themselves are
