@@ -1330,6 +1330,25 @@ long run_batch(const bcc_batch_item* items, size_t n, unsigned flags, int* ret_o
         if (r < 0) status = -1;
         else valid += r;
     };
+    // On every exit, exceptions included: no chunk slot of this thread may keep a device round in
+    // flight (the worker would go on writing the slot's rounds and verdicts while the next call
+    // reuses it, and that call's chunk_finish would take the stale future), nor a pending or
+    // prestaged round of this call.
+    struct DrainSlots {
+        ~DrainSlots() {
+            for (auto& c : tl_chunk) {
+                if (c.fut.valid()) {
+                    try {
+                        c.fut.get();
+                    } catch (...) {
+                    }
+                }
+                c.pending_round = false;
+                c.prestaged = false;
+                c.late_pending = false;
+            }
+        }
+    } drain;
     if (chunk == 0 || n < 2 * chunk) {
         ChunkRun& c = tl_chunk[0];
         chunk_start(c, items, n, flags);

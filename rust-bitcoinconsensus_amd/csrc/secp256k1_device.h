@@ -185,7 +185,16 @@ BCC_HD void fe_reduce512(fe& r, const u32 (&t)[16]) {
 // the 977-products chained through their high words, two carry chains for the rest; 4.4 % fewer
 // VALU instructions in the ladder than the round-1 reduction, profiles/r02tw4/ab_summary.txt);
 // host builds use 4 x 64-bit limbs (below) or the portable formulation above.  All compute the
-// same weak residue class.
+// same weak residue class.  Round 5: fe_reduce512_v4 (fe_asm.h: one multiply-add per limb pair,
+// one carry chain, the rare carries behind a wave-uniform branch); BCC_RED_V4=0 keeps v3.
+#ifndef BCC_RED_V4
+#define BCC_RED_V4 1
+#endif
+#if BCC_RED_V4
+#define BCC_FE_REDUCE fe_reduce512_v4
+#else
+#define BCC_FE_REDUCE fe_reduce512_v3
+#endif
 
 #if !defined(__HIP_DEVICE_COMPILE__) && defined(__SIZEOF_INT128__)
 // Host builds (the engine's host verification, host_verify.cpp, and tests/native): 4 x 64-bit limbs
@@ -252,7 +261,7 @@ BCC_HD void fe_mul(fe& r, const fe& a, const fe& b) {
     u32 t[16];
 #if defined(__HIP_DEVICE_COMPILE__)
     mul_256x256_col(t, a.v, b.v);
-    fe_reduce512_v3(r.v, t);
+    BCC_FE_REDUCE(r.v, t);
 #else
     mul_256x256(t, a.v, b.v);
     fe_reduce512(r, t);
@@ -267,7 +276,7 @@ BCC_HD void fe_sqr(fe& r, const fe& a) {
     u32 t[16];
 #if defined(__HIP_DEVICE_COMPILE__)
     sqr_256_col(t, a.v);
-    fe_reduce512_v3(r.v, t);
+    BCC_FE_REDUCE(r.v, t);
 #else
     sqr_256(t, a.v);
     fe_reduce512(r, t);

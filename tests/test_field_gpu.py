@@ -42,6 +42,17 @@ def operand_pairs(seed=7, nrand=6000):
         pairs.append((rng.getrandbits(256), rng.getrandbits(256)))
     for _ in range(500):  # both operands in [p, 2^256): double wrap-around territory
         pairs.append((P + rng.randrange(2**256 - P), P + rng.randrange(2**256 - P)))
+    # limbs drawn from {0, 1, 2^32 - 1, 2^32 - 2, p's low limb, random}: products whose high
+    # limbs sit at 2^32 - 1 take every rare carry of fe_reduce512_v4 (the D_k carries, the chain's
+    # carry out of limb 8, the top fold's carries; about 15 % of these lanes in a Python model of
+    # the reduction), mixed into waves with lanes that must pass through the rare branch unchanged
+    pick = [0, 1, 2**32 - 1, 2**32 - 2, 0xFFFFFC2F, None, None]
+
+    def limbmix():
+        return sum((rng.getrandbits(32) if (c := rng.choice(pick)) is None else c) << (32 * i)
+                   for i in range(8))
+    for _ in range(20000):
+        pairs.append((limbmix(), limbmix()))
     return pairs
 
 
