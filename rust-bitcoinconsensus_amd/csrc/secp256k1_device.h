@@ -195,6 +195,12 @@ BCC_HD void fe_reduce512(fe& r, const u32 (&t)[16]) {
 #else
 #define BCC_FE_REDUCE fe_reduce512_v3
 #endif
+// Round 5: the product columns' first multiply-adds unguarded, their rare carries flagged
+// (fe_asm_gen.h mul_256x256_col_f / sqr_cross_col_f); a wave with a flagged lane redoes the product
+// with the exact columns.  BCC_MUL_FLAG=0 keeps the exact columns only.
+#ifndef BCC_MUL_FLAG
+#define BCC_MUL_FLAG 1
+#endif
 
 #if !defined(__HIP_DEVICE_COMPILE__) && defined(__SIZEOF_INT128__)
 // Host builds (the engine's host verification, host_verify.cpp, and tests/native): 4 x 64-bit limbs
@@ -260,7 +266,13 @@ BCC_HD void fe_mul(fe& r, const fe& a, const fe& b) {
 #else
     u32 t[16];
 #if defined(__HIP_DEVICE_COMPILE__)
+#if BCC_MUL_FLAG
+    uint64_t ovf;
+    mul_256x256_col_f(t, a.v, b.v, ovf);
+    if (__builtin_expect(ovf != 0, 0)) mul_256x256_col(t, a.v, b.v);
+#else
     mul_256x256_col(t, a.v, b.v);
+#endif
     BCC_FE_REDUCE(r.v, t);
 #else
     mul_256x256(t, a.v, b.v);
@@ -275,7 +287,15 @@ BCC_HD void fe_sqr(fe& r, const fe& a) {
 #else
     u32 t[16];
 #if defined(__HIP_DEVICE_COMPILE__)
+#if BCC_MUL_FLAG
+    uint64_t ovf;
+    u32 x[16];
+    sqr_cross_col_f(x, a.v, ovf);
+    if (__builtin_expect(ovf != 0, 0)) sqr_256_col(t, a.v);
+    else sqr_tail_col(t, x, a.v);
+#else
     sqr_256_col(t, a.v);
+#endif
     BCC_FE_REDUCE(r.v, t);
 #else
     sqr_256(t, a.v);
