@@ -130,14 +130,23 @@ int bcc_set_pipeline_chunk(size_t items);
 
 /* Legacy signature checks whose serial SHA-256 chain is longer than `blocks` 64-byte blocks (the
  * preimages of many-input transactions) are hashed on the host CPU instead of in one GPU lane each,
- * while the device round's message-independent kernels run (BCC_HOST_CHAIN_BLOCKS; default 260,
- * about the Q ladder's latency in GPU-lane blocks; 0: every legacy chain on the GPU).  Single-GPU
+ * while the device round's message-independent kernels run (BCC_HOST_CHAIN_BLOCKS; default 160,
+ * below the Q ladder's latency in GPU-lane blocks; 0: every legacy chain on the GPU).  A long
+ * transaction template carries its SHA-256 midstates, so a check's chain counts only the blocks
+ * from its own input's script on (host and GPU start from the midstate alike).  Single-GPU
  * rounds only, at most 2^19 blocks per interpreter pass.  BIP143 checks of a tx whose
  * per-tx chains (hashPrevouts / hashSequence / hashOutputs) exceed BCC_HOST_BIP143_BLOCKS (default
  * 32) blocks are hashed on the host (linear in the tx).  Results never depend on either. */
 int bcc_set_host_chain_blocks(unsigned blocks);
 /* The BIP143 threshold above (BCC_HOST_BIP143_BLOCKS; default 32; 0: every BIP143 chain on the GPU). */
 int bcc_set_host_bip143_blocks(unsigned blocks);
+
+/* Early Q halves (BCC_EARLY_Q; default 1): a verify_batch call that goes to one GPU as one chunk
+ * (at most 2^18 inputs) pre-extracts the (key, signature) pairs of its standard spends after
+ * deserialization and runs their key half and Q ladder on the GPU while the host interprets; the
+ * interpreter's deferred checks with the same key and signature bytes reuse them.  0 disables it.
+ * Results never depend on it. */
+int bcc_set_early_q(int on);
 
 /* Key-hash spends (P2WPKH, and P2PKH scriptPubKeys): on an input's first interpreter run the
  * HASH160(pubkey) == program comparison of OP_EQUALVERIFY is checked on the device beside the
@@ -198,6 +207,10 @@ typedef struct bcc_batch_stats {
     /* CPU time of the whole process (every thread) during the call, and during the caller's waits
      * for device rounds: under a CFS quota the first bounds back-to-back calls */
     double process_cpu_seconds, process_cpu_in_gpu_wait_seconds;
+    /* early Q halves (bcc_set_early_q): pre-extracted rows whose key half and Q ladder ran on the
+     * GPU during the host pass, the deferred rows mapped to them, and the extraction + launch time */
+    size_t early_rows, early_mapped;
+    double early_seconds;
 } bcc_batch_stats;
 /* Statistics of the calling thread's last bitcoinconsensus_verify_batch / verify call. */
 void bcc_last_batch_stats(bcc_batch_stats* out);

@@ -215,7 +215,9 @@ class BatchStats(ctypes.Structure):
                 ("interpret_shard_max_seconds", ctypes.c_double),
                 ("interpret_shard_mean_seconds", ctypes.c_double),
                 ("process_cpu_seconds", ctypes.c_double),
-                ("process_cpu_in_gpu_wait_seconds", ctypes.c_double)]
+                ("process_cpu_in_gpu_wait_seconds", ctypes.c_double),
+                ("early_rows", ctypes.c_size_t), ("early_mapped", ctypes.c_size_t),
+                ("early_seconds", ctypes.c_double)]
 
 
 def _bind_consensus(L):
@@ -462,9 +464,21 @@ def cpu_share():
     return L.bcc_cpu_share()
 
 
+def set_early_q(on):
+    """bcc_set_early_q: pre-extracted (key, signature) rows run their Q half on the GPU during the
+    host pass of a single-chunk verify_batch call (default on)."""
+    L = lib()
+    L.bcc_set_early_q.argtypes = [ctypes.c_int]
+    L.bcc_set_early_q(1 if on else 0)
+
+
+HOST_CHAIN_BLOCKS_DEFAULT = 160  # engine.cpp g_host_chain_blocks
+
+
 def set_host_chain_blocks(blocks):
-    """bcc_set_host_chain_blocks: legacy checks whose SHA-256 chain exceeds `blocks` blocks are
-    hashed on the host CPU (0, the default: every legacy chain on the GPU)."""
+    """bcc_set_host_chain_blocks: legacy checks that hash more than `blocks` blocks from their
+    template midstate are hashed on the host CPU during the device round (default
+    HOST_CHAIN_BLOCKS_DEFAULT; 0: every legacy chain on the GPU)."""
     L = lib()
     L.bcc_set_host_chain_blocks.argtypes = [ctypes.c_uint]
     L.bcc_set_host_chain_blocks(blocks)

@@ -261,6 +261,51 @@ BCC_HD bool twist_accumulate_q(const ST& st, const QT& qt, gej& acc) {
     return inf;
 }
 
+// One GLV half of B (round 5, the latency mode of small rounds): slot 0 accumulates k1 Q over the
+// table's (x, y), slot 1 k2 lambda Q over its (beta x, y), each with its own 124 doublings and
+// odd-fix correction, so two lanes run the halves side by side and B = B_0 + B_1
+// (twist_keyq2_kernel).  The same digits and additions as twist_accumulate_q's slot.  Returns inf.
+template <class ST, class QT>
+BCC_HD bool twist_accumulate_q_half(const ST& st, const QT& qt, gej& acc, int slot) {
+    const bool kneg = (st.flags & (slot == 0 ? LS_NEG0 : LS_NEG1)) != 0;
+    const fe one = fe_one();
+    bool inf = false;
+    {
+        bool ng;
+        const u32 idx = digit_index(st.kword(slot, 0), st.kword(slot, 1), st.kword(slot, 2),
+                                    st.kword(slot, 3), TOPQ, WQ, TOPQ, ng);
+        qt.get_pair((int)idx, slot, acc.x, acc.y);
+        if (kneg) fe_neg(acc.y, acc.y);
+        acc.z = one;
+    }
+#pragma unroll 1
+    for (int pos = TOPQ; pos >= -1; pos--) {
+        if (pos >= 0 && pos != TOPQ && !inf) {
+            gej t;
+            gej_double(t, acc);
+            acc = t;
+        }
+        if (pos >= 0 && ((pos % WQ) != 0 || pos == TOPQ)) continue;
+        u32 idx;
+        bool sneg;
+        if (pos >= 0) {
+            bool dneg;
+            idx = digit_index(st.kword(slot, 0), st.kword(slot, 1), st.kword(slot, 2),
+                              st.kword(slot, 3), pos, WQ, TOPQ, dneg);
+            sneg = dneg ^ kneg;
+        } else {
+            if (!(st.flags & (LS_CORR0 << slot))) continue;  // per lane
+            idx = 0;
+            sneg = !kneg;
+        }
+        fe px, py;
+        qt.get_pair((int)idx, slot, px, py);
+        if (sneg) fe_neg(py, py);
+        acc_add(acc, inf, px, py, one, false);
+    }
+    return inf;
+}
+
 // A = u1 G on E by the fixed-base comb: one addition per window, no doublings.  Returns inf.
 template <class ST, class GC>
 BCC_HD bool twist_accumulate_g(const ST& st, const GC& gc, gej& acc) {

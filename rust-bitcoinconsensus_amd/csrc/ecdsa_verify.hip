@@ -425,9 +425,11 @@ __global__ __launch_bounds__(TLADDER_WG) __attribute__((amdgpu_waves_per_eu(BCC_
 __global__ __launch_bounds__(TLADDER_WG) __attribute__((amdgpu_waves_per_eu(BCC_LADDERQ_WAVES, BCC_LADDERQ_WAVES))) void twist_keyq_kernel(
     const uint8_t* __restrict__ tag, const uint8_t* __restrict__ px, const uint8_t* __restrict__ py,
     const uint8_t* __restrict__ pr, const uint8_t* __restrict__ ps, const u32* __restrict__ psinv,
-    size_t cnt, u32* __restrict__ qtab, u32* __restrict__ state) {
+    size_t cnt, u32* __restrict__ qtab, u32* __restrict__ state, const u32* __restrict__ emap,
+    size_t ecount) {
     const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= cnt) return;
+    if (emap && emap[t] < ecount) return;  // an early twin's result is copied (keyq_copy_kernel)
     u32* w = lane_words(state, t, TSTATE_WORDS);
     u32* lt = lane_table(qtab, t);
     {
@@ -463,6 +465,119 @@ __global__ __launch_bounds__(TLADDER_WG) __attribute__((amdgpu_waves_per_eu(BCC_
     sv.flags = w[T_FLAGS * LANE_STRIDE];
     tw_load(sv.sigma.v, w, T_SIGMA);
     twist_q_part(lt, sv);
+}
+
+// K_keyq's latency mode (round 5) for rounds of at most one wave per SIMD, where each verify's
+// single-lane chain sets the round's length (C3: K_keyq ~0.93 ms beside a ~0.6 ms sighash front):
+// two lanes per tuple.  Both parse the key and build the Q table (in their own areas of qtab2),
+// lane 2t + h accumulates GLV half h (twist_accumulate_q_half: the 124 doublings, half the
+// additions), lane 2t + 1 hands its point to lane 2t (cross-lane shuffles) and lane 2t parks
+// B = B_0 + B_1 (the exceptional sums exact, gej_add_gej) and writes the tuple's state words as
+// K_keyq does.  ~0.77x the chain of one lane, ~1.08x its instructions.
+struct HalfK {  // twist_accumulate_q_half's view of one slot's k words (kword(slot, w) for its slot)
+    u32 flags;
+    u32 k[4];
+    __device__ __forceinline__ u32 kword(int, int w) const { return k[w]; }
+};
+__device__ __forceinline__ void shfl_fe_xor1(fe& a) {
+#pragma unroll
+    for (int k = 0; k < 8; k++) a.v[k] = (u32)__shfl_xor((int)a.v[k], 1);
+}
+__global__ __launch_bounds__(TLADDER_WG) __attribute__((amdgpu_waves_per_eu(1, 2))) void twist_keyq2_kernel(
+    const uint8_t* __restrict__ tag, const uint8_t* __restrict__ px, const uint8_t* __restrict__ py,
+    const uint8_t* __restrict__ pr, const uint8_t* __restrict__ ps, const u32* __restrict__ psinv,
+    size_t cnt, u32* __restrict__ qtab, u32* __restrict__ qtab2, u32* __restrict__ state,
+    const u32* __restrict__ emap, size_t ecount) {
+    const size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const size_t t = g >> 1;
+    const int h = (int)(g & 1);
+    // a pair's lanes stay together through the shuffles: a lane past the end (or an early twin's
+    // pair) runs nothing, and so does its partner
+    const bool live = t < cnt && !(emap && emap[t] < ecount);
+    u32* lt2 = lane_table(qtab2, g);
+    TwistState st;
+    bool ok = false;
+    if (live) {
+        fe x, y;
+        load_be32(x, px + 32 * t);
+        load_be32(y, py + 32 * t);
+        QTableGlobal qt{lt2};
+        ok = twist_prep_key(tag[t], x, y, qt, st);
+        if (ok) {
+            sc r, s, si;
+            load_be32(r, pr + 32 * t);
+            load_be32(s, ps + 32 * t);
+            load_limbs(si, psinv + 8 * t);
+            ok = twist_prep_u2(st.flags, r, s, &si, st);
+        }
+    }
+    u32* w = live ? lane_words(state, t, TSTATE_WORDS) : nullptr;
+    if (live && h == 0) {
+        if (!ok) {
+            w[T_FLAGS * LANE_STRIDE] = 0u;  // K_tladder_g writes the status
+        } else {
+            tw_store(w, T_SIGMA, st.sigma.v);
+            tw_store(w, T_V, st.v.v);
+            tw_store(w, T_Y, st.ychk.v);
+#pragma unroll
+            for (int a = 0; a < 2; a++)
+#pragma unroll
+                for (int b = 0; b < 4; b++) w[(T_K + a * 4 + b) * LANE_STRIDE] = st.k[a][b];
+            w[T_FLAGS * LANE_STRIDE] = st.flags;
+            tw_store(w, T_R, st.r.v);
+        }
+    }
+    gej B;
+    bool binf = true;
+    if (live && ok) {
+        HalfK hk;  // this lane's half of the scalar words, in registers
+        hk.flags = st.flags;
+#pragma unroll
+        for (int b = 0; b < 4; b++) hk.k[b] = h ? st.k[1][b] : st.k[0][b];
+        binf = twist_accumulate_q_half(hk, QTableGlobal{lt2}, B, h);
+    }
+    // lane 2t + 1 -> lane 2t (every lane takes part: the partner's values arrive in lockstep)
+    gej B1 = B;
+    shfl_fe_xor1(B1.x);
+    shfl_fe_xor1(B1.y);
+    shfl_fe_xor1(B1.z);
+    const bool b1inf = __shfl_xor(binf ? 1 : 0, 1) != 0;
+    if (!(live && ok && h == 0)) return;
+    gej S;
+    bool sinf;
+    if (binf) {
+        S = B1;
+        sinf = b1inf;
+    } else if (b1inf) {
+        S = B;
+        sinf = false;
+    } else {
+        gej_add_gej(S, sinf, B, B1);
+    }
+    park_gej(lane_table(qtab, t) + PARK_B, S, sinf);
+}
+
+// Early Q halves (round 5, DeviceBatch::early_launch): a row whose (key, signature) bytes equal an
+// early row's takes that lane's K_keyq output -- the state words K_keyq writes (the k1 / k2 words,
+// flags, sigma, r, v, y: words [T_K, T_Y + 8)) and the parked B -- instead of recomputing it.
+constexpr int KEYQ_STATE_WORDS = T_Y + 8;
+constexpr int PARK_WORDS = 28;
+__global__ __launch_bounds__(256) void keyq_copy_kernel(const u32* __restrict__ emap, size_t cnt,
+                                                        size_t ecount, const u32* __restrict__ estate,
+                                                        const u32* __restrict__ eqtab,
+                                                        u32* __restrict__ state, u32* __restrict__ qtab) {
+    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= cnt) return;
+    const u32 e = emap[t];
+    if (e >= ecount) return;
+    const u32* src = lane_words(estate, e, TSTATE_WORDS);
+    u32* dst = lane_words(state, t, TSTATE_WORDS);
+#pragma unroll 7
+    for (int k = 0; k < KEYQ_STATE_WORDS; k++) dst[k * LANE_STRIDE] = src[k * LANE_STRIDE];
+    const uint4* ps = reinterpret_cast<const uint4*>(eqtab + (size_t)e * QTABLE_WORDS + PARK_B);
+    uint4* pd = reinterpret_cast<uint4*>(qtab + t * QTABLE_WORDS + PARK_B);
+#pragma unroll
+    for (int k = 0; k < PARK_WORDS / 4; k++) pd[k] = ps[k];
 }
 
 // The G half keeps the combine's temporaries live beside the comb accumulator: at four waves
@@ -640,12 +755,13 @@ static int device_tables(int* dev, const u32** gcomb, int* cus) {
 }
 
 SigScratch::~SigScratch() {
-    if (dev >= 0 && (sinv || chunk)) {
+    if (dev >= 0 && (sinv || chunk || qtab2)) {
         int cur = 0;
         (void)hipGetDevice(&cur);
         (void)hipSetDevice(dev);
         if (sinv) (void)hipFree(sinv);
         if (chunk) (void)hipFree(chunk);
+        if (qtab2) (void)hipFree(qtab2);
         (void)hipSetDevice(cur);
     }
 }
@@ -750,18 +866,51 @@ int ecdsa_launch_key(SigScratch& sc, const uint8_t* d_tag, const uint8_t* d_x,
 // CU's 160 KiB LDS (unused): the sighash kernels' groups (8.4 KB of LDS each) go to other CUs.
 constexpr size_t KEYQ_EXCLUSIVE_LDS = 152 * 1024;
 
-static size_t keyq_lds(size_t groups, int cus) {
-    static const bool ok = [] {
-        if (hipFuncSetAttribute((const void*)&twist_keyq_kernel,
-                                hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)KEYQ_EXCLUSIVE_LDS) == hipSuccess)
-            return true;
-        (void)hipGetLastError();
-        fprintf(stderr, "[bcc] K_keyq: no %zu-byte LDS reservation on this device; small rounds "
-                        "share CUs with the sighash kernels\n", KEYQ_EXCLUSIVE_LDS);
-        return false;
-    }();
-    return ok && groups <= (size_t)cus ? KEYQ_EXCLUSIVE_LDS : 0;
+static bool reserve_lds(const void* kernel, const char* name) {
+    const hipError_t e = hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                             (int)KEYQ_EXCLUSIVE_LDS);
+    if (e == hipSuccess) return true;
+    (void)hipGetLastError();
+    fprintf(stderr, "[bcc] %s: no %zu-byte LDS reservation on this device (%s); small rounds "
+                    "share CUs with the sighash kernels\n", name, KEYQ_EXCLUSIVE_LDS, hipGetErrorString(e));
+    return false;
+}
+
+static size_t keyq_lds(size_t groups, int cus, bool two_lane = false) {
+    static const bool ok1 = reserve_lds((const void*)&twist_keyq_kernel, "K_keyq");
+    static const bool ok2 = reserve_lds((const void*)&twist_keyq2_kernel, "K_keyq2");
+    return (two_lane ? ok2 : ok1) && groups <= (size_t)cus ? KEYQ_EXCLUSIVE_LDS : 0;
+}
+
+// K_keyq or, for a round of at most one wave per SIMD at two lanes per tuple, its latency mode
+// (twist_keyq2_kernel; BCC_KEYQ2=0 keeps K_keyq).
+static const bool g_keyq2 = [] {
+    const char* e = getenv("BCC_KEYQ2");
+    return !(e && atoi(e) == 0);
+}();
+static int launch_keyq(SigScratch& sc, int cus, const uint8_t* d_tag, const uint8_t* d_x,
+                       const uint8_t* d_y, const uint8_t* d_r, const uint8_t* d_s, size_t n,
+                       u32* qtab, u32* state, const u32* emap, size_t ecount, hipStream_t st) {
+    if (g_keyq2 && 2 * n <= (size_t)cus * 4 * 64) {
+        if (2 * n > sc.qtab2_cap) {
+            if (sc.qtab2) BCC_HIP_TRY(hipFree(sc.qtab2));
+            sc.qtab2 = nullptr;
+            sc.qtab2_cap = 0;
+            const size_t lanes = (2 * n + 255) & ~(size_t)255;
+            BCC_HIP_TRY(hipMalloc(&sc.qtab2, lanes * QTABLE_WORDS * sizeof(u32)));
+            sc.qtab2_cap = lanes;
+        }
+        const size_t groups = (2 * n + TLADDER_WG - 1) / TLADDER_WG;
+        hipLaunchKernelGGL(twist_keyq2_kernel, dim3((unsigned)groups), dim3(TLADDER_WG),
+                           (unsigned)keyq_lds(groups, cus, true), st, d_tag, d_x, d_y, d_r, d_s,
+                           (const u32*)sc.sinv, n, qtab, (u32*)sc.qtab2, state, emap, ecount);
+        return (int)hipGetLastError();
+    }
+    const size_t groups = (n + TLADDER_WG - 1) / TLADDER_WG;
+    hipLaunchKernelGGL(twist_keyq_kernel, dim3((unsigned)groups), dim3(TLADDER_WG),
+                       (unsigned)keyq_lds(groups, cus), st, d_tag, d_x, d_y, d_r, d_s,
+                       (const u32*)sc.sinv, n, qtab, state, emap, ecount);
+    return (int)hipGetLastError();
 }
 
 int ecdsa_launch_q(SigScratch& sc, const uint8_t* d_tag, const uint8_t* d_x, const uint8_t* d_y,
@@ -776,11 +925,39 @@ int ecdsa_launch_q(SigScratch& sc, const uint8_t* d_tag, const uint8_t* d_x, con
     if (n > C) return 0;
     u32* qtab = (u32*)sc.chunk;
     u32* state = qtab + C * QTABLE_WORDS;
-    const size_t groups = (n + TLADDER_WG - 1) / TLADDER_WG;
-    hipLaunchKernelGGL(twist_keyq_kernel, dim3((unsigned)groups), dim3(TLADDER_WG),
-                       (unsigned)keyq_lds(groups, cus), (hipStream_t)stream, d_tag, d_x, d_y, d_r,
-                       d_s, (const u32*)sc.sinv, n, qtab, state);
+    if (int e = launch_keyq(sc, cus, d_tag, d_x, d_y, d_r, d_s, n, qtab, state, nullptr, 0,
+                            (hipStream_t)stream))
+        return e;
+    sc.q_ready = n;
+    return 0;
+}
+
+int ecdsa_launch_q_mapped(SigScratch& sc, const SigScratch& early, size_t early_n,
+                          const uint32_t* d_emap, const uint8_t* d_tag, const uint8_t* d_x,
+                          const uint8_t* d_y, const uint8_t* d_r, const uint8_t* d_s, size_t n,
+                          void* stream) {
+    if (!d_emap || early_n == 0 || !early.chunk)
+        return ecdsa_launch_q(sc, d_tag, d_x, d_y, d_r, d_s, n, stream);
+    sc.q_ready = 0;
+    if (n == 0 || sc.key_ready != n || n > chunk_lanes()) return 0;
+    int dev = 0, cus = 0;
+    const u32* gcomb = nullptr;
+    size_t C = 0;
+    if (int e = device_tables(&dev, &gcomb, &cus)) return e;
+    if (int e = ensure_scratch(sc, dev, n, true, &C)) return e;
+    if (n > C) return 0;
+    const size_t eC = std::min(chunk_lanes(), (early_n + 255) & ~(size_t)255);
+    if (early.dev != dev || early_n > early.chunk_cap || eC > early.chunk_cap) return 0;  // cannot map: full K_keyq
+    u32* qtab = (u32*)sc.chunk;
+    u32* state = qtab + C * QTABLE_WORDS;
+    const u32* eqtab = (const u32*)early.chunk;
+    const u32* estate = eqtab + eC * QTABLE_WORDS;
+    hipLaunchKernelGGL(keyq_copy_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                       (hipStream_t)stream, d_emap, n, early_n, estate, eqtab, state, qtab);
     BCC_HIP_TRY(hipGetLastError());
+    if (int e = launch_keyq(sc, cus, d_tag, d_x, d_y, d_r, d_s, n, qtab, state, d_emap, early_n,
+                            (hipStream_t)stream))
+        return e;
     sc.q_ready = n;
     return 0;
 }

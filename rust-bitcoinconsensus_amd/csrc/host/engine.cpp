@@ -129,11 +129,13 @@ struct HostJobs {
     }
 };
 
-// Default 260: a GPU lane hashes ~4 us a block, so a chain above ~250 blocks outlasts the device
-// round's Q ladder (~0.9 ms for a small round) and would set the round's length.
+// A GPU lane hashes ~4 us a block, so a chain of more than ~200 blocks outlasts the device round's
+// Q ladder (~0.9 ms for a small round) and would set the round's length.  Since round 5 the
+// threshold applies to the blocks a job hashes from its template midstate (TPL_MID), i.e. only the
+// first inputs of a many-input tx go to the host, at about half their former cost.
 std::atomic<uint32_t> g_host_chain_blocks{[] {
     const char* e = getenv("BCC_HOST_CHAIN_BLOCKS");
-    return e ? (uint32_t)atoi(e) : 260u;
+    return e ? (uint32_t)atoi(e) : 160u;
 }()};
 
 // BIP143 checks of a tx whose hashPrevouts / hashSequence / hashOutputs chains exceed this many
@@ -177,7 +179,136 @@ struct Item {
     const uint8_t* h160_src = nullptr;
     uint32_t h160_len = 0;
     uint8_t h160[20];
+    // early Q halves: this item's pre-extracted (key, signature) candidates in its shard's
+    // EarlyShard::cands [ec_first, ec_first + ec_count)
+    uint32_t ec_first = 0, ec_count = 0;
 };
+
+// Early Q halves (round 5).  A check's tuple row depends only on the bytes of its key and its
+// signature, and K_keyq (the key half, u2 = r s^-1 and B = u2 Q) only on the row, so the rows of
+// the standard spends (P2WPKH, P2PKH, P2SH-P2WPKH, P2SH multisig candidate pairs, P2PK) are
+// pre-extracted right after deserialization and their K_keyq runs on the GPU while the host
+// interprets (DeviceBatch::early_launch).  A row the interpreter defers with exactly those key and
+// signature bytes is mapped to its early twin (TupleRows::emap), whose result K_keyq copies; the
+// match is by bytes, so a pattern that guessed wrong only wastes an early lane.
+struct EarlyCand {
+    const uint8_t* pub;
+    const uint8_t* sig;
+    uint32_t publen, siglen;
+    uint32_t row;  // in the shard's early rows
+};
+struct EarlyShard {
+    TupleRows rows;
+    std::vector<EarlyCand> cands;
+    void clear() {
+        rows.clear();
+        rows.msg_one = true;
+        rows.y_unused = true;
+        cands.clear();
+    }
+};
+
+std::atomic<int> g_early_q{[] {
+    const char* e = getenv("BCC_EARLY_Q");
+    return e ? atoi(e) : 1;
+}()};
+constexpr size_t EARLY_MAX_ITEMS = (size_t)1 << 18;
+
+// CPubKey size filter, non-empty signature, lax DER (sans the hash-type byte), r != 0, s != 0: the
+// host half of a deferred check (Round::defer); false = rejected on the host, no row.
+bool tuple_fields(const uint8_t* pub, size_t pl, const uint8_t* sig, size_t sl, uint8_t r[32],
+                  uint8_t s[32]) {
+    if (!pubkey_size_valid(pub, pl) || sl == 0 || !der_parse_lax(sig, sl - 1, r, s)) return false;
+    uint64_t rw[4], sw[4];
+    memcpy(rw, r, 32);
+    memcpy(sw, s, 32);
+    // secp256k1_ecdsa_sig_verify rejects r == 0 || s == 0
+    return (rw[0] | rw[1] | rw[2] | rw[3]) != 0 && (sw[0] | sw[1] | sw[2] | sw[3]) != 0;
+}
+
+// The pushes of a push-only script (OP_0, direct pushes, PUSHDATA1 / 2), at most `cap`; -1 on any
+// other opcode, a truncated push or more pushes.
+int script_pushes(const Span& sc, Span* out, int cap) {
+    const uint8_t* p = sc.p;
+    const size_t n = sc.n;
+    int k = 0;
+    size_t i = 0;
+    while (i < n) {
+        const uint8_t op = p[i++];
+        size_t len;
+        if (op <= 75) {
+            len = op;
+        } else if (op == 0x4c) {
+            if (i >= n) return -1;
+            len = p[i++];
+        } else if (op == 0x4d) {
+            if (i + 2 > n) return -1;
+            len = p[i] | ((size_t)p[i + 1] << 8);
+            i += 2;
+        } else {
+            return -1;
+        }
+        if (i + len > n || k >= cap) return -1;
+        out[k].p = p + i;
+        out[k].n = len;
+        k++;
+        i += len;
+    }
+    return k;
+}
+
+// The item's candidate (key, signature) pairs by the shape of its spent script and its input.
+void early_extract_item(Item& it, EarlyShard& es) {
+    it.ec_first = (uint32_t)es.cands.size();
+    it.ec_count = 0;
+    const bcc_batch_item* in = it.in;
+    const uint8_t* spk = in->script_pubkey;
+    const size_t L = in->script_pubkey_len;
+    if (!spk) return;
+    const TxIn& txin = it.tx->tx.vin[in->n_in];
+    auto add = [&](const Span& pub, const Span& sig) {
+        uint8_t r[32], s[32];
+        if (!tuple_fields(pub.p, pub.n, sig.p, sig.n, r, s)) return;
+        const bool k65 = pub.n == 65;
+        const uint32_t row = es.rows.add_lazy(pub.p[0], pub.p + 1, r, s, k65 ? pub.p + 33 : nullptr, nullptr);
+        if (k65) es.rows.y_unused = false;
+        es.cands.push_back(EarlyCand{pub.p, sig.p, (uint32_t)pub.n, (uint32_t)sig.n, row});
+        it.ec_count++;
+    };
+    const auto& wit = txin.witness;
+    if (L == 22 && spk[0] == 0x00 && spk[1] == 0x14) {  // P2WPKH: witness [sig, key]
+        if (wit.size() == 2) add(wit[1], wit[0]);
+        return;
+    }
+    Span pu[20];
+    if (L == 25 && spk[0] == 0x76 && spk[1] == 0xa9 && spk[2] == 0x14 && spk[23] == 0x88 && spk[24] == 0xac) {
+        if (script_pushes(txin.script_sig, pu, 2) == 2) add(pu[1], pu[0]);  // P2PKH: <sig> <key>
+        return;
+    }
+    if (L == 23 && spk[0] == 0xa9 && spk[1] == 0x14 && spk[22] == 0x87) {  // P2SH
+        const int k = script_pushes(txin.script_sig, pu, 20);
+        if (k < 1) return;
+        const Span& rs = pu[k - 1];
+        if (k == 1 && rs.n == 22 && rs.p[0] == 0x00 && rs.p[1] == 0x14) {  // P2SH-P2WPKH
+            if (wit.size() == 2) add(wit[1], wit[0]);
+            return;
+        }
+        // m-of-n CHECKMULTISIG redeem script: OP_m <key>... OP_n OP_CHECKMULTISIG, scriptSig
+        // OP_0 <sig_1> ... <sig_m> <redeem>: sig i meets keys i .. i + n - m (interpreter.cpp:1176-1205)
+        if (rs.n < 3 || rs.p[rs.n - 1] != 0xae) return;
+        const int m = rs.p[0] - 0x50, n = rs.p[rs.n - 2] - 0x50;
+        if (m < 1 || n < m || n > 16 || k - 2 != m || pu[0].n != 0) return;
+        Span keys[16];
+        if (script_pushes(Span{rs.p + 1, rs.n - 3}, keys, 16) != n) return;
+        if (m * (n - m + 1) > 16) return;
+        for (int i = 0; i < m; i++)
+            for (int j = i; j <= i + n - m; j++) add(keys[j], pu[1 + i]);
+        return;
+    }
+    if (((L == 35 && spk[0] == 33) || (L == 67 && spk[0] == 65)) && spk[L - 1] == 0xac) {  // P2PK
+        if (script_pushes(txin.script_sig, pu, 1) == 1) add(Span{spk + 1, L - 2}, pu[0]);
+    }
+}
 
 struct Pending {
     uint32_t item;
@@ -272,24 +403,13 @@ void add_sighash_job(SighashJobs& jobs, TxEntry& te, const bcc_batch_item& in, c
         return &rows->msg[32 * (size_t)row];
     };
     if (sv == SIGVERSION_BASE && legacy_all_type(hashtype)) {
-        // device-assembled from the tx template (pipeline.h TplJob), or a host job (a long
-        // template, while the shard's host budget lasts; the tx's later checks then go to a device
-        // copy of the same template)
-        auto place_tpl = [&](bool on_host) {
-            build_legacy_template(tx, scratch);
-            if (te.tpl < 0 && te.htpl < 0) touched.push_back(&te);
-            te.tpl_len = (uint32_t)scratch.size();
-            if (on_host) {
-                te.htpl = (int64_t)host->tpl.size();
-                host->tpl.insert(host->tpl.end(), scratch.begin(), scratch.end());
-            } else {
-                te.tpl = jobs.add_tpl(scratch.data(), scratch.size());
-            }
-        };
-        if (te.tpl < 0 && te.htpl < 0) {
-            te.tpl_len = (uint32_t)legacy_template_len(tx);
-            place_tpl(hb && SighashJobs::tpl_nblk(te.tpl_len, 1) > hb);
-        }
+        // device-assembled from the tx template (pipeline.h TplJob), or a host job.  A long
+        // template carries its midstates (TPL_MID): a job then hashes only the blocks from its
+        // splice on, and the jobs whose remainder exceeds host->chain_blocks (the first inputs of
+        // a many-input tx) go to the host while the round's budget lasts.  The template is placed
+        // on each side on first use there (host->tpl, jobs.tpl).
+        if (te.tpl < 0 && te.htpl < 0) te.tpl_len = (uint32_t)legacy_template_len(tx);
+        const bool use_mid = SighashJobs::tpl_nblk(te.tpl_len, 1) >= TPL_MID_MIN_BLOCKS;
         build_script_code_field(code, scratch);
         TplJob tj;
         tj.tpl_len = te.tpl_len;
@@ -297,12 +417,21 @@ void add_sighash_job(SighashJobs& jobs, TxEntry& te, const bcc_batch_item& in, c
         tj.code_len = (uint32_t)scratch.size();
         tj.hashtype = (uint32_t)hashtype;
         tj.row = row;
-        tj.nblk = SighashJobs::tpl_nblk(tj.tpl_len, tj.code_len);
-        const bool on_host = te.htpl >= 0 && host->take(tj.nblk);
-        if (!on_host && te.tpl < 0) {  // budget spent: this tx's remaining checks on the device
-            std::vector<uint8_t> field(scratch);
-            place_tpl(false);
-            scratch.swap(field);
+        tj.nblk = SighashJobs::tpl_nblk(tj.tpl_len, tj.code_len) | (use_mid ? TPL_MID : 0u);
+        const uint32_t work = tpl_job_blocks(tj);
+        const bool on_host = hb && work > hb && host->take(work);
+        if ((on_host ? te.htpl : (int64_t)te.tpl) < 0) {
+            static thread_local std::vector<uint8_t> tbuf;
+            static thread_local std::vector<uint32_t> mbuf;
+            build_legacy_template(tx, tbuf);
+            const uint32_t* mp = nullptr;
+            if (use_mid) {
+                tpl_midstates(tbuf.data(), (uint32_t)tbuf.size(), mbuf);
+                mp = mbuf.data();
+            }
+            if (te.tpl < 0 && te.htpl < 0) touched.push_back(&te);
+            if (on_host) te.htpl = (int64_t)append_tpl(host->tpl, tbuf.data(), tbuf.size(), mp);
+            else te.tpl = jobs.add_tpl(tbuf.data(), tbuf.size(), mp);
         }
         if (on_host) {
             msg_row();  // hash_host_jobs writes the row
@@ -436,6 +565,9 @@ public:
     HostJobs host;  // checks whose sighash the host computes (long chains)
     size_t host_rejected = 0;
     size_t key_hashes = 0;  // key-hash conditions deferred (whole call)
+    const EarlyShard* early = nullptr;  // this shard's early rows (whole call; null: none)
+    uint32_t erow0 = 0;                 // ... and their first lane in the call's early set
+    size_t early_mapped = 0;            // rows mapped to an early twin (whole call)
 
     // GenericTransactionSignatureChecker::CheckECDSASignature (interpreter.cpp:1656-1676) up to
     // the point where the sighash + secp256k1 verify would run; those become a GPU tuple.
@@ -455,18 +587,25 @@ public:
             if (consult) it.pending.push_back((uint32_t)(-2 - c.v));
             return true;                                // deferred this round: speculate
         }
+        // an early twin with the same key and signature bytes (early Q halves): its row passed the
+        // host filter and holds this check's r and s, and its K_keyq result is reused on the GPU
+        const EarlyCand* twin = nullptr;
+        if (early) {
+            for (uint32_t k = it.ec_first, e = it.ec_first + it.ec_count; k < e; k++) {
+                const EarlyCand& c = early->cands[k];
+                if (c.publen == pub.size() && c.siglen == sig.size() &&
+                    memcmp(c.pub, pub.data(), c.publen) == 0 && memcmp(c.sig, sig.data(), c.siglen) == 0) {
+                    twin = &c;
+                    break;
+                }
+            }
+        }
         // CPubKey filter, empty signature, lax-DER: decided on the host (no secp work)
         uint8_t r[32], s[32];
-        bool reject = !pubkey_size_valid(pub.data(), pub.size()) || sig.empty() ||
-                      !der_parse_lax(sig.data(), sig.size() - 1, r, s);
-        if (!reject) {
-            uint64_t rw[4], sw[4];
-            memcpy(rw, r, 32);
-            memcpy(sw, s, 32);
-            // secp256k1_ecdsa_sig_verify rejects r == 0 || s == 0
-            reject = (rw[0] | rw[1] | rw[2] | rw[3]) == 0 || (sw[0] | sw[1] | sw[2] | sw[3]) == 0;
-        }
-        if (reject) {
+        if (twin) {
+            memcpy(r, &early->rows.r[32 * (size_t)twin->row], 32);
+            memcpy(s, &early->rows.s[32 * (size_t)twin->row], 32);
+        } else if (!tuple_fields(pub.data(), pub.size(), sig.data(), sig.size(), r, s)) {
             it.cache.push_back(Item::Check{koff, klen, 0});
             host_rejected++;
             return false;
@@ -478,6 +617,10 @@ public:
         const uint32_t row = rows.add_lazy(pub[0], pub.data() + 1, r, s, key65 ? pub.data() + 33 : nullptr,
                                            nullptr);
         if (key65) rows.y_unused = false;
+        if (twin) {
+            rows.set_emap(row, erow0 + twin->row);
+            early_mapped++;
+        }
         if (key_prog) {
             rows.add_key_hash(row, key_prog);
             *key_taken = true;
@@ -529,7 +672,7 @@ bool mark_host_rows(std::vector<Round>& rds, unsigned T) {
 
 // The offloaded legacy jobs of every shard, hashed in parallel on the calling thread's team (their
 // rows' msg receive the sighash).
-void hash_host_jobs(std::vector<Round>& rds, unsigned T) {
+void hash_host_jobs(std::vector<Round>& rds, unsigned T, unsigned maxW = 0) {
     std::vector<std::pair<uint32_t, uint32_t>> work;  // (shard, job): tjobs first, then pre
     for (unsigned t = 0; t < T; t++)
         for (uint32_t k = 0; k < rds[t].host.pending(); k++) work.emplace_back(t, k);
@@ -537,9 +680,9 @@ void hash_host_jobs(std::vector<Round>& rds, unsigned T) {
     size_t blocks = 0;
     for (const auto& w : work) {
         const HostJobs& h = rds[w.first].host;
-        blocks += w.second < h.tjobs.size() ? h.tjobs[w.second].nblk : 8;
+        blocks += w.second < h.tjobs.size() ? tpl_job_blocks(h.tjobs[w.second]) : 8;
     }
-    const unsigned W = (unsigned)std::max<size_t>(1, std::min<size_t>(std::min<size_t>(T, host_threads()),
+    const unsigned W = (unsigned)std::max<size_t>(1, std::min<size_t>(std::min<size_t>(maxW ? maxW : T, host_threads()),
                                                                          blocks / 256 + 1));
     // jobs are dealt round-robin: the long ones of one tx are spread over every worker
     run_team(W, [&](unsigned w) {
@@ -548,17 +691,9 @@ void hash_host_jobs(std::vector<Round>& rds, unsigned T) {
             HostJobs& h = rd.host;
             uint8_t* out = rd.rows.msg.data();
             const uint32_t k = work[i].second;
-            uint8_t d[32];
             if (k < h.tjobs.size()) {
                 const TplJob& t = h.tjobs[k];
-                const uint8_t* T0 = &h.tpl[t.tpl_off];
-                uint8_t ht[4];
-                for (int b = 0; b < 4; b++) ht[b] = (uint8_t)(t.hashtype >> (8 * b));
-                Sha256 x;
-                x.write(T0, t.pos).write(&h.code[t.code_off], t.code_len);
-                x.write(T0 + t.pos + 1, t.tpl_len - t.pos - 1).write(ht, 4);
-                x.finalize(d);
-                sha256(d, 32, out + 32 * (size_t)t.row);
+                tpl_job_sighash(h.tpl.data(), h.code.data(), t, out + 32 * (size_t)t.row);
             } else {
                 const size_t j = k - h.tjobs.size();
                 sha256d(&h.pre[h.pre_off[j]], h.pre_off[j + 1] - h.pre_off[j],
@@ -575,10 +710,11 @@ struct LateHost {
     std::vector<Round>* rds = nullptr;
     unsigned T = 0;
     bool done = false;
+    unsigned W = 0;  // worker threads (0: at most T)
     void ensure() {
         if (done) return;
         auto h0 = std::chrono::steady_clock::now();
-        hash_host_jobs(*rds, T);
+        hash_host_jobs(*rds, T, W);
         t_stats.host_jobs_seconds +=
             std::chrono::duration<double>(std::chrono::steady_clock::now() - h0).count();
         done = true;
@@ -621,6 +757,22 @@ void run_threads(unsigned T, F f) {
     run_team(T, std::function<void(unsigned)>(f));
 }
 
+// Runs f(s) for every shard s in [0, S) on W of the calling thread's team workers: with S == W one
+// shard per worker, with more shards than workers each worker takes the next unstarted shard, so a
+// slow shard no longer sets the pass's length (round 5: C3's interpreter shards ran 1.3-1.5x the
+// mean on the slowest one at 16 shards).
+template <class F>
+void run_shards(unsigned S, unsigned W, F f) {
+    if (W >= S) {
+        run_threads(S, f);
+        return;
+    }
+    std::atomic<unsigned> next{0};
+    run_threads(W, [&](unsigned) {
+        for (unsigned s; (s = next.fetch_add(1, std::memory_order_relaxed)) < S;) f(s);
+    });
+}
+
 // Contiguous [lo, hi) share t of T over n units.
 inline size_t share_lo(size_t n, unsigned t, unsigned T) { return n * t / T; }
 
@@ -646,7 +798,9 @@ std::vector<size_t> shard_bounds(const BatchState& b, unsigned T) {
 // fills its shard's item list and run list (the items that passed the pre-checks).
 void prepare(BatchState& b, const bcc_batch_item* items, size_t n, unsigned flags, unsigned T,
              std::vector<std::vector<uint32_t>>* shards = nullptr,
-             std::vector<std::vector<uint32_t>>* runs = nullptr) {
+             std::vector<std::vector<uint32_t>>* runs = nullptr,
+             std::vector<EarlyShard>* early = nullptr, unsigned W = 0) {
+    if (W == 0 || W > T) W = T;  // worker threads over the T shards (run_shards)
     if (b.st.size() < n) b.st.resize(n);  // reused across calls: every field is (re)set below
     b.n = n;
     b.flags = flags;
@@ -662,7 +816,7 @@ void prepare(BatchState& b, const bcc_batch_item* items, size_t n, unsigned flag
             if (starts_tx(i)) b.tx_first.push_back((uint32_t)i);
     } else {
         b.tx_slices.resize(T);
-        run_threads(T, [&](unsigned t) {
+        run_shards(T, W, [&](unsigned t) {
             auto& v = b.tx_slices[t];
             v.clear();
             for (size_t i = share_lo(n, t, T); i < share_lo(n, t + 1, T); i++)
@@ -707,7 +861,7 @@ void prepare(BatchState& b, const bcc_batch_item* items, size_t n, unsigned flag
         shards->resize(T);
         runs->resize(T);
     }
-    run_threads(T, [&](unsigned t) {
+    run_shards(T, W, [&](unsigned t) {
         const auto s0 = pclk::now();
         lag[t] = std::chrono::duration<double>(s0 - d0).count();
         // this worker's txs: the entries starting in its shard [bound[t], bound[t + 1])
@@ -741,6 +895,7 @@ void prepare(BatchState& b, const bcc_batch_item* items, size_t n, unsigned flag
                 it.runs = 0;
                 it.cache.clear();
                 it.pending.clear();
+                it.ec_first = it.ec_count = 0;
                 if (!flags_ok) it.err = bitcoinconsensus_ERR_INVALID_FLAGS;
                 else if (!e.ok) it.err = bitcoinconsensus_ERR_TX_DESERIALIZE;
                 else if (items[i].n_in >= e.tx.vin.size()) it.err = bitcoinconsensus_ERR_TX_INDEX;
@@ -754,6 +909,12 @@ void prepare(BatchState& b, const bcc_batch_item* items, size_t n, unsigned flag
                     if (it.active) rl->push_back((uint32_t)i);
                 }
             }
+        }
+        if (early) {  // early Q halves: this shard's candidates while its txs are in cache
+            EarlyShard& es = (*early)[t];
+            es.clear();
+            for (size_t i = bound[t]; i < bound[t + 1]; i++)
+                if (st[i].active) early_extract_item(st[i], es);
         }
         const auto s1 = pclk::now();
         tparse[t] = std::chrono::duration<double>(s1 - s0).count();
@@ -1008,7 +1169,8 @@ struct ChunkRun {
     std::vector<std::vector<uint32_t>> shards, run_list, next_list;
     std::vector<size_t> row0;
     std::vector<uint8_t> verdict;
-    unsigned T = 1;
+    unsigned T = 1;  // shards (one Round each)
+    unsigned W = 1;  // worker threads over the shards (run_shards)
     size_t n = 0, npend = 0;
     bool pending_round = false;  // a device round for the current run lists is due
     std::future<int> fut;        // the device round in flight (pipelined)
@@ -1018,6 +1180,7 @@ struct ChunkRun {
     // the first device round of a pipelined chunk, staged by the caller (prestage_round)
     std::unique_ptr<StagedRound, void (*)(StagedRound*)> staged{nullptr, gpu_staged_free};
     bool prestaged = false;
+    std::vector<EarlyShard> early;  // per shard: pre-extracted rows (early Q halves)
     LateHost late;               // offloaded host jobs of the current pass (hashed during the round)
     // their blocks (HostJobs::take); held by pointer so that ChunkRun stays movable
     std::unique_ptr<std::atomic<uint64_t>> host_planned = std::make_unique<std::atomic<uint64_t>>(0);
@@ -1044,7 +1207,7 @@ void chunk_interpret(ChunkRun& c) {
     const bool one_gpu = device_list().size() == 1;
     c.host_planned->store(0, std::memory_order_relaxed);
     std::vector<double> ts(c.T, 0);
-    run_threads(c.T, [&](unsigned t) {
+    run_shards(c.T, c.W, [&](unsigned t) {
         auto s0 = clk::now();
         c.rds[t].reset(one_gpu);
         c.rds[t].host.planned = c.host_planned.get();
@@ -1061,7 +1224,7 @@ void chunk_interpret(ChunkRun& c) {
     t_stats.interpret_shard_mean_seconds += tsum / c.T;
     // the offloaded jobs' rows are marked now; single-GPU rounds hash the jobs themselves while the
     // device runs the message-independent kernels (LateHost), multi-GPU rounds before the round
-    c.late = LateHost{&c.rds, c.T, false};
+    c.late = LateHost{&c.rds, c.T, false, c.W};
     c.late_pending = mark_host_rows(c.rds, c.T);
     if (c.late_pending && device_list().size() != 1) {
         c.late.ensure();
@@ -1090,9 +1253,49 @@ void chunk_interpret(ChunkRun& c) {
 }
 
 constexpr size_t SHORT_PASS_ITEMS = 65536;
+// Shards per worker of a short pass (BCC_SHARDS_PER_WORKER, default 1).  Round 5 measured 2 and 4
+// (dynamically dealt, run_shards) on C3: slower (4.0-4.4 vs 4.7-5.0 M inputs/s,
+// profiles/r05/c3/shards): a many-input tx is cut into more pieces, each parsing the tx and
+// building its template (and midstates) again, which costs more than the balance gains.
+unsigned SHARDS_PER_WORKER = [] {
+    const char* e = getenv("BCC_SHARDS_PER_WORKER");
+    return e ? std::max(1, atoi(e)) : 1;
+}();
+
+// Early Q halves for a single-GPU, single-chunk call (EarlyShard): per shard the candidates of its
+// active items, then one early launch over all shards' rows (concatenated in shard order).
+// Whether a chunk of n items takes early Q halves (its candidates are extracted by prepare).
+bool early_wanted(size_t n, bool allow) {
+    return allow && g_early_q.load(std::memory_order_relaxed) && device_list().size() == 1 &&
+           n <= EARLY_MAX_ITEMS && n > host_small_round();
+}
+
+void chunk_early(ChunkRun& c, bool allow) {
+    for (unsigned t = 0; t < c.T; t++) {
+        c.rds[t].early = nullptr;
+        c.rds[t].erow0 = 0;
+        c.rds[t].early_mapped = 0;
+    }
+    if (!early_wanted(c.n, allow)) return;
+    const std::vector<int> devs = device_list();
+    auto e0 = clk::now();
+    std::vector<const TupleRows*> parts(c.T);
+    size_t E = 0;
+    for (unsigned t = 0; t < c.T; t++) {
+        c.rds[t].erow0 = (uint32_t)E;
+        E += c.early[t].rows.size();
+        parts[t] = &c.early[t].rows;
+    }
+    if (E > host_small_round() && gpu_early_launch(devs[0], parts.data(), c.T) == 0) {
+        for (unsigned t = 0; t < c.T; t++) c.rds[t].early = &c.early[t];
+        t_stats.early_rows += E;
+    }
+    t_stats.early_seconds += since(e0);
+}
 
 // prepare + shards + the first interpreter pass of items [0, n) of `items`.
-void chunk_start(ChunkRun& c, const bcc_batch_item* items, size_t n, unsigned flags) {
+void chunk_start(ChunkRun& c, const bcc_batch_item* items, size_t n, unsigned flags,
+                 bool allow_early = false) {
     auto t0 = clk::now();
     c.n = n;
     // A short host pass (a block-sized batch) on at most the CPU share: three times the quota
@@ -1100,9 +1303,13 @@ void chunk_start(ChunkRun& c, const bcc_batch_item* items, size_t n, unsigned fl
     // ~1 ms pass the extra threads only queue for the CPUs and their wake-ups
     // (C3 at 48 threads vs 16: 2.9-3.0 vs 4.7-5.4 M inputs/s, profiles/r04/c3).
     const unsigned cap = n < SHORT_PASS_ITEMS ? std::min(host_threads(), cpu_share()) : host_threads();
-    c.T = n >= 256 ? std::min<unsigned>(cap, (unsigned)(n / 64)) : 1u;
+    c.W = n >= 256 ? std::min<unsigned>(cap, (unsigned)(n / 64)) : 1u;
+    // a short pass: four shards per worker, dealt dynamically (run_shards)
+    c.T = n < SHORT_PASS_ITEMS && c.W > 1 ? std::min<unsigned>(SHARDS_PER_WORKER * c.W, (unsigned)(n / 64)) : c.W;
     const unsigned T = c.T;
-    prepare(c.b, items, n, flags, T, &c.shards, &c.run_list);  // + the shard / run lists
+    const bool early = early_wanted(n, allow_early);
+    if (early && c.early.size() < T) c.early.resize(T);
+    prepare(c.b, items, n, flags, T, &c.shards, &c.run_list, early ? &c.early : nullptr, c.W);  // + the shard / run lists
     t_stats.prepare_seconds += since(t0);
     c.next_list.resize(T);
     for (auto& v : c.next_list) v.clear();
@@ -1117,6 +1324,7 @@ void chunk_start(ChunkRun& c, const bcc_batch_item* items, size_t n, unsigned fl
     c.stage_s = 0;
     c.devices_used = 0;
     c.retries = 0;
+    chunk_early(c, allow_early);
     chunk_interpret(c);
 }
 
@@ -1173,6 +1381,15 @@ int chunk_device_round(ChunkRun& c) {
                         "again through the general path\n", e);
         c.retries++;
     }
+    struct StageW {  // more shards (staging parts) than workers: fill the image on the workers only
+        explicit StageW(const ChunkRun& c) : on(c.T > c.W) {
+            if (on) set_stage_threads(c.W);
+        }
+        ~StageW() {
+            if (on) set_stage_threads(0);
+        }
+        bool on;
+    } stage_w(c);
     return run_device_round(c.rds, c.T, c.row0, c.verdict.data(), &c.stage_s, &c.devices_used,
                             &c.retries, &c.host_rounds, late);
 }
@@ -1181,7 +1398,7 @@ int chunk_device_round(ChunkRun& c) {
 // another interpreter pass (their run lists).
 void chunk_stitch(ChunkRun& c) {
     auto& st = c.b.st;
-    run_threads(c.T, [&](unsigned t) {
+    run_shards(c.T, c.W, [&](unsigned t) {
         const Round& rd = c.rds[t];
         const uint8_t* v = c.verdict.data() + c.row0[t];
         for (size_t k = 0; k < rd.pending.size(); k++)
@@ -1251,10 +1468,11 @@ long chunk_finish(ChunkRun& c, int* ret_out, bitcoinconsensus_error* err_out, bo
     for (unsigned t = 0; t < c.T; t++) {
         t_stats.host_rejected += c.rds[t].host_rejected;
         t_stats.device_key_hashes += c.rds[t].key_hashes;
+        t_stats.early_mapped += c.rds[t].early_mapped;
     }
     auto f0 = clk::now();
     std::vector<long> vt(c.T, 0);
-    run_threads(c.T, [&](unsigned t) {  // the shards cover [0, n) contiguously
+    run_shards(c.T, c.W, [&](unsigned t) {  // the shards cover [0, n) contiguously
         long v = 0;
         for (uint32_t i : c.shards[t]) {
             Item& it = st[i];
@@ -1277,7 +1495,7 @@ long chunk_finish(ChunkRun& c, int* ret_out, bitcoinconsensus_error* err_out, bo
 void chunk_release_if_large(ChunkRun& c) {
     if (c.n <= ((size_t)1 << 22)) return;
     auto& st = c.b.st;
-    run_threads(c.T, [&](unsigned t) {
+    run_shards(c.T, c.W, [&](unsigned t) {
         for (uint32_t i : c.shards[t]) {
             decltype(st[i].cache)().swap(st[i].cache);
             std::vector<uint32_t>().swap(st[i].pending);
@@ -1351,7 +1569,7 @@ long run_batch(const bcc_batch_item* items, size_t n, unsigned flags, int* ret_o
     } drain;
     if (chunk == 0 || n < 2 * chunk) {
         ChunkRun& c = tl_chunk[0];
-        chunk_start(c, items, n, flags);
+        chunk_start(c, items, n, flags, true);
         account(chunk_finish(c, ret_out, err_out, false, &gpu_s));
         chunk_release_if_large(c);
     } else {
@@ -1584,6 +1802,11 @@ int bcc_set_host_chain_blocks(unsigned blocks) {
 
 int bcc_set_host_bip143_blocks(unsigned blocks) {
     bcc::host::g_host_bip143_blocks.store(blocks, std::memory_order_relaxed);
+    return 0;
+}
+
+int bcc_set_early_q(int on) {
+    bcc::host::g_early_q.store(on ? 1 : 0, std::memory_order_relaxed);
     return 0;
 }
 

@@ -78,6 +78,35 @@ void parallel_for(size_t n, unsigned T, F f) {
 
 }  // namespace
 
+void tpl_midstates(const uint8_t* T, uint32_t len, std::vector<uint32_t>& mid) {
+    const uint32_t nm = tpl_mid_count(len);
+    mid.resize(8 * (size_t)nm);
+    Sha256 x;
+    for (uint32_t j = 0; j < nm; j++) {
+        memcpy(&mid[8 * (size_t)j], x.s, 32);
+        if (j + 1 < nm) x.write(T + 64 * (size_t)j, 64);  // a whole block: compressed at once
+    }
+}
+
+void tpl_job_sighash(const uint8_t* tpl, const uint8_t* code, const TplJob& t, uint8_t out[32]) {
+    const uint8_t* T = tpl + t.tpl_off;
+    Sha256 x;
+    uint32_t q0 = 0;  // first message byte hashed here
+    if (tpl_has_mid(t)) {
+        const uint32_t b0 = t.pos / 64;
+        memcpy(x.s, tpl + tpl_mid_offset(t.tpl_off, t.tpl_len) + 32 * (size_t)b0, 32);
+        x.bytes = 64 * (uint64_t)b0;
+        q0 = 64 * b0;
+    }
+    const uint32_t h = t.hashtype;
+    const uint8_t ht[4] = {(uint8_t)h, (uint8_t)(h >> 8), (uint8_t)(h >> 16), (uint8_t)(h >> 24)};
+    x.write(T + q0, t.pos - q0).write(code + t.code_off, t.code_len);
+    x.write(T + t.pos + 1, t.tpl_len - t.pos - 1).write(ht, 4);
+    uint8_t d[32];
+    x.finalize(d);
+    sha256(d, 32, out);
+}
+
 void host_sighash(const SighashJobs& j, uint8_t* msg) {
     std::vector<uint8_t> auxd(32 * j.aux_off.size());
     for (size_t a = 0; a < j.aux_off.size(); a++) {
@@ -92,15 +121,7 @@ void host_sighash(const SighashJobs& j, uint8_t* msg) {
             sha256d(m, unpadded_len(m, (size_t)j.pre_nblk[k] * 64), msg + 32 * (size_t)j.pre_row[k]);
         }
     }
-    std::vector<uint8_t> buf;
-    for (const TplJob& t : j.tjobs) {
-        const uint8_t* T = &j.tpl[t.tpl_off];
-        buf.assign(T, T + t.pos);
-        buf.insert(buf.end(), &j.code[t.code_off], &j.code[t.code_off] + t.code_len);
-        buf.insert(buf.end(), T + t.pos + 1, T + t.tpl_len);
-        for (int b = 0; b < 4; b++) buf.push_back((uint8_t)(t.hashtype >> (8 * b)));
-        sha256d(buf.data(), buf.size(), msg + 32 * (size_t)t.row);
-    }
+    for (const TplJob& t : j.tjobs) tpl_job_sighash(j.tpl.data(), j.code.data(), t, msg + 32 * (size_t)t.row);
     if (!j.wjobs.empty()) {
         // BIP143 from the raw tx bytes: parse each tx once, its three aux digests on first use
         std::vector<Tx> txs(j.wtx.size());

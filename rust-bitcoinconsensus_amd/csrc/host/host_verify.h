@@ -3,6 +3,7 @@
 #pragma once
 #include <cstddef>
 #include <cstdint>
+#include <vector>
 
 #include "../pipeline.h"
 
@@ -11,6 +12,11 @@ namespace host {
 
 // msg (32 bytes per row, entering as each row's initial message) receives every job's digest.
 void host_sighash(const SighashJobs& jobs, uint8_t* msg);
+// The sighash of legacy template job t over its template / code blobs (K3' on the host): from the
+// midstate at its splice block when t carries TPL_MID (pipeline.h), else from the IV.
+void tpl_job_sighash(const uint8_t* tpl, const uint8_t* code, const TplJob& t, uint8_t out[32]);
+// mid = the tpl_mid_count(len) SHA-256 midstates of template T (8 native-order words each).
+void tpl_midstates(const uint8_t* T, uint32_t len, std::vector<uint32_t>& mid);
 // One tuple (tag 0 = rejected on the host; y ignored for 02/03): 1 valid.
 int host_verify_tuple(uint8_t tag, const uint8_t* x32, const uint8_t* y32, const uint8_t* r32,
                       const uint8_t* s32, const uint8_t* m32);

@@ -46,10 +46,50 @@ struct TplJob {
     uint32_t pos;
     uint32_t code_off;  // byte offset of code in the code blob (4-aligned)
     uint32_t code_len;
-    uint32_t hashtype;
+    uint32_t hashtype;  // serialized as le32 (a script's is the signature's last byte; the
+                        // sighash goldens use any 32-bit value)
     uint32_t row;       // tuple row whose msg receives the sighash
-    uint32_t nblk;      // padded message length in 64-byte blocks
+    uint32_t nblk;      // padded message length in 64-byte blocks | TPL_MID when T carries midstates
 };
+
+// Round 5: the template midstates.  Every legacy preimage of a tx begins with T's first
+// floor(pos / 64) blocks, so a long template is stored with the SHA-256 state after each of its
+// whole blocks (mid[j]: j blocks absorbed, mid[0] = the IV; 8 native-order words each) right
+// behind it, and a job flagged TPL_MID (in nblk) starts from mid[pos / 64] at block pos / 64: it hashes
+// only the blocks from its splice on (a 442-input tx: 284 -> 1..284 blocks, half on average),
+// on the device (K3') and on the host (hash_host_jobs) alike.
+#if defined(__HIPCC__)
+#define BCC_PL_HD __host__ __device__
+#else
+#define BCC_PL_HD
+#endif
+constexpr uint32_t TPL_MID = 0x80000000u;
+constexpr uint32_t TPL_MID_MIN_BLOCKS = 8;  // shorter templates start from the IV
+BCC_PL_HD inline uint32_t tpl_mid_count(uint32_t tpl_len) { return (tpl_len - 1) / 64 + 1; }
+BCC_PL_HD inline uint32_t tpl_mid_offset(uint32_t tpl_off, uint32_t tpl_len) {  // 4-aligned, after the 8 zero bytes
+    return tpl_off + ((tpl_len + 3) & ~3u) + 8;
+}
+BCC_PL_HD inline uint32_t tpl_nblk(const TplJob& j) { return j.nblk & ~TPL_MID; }
+BCC_PL_HD inline bool tpl_has_mid(const TplJob& j) { return (j.nblk & TPL_MID) != 0; }
+// The blocks a job hashes (from its start block: pos / 64 with midstates, else 0).
+BCC_PL_HD inline uint32_t tpl_job_blocks(const TplJob& j) {
+    return tpl_has_mid(j) ? tpl_nblk(j) - j.pos / 64 : tpl_nblk(j);
+}
+// Appends T (4-aligned, + 8 zero bytes) and, when mid != nullptr, its tpl_mid_count(n) midstates
+// (8 words each) to a template blob; returns T's offset.
+inline uint32_t append_tpl(std::vector<uint8_t>& blob, const uint8_t* m, size_t n,
+                           const uint32_t* mid) {
+    const uint32_t off = (uint32_t)blob.size();
+    blob.insert(blob.end(), m, m + n);
+    blob.resize(off + ((n + 3) & ~(size_t)3) + 8, 0);
+    if (mid) {
+        const size_t bytes = 32 * (size_t)tpl_mid_count((uint32_t)n);
+        const size_t at = blob.size();
+        blob.resize(at + bytes);
+        memcpy(&blob[at], mid, bytes);
+    }
+    return off;
+}
 
 // BIP143 jobs built on the device from the raw transaction bytes: per tx a
 // WtxRec (K_wtx parses the wire format, primitives/transaction.h:188-224 / serialize.h:318-347,
@@ -117,11 +157,8 @@ struct SighashJobs {
         wtx.push_back(r);
         return (uint32_t)wtx.size() - 1;
     }
-    uint32_t add_tpl(const uint8_t* m, size_t n) {
-        uint32_t off = (uint32_t)tpl.size();
-        tpl.insert(tpl.end(), m, m + n);
-        tpl.resize(off + ((n + 3) & ~(size_t)3) + 8, 0);
-        return off;
+    uint32_t add_tpl(const uint8_t* m, size_t n, const uint32_t* mid = nullptr) {
+        return append_tpl(tpl, m, n, mid);
     }
     // compactsize(n) || m, 4-aligned: a scriptCode field (BIP143 / legacy serialization)
     uint32_t add_code_field(const uint8_t* m, size_t n) {
@@ -182,6 +219,20 @@ struct TupleRows {
     // HASH160(its key) == hprog[20k, 20k + 20); the device ANDs that into the row's verdict.
     std::vector<uint32_t> hrow;
     std::vector<uint8_t> hprog;
+    // Early Q halves (round 5, DeviceBatch::early_launch): emap[row] = the lane of the call's early
+    // set whose (key, signature) bytes equal this row's, whose key half and Q ladder already ran
+    // (K_keyq copies it instead of recomputing); rows past emap.size() or holding NO_EARLY have none.
+    static constexpr uint32_t NO_EARLY = 0xFFFFFFFFu;
+    std::vector<uint32_t> emap;
+    void set_emap(size_t row, uint32_t e) {
+        if (emap.size() <= row) emap.resize(row + 1, NO_EARLY);
+        emap[row] = e;
+    }
+    void copy_emap(uint32_t* out, size_t lo, size_t hi) const {
+        const size_t have = std::min(std::max(emap.size(), lo), hi);
+        if (have > lo) memcpy(out, &emap[lo], 4 * (have - lo));
+        for (size_t k = have; k < hi; k++) out[k - lo] = NO_EARLY;
+    }
     size_t size() const { return tag.size(); }
     // A row that stores its y / msg only when given: y32 == nullptr reads as zero (a 33-byte key),
     // m32 == nullptr as uint256 ONE.  y and msg may then hold only a prefix of the rows; readers
@@ -245,7 +296,7 @@ struct TupleRows {
     }
     void clear() {
         tag.clear(); x.clear(); y.clear(); r.clear(); s.clear(); msg.clear();
-        hrow.clear(); hprog.clear();
+        hrow.clear(); hprog.clear(); emap.clear();
         msg_one = y_unused = false;
     }
 };
@@ -344,6 +395,8 @@ struct SigScratch {
     size_t chunk_short = 0;  // a chunk request the device could not hold (served by chunk_cap)
     size_t key_ready = 0;  // tuples whose key half of the prep ran ahead (ecdsa_launch_key)
     size_t q_ready = 0;    // tuples whose Q ladder ran ahead (ecdsa_launch_q)
+    void* qtab2 = nullptr;  // the Q tables of K_keyq's latency mode (two lanes per tuple)
+    size_t qtab2_cap = 0;   // lanes
     SigScratch() = default;
     SigScratch(const SigScratch&) = delete;
     SigScratch& operator=(const SigScratch&) = delete;
@@ -371,6 +424,13 @@ int ecdsa_launch_key(SigScratch& sc, const uint8_t* d_tag, const uint8_t* d_x, c
                      size_t n, void* stream);
 int ecdsa_launch_q(SigScratch& sc, const uint8_t* d_tag, const uint8_t* d_x, const uint8_t* d_y,
                    const uint8_t* d_r, const uint8_t* d_s, size_t n, void* stream);
+// The same for rows that may have an early twin (TupleRows::emap, device copy d_emap): a mapped
+// row's key half and Q ladder are copied from lane emap[row] of `early` (an ecdsa_launch_q over
+// the call's early set, ordered before this on `stream`); K_keyq computes only the others.
+int ecdsa_launch_q_mapped(SigScratch& sc, const SigScratch& early, size_t early_n,
+                          const uint32_t* d_emap, const uint8_t* d_tag, const uint8_t* d_x,
+                          const uint8_t* d_y, const uint8_t* d_r, const uint8_t* d_s, size_t n,
+                          void* stream);
 // ev_rows_read (optional hipEvent_t) is recorded on `stream` once the last kernel that reads the
 // s / m / key rows and the s^-1 rows has been launched (the prep kernel): later writers of those
 // rows (the next run's front kernels) need only wait for it, not for the ladder.
@@ -469,7 +529,33 @@ private:
     size_t n_hash_ = 0;
     uint32_t* d_hrow_ = nullptr;
     uint8_t* d_hprog_ = nullptr;
+    uint32_t* d_emap_ = nullptr;  // staged TupleRows::emap (null: no row has an early twin)
+
+public:
+    // Early Q halves (round 5): the key half, u2 and the Q ladder (K_inv + K_keyq) of a call's
+    // pre-extracted (key, signature) rows, launched on a stream of their own while the host still
+    // interprets the call; a later round whose rows carry TupleRows::emap copies them instead of
+    // running its own K_keyq on those rows.  early_reset forgets the set (a new call).
+    int early_launch(const TupleRows* const* rows, size_t P);
+    void early_reset();
+    size_t early_rows() const { return early_n_; }
+
+private:
+    void* early_stream_ = nullptr;  // hipStream_t
+    void* ev_early_ = nullptr;      // hipEvent_t: the early K_keyq done
+    bool early_pending_ = false;    // ev_early_ recorded and maybe not reached yet
+    size_t early_n_ = 0;            // rows of the current early set (0: none)
+    SigScratch early_scratch_;
+    void* early_arena_ = nullptr;   // tag | x | y | r | s rows of the early set
+    size_t early_cap_ = 0;
+    void* early_host_ = nullptr;    // pinned image of early_arena_
+    size_t early_host_cap_ = 0;
 };
+
+// The calling thread's device batch on `device` (the one gpu_verify_parts runs): early Q halves
+// for the call's pre-extracted rows (DeviceBatch::early_launch), and the reset of a new call.
+int gpu_early_launch(int device, const TupleRows* const* rows, size_t P);
+void gpu_early_reset(int device);
 
 // Threads the calling thread's device batches use to fill their pinned staging image (0: one per
 // part, the default).  The batch engine lowers it on its pipeline worker, whose staging runs

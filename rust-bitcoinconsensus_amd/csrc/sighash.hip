@@ -223,7 +223,7 @@ __device__ __forceinline__ void sha256d_tpl_lane(const uint8_t* __restrict__ tpl
     m.s3 = j.pos + j.code_len;
     m.L = j.tpl_len - 1 + j.code_len + 4;
     m.e3 = m.L - 4;
-    m.tail = j.nblk * 64 - 8;
+    m.tail = tpl_nblk(j) * 64 - 8;
     m.ht = j.hashtype;
     TplGeom g;
     g.pos = (int32_t)m.pos;
@@ -236,16 +236,25 @@ __device__ __forceinline__ void sha256d_tpl_lane(const uint8_t* __restrict__ tpl
     g.sel_c = (uint32_t)(g.oc & 3) * 0x01010101u + 0x00010203u;
     const uint32_t fast_blocks = m.e3 / 64;  // blocks wholly before the hashtype trailer
     uint32_t st[8];
-    sha256_init_state(st);
+    uint32_t b0 = 0;  // first block hashed: the splice's block when T carries midstates
+    if (tpl_has_mid(j)) {
+        b0 = j.pos / 64;  // <= (tpl_len - 1) / 64 <= fast_blocks
+        const uint32_t* mid = reinterpret_cast<const uint32_t*>(tpl + tpl_mid_offset(j.tpl_off, j.tpl_len)) + 8 * b0;
+#pragma unroll
+        for (int k = 0; k < 8; k++) st[k] = mid[k];
+    } else {
+        sha256_init_state(st);
+    }
     TplSrc nxt;
-    if (fast_blocks) tpl_fetch(m, g, 0, nxt);
-    for (uint32_t b = 0; b < fast_blocks; b++) {
+    if (b0 < fast_blocks) tpl_fetch(m, g, 64 * b0, nxt);
+    for (uint32_t b = b0; b < fast_blocks; b++) {
         uint32_t w[16];
         tpl_words(g, 64 * b, nxt, w);
         if (b + 1 < fast_blocks) tpl_fetch(m, g, 64 * (b + 1), nxt);
         sha256_compress(st, w);
     }
-    for (uint32_t b = fast_blocks; b < j.nblk; b++) {  // the trailer: byte by byte
+    const uint32_t nblk = tpl_nblk(j);
+    for (uint32_t b = fast_blocks; b < nblk; b++) {  // the trailer: byte by byte
         uint32_t w[16];
 #pragma unroll
         for (int k = 0; k < 16; k++) w[k] = tpl_word(m, 64 * b + 4 * k);
@@ -888,7 +897,93 @@ DeviceBatch::~DeviceBatch() {
     if (vbuf_) (void)hipHostFree(vbuf_);
     if (late_host_) (void)hipHostFree(late_host_);
     if (late_dev_) (void)hipFree(late_dev_);
+    if (early_stream_) {
+        (void)hipStreamSynchronize((hipStream_t)early_stream_);
+        (void)hipStreamDestroy((hipStream_t)early_stream_);
+    }
+    if (ev_early_) (void)hipEventDestroy((hipEvent_t)ev_early_);
+    if (early_arena_) (void)hipFree(early_arena_);
+    if (early_host_) (void)hipHostFree(early_host_);
 }
+
+// Early Q halves: the rows go up on the batch's early stream, then K_inv and K_keyq over them into
+// early_scratch_ (their own scratch: the round's K_keyq copies from it).  The previous set's work
+// (a call whose rounds never needed it) is waited for before its image and scratch are reused.
+int DeviceBatch::early_launch(const TupleRows* const* Rw, size_t P) {
+    early_n_ = 0;
+    BCC_HIP_TRY(hipSetDevice(dev_));
+    if (!early_stream_) {
+        hipStream_t s = nullptr;
+        hipEvent_t e = nullptr;
+        BCC_HIP_TRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+        BCC_HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        early_stream_ = s;
+        ev_early_ = e;
+    }
+    hipStream_t es = (hipStream_t)early_stream_;
+    if (early_pending_) {
+        BCC_HIP_TRY(hipStreamSynchronize(es));
+        early_pending_ = false;
+    }
+    std::vector<size_t> row0(P + 1, 0);
+    bool need_y = false;
+    for (size_t p = 0; p < P; p++) {
+        row0[p + 1] = row0[p] + Rw[p]->size();
+        need_y |= !Rw[p]->y_unused && Rw[p]->size() != 0;
+    }
+    const size_t R = row0[P];
+    if (R == 0) return 0;
+    // tag | x | y | r | s, each 256-aligned
+    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    const size_t o_tag = 0, o_x = al(R), o_y = o_x + al(32 * R), o_r = o_y + al(32 * R),
+                 o_s = o_r + al(32 * R), total = o_s + al(32 * R);
+    if (total > early_cap_) {
+        if (early_arena_) BCC_HIP_TRY(hipFree(early_arena_));
+        early_arena_ = nullptr;
+        early_cap_ = 0;
+        BCC_HIP_TRY(hipMalloc(&early_arena_, total));
+        early_cap_ = total;
+    }
+    if (total > early_host_cap_) {
+        if (early_host_) BCC_HIP_TRY(hipHostFree(early_host_));
+        early_host_ = nullptr;
+        early_host_cap_ = 0;
+        BCC_HIP_TRY(hipHostMalloc(&early_host_, total, hipHostMallocDefault));
+        early_host_cap_ = total;
+    }
+    uint8_t* h = (uint8_t*)early_host_;
+    auto fill = [&](size_t p) {
+        const TupleRows& rw = *Rw[p];
+        const size_t r0 = row0[p], nr = rw.size();
+        if (!nr) return;
+        memcpy(h + o_tag + r0, rw.tag.data(), nr);
+        memcpy(h + o_x + 32 * r0, rw.x.data(), 32 * nr);
+        if (need_y) rw.copy_y(h + o_y + 32 * r0, 0, nr);
+        memcpy(h + o_r + 32 * r0, rw.r.data(), 32 * nr);
+        memcpy(h + o_s + 32 * r0, rw.s.data(), 32 * nr);
+    };
+    if (P > 1 && R >= 4096) host::run_team((unsigned)std::min<size_t>(P, 16), [&](unsigned t) {
+        for (size_t p = t; p < P; p += std::min<size_t>(P, 16)) fill(p);
+    });
+    else
+        for (size_t p = 0; p < P; p++) fill(p);
+    uint8_t* a = (uint8_t*)early_arena_;
+    BCC_HIP_TRY(hipMemcpyAsync(a, h, need_y ? total : o_y, hipMemcpyHostToDevice, es));
+    if (!need_y) BCC_HIP_TRY(hipMemcpyAsync(a + o_r, h + o_r, total - o_r, hipMemcpyHostToDevice, es));
+    const uint8_t *dt = a + o_tag, *dx = a + o_x, *dy = a + o_y, *dr = a + o_r, *ds = a + o_s;
+    if (int e = ecdsa_launch_pre(early_scratch_, dt, dx, dy, ds, R, es)) return e;
+    if (int e = ecdsa_launch_key(early_scratch_, dt, dx, dy, R, es)) return e;
+    if (int e = ecdsa_launch_q(early_scratch_, dt, dx, dy, dr, ds, R, es)) return e;
+    const bool launched = early_scratch_.q_ready == R;
+    early_scratch_.key_ready = 0;
+    early_scratch_.q_ready = 0;
+    BCC_HIP_TRY(hipEventRecord((hipEvent_t)ev_early_, es));
+    early_pending_ = true;
+    if (launched) early_n_ = R;
+    return 0;
+}
+
+void DeviceBatch::early_reset() { early_n_ = 0; }
 
 void* DeviceBatch::pick(void* stream) {
     if (!stream) {
@@ -958,7 +1053,7 @@ int DeviceBatch::stage_parts(const SighashJobs* const* J, const TupleRows* const
         wj0[p + 1] = wj0[p] + J[p]->wjobs.size();
         win0[p + 1] = win0[p] + J[p]->win_entries;
         h0[p + 1] = h0[p] + Rw[p]->hrow.size();
-        for (const auto& t : J[p]->tjobs) tjblk += t.nblk;
+        for (const auto& t : J[p]->tjobs) tjblk += tpl_job_blocks(t);
     }
     const size_t LIM = (size_t)1 << 32;
     if (auxb0[P] >= LIM || preb0[P] >= LIM || tpl0[P] >= LIM || code0[P] >= LIM ||
@@ -987,16 +1082,19 @@ int DeviceBatch::stage_parts(const SighashJobs* const* J, const TupleRows* const
     const size_t R = n_rows_;
     // regions filled from the host image first (one copy), device-written ones after them
     // Y and M go up only when some part needs them (TupleRows::y_unused / msg_one)
-    enum { TAG, X, RR, S, AUX, PRE, AUX_OFF, AUX_NBLK, PRE_OFF, PRE_NBLK, PRE_ROW, PATCH,
+    enum { TAG, X, RR, S, EMAP, AUX, PRE, AUX_OFF, AUX_NBLK, PRE_OFF, PRE_NBLK, PRE_ROW, PATCH,
            TPL, CODE, TJOB, TXRAW, WTX, WJOB, HROW, HPROG, ZEROS, UPLOADED, Y = UPLOADED, M, V, AUXD, INTAB, TXD,
            NB };
-    bool need_y = false, need_m = false;
+    bool need_y = false, need_m = false, need_e = false;
     for (size_t p = 0; p < P; p++) {
         need_y |= !Rw[p]->y_unused && Rw[p]->size() != 0;
         need_m |= !Rw[p]->msg_one && Rw[p]->size() != 0;
+        need_e |= !Rw[p]->emap.empty();
     }
+    need_e = need_e && early_n_ != 0;  // early twins exist for this batch's call (early_launch)
     size_t sizes[NB] = {};
     sizes[TAG] = R; sizes[X] = sizes[Y] = sizes[RR] = sizes[S] = sizes[M] = 32 * R;
+    sizes[EMAP] = need_e ? 4 * R : 0;
     sizes[AUX] = auxb0[P]; sizes[PRE] = preb0[P];
     sizes[AUX_OFF] = sizes[AUX_NBLK] = 4 * n_aux_;
     sizes[PRE_OFF] = sizes[PRE_NBLK] = sizes[PRE_ROW] = 4 * n_pre_;
@@ -1037,6 +1135,7 @@ int DeviceBatch::stage_parts(const SighashJobs* const* J, const TupleRows* const
     d_txraw_ = a + off[TXRAW]; d_wtx_ = (WtxRec*)(a + off[WTX]); d_wjob_ = (WinJob*)(a + off[WJOB]);
     d_hrow_ = (uint32_t*)(a + off[HROW]); d_hprog_ = a + off[HPROG];
     d_zeros_ = a + off[ZEROS]; d_intab_ = (uint32_t*)(a + off[INTAB]); d_txd_ = a + off[TXD];
+    d_emap_ = need_e ? (uint32_t*)(a + off[EMAP]) : nullptr;
     uint8_t* h = (uint8_t*)host_image_;
     memset(h + off[ZEROS], 0, 64);
     // the rows of part p in [lo, hi): the bulk of a tuple batch, copied in blocks by the team
@@ -1052,6 +1151,7 @@ int DeviceBatch::stage_parts(const SighashJobs* const* J, const TupleRows* const
         cp(RR, 32 * r0, rw.r.data() + 32 * lo, 32 * nr);
         cp(S, 32 * r0, rw.s.data() + 32 * lo, 32 * nr);
         if (need_m && nr) rw.copy_msg(h + off[M] + 32 * r0, lo, hi);  // past the stored prefix: ONE
+        if (need_e && nr) rw.copy_emap((uint32_t*)(h + off[EMAP]) + r0, lo, hi);
     };
     // part p's jobs and key-hash records (offsets fixed up for the concatenation)
     auto fill = [&](size_t p) {
@@ -1353,7 +1453,14 @@ int DeviceBatch::run_stages(void* stream, const LateMsgFill* late) {
     BCC_HIP_TRY(hipEventRecord((hipEvent_t)ev_up_, side));  // the tuple rows are on the device
     if (int e = ecdsa_launch_pre(scratch_, d_tag, d_x, d_y, d_s, n_rows_, side)) return e;
     if (int e = ecdsa_launch_key(scratch_, d_tag, d_x, d_y, n_rows_, side)) return e;
-    if (int e = ecdsa_launch_q(scratch_, d_tag, d_x, d_y, d_r, d_s, n_rows_, side)) return e;
+    if (d_emap_ && early_n_) {  // rows with early twins: their K_keyq results are copied
+        BCC_HIP_TRY(hipStreamWaitEvent(side, (hipEvent_t)ev_early_, 0));
+        if (int e = ecdsa_launch_q_mapped(scratch_, early_scratch_, early_n_, d_emap_, d_tag, d_x, d_y,
+                                          d_r, d_s, n_rows_, side))
+            return e;
+    } else if (int e = ecdsa_launch_q(scratch_, d_tag, d_x, d_y, d_r, d_s, n_rows_, side)) {
+        return e;
+    }
     BCC_HIP_TRY(hipEventRecord((hipEvent_t)ev_join_, side));
     if (int e = launch_front(st)) return e;
     if (n_hash_) {
@@ -1411,6 +1518,24 @@ int gpu_verify_batch(int device, const SighashJobs& jobs, const TupleRows& rows,
 // one cached batch per (thread, device): repeated calls reuse the device arena, the pinned host
 // image, scratch and streams, and concurrent callers never share any of them
 thread_local std::vector<std::unique_ptr<DeviceBatch>> tl_batches;
+
+static DeviceBatch* thread_batch(int device) {
+    auto& cache = tl_batches;
+    if (device < 0) return nullptr;
+    if ((int)cache.size() <= device) cache.resize(device + 1);
+    if (!cache[device]) cache[device] = std::make_unique<DeviceBatch>(device);
+    return cache[device].get();
+}
+
+int gpu_early_launch(int device, const TupleRows* const* rows, size_t P) {
+    DeviceBatch* b = thread_batch(device);
+    if (!b) return (int)hipErrorInvalidDevice;
+    return b->early_launch(rows, P);
+}
+
+void gpu_early_reset(int device) {
+    if (device >= 0 && device < (int)tl_batches.size() && tl_batches[device]) tl_batches[device]->early_reset();
+}
 
 int gpu_verify_parts(int device, const SighashJobs* const* jobs, const TupleRows* const* rows,
                      size_t parts, uint8_t* verdict, double* stage_seconds, const LateMsgFill* late) {

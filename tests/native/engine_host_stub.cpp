@@ -5,6 +5,8 @@
 // the device pipeline (csrc/sighash.hip + ecdsa_verify.hip) with the ORACLE (oracle/bcc_oracle.c)
 // evaluating the very jobs the host built (unpad -> SHA-256d -> patch -> SHA-256d -> ECDSA).
 // It is linked only into tests/native/_build/engine_host.so, never into librbc_amd.so.
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -26,6 +28,43 @@ static void stub_ecdsa(const TupleRows& rows, const uint8_t* msg, uint8_t* verdi
 void set_stage_threads(unsigned) {}  // the device batch is stubbed out
 void release_device_thread_state() {}
 void release_tuple_thread_state() {}
+// Early Q halves: the stub keeps the calling thread's early rows and checks that every row the
+// engine maps to an early twin (TupleRows::emap) is that twin byte for byte (tag, x, y, r, s) --
+// the property DeviceBatch's K_keyq copy relies on; the verdicts are computed in full regardless.
+thread_local TupleRows tl_early;
+thread_local size_t tl_early_checked = 0;
+int gpu_early_launch(int, const TupleRows* const* rows, size_t P) {
+    tl_early.clear();
+    for (size_t p = 0; p < P; p++) {
+        TupleRows r = *rows[p];
+        r.materialize();
+        tl_early.tag.insert(tl_early.tag.end(), r.tag.begin(), r.tag.end());
+        tl_early.x.insert(tl_early.x.end(), r.x.begin(), r.x.end());
+        tl_early.y.insert(tl_early.y.end(), r.y.begin(), r.y.end());
+        tl_early.r.insert(tl_early.r.end(), r.r.begin(), r.r.end());
+        tl_early.s.insert(tl_early.s.end(), r.s.begin(), r.s.end());
+    }
+    return 0;
+}
+void gpu_early_reset(int) { tl_early.clear(); }
+static void check_early_twins(const TupleRows& rw) {  // rw materialized
+    for (size_t k = 0; k < rw.emap.size() && k < rw.size(); k++) {
+        const uint32_t e = rw.emap[k];
+        if (e == TupleRows::NO_EARLY) continue;
+        const bool same = e < tl_early.size() && rw.tag[k] == tl_early.tag[e] &&
+                          memcmp(&rw.x[32 * k], &tl_early.x[32 * (size_t)e], 32) == 0 &&
+                          (rw.tag[k] == 2 || rw.tag[k] == 3 ||
+                           memcmp(&rw.y[32 * k], &tl_early.y[32 * (size_t)e], 32) == 0) &&
+                          memcmp(&rw.r[32 * k], &tl_early.r[32 * (size_t)e], 32) == 0 &&
+                          memcmp(&rw.s[32 * k], &tl_early.s[32 * (size_t)e], 32) == 0;
+        if (!same) {
+            fprintf(stderr, "engine_host_stub: row %zu mapped to early row %u differs\n", k, e);
+            abort();
+        }
+        tl_early_checked++;
+    }
+}
+extern "C" size_t stub_early_checked(void) { return tl_early_checked; }
 // As DeviceBatch: the rows are copied (staged) first, the sighash jobs hash into the copy, then the
 // late rows (host-hashed while the device runs) land in it (put_late), then the ECDSA stage.
 int gpu_verify_parts(int, const SighashJobs* const* jobs, const TupleRows* const* rows, size_t parts,
@@ -35,6 +74,7 @@ int gpu_verify_parts(int, const SighashJobs* const* jobs, const TupleRows* const
     for (size_t p = 0; p < parts; p++) {
         staged[p] = *rows[p];
         staged[p].materialize();  // rows stored without y / msg (TupleRows::add_lazy): zero / ONE
+        check_early_twins(staged[p]);
         std::vector<uint8_t> m = staged[p].msg;
         stub_sighash(*jobs[p], m);
         msg.insert(msg.end(), m.begin(), m.end());
@@ -111,6 +151,14 @@ static void stub_sighash(const SighashJobs& j, std::vector<uint8_t>& msg) {
                  j.tpl.begin() + t.tpl_off + t.tpl_len);
         for (int b = 0; b < 4; b++) m.push_back((uint8_t)(t.hashtype >> (8 * b)));
         bcco_sha256d(m.data(), m.size(), &msg[32 * t.row]);
+        if (tpl_has_mid(t)) {  // the product's midstate path must give the same digest
+            uint8_t d[32];
+            host::tpl_job_sighash(j.tpl.data(), j.code.data(), t, d);
+            if (memcmp(d, &msg[32 * t.row], 32) != 0) {
+                fprintf(stderr, "engine_host_stub: template midstate digest mismatch (row %u)\n", t.row);
+                abort();
+            }
+        }
     }
     for (const WinJob& w : j.wjobs) {  // BIP143 from the raw tx: the oracle's own sighash
         const WtxRec& r = j.wtx[w.tx];

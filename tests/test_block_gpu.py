@@ -40,7 +40,7 @@ def test_block_workload_all_valid_and_matches_reference(wl, chain_blocks, bip143
         n_valid, ret = wl.verify_batch()
         st = B.last_batch_stats()
     finally:
-        B.set_host_chain_blocks(260)
+        B.set_host_chain_blocks(B.HOST_CHAIN_BLOCKS_DEFAULT)
         B.set_host_bip143_blocks(32)
     assert (st["host_hashed"] > 0) == (chain_blocks + bip143_blocks > 0)
     assert n_valid == wl.n and all(r == 1 for r in ret)
@@ -67,7 +67,7 @@ def test_block_workload_mutations_match_reference(wl, chain_blocks):
         if chain_blocks:
             assert B.last_batch_stats()["host_hashed"] > 0
     finally:
-        B.set_host_chain_blocks(260)
+        B.set_host_chain_blocks(B.HOST_CHAIN_BLOCKS_DEFAULT)
 
 
 def _mutations(B, wl):

@@ -20,6 +20,7 @@ from fixtures import load_json
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 SO = os.path.join(HERE, "native", "_build", "engine_host.so")
+HOST_CHAIN_BLOCKS_DEFAULT = 160  # engine.cpp g_host_chain_blocks
 
 
 class Item(ctypes.Structure):
@@ -161,7 +162,7 @@ def test_script_cases_host_hashed_chains(eng, blocks):
             test_script_cases_single_calls(eng)
             test_crate_vectors(eng)
     finally:
-        eng.bcc_set_host_chain_blocks(260)
+        eng.bcc_set_host_chain_blocks(HOST_CHAIN_BLOCKS_DEFAULT)
         eng.bcc_set_host_bip143_blocks(32)
 
 
@@ -445,3 +446,100 @@ def test_pubkey_verify_batch_sharded(eng):
         engine_stub.set_devices(eng, [])
     assert many == one
     assert list(one) == [t["verdict"] for t in ts]
+
+
+def _many_input_legacy_tx(R, O, n_in, seed):
+    """A version-1 tx with n_in P2PKH inputs signed SIGHASH_ALL by the reference; returns
+    (tx bytes, [spk per input])."""
+    import hashlib
+    import random
+    from script_asm import hash160
+    rng = random.Random(seed)
+
+    def ser_var(n):
+        return bytes([n]) if n < 253 else b"\xfd" + n.to_bytes(2, "little")
+
+    def push(b):
+        return (bytes([len(b)]) if len(b) < 76 else b"\x4c" + bytes([len(b)])) + b
+
+    keys, spks = [], []
+    for i in range(n_in):
+        sk = hashlib.sha256(b"tplmid%d-%d" % (seed, i)).digest()
+        pub = R.pubkey_create(sk, compressed=(i % 3 != 0))
+        h = hash160(pub)
+        keys.append((sk, pub))
+        spks.append(b"\x76\xa9\x14" + h + b"\x88\xac")
+    prev = [rng.randbytes(32) + rng.getrandbits(8).to_bytes(4, "little") for _ in range(n_in)]
+    outs = b"".join((1000 + k).to_bytes(8, "little") + push(b"\x76\xa9\x14" + rng.randbytes(20) + b"\x88\xac")
+                    for k in range(2))
+
+    def ser(script_sigs):
+        v = (1).to_bytes(4, "little") + ser_var(n_in)
+        for i in range(n_in):
+            v += prev[i] + ser_var(len(script_sigs[i])) + script_sigs[i] + b"\xff\xff\xff\xff"
+        return v + ser_var(2) + outs + (0).to_bytes(4, "little")
+
+    unsigned = ser([b""] * n_in)
+    sigs = []
+    for i in range(n_in):
+        m = O.sighash(unsigned, i, spks[i], 1, 0, 0)
+        sigs.append(push(R.sign(keys[i][0], m) + b"\x01") + push(keys[i][1]))
+    return ser(sigs), spks
+
+
+@pytest.mark.parametrize("chain_blocks,early", [(0, 1), (1, 1), (12, 0), (160, 1), (160, 0)])
+def test_many_input_legacy_tx_template_midstates(eng, chain_blocks, early):
+    """Legacy txs of 12..90 P2PKH inputs (templates of 8..58 blocks: every job carries the
+    template midstates, TPL_MID) through verify_batch: the stub evaluates each template job from
+    the full preimage with the oracle and aborts if the product's midstate path disagrees; jobs
+    whose remaining blocks exceed chain_blocks are hashed on the host from their midstate.  All
+    inputs valid, and a byte flipped in the 40-input tx's first inputs or the 90-input tx's first
+    outpoint gives the reference's (ret, err) for every input.  early: the P2PKH (key, signature)
+    pairs are pre-extracted (bcc_set_early_q) and every deferred row is mapped to its early twin,
+    which the stub checks byte for byte (engine_host_stub.cpp check_early_twins)."""
+    from oracle_ctypes import Oracle, Reference, reference_available
+    if not reference_available():
+        pytest.skip("oracle/_ref not built")
+    R, O = Reference(), Oracle()
+    eng.bcc_set_host_chain_blocks.argtypes = [ctypes.c_uint]
+    txs = [_many_input_legacy_tx(R, O, n, 11 + n) for n in (12, 40, 90)]
+    # mutations: byte 200 of the 40-input tx (its first inputs), an outpoint byte of input 0
+    tx40 = bytearray(txs[1][0])
+    tx40[200] ^= 0x01
+    tx90 = bytearray(txs[2][0])
+    tx90[5 + 3] ^= 0x10
+    txs += [(bytes(tx40), txs[1][1]), (bytes(tx90), txs[2][1])]
+    items, keep, exp = [], [], []
+    for tx, spks in txs:
+        bt = ctypes.create_string_buffer(tx, len(tx))
+        keep.append(bt)
+        for i, spk in enumerate(spks):
+            bs = ctypes.create_string_buffer(spk, len(spk))
+            keep.append(bs)
+            items.append(Item(ctypes.addressof(bs), len(spk), 0, ctypes.addressof(bt), len(tx), i))
+            exp.append(R.verify_script_with_amount(spk, 0, tx, i, 0x805))
+    arr = (Item * len(items))(*items)
+    ret = (ctypes.c_int * len(arr))()
+    err = (ctypes.c_int * len(arr))()
+    eng.bcc_set_early_q.argtypes = [ctypes.c_int]
+    eng.stub_early_checked.restype = ctypes.c_size_t
+    checked0 = eng.stub_early_checked()
+    try:
+        eng.bcc_set_host_chain_blocks(chain_blocks)
+        eng.bcc_set_early_q(early)
+        eng.bitcoinconsensus_verify_batch(arr, len(arr), 0x805, ret, err)
+        st = Stats()
+        eng.bcc_last_batch_stats(ctypes.byref(st))
+    finally:
+        eng.bcc_set_host_chain_blocks(HOST_CHAIN_BLOCKS_DEFAULT)
+        eng.bcc_set_early_q(1)
+    assert list(zip(ret, err)) == exp
+    if early:
+        # every input is a P2PKH spend with one check: one early row each, and the first round's
+        # rows (the only round) all mapped to their twins
+        assert st.early_rows == len(items) and st.early_mapped == len(items)
+        assert eng.stub_early_checked() - checked0 == len(items)
+    else:
+        assert st.early_rows == 0 and st.early_mapped == 0
+    # the originals all valid; both flips sit in bytes every legacy preimage of their tx contains
+    assert sum(r for r, _ in exp) == 12 + 40 + 90
