@@ -457,8 +457,8 @@ class TupleJob:
 
     def end_to_end(self, h, reps=2):
         """The same n tuples through bcc_pubkey_verify_batch from host buffers: N x
-        CPubKey(pub).Verify(hash, sig) (pubkey.cpp:191-207): host length filter + lax DER, H2D,
-        kernels, verdicts back.  Reported beside value, never as value."""
+        CPubKey(pub).Verify(hash, sig) (pubkey.cpp:191-207): the caller's blobs copied and uploaded as
+        they are, the length filter + lax DER on the device (K_der), kernels, verdicts back.  Reported beside value, never as value."""
         import ctypes
         import numpy as np
         import bitcoinconsensus_amd as BB

@@ -567,8 +567,8 @@ def _blob(parts):
 
 def pubkey_verify_batch(tuples, device=0):
     """[CPubKey(pub).Verify(hash32, der_sig) for (pub, hash32, der_sig) in tuples] as a bytes of
-    0/1 (depend/bitcoin/src/pubkey.cpp:191-207): length filter + lax DER on the host, the
-    secp256k1 work on the GPU (include/bcc_amd.h bcc_pubkey_verify_batch).  device=-1 shards the
+    0/1 (depend/bitcoin/src/pubkey.cpp:191-207): length filter + lax DER on the GPU (K_der,
+    over the blobs as they are), the secp256k1 work on the GPU (include/bcc_amd.h bcc_pubkey_verify_batch).  device=-1 shards the
     tuples over the set_devices() GPUs."""
     n = len(tuples)
     if n == 0:

@@ -866,20 +866,26 @@ int ecdsa_launch_key(SigScratch& sc, const uint8_t* d_tag, const uint8_t* d_x,
 // CU's 160 KiB LDS (unused): the sighash kernels' groups (8.4 KB of LDS each) go to other CUs.
 constexpr size_t KEYQ_EXCLUSIVE_LDS = 152 * 1024;
 
-static bool reserve_lds(const void* kernel, const char* name) {
-    const hipError_t e = hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                             (int)KEYQ_EXCLUSIVE_LDS);
-    if (e == hipSuccess) return true;
+// The dynamic LDS that makes a group's total KEYQ_EXCLUSIVE_LDS (the kernel's static LDS counts:
+// the two-lane kernel's low occupancy lets hipcc keep ~49 KiB of lane temporaries in LDS), or 0.
+static size_t reserve_lds(const void* kernel, const char* name) {
+    hipFuncAttributes fa;
+    size_t fixed = 0;
+    if (hipFuncGetAttributes(&fa, kernel) == hipSuccess) fixed = fa.sharedSizeBytes;
+    else (void)hipGetLastError();
+    const size_t dyn = fixed < KEYQ_EXCLUSIVE_LDS ? KEYQ_EXCLUSIVE_LDS - fixed : 0;
+    const hipError_t e = hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn);
+    if (e == hipSuccess) return dyn;
     (void)hipGetLastError();
     fprintf(stderr, "[bcc] %s: no %zu-byte LDS reservation on this device (%s); small rounds "
-                    "share CUs with the sighash kernels\n", name, KEYQ_EXCLUSIVE_LDS, hipGetErrorString(e));
-    return false;
+                    "share CUs with the sighash kernels\n", name, dyn, hipGetErrorString(e));
+    return 0;
 }
 
 static size_t keyq_lds(size_t groups, int cus, bool two_lane = false) {
-    static const bool ok1 = reserve_lds((const void*)&twist_keyq_kernel, "K_keyq");
-    static const bool ok2 = reserve_lds((const void*)&twist_keyq2_kernel, "K_keyq2");
-    return (two_lane ? ok2 : ok1) && groups <= (size_t)cus ? KEYQ_EXCLUSIVE_LDS : 0;
+    static const size_t dyn1 = reserve_lds((const void*)&twist_keyq_kernel, "K_keyq");
+    static const size_t dyn2 = reserve_lds((const void*)&twist_keyq2_kernel, "K_keyq2");
+    return groups <= (size_t)cus ? (two_lane ? dyn2 : dyn1) : 0;
 }
 
 // K_keyq or, for a round of at most one wave per SIMD at two lanes per tuple, its latency mode

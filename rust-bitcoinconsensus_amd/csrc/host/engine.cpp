@@ -634,7 +634,7 @@ public:
         return true;  // speculative
     }
 
-    // legacy_host: legacy chains may go to the host (single-GPU rounds, chunk_interpret)
+    // legacy_host: legacy chains may go to the host (chunk_interpret: every round, one or more GPUs)
     void reset(bool legacy_host = true) {
         jobs.clear();
         rows.clear();
@@ -706,17 +706,23 @@ void hash_host_jobs(std::vector<Round>& rds, unsigned T, unsigned maxW = 0) {
 // A round's offloaded jobs hashed while the device runs (single-GPU rounds): the device round
 // calls ensure() through its LateMsgFill once the message-independent kernels are queued; every
 // host path that needs the messages calls it first.  Hashes once per interpreter pass.
+// Round 5: the device workers of a multi-GPU round call ensure() concurrently (the first hashes on
+// its team, the others wait for it), and the hashing time is kept here for the caller's statistics
+// (chunk_finish), not added to the calling thread's t_stats: on a pipeline or device worker that
+// would have been the worker's.
 struct LateHost {
     std::vector<Round>* rds = nullptr;
     unsigned T = 0;
     bool done = false;
-    unsigned W = 0;  // worker threads (0: at most T)
+    unsigned W = 0;       // worker threads (0: at most T)
+    double seconds = 0;   // hashing time, collected by chunk_finish
+    std::shared_ptr<std::mutex> mu = std::make_shared<std::mutex>();
     void ensure() {
+        std::lock_guard<std::mutex> lk(*mu);
         if (done) return;
         auto h0 = std::chrono::steady_clock::now();
         hash_host_jobs(*rds, T, W);
-        t_stats.host_jobs_seconds +=
-            std::chrono::duration<double>(std::chrono::steady_clock::now() - h0).count();
+        seconds += std::chrono::duration<double>(std::chrono::steady_clock::now() - h0).count();
         done = true;
     }
 };
@@ -1131,10 +1137,6 @@ int run_device_round(const std::vector<Round>& rds, unsigned T, const std::vecto
         return host_verify_parts(pj.data(), pr.data(), T, verdict, host_threads());
     }
     const std::vector<int> devs = device_list();
-    if (late && devs.size() != 1) {  // the late hook is for single-GPU rounds (chunk_interpret)
-        late->ensure();
-        late = nullptr;
-    }
     std::vector<size_t> w(T);
     for (unsigned t = 0; t < T; t++) w[t] = rds[t].pending.size();
     const size_t D = std::min<size_t>(devs.size(), T);
@@ -1204,12 +1206,11 @@ inline double process_cpu() {
 void chunk_interpret(ChunkRun& c) {
     std::vector<char> ran(c.T, 0);
     auto i0 = clk::now();
-    const bool one_gpu = device_list().size() == 1;
     c.host_planned->store(0, std::memory_order_relaxed);
     std::vector<double> ts(c.T, 0);
     run_shards(c.T, c.W, [&](unsigned t) {
         auto s0 = clk::now();
-        c.rds[t].reset(one_gpu);
+        c.rds[t].reset(true);
         c.rds[t].host.planned = c.host_planned.get();
         ran[t] = interpret_shard(c.b, c.run_list[t], c.rds[t]);
         ts[t] = since(s0);
@@ -1222,14 +1223,11 @@ void chunk_interpret(ChunkRun& c) {
     }
     t_stats.interpret_shard_max_seconds += tmax;
     t_stats.interpret_shard_mean_seconds += tsum / c.T;
-    // the offloaded jobs' rows are marked now; single-GPU rounds hash the jobs themselves while the
-    // device runs the message-independent kernels (LateHost), multi-GPU rounds before the round
+    // the offloaded jobs' rows are marked now; the host hashes the jobs while the device(s) run the
+    // message-independent kernels (LateHost; every device worker's round waits for them)
+    t_stats.host_jobs_seconds += c.late.seconds;  // a previous pass's hashing (pipelined chunks)
     c.late = LateHost{&c.rds, c.T, false, c.W};
     c.late_pending = mark_host_rows(c.rds, c.T);
-    if (c.late_pending && device_list().size() != 1) {
-        c.late.ensure();
-        c.late_pending = false;
-    }
     size_t npend = 0;
     bool any = false;
     for (unsigned t = 0; t < c.T; t++) {
@@ -1438,6 +1436,8 @@ long chunk_finish(ChunkRun& c, int* ret_out, bitcoinconsensus_error* err_out, bo
         }
         *gpu_s += since(g0);
         t_stats.process_cpu_in_gpu_wait_seconds += process_cpu() - p0;
+        t_stats.host_jobs_seconds += c.late.seconds;  // hashed during the round, maybe on a worker
+        c.late.seconds = 0;
         t_stats.stage_seconds += c.stage_s;
         t_stats.device_retries += c.retries;
         t_stats.host_rounds += c.host_rounds;

@@ -1,11 +1,16 @@
 // Tuple level of the hot path, without a script around it: bcc_pubkey_verify_batch =
 // N x CPubKey(pub).Verify(hash, sig) (pubkey.cpp:191-207).  The CPubKey length filter
-// (pubkey.h:58-94), lax DER (pubkey.cpp:28-168) and the r / s == 0 rule are decided on the host,
-// threaded; every surviving tuple goes to the GPU ECDSA kernels (normalisation is implicit: the
-// verdict is invariant under s -> n - s).
+// (pubkey.h:58-94), lax DER (pubkey.cpp:28-168) and the r / s == 0 rule are decided on the device
+// (round 5: K_der, der.hip, over the caller's blobs copied as they are); the host restatement here
+// (parse_rows) serves small rounds on the host lane code and the device-failure path.  Every
+// surviving tuple goes to the GPU ECDSA kernels (normalisation is implicit: the verdict is
+// invariant under s -> n - s).
 #include "tuples.h"
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <thread>
 #include <memory>
@@ -76,7 +81,8 @@ void parse_rows(const uint8_t* pub_blob, const uint64_t* pub_off, const uint8_t*
 // fresh vectors on one thread before the parallel parse, and unmaps them afterwards.
 thread_local bcc::TupleRows tl_pubkey_rows;
 
-// The pipelined form (tuple_rounds): two row sets and two staged device rounds per thread.
+// The pipelined form (tuple_rounds): two staged device rounds per thread (and the host rows a
+// failed round is re-run from).
 struct TupleSlot {
     bcc::TupleRows rows;
     std::unique_ptr<bcc::StagedRound, void (*)(bcc::StagedRound*)> staged{nullptr,
@@ -84,6 +90,12 @@ struct TupleSlot {
     int dev = -1;
     size_t lo = 0, n = 0;  // the rows' range in the caller's arrays (n == 0: nothing in flight)
 };
+
+// A round's raw tuples go to the device as they are (K_der) unless their blobs are unusually large
+// (more than DER_BLOB_LIMIT bytes for the round: the pinned image would grow with them); such a round
+// is parsed on the host (parse_rows) and its fixed-size rows staged instead.
+constexpr uint64_t DER_BLOB_LIMIT = (uint64_t)1 << 31;
+bool der_on_device(const bcc::DerTuples& t) { return t.pub_bytes() + t.sig_bytes() <= DER_BLOB_LIMIT; }
 thread_local TupleSlot tl_tuple_slots[2];
 
 void release_pubkey_rows() {
@@ -107,48 +119,122 @@ int tuple_round(int dev, const bcc::TupleRows& rows, uint8_t* verdict) {
                            "pubkey_verify_batch");
 }
 
-// Rounds of about TUPLE_ROUND tuples, pipelined: round k's rows are parsed and staged on the
+// Pipelined rounds (sizes below): round k's raw tuples are copied into its pinned image by the
 // calling thread's team while round k - 1 runs, and round k's upload (its own device batch and
 // streams) runs beside round k - 1's kernels.  A staging or device error sends the round through
-// tuple_round (retry on a fresh batch, then the failure policy).
+// the host parse and tuple_round (retry on a fresh batch, then the failure policy).  Measured on
+// 8M C4 tuples (profiles/r05/c4_der): 256k-first doubling to 2M rounds 100-101 M/s, fixed 1M
+// rounds 90 M/s, a 4M cap 95 M/s; the host side is ~13 ms of copying in ~80 ms.
 constexpr size_t TUPLE_ROUND = (size_t)1 << 20;
+static size_t env_size(const char* name, size_t dflt) {
+    const char* e = getenv(name);
+    return e && atoll(e) > 0 ? (size_t)atoll(e) : dflt;
+}
+// Round sizes: the first round (the only one whose staging and upload the GPU waits for) is small,
+// and each next one doubles up to the cap while the previous round's kernels hide its staging and
+// upload (~1 + 2.8 ms per 1M tuples against ~8 ms of kernels); a remainder under half the cap joins
+// the last round (fewer kernel tails).
+static const size_t g_tuple_first = env_size("BCC_TUPLE_FIRST", TUPLE_ROUND / 4);
+static const size_t g_tuple_round = env_size("BCC_TUPLE_ROUND", 2 * TUPLE_ROUND);
+static const bool g_tuple_ramp = env_size("BCC_TUPLE_RAMP", 1) != 0;
+static const bool g_tuple_trace = getenv("BCC_TUPLE_TRACE") != nullptr;
+
+// Raw tuples [lo, lo + m) of the caller's arrays.
+static bcc::DerTuples der_range(const uint8_t* pub_blob, const uint64_t* pub_off, const uint8_t* msg32,
+                                const uint8_t* sig_blob, const uint64_t* sig_off, size_t lo, size_t m) {
+    bcc::DerTuples t;
+    t.pub_blob = pub_blob;
+    t.pub_off = pub_off + lo;
+    t.msg32 = msg32 + 32 * lo;
+    t.sig_blob = sig_blob;
+    t.sig_off = sig_off + lo;
+    t.n = m;
+    return t;
+}
+
+// One round of raw tuples: K_der + the kernels on the device; a host-lane round, an oversized
+// blob or a device error (retried on a fresh batch, then the failure policy: tuple_round) goes
+// through the host rows.
+int der_round(int dev, const bcc::DerTuples& t, bcc::TupleRows& rows, uint8_t* verdict) {
+    if (t.n > host_small_round() && der_on_device(t) && injected_device_fault() == 0 &&
+        bcc::gpu_verify_der(dev, t, verdict) == 0)
+        return 0;
+    parse_rows(t.pub_blob, t.pub_off, t.msg32, t.sig_blob, t.sig_off, t.n, rows);
+    return tuple_round(dev, rows, verdict);
+}
 
 int tuple_rounds(int dev, const uint8_t* pub_blob, const uint64_t* pub_off, const uint8_t* msg32,
                  const uint8_t* sig_blob, const uint64_t* sig_off, size_t n, uint8_t* verdict) {
+    auto host_rows = [&](TupleSlot& s) -> bcc::TupleRows& {  // a failed round's rows, on the host
+        const bcc::DerTuples t = der_range(pub_blob, pub_off, msg32, sig_blob, sig_off, s.lo, s.n);
+        parse_rows(t.pub_blob, t.pub_off, t.msg32, t.sig_blob, t.sig_off, t.n, s.rows);
+        return s.rows;
+    };
     auto finish = [&](TupleSlot& s) -> int {
         if (s.n == 0) return 0;
         const size_t lo = s.lo;
+        if (bcc::gpu_staged_finish(s.staged.get(), verdict + lo) == 0) {
+            s.n = 0;
+            return 0;
+        }
+        bcc::TupleRows& rows = host_rows(s);
         s.n = 0;
-        if (bcc::gpu_staged_finish(s.staged.get(), verdict + lo) == 0) return 0;
-        return tuple_round(dev, s.rows, verdict + lo);
+        return tuple_round(dev, rows, verdict + lo);
     };
     int err = 0;
     size_t k = 0;
-    for (size_t lo = 0; lo < n && !err; lo += TUPLE_ROUND, k++) {
+    using clk = std::chrono::steady_clock;
+    auto sec = [](clk::time_point a) { return std::chrono::duration<double>(clk::now() - a).count(); };
+    const auto c0 = clk::now();
+    double t_stage = 0, t_wait = 0;
+    size_t m = 0;
+    for (size_t lo = 0; lo < n && !err; lo += m, k++) {
         TupleSlot& s = tl_tuple_slots[k & 1];
-        const size_t m = std::min(TUPLE_ROUND, n - lo);
+        m = k == 0 ? g_tuple_first : g_tuple_ramp ? std::min(2 * m, g_tuple_round) : g_tuple_round;
+        if (m >= n - lo || n - lo - m < m / 2) m = n - lo;
+        auto w0 = clk::now();
         if (int e = finish(s)) err = e;  // (only after an error) this slot's last round
-        parse_rows(pub_blob, pub_off + lo, msg32 + 32 * lo, sig_blob, sig_off + lo, m, s.rows);
+        t_wait += sec(w0);
+        w0 = clk::now();
         if (!s.staged || s.dev != dev) {
             s.staged.reset(bcc::gpu_staged_new(dev));
             s.dev = dev;
         }
-        const bcc::SighashJobs none;
-        const bcc::SighashJobs* jp = &none;
-        const bcc::TupleRows* rp = &s.rows;
+        const bcc::DerTuples t = der_range(pub_blob, pub_off, msg32, sig_blob, sig_off, lo, m);
         double st = 0;
         s.lo = lo;
         s.n = m;
-        if (injected_device_fault() != 0 ||
-            bcc::gpu_staged_stage(s.staged.get(), &jp, &rp, 1, &st) != 0 ||
-            bcc::gpu_staged_launch(s.staged.get(), nullptr) != 0) {
-            s.n = 0;
-            if (int e = tuple_round(dev, s.rows, verdict + lo)) err = e;
+        bool staged;
+        if (der_on_device(t)) {
+            staged = injected_device_fault() == 0 &&
+                     bcc::gpu_staged_stage_der(s.staged.get(), t, &st) == 0 &&
+                     bcc::gpu_staged_launch(s.staged.get(), nullptr) == 0;
+        } else {  // oversized blobs: host rows, staged
+            parse_rows(t.pub_blob, t.pub_off, t.msg32, t.sig_blob, t.sig_off, m, s.rows);
+            const bcc::SighashJobs none;
+            const bcc::SighashJobs* jp = &none;
+            const bcc::TupleRows* rp = &s.rows;
+            staged = injected_device_fault() == 0 &&
+                     bcc::gpu_staged_stage(s.staged.get(), &jp, &rp, 1, &st) == 0 &&
+                     bcc::gpu_staged_launch(s.staged.get(), nullptr) == 0;
         }
+        if (!staged) {
+            bcc::TupleRows& rows = host_rows(s);
+            s.n = 0;
+            if (int e = tuple_round(dev, rows, verdict + lo)) err = e;
+        }
+        t_stage += sec(w0);
+        w0 = clk::now();
         if (int e = finish(tl_tuple_slots[(k + 1) & 1])) err = err ? err : e;  // round k - 1
+        t_wait += sec(w0);
     }
+    const auto w0 = clk::now();
     for (auto& s : tl_tuple_slots)
         if (int e = finish(s)) err = err ? err : e;
+    t_wait += sec(w0);
+    if (g_tuple_trace)
+        fprintf(stderr, "[bcc] tuple_rounds: %zu tuples, %zu rounds, %.2f ms: stage+launch %.2f ms, "
+                        "waits %.2f ms\n", n, k, 1e3 * sec(c0), 1e3 * t_stage, 1e3 * t_wait);
     return err;
 }
 
@@ -161,6 +247,7 @@ extern "C" int bcc_pubkey_verify_batch(const uint8_t* pub_blob, const uint64_t* 
                                        int device) {
     if (n == 0) return 0;
     if (!pub_off || !sig_off || !msg32 || !verdict) return -1;
+    if (pub_off[n] < pub_off[0] || sig_off[n] < sig_off[0]) return -1;  // offsets run backwards
     bcc::host::ActiveCaller active;
     std::vector<int> devs = device < 0 ? bcc::host::device_list() : std::vector<int>{device};
     const size_t D = std::min<size_t>(devs.size(), (n + 4095) / 4096);
@@ -168,13 +255,13 @@ extern "C" int bcc_pubkey_verify_batch(const uint8_t* pub_blob, const uint64_t* 
     for (size_t d = 0; d < D; d++) {
         const size_t lo = n * d / D, hi = n * (d + 1) / D;
         jobs.push_back([=] {  // contiguous equal range on devs[d] (offsets stay absolute)
-            if (hi - lo >= 2 * bcc::host::TUPLE_ROUND)
+            if (hi - lo >= 2 * bcc::host::g_tuple_first)
                 return bcc::host::tuple_rounds(devs[d], pub_blob, pub_off + lo, msg32 + 32 * lo,
                                                sig_blob, sig_off + lo, hi - lo, verdict + lo);
-            bcc::TupleRows& rows = bcc::host::tl_pubkey_rows;
-            bcc::host::parse_rows(pub_blob, pub_off + lo, msg32 + 32 * lo, sig_blob, sig_off + lo,
-                                  hi - lo, rows);
-            return bcc::host::tuple_round(devs[d], rows, verdict + lo);
+            return bcc::host::der_round(devs[d],
+                                        bcc::host::der_range(pub_blob, pub_off, msg32, sig_blob,
+                                                             sig_off, lo, hi - lo),
+                                        bcc::host::tl_pubkey_rows, verdict + lo);
         });
     }
     devs.resize(D);

@@ -443,6 +443,25 @@ int ecdsa_launch_after_pre(SigScratch& sc, const uint8_t* d_tag, const uint8_t* 
 int schnorr_launch(SigScratch& sc, const uint8_t* d_sig64, const uint8_t* d_msg32,
                    const uint8_t* d_xonly32, uint8_t* d_verdict, size_t n, void* stream);
 
+// Raw CPubKey::Verify tuples of bcc_pubkey_verify_batch (round 5): the caller's blobs as they are,
+// parsed on the device by K_der (der.hip: the length filter, lax DER, r / s == 0) into the rows the
+// ECDSA kernels read, so that the host only copies bytes.  Offsets are absolute (n + 1 each).
+struct DerTuples {
+    const uint8_t* pub_blob = nullptr;
+    const uint64_t* pub_off = nullptr;
+    const uint8_t* msg32 = nullptr;
+    const uint8_t* sig_blob = nullptr;
+    const uint64_t* sig_off = nullptr;
+    size_t n = 0;
+    uint64_t pub_bytes() const { return pub_off[n] - pub_off[0]; }
+    uint64_t sig_bytes() const { return sig_off[n] - sig_off[0]; }
+};
+// K_der over n tuples whose blobs / offsets are in HBM (blob bytes [0, *_bytes) hold offsets
+// [*_base, *_base + *_bytes)): rows tag / x / y / r / s.
+int der_launch(const uint8_t* pub, const uint64_t* pub_off, uint64_t pub_base, uint64_t pub_bytes,
+               const uint8_t* sig, const uint64_t* sig_off, uint64_t sig_base, uint64_t sig_bytes,
+               size_t n, uint8_t* tag, uint8_t* x, uint8_t* y, uint8_t* r, uint8_t* s, void* stream);
+
 // Device-resident batch (one per device / per caller thread).  stage() uploads, run() only
 // launches kernels (graph-capturable: no allocation, no synchronisation, once the scratch has
 // grown to the batch).  A null stream means the batch's own non-blocking stream.
@@ -459,6 +478,8 @@ public:
     int stage(const SighashJobs& jobs, const TupleRows& rows);
     // the concatenation of P parts (row / message / job indices fixed up per part)
     int stage_parts(const SighashJobs* const* jobs, const TupleRows* const* rows, size_t P);
+    // raw tuples (DerTuples): blobs, offsets and messages staged; run() starts with K_der
+    int stage_der(const DerTuples& t);
     int run(void* stream, const LateMsgFill* late = nullptr);  // K1..K4
     int run_sighash(void* stream);               // K1..K3 only
     int run_ecdsa(void* stream);                 // K4 only
@@ -530,6 +551,11 @@ private:
     uint32_t* d_hrow_ = nullptr;
     uint8_t* d_hprog_ = nullptr;
     uint32_t* d_emap_ = nullptr;  // staged TupleRows::emap (null: no row has an early twin)
+    // stage_der: the rows come from K_der over these (n_der_ = 0: rows staged by stage_parts)
+    size_t n_der_ = 0;
+    const uint8_t *d_pub_ = nullptr, *d_sig_ = nullptr;
+    const uint64_t *d_pub_off_ = nullptr, *d_sig_off_ = nullptr;
+    uint64_t pub_base_ = 0, pub_bytes_ = 0, sig_base_ = 0, sig_bytes_ = 0;
 
 public:
     // Early Q halves (round 5): the key half, u2 and the Q ladder (K_inv + K_keyq) of a call's
@@ -582,6 +608,10 @@ void gpu_staged_free(StagedRound* s);
 // Fills s's pinned image from the parts (which must stay unchanged until gpu_staged_run returns).
 int gpu_staged_stage(StagedRound* s, const SighashJobs* const* jobs, const TupleRows* const* rows,
                      size_t parts, double* stage_seconds);
+// Fills s's pinned image with raw tuples (DeviceBatch::stage_der; the caller's buffers are copied).
+int gpu_staged_stage_der(StagedRound* s, const DerTuples& t, double* stage_seconds);
+// One synchronous round of raw tuples on the calling thread's batch of `device`.
+int gpu_verify_der(int device, const DerTuples& t, uint8_t* verdict);
 // Runs the staged round on the calling thread (any thread): verdict rows in order.  On an error
 // the batch is dropped (the next stage starts from a fresh one).
 int gpu_staged_run(StagedRound* s, uint8_t* verdict, const LateMsgFill* late);

@@ -1034,6 +1034,7 @@ int DeviceBatch::stage(const SighashJobs& j, const TupleRows& rows) {
 // jobs and no pageable-memory staging.
 int DeviceBatch::stage_parts(const SighashJobs* const* J, const TupleRows* const* Rw, size_t P) {
     if (int e = sync()) return e;  // the previous run may still read the arena / the image
+    n_der_ = 0;
     std::vector<size_t> row0(P + 1, 0), auxb0(P + 1, 0), preb0(P + 1, 0), auxi0(P + 1, 0),
         prei0(P + 1, 0), pat0(P + 1, 0), tpl0(P + 1, 0), code0(P + 1, 0), tj0(P + 1, 0),
         raw0(P + 1, 0), wtx0(P + 1, 0), wj0(P + 1, 0), win0(P + 1, 0), h0(P + 1, 0);
@@ -1250,6 +1251,86 @@ int DeviceBatch::stage_parts(const SighashJobs* const* J, const TupleRows* const
     return 0;
 }
 
+// Raw tuples (bcc_pubkey_verify_batch from host buffers): the caller's pubkey / signature blobs,
+// both offset arrays and the messages are copied as they are into the pinned image (by the team, in
+// 2 MiB pieces), go up in one DMA copy, and K_der writes the rows on the device (run_ecdsa).  The
+// host neither parses nor touches a row.
+int DeviceBatch::stage_der(const DerTuples& t) {
+    if (int e = sync()) return e;
+    const size_t R = t.n;
+    const uint64_t pb = t.pub_bytes(), sb = t.sig_bytes();
+    n_rows_ = R;
+    n_pre_ = n_aux_ = n_patch_ = pre_blocks_ = aux_blocks_ = n_tjob_ = tjob_blocks_ = 0;
+    n_wtx_ = n_wjob_ = n_win_ = n_hash_ = sighash_bytes_ = 0;
+    d_emap_ = nullptr;
+    n_der_ = 0;
+    enum { PUB, SIG, POFF, SOFF, M, UPLOADED, TAG = UPLOADED, X, Y, RR, S, V, NB };
+    size_t sizes[NB] = {};
+    sizes[PUB] = pb; sizes[SIG] = sb; sizes[POFF] = sizes[SOFF] = 8 * (R + 1);
+    sizes[M] = sizes[X] = sizes[Y] = sizes[RR] = sizes[S] = 32 * R;
+    sizes[TAG] = sizes[V] = R;
+    size_t off[NB], total = 0;
+    for (int i = 0; i < NB; i++) {
+        off[i] = total;
+        total += align256(sizes[i]);
+    }
+    const size_t upload = off[UPLOADED];
+    if (total > cap_) {
+        if (arena_) BCC_HIP_TRY(hipFree(arena_));
+        arena_ = nullptr;
+        cap_ = 0;
+        BCC_HIP_TRY(hipMalloc(&arena_, total));
+        cap_ = total;
+    }
+    if (upload > host_cap_) {
+        if (host_image_) BCC_HIP_TRY(hipHostFree(host_image_));
+        host_image_ = nullptr;
+        host_cap_ = 0;
+        BCC_HIP_TRY(hipHostMalloc(&host_image_, upload, hipHostMallocDefault));
+        host_cap_ = upload;
+    }
+    uint8_t* a = (uint8_t*)arena_;
+    d_tag = a + off[TAG]; d_x = a + off[X]; d_y = a + off[Y]; d_r = a + off[RR]; d_s = a + off[S];
+    d_m = a + off[M]; d_v = a + off[V];
+    d_pub_ = a + off[PUB]; d_sig_ = a + off[SIG];
+    d_pub_off_ = (const uint64_t*)(a + off[POFF]); d_sig_off_ = (const uint64_t*)(a + off[SOFF]);
+    uint8_t* h = (uint8_t*)host_image_;
+    struct Piece {
+        uint8_t* dst;
+        const uint8_t* src;
+        size_t len;
+    };
+    std::vector<Piece> work;
+    constexpr size_t PIECE = (size_t)2 << 20;
+    auto add = [&](int b, const void* src, size_t len) {
+        for (size_t o = 0; o < len; o += PIECE)
+            work.push_back(Piece{h + off[b] + o, (const uint8_t*)src + o, std::min(PIECE, len - o)});
+    };
+    add(PUB, t.pub_blob + t.pub_off[0], pb);
+    add(SIG, t.sig_blob + t.sig_off[0], sb);
+    add(POFF, t.pub_off, 8 * (R + 1));
+    add(SOFF, t.sig_off, 8 * (R + 1));
+    add(M, t.msg32, 32 * R);
+    const size_t want = tl_stage_threads ? tl_stage_threads : 16;
+    const size_t nth = std::min(work.size(), want);
+    if (nth <= 1) {
+        for (const Piece& w : work) memcpy(w.dst, w.src, w.len);
+    } else {
+        host::run_team((unsigned)nth, [&](unsigned k0) {
+            for (size_t k = k0; k < work.size(); k += nth) memcpy(work[k].dst, work[k].src, work[k].len);
+        });
+    }
+    BCC_HIP_TRY(hipSetDevice(dev_));
+    up_pending_ = true;
+    up_rows_ = up_total_ = upload;
+    n_der_ = R;
+    pub_base_ = t.pub_off[0];
+    pub_bytes_ = pb;
+    sig_base_ = t.sig_off[0];
+    sig_bytes_ = sb;
+    return 0;
+}
+
 // The staged image's pending upload: all of it on `rows_stream` when `rest_stream` is null, else
 // the tuple rows on `rows_stream` and the rest on `rest_stream`.  Stream order puts every kernel
 // launched after it on the same stream behind its bytes.
@@ -1317,6 +1398,10 @@ int DeviceBatch::run_ecdsa(void* stream) {
     void* st = pick(stream);
     if (!st) return (int)hipErrorOutOfMemory;
     if (int e = upload_on((hipStream_t)st, nullptr)) return e;
+    if (n_der_)  // raw tuples (stage_der): K_der writes the rows first
+        if (int e = der_launch(d_pub_, d_pub_off_, pub_base_, pub_bytes_, d_sig_, d_sig_off_, sig_base_,
+                               sig_bytes_, n_der_, d_tag, d_x, d_y, d_r, d_s, st))
+            return e;
     if (int e = ecdsa_launch(scratch_, d_tag, d_x, d_y, d_r, d_s, d_m, d_v, n_rows_, st)) return e;
     return launch_key_hash((hipStream_t)st);
 }
@@ -1557,6 +1642,18 @@ int gpu_verify_parts(int device, const SighashJobs* const* jobs, const TupleRows
     return e;
 }
 
+int gpu_verify_der(int device, const DerTuples& t, uint8_t* verdict) {
+    if (t.n == 0) return 0;
+    DeviceBatch* b = thread_batch(device);
+    if (!b) return (int)hipErrorInvalidDevice;
+    BCC_HIP_TRY(hipSetDevice(device));
+    int e = b->stage_der(t);
+    if (!e) e = b->run(nullptr, nullptr);
+    if (!e) e = b->fetch_verdicts(verdict);
+    if (e) tl_batches[device].reset();  // a retry starts from a fresh batch
+    return e;
+}
+
 struct StagedRound {
     int dev;
     std::unique_ptr<DeviceBatch> b;
@@ -1572,6 +1669,18 @@ int gpu_staged_stage(StagedRound* s, const SighashJobs* const* jobs, const Tuple
     if (!s->b) s->b = std::make_unique<DeviceBatch>(s->dev);
     auto t0 = std::chrono::steady_clock::now();
     int e = s->b->stage_parts(jobs, rows, parts);
+    if (!e && stage_seconds)
+        *stage_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (e) s->b.reset();
+    return e;
+}
+
+int gpu_staged_stage_der(StagedRound* s, const DerTuples& t, double* stage_seconds) {
+    if (s->dev < 0) return (int)hipErrorInvalidDevice;
+    BCC_HIP_TRY(hipSetDevice(s->dev));
+    if (!s->b) s->b = std::make_unique<DeviceBatch>(s->dev);
+    auto t0 = std::chrono::steady_clock::now();
+    int e = s->b->stage_der(t);
     if (!e && stage_seconds)
         *stage_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     if (e) s->b.reset();

@@ -103,13 +103,15 @@ struct StagedRound {
     std::vector<const SighashJobs*> jobs;
     std::vector<const TupleRows*> rows;
     std::vector<uint8_t> verdicts;  // gpu_staged_launch's
+    bool der = false;               // staged by gpu_staged_stage_der (verdicts already computed)
 };
-StagedRound* gpu_staged_new(int device) { return new StagedRound{device, {}, {}, {}}; }
+StagedRound* gpu_staged_new(int device) { return new StagedRound{device, {}, {}, {}, false}; }
 void gpu_staged_free(StagedRound* s) { delete s; }
 int gpu_staged_stage(StagedRound* s, const SighashJobs* const* jobs, const TupleRows* const* rows,
                      size_t parts, double*) {
     s->jobs.assign(jobs, jobs + parts);
     s->rows.assign(rows, rows + parts);
+    s->der = false;
     return 0;
 }
 int gpu_staged_run(StagedRound* s, uint8_t* verdict, const LateMsgFill* late) {
@@ -118,6 +120,7 @@ int gpu_staged_run(StagedRound* s, uint8_t* verdict, const LateMsgFill* late) {
 }
 // launch evaluates at once (the caller may rebuild its rows afterwards), finish copies
 int gpu_staged_launch(StagedRound* s, const LateMsgFill* late) {
+    if (s->der) return 0;
     size_t n = 0;
     for (const TupleRows* r : s->rows) n += r->size();
     std::vector<uint8_t>& v = s->verdicts;
@@ -126,6 +129,31 @@ int gpu_staged_launch(StagedRound* s, const LateMsgFill* late) {
 }
 int gpu_staged_finish(StagedRound* s, uint8_t* verdict) {
     if (!s->verdicts.empty()) memcpy(verdict, s->verdicts.data(), s->verdicts.size());
+    return 0;
+}
+
+// Raw tuples (bcc_pubkey_verify_batch, K_der on the device): the oracle's own CPubKey::Verify per
+// tuple, from the caller's blobs -- so the CPU suite checks the entry point's slicing and offsets
+// against the oracle, not the product's host parse against itself.
+static void stub_der(const DerTuples& t, uint8_t* verdict) {
+    for (size_t i = 0; i < t.n; i++) {
+        const uint64_t p0 = t.pub_off[i], p1 = t.pub_off[i + 1], s0 = t.sig_off[i], s1 = t.sig_off[i + 1];
+        verdict[i] = (p0 <= p1 && s0 <= s1)
+                         ? (uint8_t)bcco_pubkey_verify(t.pub_blob + p0, p1 - p0, t.msg32 + 32 * i,
+                                                       t.sig_blob + s0, s1 - s0)
+                         : 0;
+    }
+}
+int gpu_verify_der(int, const DerTuples& t, uint8_t* verdict) {
+    stub_der(t, verdict);
+    return 0;
+}
+int gpu_staged_stage_der(StagedRound* s, const DerTuples& t, double*) {
+    s->jobs.clear();
+    s->rows.clear();
+    s->verdicts.assign(t.n, 0);  // evaluated now (the caller's buffers outlive the round anyway)
+    stub_der(t, s->verdicts.data());
+    s->der = true;
     return 0;
 }
 

@@ -487,8 +487,9 @@ def _many_input_legacy_tx(R, O, n_in, seed):
     return ser(sigs), spks
 
 
-@pytest.mark.parametrize("chain_blocks,early", [(0, 1), (1, 1), (12, 0), (160, 1), (160, 0)])
-def test_many_input_legacy_tx_template_midstates(eng, chain_blocks, early):
+@pytest.mark.parametrize("chain_blocks,early,devs", [(0, 1, []), (1, 1, []), (12, 0, []), (160, 1, []),
+                                                     (160, 0, []), (1, 1, [0, 1, 2]), (12, 1, [0, 0])])
+def test_many_input_legacy_tx_template_midstates(eng, chain_blocks, early, devs):
     """Legacy txs of 12..90 P2PKH inputs (templates of 8..58 blocks: every job carries the
     template midstates, TPL_MID) through verify_batch: the stub evaluates each template job from
     the full preimage with the oracle and aborts if the product's midstate path disagrees; jobs
@@ -496,7 +497,9 @@ def test_many_input_legacy_tx_template_midstates(eng, chain_blocks, early):
     inputs valid, and a byte flipped in the 40-input tx's first inputs or the 90-input tx's first
     outpoint gives the reference's (ret, err) for every input.  early: the P2PKH (key, signature)
     pairs are pre-extracted (bcc_set_early_q) and every deferred row is mapped to its early twin,
-    which the stub checks byte for byte (engine_host_stub.cpp check_early_twins)."""
+    which the stub checks byte for byte (engine_host_stub.cpp check_early_twins).  devs: a
+    multi-device list (no early rows there), whose device workers all wait for the one host pass
+    over the offloaded chains (LateHost) before their G ladders."""
     from oracle_ctypes import Oracle, Reference, reference_available
     if not reference_available():
         pytest.skip("oracle/_ref not built")
@@ -527,14 +530,20 @@ def test_many_input_legacy_tx_template_midstates(eng, chain_blocks, early):
     try:
         eng.bcc_set_host_chain_blocks(chain_blocks)
         eng.bcc_set_early_q(early)
+        engine_stub.set_devices(eng, devs)
         eng.bitcoinconsensus_verify_batch(arr, len(arr), 0x805, ret, err)
         st = Stats()
         eng.bcc_last_batch_stats(ctypes.byref(st))
     finally:
+        engine_stub.set_devices(eng, [])
         eng.bcc_set_host_chain_blocks(HOST_CHAIN_BLOCKS_DEFAULT)
         eng.bcc_set_early_q(1)
     assert list(zip(ret, err)) == exp
-    if early:
+    if chain_blocks in (1, 12):
+        assert st.host_hashed > 0
+    if len(devs) > 1:
+        assert st.devices == len(devs) and st.early_rows == 0
+    elif early:
         # every input is a P2PKH spend with one check: one early row each, and the first round's
         # rows (the only round) all mapped to their twins
         assert st.early_rows == len(items) and st.early_mapped == len(items)

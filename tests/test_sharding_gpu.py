@@ -121,3 +121,46 @@ def test_eight_entry_device_list():
     assert st["devices"] == 8
     assert multi == single and all(r == 1 for r, _ in multi)
     assert many == one and list(one) == [t["verdict"] for t in ts]
+
+
+def test_sharded_round_with_host_chains(two_workers):
+    """Round 5: multi-device rounds offload long legacy chains too (LateHost).  Device list [0, 0]
+    over the block shape's largest tx among ordinary ones, chains above 16 blocks hashed on the host
+    while both workers' device batches run their message-independent kernels (each worker's round
+    waits for the one host pass): host_hashed > 0, two devices used, verdicts equal to the
+    single-device run, and (mutated) equal to the reference item by item."""
+    B = two_workers
+    import json
+    import os
+    import random
+    shape = [tuple(t) for t in json.load(open(os.path.join(
+        os.path.dirname(os.path.abspath(__file__)), "golden", "block413567_shape.json")))["txs"]]
+    big = max(shape, key=lambda t: t[0])
+    wl = B.Workload(kind="block", shape=shape[:120] + [big] + shape[-60:], seed=0x5EED0023)
+    items = [wl.item(i) for i in range(wl.n)]
+    rng = random.Random(11)
+    mut = []
+    for spk, amt, tx, nin in items:
+        tx = bytearray(tx)
+        if rng.random() < 0.2:
+            tx[rng.randrange(len(tx))] ^= 1 << rng.randrange(8)
+        mut.append((spk, amt, bytes(tx), nin))
+    B.set_host_chain_blocks(16)
+    try:
+        B.set_devices([])
+        single = B.verify_batch(items)
+        single_mut = B.verify_batch(mut)
+        B.set_devices([0, 0])
+        multi = B.verify_batch(items)
+        st = B.last_batch_stats()
+        multi_mut = B.verify_batch(mut)
+        st_mut = B.last_batch_stats()
+    finally:
+        B.set_host_chain_blocks(B.HOST_CHAIN_BLOCKS_DEFAULT)
+    assert st["devices"] == 2 and st["host_hashed"] > 0 and st_mut["host_hashed"] > 0
+    assert multi == single and all(r == 1 for r, _ in multi)
+    assert multi_mut == single_mut
+    if reference_available():
+        from oracle_ctypes import Reference
+        exp, _ = Reference().bulk_verify_script(mut, B.VERIFY_ALL)
+        assert [(r, int(e)) for r, e in multi_mut] == exp

@@ -207,3 +207,111 @@ def test_c4_c5_bench_sizes_match_labels():
             got = v[idx]
             assert np.array_equal(got, ref), (kind, np.nonzero(got != ref)[0][:20])
         del ts
+
+
+def _der_int(v, pad=0, longform=0):
+    """DER INTEGER of big-endian bytes v with `pad` extra leading zero bytes; longform k > 0 writes
+    the length as 0x80 | k followed by k bytes (leading zero bytes included)."""
+    body = b"\x00" * pad + v
+    if longform:
+        ln = bytes([0x80 | longform]) + len(body).to_bytes(longform, "big")
+    else:
+        ln = bytes([len(body)])
+    return b"\x02" + ln + body
+
+
+def _der_split(sig):
+    """(r, s) big-endian minimal bytes of a strict DER signature."""
+    assert sig[0] == 0x30
+    rl = sig[3]
+    r = sig[4:4 + rl]
+    s = sig[6 + rl:6 + rl + sig[5 + rl]]
+    return r.lstrip(b"\x00") or b"\x00", s.lstrip(b"\x00") or b"\x00"
+
+
+def _der_variants(r, s, rng):
+    """Lax-DER encodings of (r, s) (pubkey.cpp:28-168): the ones a lax parser accepts with the same
+    (r, s), the ones it maps to (0, 0) (an integer > 32 bytes or >= n: overflow), and malformed
+    ones (parse failure)."""
+    n = (0xFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFEBAAEDCE6AF48A03BBFD25E8CD0364141).to_bytes(32, "big")
+    seq = lambda b, hdr=None: b"\x30" + (bytes([len(b)]) if hdr is None else hdr) + b  # noqa: E731
+    ri, si = _der_int(r), _der_int(s)
+    out = [
+        seq(ri + si),                                        # strict
+        seq(_der_int(r, pad=3) + si),                        # zero-padded r (r_zeropad), lax ok
+        seq(ri + _der_int(s, pad=40)),                       # s padded past 32 bytes: still s
+        seq(_der_int(r, longform=2) + si),                   # long-form length of r
+        seq(ri + _der_int(s, longform=3)),                   # 3 length bytes (< 4): ok
+        seq(ri + _der_int(s, longform=4)),                   # 4 length bytes, zeros skipped: ok
+        seq(ri + b"\x02\x84\x01\x00\x00\x20" + s),            # 4 significant length bytes: failure
+        seq(_der_int(r, longform=1, pad=1) + si),
+        seq(ri + si, hdr=b"\x85\x00\x00\x00\x00\x00"),       # sequence long form (skipped)
+        seq(ri + si, hdr=b"\x00"),                           # sequence length ignored
+        seq(ri + si, hdr=b"\x88"),                           # sequence long form past the end
+        seq(ri + si) + bytes(rng.randrange(1, 9)),           # trailing bytes (lax: ignored)
+        seq(_der_int(b"\x01" + r.rjust(32, b"\x00")) + si),  # 33 significant bytes: overflow
+        seq(_der_int(n) + si),                               # r = n: overflow
+        seq(ri + _der_int(n)),                               # s = n
+        seq(_der_int(b"\x00") + si),                         # r = 0
+        seq(ri + _der_int(b"")),                             # s empty
+        seq(ri + si)[:rng.randrange(1, 8 + len(r))],         # truncated
+        b"", b"\x30", b"\x30\x00\x02", b"\x31" + seq(ri + si)[1:],
+        seq(ri + b"\x03" + si[1:]),                          # wrong tag of S
+        bytes(rng.randrange(256) for _ in range(rng.randrange(1, 80))),
+    ]
+    return out
+
+
+@pytest.mark.skipif(not reference_available(), reason="oracle/_ref not built")
+def test_der_on_device_matches_reference():
+    """K_der (der.hip, round 5): bcc_pubkey_verify_batch parses the caller's blobs on the device.
+    Lax-DER variants of valid signatures (zero padding, long-form lengths, sequence-length garbage,
+    trailing bytes, >32-byte integers, r or s >= n, zero, truncation, wrong tags, random bytes),
+    pubkeys of every header and wrong lengths, all against the reference's CPubKey::Verify tuple by
+    tuple, through one round and through the pipelined rounds (tuple_rounds), and equal to the host
+    parse (a host-lane round)."""
+    import random
+    import bitcoinconsensus_amd as B
+    rng = random.Random(0xDE5)
+    base = [t for t in ecdsa_tuples() if t["verdict"] == 1 and t["sig"][:1] == b"\x30"]
+    tuples = []
+    for t in base[:400]:
+        try:
+            r, s = _der_split(t["sig"])
+        except (IndexError, AssertionError):
+            continue
+        pub = t["pub"]
+        pubs = [pub]
+        if len(pub) == 65:  # hybrid headers (both parities), a truncated key
+            pubs += [bytes([6]) + pub[1:], bytes([7]) + pub[1:], pub[:33]]
+        else:
+            pubs += [b"\x04" + pub[1:], pub + b"\x00", b""]
+        for sig in _der_variants(r, s, rng):
+            tuples.append((pub, t["hash"], sig))
+        for p in pubs[1:]:
+            tuples.append((p, t["hash"], t["sig"]))
+    rng.shuffle(tuples)
+    assert len(tuples) > 5000
+    pb = np.frombuffer(b"".join(t[0] for t in tuples) + b"\0", np.uint8)
+    po = np.zeros(len(tuples) + 1, np.uint64)
+    po[1:] = np.cumsum([len(t[0]) for t in tuples])
+    sb = np.frombuffer(b"".join(t[2] for t in tuples) + b"\0", np.uint8)
+    so = np.zeros(len(tuples) + 1, np.uint64)
+    so[1:] = np.cumsum([len(t[2]) for t in tuples])
+    msg = np.frombuffer(b"".join(t[1] for t in tuples), np.uint8)
+    ref, _ = Reference().pubkey_verify_blob(pb, po, msg, sb, so, threads=THREADS)
+    got = np.frombuffer(B.pubkey_verify_batch(tuples), np.uint8)
+    assert np.array_equal(got, ref), np.nonzero(got != ref)[0][:20]
+    assert 0.2 < ref.mean() < 0.8  # both outcomes well represented
+    # the host parse (every round on the host lane code) agrees
+    B.set_host_small_round(1 << 30)
+    try:
+        host = np.frombuffer(B.pubkey_verify_batch(tuples[:3000]), np.uint8)
+    finally:
+        B.set_host_small_round(B.HOST_SMALL_ROUND_DEFAULT)
+    assert np.array_equal(host, ref[:3000])
+    # the pipelined rounds (>= 2M tuples: 1M-tuple rounds staged while the previous one runs)
+    reps = (2_100_000 + len(tuples) - 1) // len(tuples)
+    big = tuples * reps
+    got_big = np.frombuffer(B.pubkey_verify_batch(big), np.uint8)
+    assert np.array_equal(got_big, np.tile(ref, reps))

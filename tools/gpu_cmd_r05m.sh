@@ -1,0 +1,3 @@
+set -o pipefail
+run() { timeout -k 10 120 env "$@" python3 tools/tuple_e2e.py 8000000 4 2>&1 | grep -v amdgpu.ids; }
+run BCC_TUPLE_TRACE=1 && run BCC_TUPLE_TRACE=1 BCC_TUPLE_ROUND=4194304 && run BCC_TUPLE_TRACE=1 BCC_TUPLE_FIRST=131072 && run BCC_TUPLE_TRACE=1 BCC_TUPLE_RAMP=0 && run BCC_TUPLE_TRACE=1
