@@ -92,8 +92,12 @@ int bcc_taproot_verify_batch(const bcc_taproot_check* items, size_t n, int* ret_
  * verdict[i] = CPubKey(pub_i).Verify(msg_i, sig_i) (depend/bitcoin/src/pubkey.cpp:191-207) for n
  * tuples: pub_i = pub_blob[pub_off[i] .. pub_off[i+1]) (any length; the CPubKey length filter,
  * pubkey.h:58-94, applies), sig_i = sig_blob[sig_off[i] .. sig_off[i+1]) = DER without the
- * hashtype byte, parsed laxly (pubkey.cpp:28-168).  Synchronous on `device`, or, for device = -1,
- * sharded in contiguous equal ranges over the bcc_set_devices() GPUs.  0 or an error. */
+ * hashtype byte, parsed laxly (pubkey.cpp:28-168).  The blobs go to the GPU as they are and the
+ * length filter and lax DER run there (K_der, csrc/der.hip), in pipelined rounds of 256k doubling
+ * to 2M tuples; small rounds run on the host lane code.  Synchronous on `device`, or, for
+ * device = -1, sharded in contiguous equal ranges over the bcc_set_devices() GPUs.  0, or -1 for
+ * null arrays or offsets that run backwards (pub_off[n] < pub_off[0] or sig_off[n] < sig_off[0]),
+ * or a device error.  A tuple whose own offsets run backwards or past the blob is invalid (0). */
 int bcc_pubkey_verify_batch(const uint8_t* pub_blob, const uint64_t* pub_off,
                             const uint8_t* msg32, const uint8_t* sig_blob,
                             const uint64_t* sig_off, uint8_t* verdict, size_t n, int device);

@@ -69,10 +69,16 @@ void parse_rows(const uint8_t* pub_blob, const uint64_t* pub_off, const uint8_t*
     rows.msg_one = rows.y_unused = false;
     rows.hrow.clear();
     rows.hprog.clear();
+    // a tuple's offsets must lie in order inside the round's [off[0], off[n]] (as K_der checks);
+    // otherwise it is invalid (its bytes are never read)
+    const uint64_t p0 = pub_off[0], p1 = pub_off[n], s0 = sig_off[0], s1 = sig_off[n];
     pfor(n, 4096, [&](size_t lo, size_t hi) {
-        for (size_t i = lo; i < hi; i++)
-            parse_row(pub_blob + pub_off[i], pub_off[i + 1] - pub_off[i], msg32 + 32 * i,
-                      sig_blob + sig_off[i], sig_off[i + 1] - sig_off[i], rows, i);
+        for (size_t i = lo; i < hi; i++) {
+            const uint64_t pa = pub_off[i], pb = pub_off[i + 1], sa = sig_off[i], sb = sig_off[i + 1];
+            const bool ok = p0 <= pa && pa <= pb && pb <= p1 && s0 <= sa && sa <= sb && sb <= s1;
+            parse_row(pub_blob + (ok ? pa : p0), ok ? pb - pa : 0, msg32 + 32 * i,
+                      sig_blob + (ok ? sa : s0), ok ? sb - sa : 0, rows, i);
+        }
     });
 }
 

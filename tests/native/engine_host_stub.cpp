@@ -136,9 +136,10 @@ int gpu_staged_finish(StagedRound* s, uint8_t* verdict) {
 // tuple, from the caller's blobs -- so the CPU suite checks the entry point's slicing and offsets
 // against the oracle, not the product's host parse against itself.
 static void stub_der(const DerTuples& t, uint8_t* verdict) {
+    const uint64_t pl = t.pub_off[0], ph = t.pub_off[t.n], sl = t.sig_off[0], sh = t.sig_off[t.n];
     for (size_t i = 0; i < t.n; i++) {
         const uint64_t p0 = t.pub_off[i], p1 = t.pub_off[i + 1], s0 = t.sig_off[i], s1 = t.sig_off[i + 1];
-        verdict[i] = (p0 <= p1 && s0 <= s1)
+        verdict[i] = (pl <= p0 && p0 <= p1 && p1 <= ph && sl <= s0 && s0 <= s1 && s1 <= sh)
                          ? (uint8_t)bcco_pubkey_verify(t.pub_blob + p0, p1 - p0, t.msg32 + 32 * i,
                                                        t.sig_blob + s0, s1 - s0)
                          : 0;

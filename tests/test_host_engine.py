@@ -206,9 +206,14 @@ def test_script_cases_key_hash_where(eng, on):
         eng.bcc_set_device_key_hash(1)
 
 
-def test_pubkey_verify_batch_front_end(eng):
-    """bcc_pubkey_verify_batch's host front end (CPubKey length filter, lax DER, r/s == 0; the
-    curve work stubbed by the oracle) on the reference-labelled adversarial tuple fixtures."""
+@pytest.mark.parametrize("host_lane", [False, True])
+def test_pubkey_verify_batch_front_end(eng, host_lane):
+    """bcc_pubkey_verify_batch on the reference-labelled adversarial tuple fixtures.  host_lane:
+    every round on the host lane code, i.e. the product's host front end (parse_rows: CPubKey
+    length filter, lax DER, r/s == 0; the host_verify_rows curve code); else the device round
+    (stubbed by the oracle's CPubKey::Verify over the same blob slices).  Offsets out of order or
+    past the round's blob make just those tuples invalid, and offsets running backwards over the
+    whole call are an argument error."""
     from fixtures import ecdsa_tuples
     ts = ecdsa_tuples()
 
@@ -222,10 +227,24 @@ def test_pubkey_verify_batch_front_end(eng):
     sb, so = blob([t["sig"] for t in ts])
     msg = b"".join(t["hash"] for t in ts)
     out = ctypes.create_string_buffer(len(ts))
-    u64p = ctypes.POINTER(ctypes.c_uint64)
-    assert eng.bcc_pubkey_verify_batch(pb, po, msg, sb, so, out, len(ts), 0) == 0
-    bad = [(t["cls"], i) for i, t in enumerate(ts) if out.raw[i] != t["verdict"]]
-    assert not bad, bad[:20]
+    eng.bcc_set_host_small_round.argtypes = [ctypes.c_size_t]
+    eng.bcc_set_host_small_round(1 << 30 if host_lane else 16)
+    try:
+        assert eng.bcc_pubkey_verify_batch(pb, po, msg, sb, so, out, len(ts), 0) == 0
+        bad = [(t["cls"], i) for i, t in enumerate(ts) if out.raw[i] != t["verdict"]]
+        assert not bad, bad[:20]
+        po[10] = 1 << 40
+        so[20] = so[19] - 1
+        assert eng.bcc_pubkey_verify_batch(pb, po, msg, sb, so, out, len(ts), 0) == 0
+        want = [t["verdict"] for t in ts]
+        want[9] = want[10] = want[19] = 0
+        got = list(out.raw)
+        del got[20], want[20]
+        assert got == want
+        po[0], po[len(ts)] = 1, 0
+        assert eng.bcc_pubkey_verify_batch(pb, po, msg, sb, so, out, len(ts), 0) == -1
+    finally:
+        eng.bcc_set_host_small_round(16)
 
 
 def _batch(eng, vs, flags=None):

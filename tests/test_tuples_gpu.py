@@ -310,7 +310,31 @@ def test_der_on_device_matches_reference():
     finally:
         B.set_host_small_round(B.HOST_SMALL_ROUND_DEFAULT)
     assert np.array_equal(host, ref[:3000])
-    # the pipelined rounds (>= 2M tuples: 1M-tuple rounds staged while the previous one runs)
+    # offsets out of order or past the round's blob: those tuples are invalid (never read), on the
+    # device and on the host lane code alike; the other tuples keep their verdicts
+    import ctypes
+    L = ctypes.CDLL(B.lib()._name)
+    u64p, vp = ctypes.POINTER(ctypes.c_uint64), ctypes.c_void_p
+    f = L.bcc_pubkey_verify_batch
+    f.argtypes = [vp, u64p, vp, vp, u64p, vp, ctypes.c_size_t, ctypes.c_int]
+    m = 4000
+    po2, so2 = po[:m + 1].copy(), so[:m + 1].copy()
+    po2[100] = 1 << 40            # tuples 99, 100: past the blob
+    so2[200] = so2[199] - 1       # tuple 199 backwards; 200 starts before 199 ends (in order: valid)
+    want = ref[:m].copy()
+    want[[99, 100, 199]] = 0
+    for small in (B.HOST_SMALL_ROUND_DEFAULT, 1 << 30):
+        B.set_host_small_round(small)
+        try:
+            out = np.zeros(m, np.uint8)
+            assert f(pb.ctypes.data, po2.ctypes.data_as(u64p), msg.ctypes.data, sb.ctypes.data,
+                     so2.ctypes.data_as(u64p), out.ctypes.data, m, 0) == 0
+        finally:
+            B.set_host_small_round(B.HOST_SMALL_ROUND_DEFAULT)
+        mask = np.ones(m, bool)
+        mask[200] = False  # its bytes are shifted by one: the verdict is whatever they parse to
+        assert np.array_equal(out[mask], want[mask]), (small, np.nonzero(out[mask] != want[mask])[0][:10])
+    # the pipelined rounds (>= 512k tuples: rounds staged while the previous one runs)
     reps = (2_100_000 + len(tuples) - 1) // len(tuples)
     big = tuples * reps
     got_big = np.frombuffer(B.pubkey_verify_batch(big), np.uint8)
