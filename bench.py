@@ -300,15 +300,17 @@ class C2:
         # sustained: calls back to back (a CFS CPU quota lets one call burst above it, a run of
         # calls pays for that in throttling), whole-run wall time
         calls = 10
-        t0 = time.perf_counter()
+        t0, c0 = time.perf_counter(), time.process_time()
         for _ in range(calls):
             self.wl.verify_batch()
-        sus = time.perf_counter() - t0
+        sus, cpu_s = time.perf_counter() - t0, time.process_time() - c0
         return dict(inputs_per_s=self.n / best, ms=best * 1e3, valid=nv,
                     host_ms=st["host_seconds"] * 1e3, gpu_ms=st["gpu_seconds"] * 1e3,
                     h2d_ms=st["stage_seconds"] * 1e3, host_threads=self.B.host_threads(),
                     cpu_share=self.B.cpu_share(), sustained_inputs_per_s=calls * self.n / sus,
-                    sustained_calls=calls)
+                    sustained_calls=calls,
+                    # process CPU (every thread) per 1M inputs over the sustained calls
+                    sustained_cpu_s_per_M=cpu_s / (calls * self.n) * 1e6)
 
     def cpu(self, sample):
         sample = min(sample, self.n)

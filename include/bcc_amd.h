@@ -162,8 +162,7 @@ int bcc_set_device_key_hash(int on);
 
 /* Host worker threads of a batch pass (verify_batch interpreter shards, tuple / Taproot front
  * ends, host-verified rounds).  0 restores the default: BCC_HOST_THREADS, else the CPUs of the
- * affinity mask, or 3 x the cgroup CPU quota when that is smaller (a quota bounds the average
- * and a call alternates the host pass with a one-thread device wait), at most 64.  Results never
+ * affinity mask, or the cgroup CPU quota when that is smaller, at most 64.  Results never
  * depend on it. */
 int bcc_set_host_threads(unsigned n);
 unsigned bcc_get_host_threads(void);

@@ -444,7 +444,7 @@ def set_host_small_round(tuples):
 
 
 def set_host_threads(n):
-    """bcc_set_host_threads: host worker threads of a batch pass (0: the default: the affinity CPUs, or 3 x cpu_share() under a smaller cgroup quota, at most 64)."""
+    """bcc_set_host_threads: host worker threads of a batch pass (0: the default: the affinity CPUs, or cpu_share() under a smaller cgroup quota, at most 64)."""
     L = lib()
     L.bcc_set_host_threads.argtypes = [ctypes.c_uint]
     if L.bcc_set_host_threads(n) != 0:

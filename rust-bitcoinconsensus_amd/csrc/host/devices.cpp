@@ -212,19 +212,20 @@ unsigned cpu_share() {
     return share;
 }
 
-// Default: the CPUs the process may run on, and under a CFS quota (cpu.max) three times the quota.
-// The quota bounds the AVERAGE over a period, and a verify_batch call alternates a parallel host
-// pass with a device wait on one thread, so a host pass on quota-many threads leaves half the
-// quota unused: in 20 back-to-back 1M-input C2 calls on the GPU box (quota 16 of 256 CPUs,
-// profiles/r03/threads) 16 threads kept 8 CPUs busy (12.8-14.5 M inputs/s), 48 threads 15.8 of 16
-// (20.1-21.3 M/s, a few throttled periods), 64 threads hit the quota hard (17.2-19.0 M/s).
+// Default: the CPUs the process may run on, capped at the CFS quota (cpu.max) when there is one.
+// Rounds 3-4 used three times the quota: 16 threads then kept only 8 CPUs busy, which round 5
+// traced to false sharing in the parse pass (per-shard vector headers on shared cache lines, each
+// push_back taking the line from the other workers: 10x the single-threaded cost per item), not to
+// the quota.  With that fixed, 20 back-to-back 1M-input C2 calls on the GPU box (quota 16,
+// profiles/r05/dropin): 16 threads 36.5-37.5 M inputs/s at 0.245 CPU-s per 1M inputs, 24 threads
+// 36.8-39.0 at 0.27-0.32, 48 threads 31.6-38.0 at 0.40-0.51.
 unsigned host_threads() {
     if (unsigned v = g_host_threads.load(std::memory_order_relaxed)) return v;
     static const unsigned dflt = [] {
         if (const char* e = getenv("BCC_HOST_THREADS"))
             if (atoi(e) > 0) return (unsigned)atoi(e);
         const unsigned aff = affinity_cpus(), share = cpu_share();
-        const unsigned n = share < aff ? std::min(aff, 3 * share) : aff;
+        const unsigned n = std::min(aff, share);
         return std::min(64u, n);
     }();
     return dflt;

@@ -197,7 +197,7 @@ struct EarlyCand {
     uint32_t publen, siglen;
     uint32_t row;  // in the shard's early rows
 };
-struct EarlyShard {
+struct alignas(64) EarlyShard {  // one per shard, written by its worker: own cache lines
     TupleRows rows;
     std::vector<EarlyCand> cands;
     void clear() {
@@ -552,8 +552,9 @@ private:
     bool kh_taken_ = false;             // ... which a new device row carries
 };
 
-// One GPU round: the tuples deferred by this round's interpreter runs.
-class Round {
+// One GPU round: the tuples deferred by this round's interpreter runs.  One per shard, written by
+// its worker: cache-line aligned so that neighbouring shards' Rounds share no line.
+class alignas(64) Round {
 public:
     SighashJobs jobs;
     TupleRows rows;
@@ -807,7 +808,11 @@ void prepare(BatchState& b, const bcc_batch_item* items, size_t n, unsigned flag
              std::vector<std::vector<uint32_t>>* runs = nullptr,
              std::vector<EarlyShard>* early = nullptr, unsigned W = 0) {
     if (W == 0 || W > T) W = T;  // worker threads over the T shards (run_shards)
+    static const bool trace = getenv("BCC_PREPARE_TRACE") != nullptr;
+    const auto q0 = std::chrono::steady_clock::now();
+    auto qms = [&] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - q0).count(); };
     if (b.st.size() < n) b.st.resize(n);  // reused across calls: every field is (re)set below
+    const double q_st = trace ? qms() : 0;
     b.n = n;
     b.flags = flags;
     auto& st = b.st;
@@ -823,10 +828,15 @@ void prepare(BatchState& b, const bcc_batch_item* items, size_t n, unsigned flag
     } else {
         b.tx_slices.resize(T);
         run_shards(T, W, [&](unsigned t) {
-            auto& v = b.tx_slices[t];
+            // appended through a local header (swapped in and out): the shards' vector headers
+            // share cache lines, and a push_back per item on them cost every writer its line
+            // (round 5: prepare's per-item time 10x single-threaded at 8-16 threads)
+            std::vector<uint32_t> v;
+            v.swap(b.tx_slices[t]);
             v.clear();
             for (size_t i = share_lo(n, t, T); i < share_lo(n, t + 1, T); i++)
                 if (starts_tx(i)) v.push_back((uint32_t)i);
+            v.swap(b.tx_slices[t]);
         });
         size_t total = 0;
         for (unsigned t = 0; t < T; t++) total += b.tx_slices[t].size();
@@ -856,8 +866,10 @@ void prepare(BatchState& b, const bcc_batch_item* items, size_t n, unsigned flag
             b.tx_first.swap(cut);
         }
     }
+    const double q_scan = trace ? qms() : 0;
     const size_t E = b.tx_first.size();
     if (b.txs.size() < E) b.txs.resize(E);  // grow only, like st
+    const double q_txs = trace ? qms() : 0;
     // per-thread timing (bcc_batch_stats prepare_*): dispatch -> start lag, parse, batched HASH160
     using pclk = std::chrono::steady_clock;
     std::vector<double> lag(T, 0), tparse(T, 0), thash(T, 0);
@@ -875,9 +887,13 @@ void prepare(BatchState& b, const bcc_batch_item* items, size_t n, unsigned flag
                                                      (uint32_t)bound[t]) - b.tx_first.begin());
         const size_t khi = (size_t)(std::lower_bound(b.tx_first.begin(), b.tx_first.end(),
                                                      (uint32_t)bound[t + 1]) - b.tx_first.begin());
-        std::vector<uint32_t>* sh = shards ? &(*shards)[t] : nullptr;
-        std::vector<uint32_t>* rl = shards ? &(*runs)[t] : nullptr;
+        // the shard / run lists through local headers (see tx_slices above)
+        std::vector<uint32_t> lsh, lrl;
+        std::vector<uint32_t>* sh = shards ? &lsh : nullptr;
+        std::vector<uint32_t>* rl = shards ? &lrl : nullptr;
         if (sh) {
+            lsh.swap((*shards)[t]);
+            lrl.swap((*runs)[t]);
             sh->clear();
             rl->clear();
         }
@@ -915,6 +931,10 @@ void prepare(BatchState& b, const bcc_batch_item* items, size_t n, unsigned flag
                     if (it.active) rl->push_back((uint32_t)i);
                 }
             }
+        }
+        if (sh) {
+            lsh.swap((*shards)[t]);
+            lrl.swap((*runs)[t]);
         }
         if (early) {  // early Q halves: this shard's candidates while its txs are in cache
             EarlyShard& es = (*early)[t];
@@ -956,6 +976,16 @@ void prepare(BatchState& b, const bcc_batch_item* items, size_t n, unsigned flag
         flush();
         thash[t] = std::chrono::duration<double>(pclk::now() - s1).count();
     });
+    if (trace) {
+        double pmax = 0, psum = 0, hmax = 0;
+        for (unsigned t = 0; t < T; t++) {
+            pmax = std::max(pmax, tparse[t]);
+            psum += tparse[t];
+            hmax = std::max(hmax, thash[t]);
+        }
+        fprintf(stderr, "[bcc] prepare n=%zu T=%u W=%u E=%zu: st %.2f scan %.2f txs %.2f parallel-end %.2f ms; parse max %.2f mean %.2f hash max %.2f ms\n",
+                n, T, W, E, q_st, q_scan, q_txs, qms(), 1e3 * pmax, 1e3 * psum / T, 1e3 * hmax);
+    }
     for (unsigned t = 0; t < T; t++) {
         t_stats.prepare_lag_seconds = std::max(t_stats.prepare_lag_seconds, lag[t]);
         t_stats.prepare_parse_seconds = std::max(t_stats.prepare_parse_seconds, tparse[t]);
@@ -1296,10 +1326,10 @@ void chunk_start(ChunkRun& c, const bcc_batch_item* items, size_t n, unsigned fl
                  bool allow_early = false) {
     auto t0 = clk::now();
     c.n = n;
-    // A short host pass (a block-sized batch) on at most the CPU share: three times the quota
-    // pays off for long passes alternating with long device waits (host_threads()), but for a
-    // ~1 ms pass the extra threads only queue for the CPUs and their wake-ups
-    // (C3 at 48 threads vs 16: 2.9-3.0 vs 4.7-5.4 M inputs/s, profiles/r04/c3).
+    // A short host pass (a block-sized batch) on at most the CPU share (C3 at 48 threads vs 16:
+    // 2.9-3.0 vs 4.7-5.4 M inputs/s, profiles/r04/c3); round 5 made the share the default for
+    // every pass (host_threads()), an explicit bcc_set_host_threads above it still applies to long
+    // passes only.
     const unsigned cap = n < SHORT_PASS_ITEMS ? std::min(host_threads(), cpu_share()) : host_threads();
     c.W = n >= 256 ? std::min<unsigned>(cap, (unsigned)(n / 64)) : 1u;
     // a short pass: four shards per worker, dealt dynamically (run_shards)

@@ -34,7 +34,7 @@ inline void put_le(std::vector<uint8_t>& b, uint64_t v, int k) {
 }
 
 // One part of a round: the jobs of a contiguous item range (built by one host thread).
-struct Part {
+struct alignas(64) Part {  // one per worker, appended per check: no cache line shared with the next
     TaprootJobs jobs;
     std::vector<uint32_t> item_of_row;  // row -> item index (absolute)
 };

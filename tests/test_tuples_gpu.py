@@ -209,6 +209,12 @@ def test_c4_c5_bench_sizes_match_labels():
         del ts
 
 
+def _small_round_env():
+    """The host small-round setting the suite runs under (conftest.py sets BCC_HOST_SMALL_ROUND)."""
+    import os
+    return int(os.environ.get("BCC_HOST_SMALL_ROUND", "16"))
+
+
 def _der_int(v, pad=0, longform=0):
     """DER INTEGER of big-endian bytes v with `pad` extra leading zero bytes; longform k > 0 writes
     the length as 0x80 | k followed by k bytes (leading zero bytes included)."""
@@ -308,7 +314,7 @@ def test_der_on_device_matches_reference():
     try:
         host = np.frombuffer(B.pubkey_verify_batch(tuples[:3000]), np.uint8)
     finally:
-        B.set_host_small_round(B.HOST_SMALL_ROUND_DEFAULT)
+        B.set_host_small_round(_small_round_env())
     assert np.array_equal(host, ref[:3000])
     # offsets out of order or past the round's blob: those tuples are invalid (never read), on the
     # device and on the host lane code alike; the other tuples keep their verdicts
@@ -323,14 +329,14 @@ def test_der_on_device_matches_reference():
     so2[200] = so2[199] - 1       # tuple 199 backwards; 200 starts before 199 ends (in order: valid)
     want = ref[:m].copy()
     want[[99, 100, 199]] = 0
-    for small in (B.HOST_SMALL_ROUND_DEFAULT, 1 << 30):
+    for small in (_small_round_env(), 1 << 30):
         B.set_host_small_round(small)
         try:
             out = np.zeros(m, np.uint8)
             assert f(pb.ctypes.data, po2.ctypes.data_as(u64p), msg.ctypes.data, sb.ctypes.data,
                      so2.ctypes.data_as(u64p), out.ctypes.data, m, 0) == 0
         finally:
-            B.set_host_small_round(B.HOST_SMALL_ROUND_DEFAULT)
+            B.set_host_small_round(_small_round_env())
         mask = np.ones(m, bool)
         mask[200] = False  # its bytes are shifted by one: the verdict is whatever they parse to
         assert np.array_equal(out[mask], want[mask]), (small, np.nonzero(out[mask] != want[mask])[0][:10])

@@ -48,6 +48,16 @@ int gpu_staged_run(StagedRound* s, uint8_t* verdict, const LateMsgFill* late) {
     return gpu_verify_parts(0, nullptr, s->rows.data(), s->rows.size(), verdict, nullptr, late);
 }
 int gpu_staged_launch(StagedRound*, const LateMsgFill*) { return 0; }
+int gpu_early_launch(int, const TupleRows* const*, size_t) { return 0; }  // early Q halves: no-op
+void gpu_early_reset(int) {}
+int gpu_verify_der(int, const DerTuples& t, uint8_t* verdict) {
+    memset(verdict, 1, t.n);
+    return 0;
+}
+int gpu_staged_stage_der(StagedRound* s, const DerTuples&, double*) {
+    s->rows.clear();
+    return 0;
+}
 int gpu_staged_finish(StagedRound* s, uint8_t* verdict) {
     return gpu_staged_run(s, verdict, nullptr);
 }
@@ -118,6 +128,11 @@ int main(int argc, char** argv) {
                1e3 * st.prepare_seconds, 1e3 * st.interpret_seconds, 1e3 * st.merge_seconds,
                1e3 * st.stage_seconds, 1e3 * st.gpu_seconds, 1e3 * st.host_seconds,
                1e3 * st.total_seconds, st.device_key_hashes);
+        printf("    prepare lag %.2f parse(max) %.2f hash %.2f | interpret shard max %.2f mean %.2f | "
+               "stitch %.2f finish %.2f ms | process cpu %.1f ms\n",
+               1e3 * st.prepare_lag_seconds, 1e3 * st.prepare_parse_seconds, 1e3 * st.prepare_hash_seconds,
+               1e3 * st.interpret_shard_max_seconds, 1e3 * st.interpret_shard_mean_seconds,
+               1e3 * st.stitch_seconds, 1e3 * st.finish_seconds, 1e3 * st.process_cpu_seconds);
     }
     return 0;
 }
