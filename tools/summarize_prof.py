@@ -58,7 +58,7 @@ def main(d):
     # bench.py --steps 1 --warmup 0: one timed step + 3 HIP-event timing repetitions = 4 stages,
     # plus, for the C2 line (which carries drop_in_end_to_end), 3 drop-in verify_batch runs over
     # the same inputs = 7.  A stage may launch a kernel once per lane chunk (C4 at 8M, C5 at 16M).
-    stages = {"ecdsa": ["batch_sinv_kernel", "ecdsa_tprep_kernel", "twist_keyq_kernel",
+    stages = {"ecdsa": ["batch_sinv_kernel", "ecdsa_tprep_kernel", "twist_keyq_kernel", "twist_keyq2_kernel",
                         "twist_ladder_g_kernel", "void twist_ladder_kernel<false>",
                         "void twist_fin_kernel<false>"],
               "schnorr": ["schnorr_tladder_kernel", "schnorr_tprep_kernel", "void twist_ladder_kernel<true>",
