@@ -294,11 +294,14 @@ class Workload:
             raise RuntimeError(f"bcc_workload_run_ecdsa: {rc}")
 
     def verdicts(self):
-        out = ctypes.create_string_buffer(max(1, self.n))
+        """One byte per staged tuple row (a block workload's multisig inputs have several rows:
+        the buffer is sized by rows, not items)."""
+        t = self.shape()["tuples"]
+        out = ctypes.create_string_buffer(max(1, t))
         rc = blib().bcc_workload_verdicts(self.h, out)
         if rc:
             raise RuntimeError(f"bcc_workload_verdicts: {rc}")
-        return out.raw[: self.shape()["tuples"]]
+        return out.raw[:t]
 
     def tuple_items(self):
         """Item index of every staged tuple row."""
