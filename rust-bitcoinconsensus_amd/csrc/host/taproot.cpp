@@ -9,6 +9,9 @@
 // :1556-1561).  Every SHA-256 compression and the BIP340 verification run on the GPU
 // (sighash.hip gpu_taproot_verify: aux hashes, digest patching, TapSighash from the tag
 // midstate, then the Schnorr kernels).
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <algorithm>
 #include <cstring>
 #include <functional>
@@ -47,7 +50,7 @@ struct RoundOut {
     std::vector<uint32_t> item_of_row;
     std::vector<uint8_t> verdict, msg;
 };
-thread_local RoundOut tl_round_out[2];
+thread_local RoundOut tl_round_out[TAPROOT_SLOTS];
 
 // The parsed tx (and spent outputs) an adjacent run of items shares, and its TtxRec in the
 // current part.
@@ -280,14 +283,21 @@ int run_range(const bcc_taproot_check* items, size_t lo, size_t hi, int* ret, in
 }
 
 // Rounds of about PIPE_ROUND checks, pipelined (a batch of at least two): round k's host parts
-// are built while round k - 1 runs on the GPU, and round k's upload (on the other context's
-// stream) runs beside round k - 1's kernels.  One C5T round of 1M checks spent ≈6 ms building
-// parts, ≈6 ms uploading and ≈12 ms in kernels, back to back; pipelined in 131,072-check rounds
-// 1M checks take 16-19 ms (262,144: 19.5-20; 500,000: 18.4-18.5; profiles/r04/c5t).
+// are built while rounds k - 1 and k - 2 are on the GPU (TAPROOT_SLOTS = 3 contexts), and round
+// k's upload runs beside their kernels.  Round 4 had two slots (16-19 ms per 1M checks in 131,072
+// rounds, profiles/r04/c5t): round k + 1 was built only after round k - 1 finished, and round k - 1's
+// verdict copy queued behind round k's upload in the one copy queue (profiles/r05/c5t timelines).
+// Round 5: verdicts written to pinned memory by a kernel behind the round (gpu_taproot_begin), three
+// slots, 65,536-check rounds (two overlap on the GPU): 13.3-13.9 ms per 1M (131,072: 13.5-15.7;
+// 81,920: 14.9-15.9; 49,152: 15.0-17.6; profiles/r05/c5t/rounds.txt).
 #ifndef BCC_TAPROOT_PIPE_ROUND
-#define BCC_TAPROOT_PIPE_ROUND 131072
+#define BCC_TAPROOT_PIPE_ROUND 65536
 #endif
-constexpr size_t PIPE_ROUND = BCC_TAPROOT_PIPE_ROUND;
+static const size_t PIPE_ROUND = [] {  // BCC_TAPROOT_ROUND overrides (experiments)
+    const char* e = getenv("BCC_TAPROOT_ROUND");
+    return e && atoll(e) > 0 ? (size_t)atoll(e) : (size_t)BCC_TAPROOT_PIPE_ROUND;
+}();
+static const bool g_tap_trace = getenv("BCC_TAPROOT_TRACE") != nullptr;
 
 int run_pipelined(const bcc_taproot_check* items, size_t lo, size_t hi, int* ret, int* serr,
                   unsigned char* sighash_out, int device) {
@@ -300,25 +310,53 @@ int run_pipelined(const bcc_taproot_check* items, size_t lo, size_t hi, int* ret
         while (c < hi && items[c].tx == items[c - 1].tx) c++;
         cut.push_back(c);
     }
-    int prev = -1;  // slot of the round in flight
+    // rounds in flight: launched, not yet finished (at most TAPROOT_SLOTS - 1 while the host builds
+    // the next: round k is launched before round k - 2 is finished)
+    std::vector<int> inflight;
     int err = 0;
+    using clk = std::chrono::steady_clock;
+    auto ms = [](clk::time_point a) { return std::chrono::duration<double, std::milli>(clk::now() - a).count(); };
+    double t_build = 0, t_launch = 0, t_finish = 0;
+    const auto c0 = clk::now();
     for (size_t k = 0; k + 1 < cut.size() && !err; k++) {
-        const int slot = (int)(k & 1);
+        const int slot = (int)(k % TAPROOT_SLOTS);
+        auto q = clk::now();
+        auto ns = [](clk::time_point t) { return (long long)std::chrono::duration_cast<std::chrono::nanoseconds>(t.time_since_epoch()).count(); };
+        if (g_tap_trace) fprintf(stderr, "[bcc] tap k=%zu build_start %lld\n", k, ns(q));
         const size_t NP = build_round(items, cut[k], cut[k + 1], ret, serr);
+        t_build += ms(q);
+        if (g_tap_trace) fprintf(stderr, "[bcc] tap k=%zu build_end %lld\n", k, ns(clk::now()));
         if (NP == 0) {  // too large for one launch: this round alone, unpipelined
-            if (prev >= 0) err = finish_round(device, prev, tl_round_out[prev], ret, serr, sighash_out);
-            prev = -1;
+            for (int p : inflight)
+                if (int e = finish_round(device, p, tl_round_out[p], ret, serr, sighash_out)) err = err ? err : e;
+            inflight.clear();
             if (!err) err = run_range(items, cut[k], cut[k + 1], ret, serr, sighash_out, device);
             continue;
         }
+        q = clk::now();
         err = launch_round(NP, device, slot, tl_round_out[slot]);
-        if (prev >= 0) {
-            const int e = finish_round(device, prev, tl_round_out[prev], ret, serr, sighash_out);
+        t_launch += ms(q);
+        if (g_tap_trace) fprintf(stderr, "[bcc] tap k=%zu launch_end %lld\n", k, ns(clk::now()));
+        if (!err) inflight.push_back(slot);
+        q = clk::now();
+        while ((int)inflight.size() > TAPROOT_SLOTS - 1 || (err && !inflight.empty())) {
+            const int p = inflight.front();
+            inflight.erase(inflight.begin());
+            const int e = finish_round(device, p, tl_round_out[p], ret, serr, sighash_out);
             if (!err) err = e;
         }
-        prev = err ? -1 : slot;
+        t_finish += ms(q);
+        if (g_tap_trace) fprintf(stderr, "[bcc] tap k=%zu finish_prev_end %lld\n", k, ns(clk::now()));
     }
-    if (prev >= 0 && !err) err = finish_round(device, prev, tl_round_out[prev], ret, serr, sighash_out);
+    auto q = clk::now();
+    for (int p : inflight) {  // in launch order; every launched round is finished, even after an error
+        const int e = finish_round(device, p, tl_round_out[p], ret, serr, sighash_out);
+        if (!err) err = e;
+    }
+    t_finish += ms(q);
+    if (g_tap_trace)
+        fprintf(stderr, "[bcc] taproot rounds: %zu checks, %zu rounds, %.2f ms: build %.2f launch(stage+issue) %.2f finish(wait) %.2f ms\n",
+                hi - lo, cut.size() - 1, ms(c0), t_build, t_launch, t_finish);
     return err;
 }
 

@@ -375,10 +375,12 @@ int gpu_taproot_verify(int device, const TaprootJobs& jobs, uint8_t* verdict, ui
 // The same over the concatenation of P parts (rows in part order).
 int gpu_taproot_verify_parts(int device, const TaprootJobs* const* parts, size_t P,
                              uint8_t* verdict, uint8_t* msg32_out);
-// The same in two phases on one of two contexts per (thread, device): begin stages, uploads and
-// launches on `slot`'s stream and returns; end waits for it and copies the verdicts (and, with
-// msg32_out, the sighashes) back.  The pipelined bcc_taproot_verify_batch alternates the slots, so
-// a round's upload runs beside the previous round's kernels.  Each begin is matched by an end.
+// The same in two phases on one of TAPROOT_SLOTS contexts per (thread, device): begin stages,
+// uploads and launches on `slot`'s stream and returns; end waits for it and copies the verdicts
+// (and, with msg32_out, the sighashes) back.  The pipelined bcc_taproot_verify_batch rotates the
+// slots (two rounds in flight while the host builds a third), so a round's upload runs beside the
+// previous round's kernels.  Each begin is matched by an end.
+constexpr int TAPROOT_SLOTS = 3;
 int gpu_taproot_begin(int device, int slot, const TaprootJobs* const* parts, size_t P);
 int gpu_taproot_end(int device, int slot, uint8_t* verdict, uint8_t* msg32_out);
 
@@ -534,6 +536,13 @@ private:
     size_t host_cap_ = 0;
     void* vbuf_ = nullptr;        // pinned verdict buffer (fetch_verdicts)
     size_t vcap_ = 0;
+    // Round 5: the verdicts reach vbuf_ through a kernel queued behind the round's last kernel
+    // (queue_verdicts), not a copy-engine D2H issued at fetch time, which waited in the one copy
+    // queue behind the next pipelined round's upload
+    void* vbuf_dev_ = nullptr;    // vbuf_ as the device addresses it
+    bool v_queued_ = false;       // the current run's verdicts are on their way to vbuf_
+    int ensure_vbuf();            // vbuf_ for n_rows_ (stage time: run() allocates nothing)
+    int queue_verdicts(struct ihipStream_t* st);
     size_t n_rows_ = 0, n_pre_ = 0, n_aux_ = 0, n_patch_ = 0, pre_blocks_ = 0, aux_blocks_ = 0;
     uint8_t *d_aux_ = nullptr, *d_pre_ = nullptr, *d_auxd_ = nullptr;
     uint32_t *d_aux_off_ = nullptr, *d_aux_nblk_ = nullptr, *d_pre_off_ = nullptr,
