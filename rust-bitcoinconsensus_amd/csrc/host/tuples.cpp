@@ -102,7 +102,10 @@ struct TupleSlot {
 // is parsed on the host (parse_rows) and its fixed-size rows staged instead.
 constexpr uint64_t DER_BLOB_LIMIT = (uint64_t)1 << 31;
 bool der_on_device(const bcc::DerTuples& t) { return t.pub_bytes() + t.sig_bytes() <= DER_BLOB_LIMIT; }
-thread_local TupleSlot tl_tuple_slots[2];
+// three: rounds k - 1 and k on the device while round k + 1 is staged (round 5; two slots made the
+// staging of round k + 1 wait for round k - 1, which shares the GPU with round k: 8 ms idle gaps)
+constexpr unsigned TUPLE_SLOTS_MAX = 3;
+thread_local TupleSlot tl_tuple_slots[TUPLE_SLOTS_MAX];
 
 void release_pubkey_rows() {
     tl_pubkey_rows = bcc::TupleRows();
@@ -130,7 +133,10 @@ int tuple_round(int dev, const bcc::TupleRows& rows, uint8_t* verdict) {
 // streams) runs beside round k - 1's kernels.  A staging or device error sends the round through
 // the host parse and tuple_round (retry on a fresh batch, then the failure policy).  Measured on
 // 8M C4 tuples (profiles/r05/c4_der): 256k-first doubling to 2M rounds 100-101 M/s, fixed 1M
-// rounds 90 M/s, a 4M cap 95 M/s; the host side is ~13 ms of copying in ~80 ms.
+// rounds 90 M/s, a 4M cap 95 M/s; the host side is ~13 ms of copying in ~80 ms.  With two slots
+// round k + 1 was staged only after round k - 1 finished, and k - 1 shares the GPU with round k
+// (timeline_2slots.txt: 8 ms idle before the last round); three slots: 126.4-126.8 M/s against
+// 103.8-104.9 with two (slots.txt), the staged kernels alone 131.
 constexpr size_t TUPLE_ROUND = (size_t)1 << 20;
 static size_t env_size(const char* name, size_t dflt) {
     const char* e = getenv(name);
@@ -144,6 +150,7 @@ static const size_t g_tuple_first = env_size("BCC_TUPLE_FIRST", TUPLE_ROUND / 4)
 static const size_t g_tuple_round = env_size("BCC_TUPLE_ROUND", 2 * TUPLE_ROUND);
 static const bool g_tuple_ramp = env_size("BCC_TUPLE_RAMP", 1) != 0;
 static const bool g_tuple_trace = getenv("BCC_TUPLE_TRACE") != nullptr;
+static const unsigned g_tuple_slots = (unsigned)std::min<size_t>(3, std::max<size_t>(2, env_size("BCC_TUPLE_SLOTS", 3)));
 
 // Raw tuples [lo, lo + m) of the caller's arrays.
 static bcc::DerTuples der_range(const uint8_t* pub_blob, const uint64_t* pub_off, const uint8_t* msg32,
@@ -195,7 +202,7 @@ int tuple_rounds(int dev, const uint8_t* pub_blob, const uint64_t* pub_off, cons
     double t_stage = 0, t_wait = 0;
     size_t m = 0;
     for (size_t lo = 0; lo < n && !err; lo += m, k++) {
-        TupleSlot& s = tl_tuple_slots[k & 1];
+        TupleSlot& s = tl_tuple_slots[k % g_tuple_slots];
         m = k == 0 ? g_tuple_first : g_tuple_ramp ? std::min(2 * m, g_tuple_round) : g_tuple_round;
         if (m >= n - lo || n - lo - m < m / 2) m = n - lo;
         auto w0 = clk::now();
@@ -230,9 +237,16 @@ int tuple_rounds(int dev, const uint8_t* pub_blob, const uint64_t* pub_off, cons
             if (int e = tuple_round(dev, rows, verdict + lo)) err = e;
         }
         t_stage += sec(w0);
+        if (g_tuple_trace)
+            fprintf(stderr, "[bcc] tup k=%zu m=%zu launched %lld\n", k, m,
+                    (long long)std::chrono::duration_cast<std::chrono::nanoseconds>(clk::now().time_since_epoch()).count());
         w0 = clk::now();
-        if (int e = finish(tl_tuple_slots[(k + 1) & 1])) err = err ? err : e;  // round k - 1
+        // the round that next reuses a slot: k + 1 - slots (with 3 slots round k - 2)
+        if (int e = finish(tl_tuple_slots[(k + 1) % g_tuple_slots])) err = err ? err : e;
         t_wait += sec(w0);
+        if (g_tuple_trace)
+            fprintf(stderr, "[bcc] tup k=%zu finished_prev %lld\n", k,
+                    (long long)std::chrono::duration_cast<std::chrono::nanoseconds>(clk::now().time_since_epoch()).count());
     }
     const auto w0 = clk::now();
     for (auto& s : tl_tuple_slots)
