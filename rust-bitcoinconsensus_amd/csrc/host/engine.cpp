@@ -1212,6 +1212,7 @@ struct ChunkRun {
     // the first device round of a pipelined chunk, staged by the caller (prestage_round)
     std::unique_ptr<StagedRound, void (*)(StagedRound*)> staged{nullptr, gpu_staged_free};
     bool prestaged = false;
+    bool launched = false;  // the prestaged round is already queued on the GPU (chunk_launch)
     std::vector<EarlyShard> early;  // per shard: pre-extracted rows (early Q halves)
     LateHost late;               // offloaded host jobs of the current pass (hashed during the round)
     // their blocks (HostJobs::take); held by pointer so that ChunkRun stays movable
@@ -1388,10 +1389,35 @@ void prestage_round(ChunkRun& c) {
     c.prestaged = true;
 }
 
+// Round 5: a prestaged round without late host jobs is queued on the GPU by the caller right
+// after its staging (upload + kernels, non-blocking), so the next chunk's upload runs beside the
+// previous chunk's kernels instead of after them; chunk_device_round then only waits for it.
+void chunk_launch(ChunkRun& c) {
+    c.launched = false;
+    if (!c.prestaged || c.late_pending) return;
+    if (take_injected_fault() != 0 || gpu_staged_launch(c.staged.get(), nullptr) != 0) {
+        c.prestaged = false;  // the general path (retry, failure policy) runs it
+        c.retries++;
+        return;
+    }
+    c.prestaged = false;
+    c.launched = true;
+}
+
 // The chunk's pending device round (its arguments stay valid until the chunk's next pass).
 int chunk_device_round(ChunkRun& c) {
     LateHost* late = c.late_pending ? &c.late : nullptr;
-    if (c.prestaged) {
+    if (c.launched) {
+        c.launched = false;
+        const int e = gpu_staged_finish(c.staged.get(), c.verdict.data());
+        if (e == 0) {
+            c.devices_used = std::max<size_t>(c.devices_used, 1);
+            return 0;
+        }
+        fprintf(stderr, "[bcc] verify_batch: staged device round failed (hip error %d): running it "
+                        "again through the general path\n", e);
+        c.retries++;
+    } else if (c.prestaged) {
         c.prestaged = false;
         int e = take_injected_fault();
         if (!e) {
@@ -1459,7 +1485,7 @@ long chunk_finish(ChunkRun& c, int* ret_out, bitcoinconsensus_error* err_out, bo
         int e;
         if (c.fut.valid()) {
             e = c.fut.get();
-        } else if (async) {
+        } else if (async && !c.launched) {
             e = run_async([&c] { return chunk_device_round(c); }).get();
         } else {
             e = chunk_device_round(c);
@@ -1538,6 +1564,13 @@ void chunk_release_if_large(ChunkRun& c) {
     c.rds = std::vector<Round>();
 }
 
+// Round 5: stage and queue a pipelined chunk's device round before waiting for the previous chunk
+// (BCC_CHUNK_LAUNCH_EARLY=0: the round-4 order, staged after that wait and run on the worker).
+const bool g_chunk_launch_early = [] {
+    const char* e = getenv("BCC_CHUNK_LAUNCH_EARLY");
+    return e ? atoi(e) != 0 : true;
+}();
+
 // Items per pipelined chunk (bcc_set_pipeline_chunk, BCC_PIPELINE_CHUNK; 0 disables pipelining).
 // Round 4: chunk k's device round on the pipeline worker beside chunk k + 1's host pass, default
 // 500000 items: 1M C2 inputs 24.9-25.2 -> 28.1-28.5 M inputs/s sustained over 10-call runs on the
@@ -1591,6 +1624,11 @@ long run_batch(const bcc_batch_item* items, size_t n, unsigned flags, int* ret_o
                     } catch (...) {
                     }
                 }
+                if (c.launched) {  // queued on the GPU: let it finish before the slot is reused
+                    std::vector<uint8_t> v(std::max<size_t>(1, c.npend));
+                    (void)gpu_staged_finish(c.staged.get(), v.data());
+                    c.launched = false;
+                }
                 c.pending_round = false;
                 c.prestaged = false;
                 c.late_pending = false;
@@ -1615,12 +1653,18 @@ long run_batch(const bcc_batch_item* items, size_t n, unsigned flags, int* ret_o
         for (size_t k = 0; k + 1 < cut.size(); k++) {
             ChunkRun& c = tl_chunk[k & 1];
             chunk_start(c, items + cut[k], cut[k + 1] - cut[k], flags);
+            if (c.pending_round && g_chunk_launch_early) {
+                // staged and queued before the previous chunk is waited for: its upload runs
+                // beside the previous chunk's kernels (chunk_launch)
+                prestage_round(c);
+                chunk_launch(c);
+            }
             if (prev) {
                 account(chunk_finish(*prev, ret_out + prev_lo, err_out ? err_out + prev_lo : nullptr,
                                      true, &gpu_s));
             }
-            if (c.pending_round) {
-                prestage_round(c);  // the pinned image filled here, with the caller's team
+            if (c.pending_round && !c.launched) {
+                if (!g_chunk_launch_early) prestage_round(c);  // the pinned image, with the caller's team
                 c.fut = run_async([&c] {
                     set_stage_threads(PIPELINE_STAGE_THREADS);  // re-runs stage beside the host pass
                     return chunk_device_round(c);
