@@ -275,7 +275,9 @@ extern "C" int bcc_pubkey_verify_batch(const uint8_t* pub_blob, const uint64_t* 
     for (size_t d = 0; d < D; d++) {
         const size_t lo = n * d / D, hi = n * (d + 1) / D;
         jobs.push_back([=] {  // contiguous equal range on devs[d] (offsets stay absolute)
-            if (hi - lo >= 2 * bcc::host::g_tuple_first)
+            // (a range the host small round covers goes to the host lane code in one round: the
+            // pipelined rounds are device rounds)
+            if (hi - lo >= 2 * bcc::host::g_tuple_first && hi - lo > bcc::host::host_small_round())
                 return bcc::host::tuple_rounds(devs[d], pub_blob, pub_off + lo, msg32 + 32 * lo,
                                                sig_blob, sig_off + lo, hi - lo, verdict + lo);
             return bcc::host::der_round(devs[d],
