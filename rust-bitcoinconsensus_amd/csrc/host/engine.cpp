@@ -808,11 +808,7 @@ void prepare(BatchState& b, const bcc_batch_item* items, size_t n, unsigned flag
              std::vector<std::vector<uint32_t>>* runs = nullptr,
              std::vector<EarlyShard>* early = nullptr, unsigned W = 0) {
     if (W == 0 || W > T) W = T;  // worker threads over the T shards (run_shards)
-    static const bool trace = getenv("BCC_PREPARE_TRACE") != nullptr;
-    const auto q0 = std::chrono::steady_clock::now();
-    auto qms = [&] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - q0).count(); };
     if (b.st.size() < n) b.st.resize(n);  // reused across calls: every field is (re)set below
-    const double q_st = trace ? qms() : 0;
     b.n = n;
     b.flags = flags;
     auto& st = b.st;
@@ -866,10 +862,8 @@ void prepare(BatchState& b, const bcc_batch_item* items, size_t n, unsigned flag
             b.tx_first.swap(cut);
         }
     }
-    const double q_scan = trace ? qms() : 0;
     const size_t E = b.tx_first.size();
     if (b.txs.size() < E) b.txs.resize(E);  // grow only, like st
-    const double q_txs = trace ? qms() : 0;
     // per-thread timing (bcc_batch_stats prepare_*): dispatch -> start lag, parse, batched HASH160
     using pclk = std::chrono::steady_clock;
     std::vector<double> lag(T, 0), tparse(T, 0), thash(T, 0);
@@ -976,16 +970,6 @@ void prepare(BatchState& b, const bcc_batch_item* items, size_t n, unsigned flag
         flush();
         thash[t] = std::chrono::duration<double>(pclk::now() - s1).count();
     });
-    if (trace) {
-        double pmax = 0, psum = 0, hmax = 0;
-        for (unsigned t = 0; t < T; t++) {
-            pmax = std::max(pmax, tparse[t]);
-            psum += tparse[t];
-            hmax = std::max(hmax, thash[t]);
-        }
-        fprintf(stderr, "[bcc] prepare n=%zu T=%u W=%u E=%zu: st %.2f scan %.2f txs %.2f parallel-end %.2f ms; parse max %.2f mean %.2f hash max %.2f ms\n",
-                n, T, W, E, q_st, q_scan, q_txs, qms(), 1e3 * pmax, 1e3 * psum / T, 1e3 * hmax);
-    }
     for (unsigned t = 0; t < T; t++) {
         t_stats.prepare_lag_seconds = std::max(t_stats.prepare_lag_seconds, lag[t]);
         t_stats.prepare_parse_seconds = std::max(t_stats.prepare_parse_seconds, tparse[t]);
