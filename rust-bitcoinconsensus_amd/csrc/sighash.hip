@@ -1610,14 +1610,9 @@ int DeviceBatch::fetch_verdicts(uint8_t* out) {
         memcpy(out, vbuf_, n_rows_);
         return 0;
     }
-    if (n_rows_ > vcap_) {
-        if (vbuf_) BCC_HIP_TRY(hipHostFree(vbuf_));
-        vbuf_ = nullptr;
-        vcap_ = 0;
-        BCC_HIP_TRY(hipHostMalloc(&vbuf_, n_rows_, hipHostMallocDefault));
-        vcap_ = n_rows_;
-    }
     BCC_HIP_TRY(hipSetDevice(dev_));
+    if (n_rows_ > vcap_)  // (stage sized it; kept in step with vbuf_dev_ either way)
+        if (int e = ensure_vbuf()) return e;
     hipStream_t st = (hipStream_t)pick(last_stream_);
     BCC_HIP_TRY(hipMemcpyAsync(vbuf_, d_v, n_rows_, hipMemcpyDeviceToHost, st));
     if (int e = wait(st)) return e;
