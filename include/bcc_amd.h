@@ -214,6 +214,9 @@ typedef struct bcc_batch_stats {
      * GPU during the host pass, the deferred rows mapped to them, and the extraction + launch time */
     size_t early_rows, early_mapped;
     double early_seconds;
+    /* ... and the mapped rows whose legacy sighash came from the early set too (early sighashes:
+     * long-template SIGHASH_ALL jobs hashed during the host pass, the round's copy skipped) */
+    size_t early_msgs;
 } bcc_batch_stats;
 /* Statistics of the calling thread's last bitcoinconsensus_verify_batch / verify call. */
 void bcc_last_batch_stats(bcc_batch_stats* out);

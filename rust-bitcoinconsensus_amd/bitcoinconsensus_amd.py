@@ -217,7 +217,7 @@ class BatchStats(ctypes.Structure):
                 ("process_cpu_seconds", ctypes.c_double),
                 ("process_cpu_in_gpu_wait_seconds", ctypes.c_double),
                 ("early_rows", ctypes.c_size_t), ("early_mapped", ctypes.c_size_t),
-                ("early_seconds", ctypes.c_double)]
+                ("early_seconds", ctypes.c_double), ("early_msgs", ctypes.c_size_t)]
 
 
 def _bind_consensus(L):

@@ -83,6 +83,8 @@ struct TxEntry {
     int32_t wtx = -1;               // WtxRec index in the current round (-1: none)
     int64_t htpl = -1;              // host-kept legacy template offset (HostJobs::tpl), -1: none
     int32_t hdig = -1;              // host-computed BIP143 per-tx digests (HostJobs::dig), -1: none
+    int64_t etpl = -1;              // legacy template offset in the shard's early jobs, -1: none
+    uint32_t etpl_len = 0;          // ... its length (0: not measured yet this call)
 };
 
 // Long serial SHA chains stay on the host.  One GPU lane compresses one block
@@ -196,15 +198,22 @@ struct EarlyCand {
     const uint8_t* sig;
     uint32_t publen, siglen;
     uint32_t row;  // in the shard's early rows
+    // early sighash (legacy SIGHASH_ALL over a long template): the row's message is hashed in the
+    // early set from this scriptCode; a deferred check with the same code bytes takes it (TPL_EARLY)
+    const uint8_t* code = nullptr;
+    uint32_t code_len = 0;
+    bool msg = false;
 };
 struct alignas(64) EarlyShard {  // one per shard, written by its worker: own cache lines
     TupleRows rows;
     std::vector<EarlyCand> cands;
+    SighashJobs jobs;  // the early sighash template jobs (rows: the early rows above)
     void clear() {
         rows.clear();
         rows.msg_one = true;
         rows.y_unused = true;
         cands.clear();
+        jobs.clear();
     }
 };
 
@@ -213,6 +222,20 @@ std::atomic<int> g_early_q{[] {
     return e ? atoi(e) : 1;
 }()};
 constexpr size_t EARLY_MAX_ITEMS = (size_t)1 << 18;
+// early sighashes (BCC_EARLY_SIGHASH, default 1): legacy template jobs with the early rows.  Only
+// the chains between BCC_EARLY_SIGHASH_MIN blocks (from the midstate) and the host's share
+// (host_chain_blocks) go early: C3 5.4-5.7 -> 5.7-6.6 M inputs/s at 96 (64: 5.2-6.4; every long
+// template, no cap: 4.9-5.2, the early chains then crowd the early K_keyq and duplicate the host's;
+// profiles/r05/c3/early_sighash.txt).
+const bool g_early_sighash = [] {
+    const char* e = getenv("BCC_EARLY_SIGHASH");
+    return e ? atoi(e) != 0 : true;
+}();
+// ... for jobs of at least this many blocks from their midstate (BCC_EARLY_SIGHASH_MIN)
+const uint32_t g_early_sighash_min = [] {
+    const char* e = getenv("BCC_EARLY_SIGHASH_MIN");
+    return e ? (uint32_t)atoi(e) : 96u;
+}();
 
 // CPubKey size filter, non-empty signature, lax DER (sans the hash-type byte), r != 0, s != 0: the
 // host half of a deferred check (Round::defer); false = rejected on the host, no row.
@@ -257,7 +280,13 @@ int script_pushes(const Span& sc, Span* out, int cap) {
     return k;
 }
 
+bool early_sighash_job(EarlyShard& es, TxEntry& te, unsigned nin, const Span& code, int hashtype,
+                       uint32_t row);
+
 // The item's candidate (key, signature) pairs by the shape of its spent script and its input.
+// Legacy candidates (P2PKH, P2SH multisig, P2PK) of a long template with SIGHASH_ALL also get an
+// early sighash job over the scriptCode the interpreter will use (the spent script, or the redeem
+// script), so that the round's longest chains run during the host pass too.
 void early_extract_item(Item& it, EarlyShard& es) {
     it.ec_first = (uint32_t)es.cands.size();
     it.ec_count = 0;
@@ -266,13 +295,21 @@ void early_extract_item(Item& it, EarlyShard& es) {
     const size_t L = in->script_pubkey_len;
     if (!spk) return;
     const TxIn& txin = it.tx->tx.vin[in->n_in];
-    auto add = [&](const Span& pub, const Span& sig) {
+    // code.n != 0: a legacy check over that scriptCode (early sighash when the template is long)
+    auto add = [&](const Span& pub, const Span& sig, const Span& code = Span{}) {
         uint8_t r[32], s[32];
         if (!tuple_fields(pub.p, pub.n, sig.p, sig.n, r, s)) return;
         const bool k65 = pub.n == 65;
         const uint32_t row = es.rows.add_lazy(pub.p[0], pub.p + 1, r, s, k65 ? pub.p + 33 : nullptr, nullptr);
         if (k65) es.rows.y_unused = false;
-        es.cands.push_back(EarlyCand{pub.p, sig.p, (uint32_t)pub.n, (uint32_t)sig.n, row});
+        EarlyCand c{pub.p, sig.p, (uint32_t)pub.n, (uint32_t)sig.n, row};
+        if (code.n && g_early_sighash && legacy_all_type(sig.p[sig.n - 1]) &&
+            early_sighash_job(es, *it.tx, in->n_in, code, sig.p[sig.n - 1], row)) {
+            c.code = code.p;
+            c.code_len = (uint32_t)code.n;
+            c.msg = true;
+        }
+        es.cands.push_back(c);
         it.ec_count++;
     };
     const auto& wit = txin.witness;
@@ -282,7 +319,7 @@ void early_extract_item(Item& it, EarlyShard& es) {
     }
     Span pu[20];
     if (L == 25 && spk[0] == 0x76 && spk[1] == 0xa9 && spk[2] == 0x14 && spk[23] == 0x88 && spk[24] == 0xac) {
-        if (script_pushes(txin.script_sig, pu, 2) == 2) add(pu[1], pu[0]);  // P2PKH: <sig> <key>
+        if (script_pushes(txin.script_sig, pu, 2) == 2) add(pu[1], pu[0], Span{spk, L});  // P2PKH
         return;
     }
     if (L == 23 && spk[0] == 0xa9 && spk[1] == 0x14 && spk[22] == 0x87) {  // P2SH
@@ -302,11 +339,11 @@ void early_extract_item(Item& it, EarlyShard& es) {
         if (script_pushes(Span{rs.p + 1, rs.n - 3}, keys, 16) != n) return;
         if (m * (n - m + 1) > 16) return;
         for (int i = 0; i < m; i++)
-            for (int j = i; j <= i + n - m; j++) add(keys[j], pu[1 + i]);
+            for (int j = i; j <= i + n - m; j++) add(keys[j], pu[1 + i], rs);
         return;
     }
     if (((L == 35 && spk[0] == 33) || (L == 67 && spk[0] == 65)) && spk[L - 1] == 0xac) {  // P2PK
-        if (script_pushes(txin.script_sig, pu, 1) == 1) add(Span{spk + 1, L - 2}, pu[0]);
+        if (script_pushes(txin.script_sig, pu, 1) == 1) add(Span{spk + 1, L - 2}, pu[0], Span{spk, L});
     }
 }
 
@@ -390,10 +427,14 @@ void host_bip143_sighash(HostJobs& host, TxEntry& te, unsigned nin, const Bytes&
 // `host` (optional): legacy checks whose SHA chain exceeds host->chain_blocks, and every BIP143
 // check of a tx whose per-tx chains exceed host->bip143_blocks, are hashed on the host (HostJobs);
 // their msg rows in `rows` are materialized (the other rows stay lazy ONE).
-void add_sighash_job(SighashJobs& jobs, TxEntry& te, const bcc_batch_item& in, const Bytes& code,
+// early (round 5): the row's digest also exists in the call's early set; a device template job is
+// then flagged TPL_EARLY (the front skips it, the round copies the early digest).  Returns whether
+// it was so flagged.
+bool add_sighash_job(SighashJobs& jobs, TxEntry& te, const bcc_batch_item& in, const Bytes& code,
                      SigVersion sv, int hashtype, uint32_t row, std::vector<uint8_t>& scratch,
                      Bip143Job& bip143, std::vector<TxEntry*>& touched, HostJobs* host = nullptr,
-                     TupleRows* rows = nullptr) {
+                     TupleRows* rows = nullptr, bool early = false) {
+    bool flagged = false;
     const Tx& tx = te.tx;
     const unsigned nin = in.n_in;
     const uint32_t hb = host && rows ? host->chain_blocks : 0;
@@ -442,6 +483,8 @@ void add_sighash_job(SighashJobs& jobs, TxEntry& te, const bcc_batch_item& in, c
         } else {
             tj.tpl_off = (uint32_t)te.tpl;
             tj.code_off = jobs.add_code(scratch.data(), scratch.size());
+            if (early) tj.nblk |= TPL_EARLY;
+            flagged = early;
             jobs.tjobs.push_back(tj);
         }
     } else if (sv == SIGVERSION_BASE) {
@@ -511,6 +554,47 @@ void add_sighash_job(SighashJobs& jobs, TxEntry& te, const bcc_batch_item& in, c
             jobs.patches.push_back(PatchRec{(uint32_t)(base + job.off[k]), (uint32_t)aux});
         }
     }
+    return flagged;
+}
+
+// An early sighash job (early Q halves, round 5): the legacy SIGHASH_ALL template job of input
+// nin over `code`, as add_sighash_job would build it, with the early row `row` as its output.
+// Only long templates (>= TPL_MID_MIN_BLOCKS blocks: the chains that set a small round's front)
+// qualify; false = no job.  The template (with midstates) is placed once per tx and shard.
+bool early_sighash_job(EarlyShard& es, TxEntry& te, unsigned nin, const Span& code, int hashtype,
+                       uint32_t row) {
+    const Tx& tx = te.tx;
+    if (te.etpl < 0 && te.etpl_len == 0) te.etpl_len = (uint32_t)legacy_template_len(tx);
+    if (SighashJobs::tpl_nblk(te.etpl_len, 1) < TPL_MID_MIN_BLOCKS) return false;
+    // only the chains that set the round's front: blocks from the splice's midstate on
+    const uint32_t pos = (uint32_t)legacy_template_pos(tx, nin);
+    const uint32_t cfield = (uint32_t)code.n + (code.n < 253 ? 1 : code.n <= 0xFFFF ? 3 : 5);
+    const uint32_t work = SighashJobs::tpl_nblk(te.etpl_len, cfield) - pos / 64;
+    const uint32_t hb = g_host_chain_blocks.load(std::memory_order_relaxed);
+    if (work < g_early_sighash_min || (hb && work > hb)) return false;  // (longer: the host's)
+    SighashJobs& jobs = es.jobs;
+    if (te.etpl < 0) {
+        static thread_local std::vector<uint8_t> tbuf;
+        static thread_local std::vector<uint32_t> mbuf;
+        build_legacy_template(tx, tbuf);
+        tpl_midstates(tbuf.data(), (uint32_t)tbuf.size(), mbuf);
+        te.etpl = jobs.add_tpl(tbuf.data(), tbuf.size(), mbuf.data());
+        te.etpl_len = (uint32_t)tbuf.size();
+    }
+    static thread_local std::vector<uint8_t> field;
+    const Bytes c(code.p, code.p + code.n);
+    build_script_code_field(c, field);
+    TplJob tj;
+    tj.tpl_off = (uint32_t)te.etpl;
+    tj.tpl_len = te.etpl_len;
+    tj.pos = pos;
+    tj.code_off = jobs.add_code(field.data(), field.size());
+    tj.code_len = (uint32_t)field.size();
+    tj.hashtype = (uint32_t)hashtype;
+    tj.row = row;
+    tj.nblk = SighashJobs::tpl_nblk(tj.tpl_len, tj.code_len) | TPL_MID;
+    jobs.tjobs.push_back(tj);
+    return true;
 }
 
 class Round;
@@ -569,6 +653,7 @@ public:
     const EarlyShard* early = nullptr;  // this shard's early rows (whole call; null: none)
     uint32_t erow0 = 0;                 // ... and their first lane in the call's early set
     size_t early_mapped = 0;            // rows mapped to an early twin (whole call)
+    size_t early_msgs = 0;              // ... of which take its early sighash (TPL_EARLY)
 
     // GenericTransactionSignatureChecker::CheckECDSASignature (interpreter.cpp:1656-1676) up to
     // the point where the sighash + secp256k1 verify would run; those become a GPU tuple.
@@ -627,8 +712,17 @@ public:
             *key_taken = true;
             key_hashes++;
         }
-        add_sighash_job(jobs, *it.tx, *it.in, code, sv, hashtype, row, scratch, bip143, touched,
-                        &host, &rows);
+        // the twin's early sighash is this check's when the interpreter's scriptCode is the one
+        // the early job used (legacy, same bytes: FindAndDelete left it alone) -- the hashtype is
+        // the signature's last byte, equal by the twin match
+        const bool early_msg = twin && twin->msg && sv == SIGVERSION_BASE &&
+                               twin->code_len == code.size() &&
+                               memcmp(twin->code, code.data(), code.size()) == 0;
+        if (add_sighash_job(jobs, *it.tx, *it.in, code, sv, hashtype, row, scratch, bip143, touched,
+                            &host, &rows, early_msg)) {
+            rows.set_mmap(row, erow0 + twin->row);
+            early_msgs++;
+        }
         it.cache.push_back(Item::Check{koff, klen, -2 - (int32_t)pending.size()});
         if (consult) it.pending.push_back((uint32_t)pending.size());
         pending.push_back(Pending{item_idx, (uint32_t)(it.cache.size() - 1)});
@@ -899,6 +993,8 @@ void prepare(BatchState& b, const bcc_batch_item* items, size_t n, unsigned flag
             e.wtx = -1;
             e.htpl = -1;
             e.hdig = -1;
+            e.etpl = -1;
+            e.etpl_len = 0;
             e.ok = flags_ok && in->tx_to != nullptr && parse_tx(in->tx_to, in->tx_to_len, e.tx);
             const size_t end = k + 1 < E ? b.tx_first[k + 1] : n;
             for (size_t i = b.tx_first[k]; i < end; i++) {
@@ -1288,18 +1384,21 @@ void chunk_early(ChunkRun& c, bool allow) {
         c.rds[t].early = nullptr;
         c.rds[t].erow0 = 0;
         c.rds[t].early_mapped = 0;
+        c.rds[t].early_msgs = 0;
     }
     if (!early_wanted(c.n, allow)) return;
     const std::vector<int> devs = device_list();
     auto e0 = clk::now();
     std::vector<const TupleRows*> parts(c.T);
     size_t E = 0;
+    std::vector<const SighashJobs*> jparts(c.T);
     for (unsigned t = 0; t < c.T; t++) {
         c.rds[t].erow0 = (uint32_t)E;
         E += c.early[t].rows.size();
         parts[t] = &c.early[t].rows;
+        jparts[t] = &c.early[t].jobs;
     }
-    if (E > host_small_round() && gpu_early_launch(devs[0], parts.data(), c.T) == 0) {
+    if (E > host_small_round() && gpu_early_launch(devs[0], parts.data(), c.T, jparts.data()) == 0) {
         for (unsigned t = 0; t < c.T; t++) c.rds[t].early = &c.early[t];
         t_stats.early_rows += E;
     }
@@ -1509,6 +1608,7 @@ long chunk_finish(ChunkRun& c, int* ret_out, bitcoinconsensus_error* err_out, bo
         t_stats.host_rejected += c.rds[t].host_rejected;
         t_stats.device_key_hashes += c.rds[t].key_hashes;
         t_stats.early_mapped += c.rds[t].early_mapped;
+        t_stats.early_msgs += c.rds[t].early_msgs;
     }
     auto f0 = clk::now();
     std::vector<long> vt(c.T, 0);

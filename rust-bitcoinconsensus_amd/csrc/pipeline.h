@@ -65,11 +65,18 @@ struct TplJob {
 #endif
 constexpr uint32_t TPL_MID = 0x80000000u;
 constexpr uint32_t TPL_MID_MIN_BLOCKS = 8;  // shorter templates start from the IV
+// Round 5, early sighashes: a job flagged TPL_EARLY (in nblk) has the same digest already computed
+// in the call's early set (DeviceBatch::early_launch; its row's TupleRows::mmap names the early
+// row), so the device's front lane skips it and the round copies that digest into the row instead.
+// The host (fallback, small rounds) hashes it like any job; staging clears the flag when the early
+// digests are not live for the round.
+constexpr uint32_t TPL_EARLY = 0x40000000u;
 BCC_PL_HD inline uint32_t tpl_mid_count(uint32_t tpl_len) { return (tpl_len - 1) / 64 + 1; }
 BCC_PL_HD inline uint32_t tpl_mid_offset(uint32_t tpl_off, uint32_t tpl_len) {  // 4-aligned, after the 8 zero bytes
     return tpl_off + ((tpl_len + 3) & ~3u) + 8;
 }
-BCC_PL_HD inline uint32_t tpl_nblk(const TplJob& j) { return j.nblk & ~TPL_MID; }
+BCC_PL_HD inline uint32_t tpl_nblk(const TplJob& j) { return j.nblk & ~(TPL_MID | TPL_EARLY); }
+BCC_PL_HD inline bool tpl_early(const TplJob& j) { return (j.nblk & TPL_EARLY) != 0; }
 BCC_PL_HD inline bool tpl_has_mid(const TplJob& j) { return (j.nblk & TPL_MID) != 0; }
 // The blocks a job hashes (from its start block: pos / 64 with midstates, else 0).
 BCC_PL_HD inline uint32_t tpl_job_blocks(const TplJob& j) {
@@ -228,9 +235,18 @@ struct TupleRows {
         if (emap.size() <= row) emap.resize(row + 1, NO_EARLY);
         emap[row] = e;
     }
-    void copy_emap(uint32_t* out, size_t lo, size_t hi) const {
-        const size_t have = std::min(std::max(emap.size(), lo), hi);
-        if (have > lo) memcpy(out, &emap[lo], 4 * (have - lo));
+    void copy_emap(uint32_t* out, size_t lo, size_t hi) const { copy_map(emap, out, lo, hi); }
+    // Early sighashes (TPL_EARLY): mmap[row] = the early row whose message (the same legacy
+    // sighash job) the device copies into this row; NO_EARLY: none.
+    std::vector<uint32_t> mmap;
+    void set_mmap(size_t row, uint32_t e) {
+        if (mmap.size() <= row) mmap.resize(row + 1, NO_EARLY);
+        mmap[row] = e;
+    }
+    void copy_mmap(uint32_t* out, size_t lo, size_t hi) const { copy_map(mmap, out, lo, hi); }
+    static void copy_map(const std::vector<uint32_t>& m, uint32_t* out, size_t lo, size_t hi) {
+        const size_t have = std::min(std::max(m.size(), lo), hi);
+        if (have > lo) memcpy(out, &m[lo], 4 * (have - lo));
         for (size_t k = have; k < hi; k++) out[k - lo] = NO_EARLY;
     }
     size_t size() const { return tag.size(); }
@@ -296,7 +312,7 @@ struct TupleRows {
     }
     void clear() {
         tag.clear(); x.clear(); y.clear(); r.clear(); s.clear(); msg.clear();
-        hrow.clear(); hprog.clear(); emap.clear();
+        hrow.clear(); hprog.clear(); emap.clear(); mmap.clear();
         msg_one = y_unused = false;
     }
 };
@@ -560,6 +576,7 @@ private:
     uint32_t* d_hrow_ = nullptr;
     uint8_t* d_hprog_ = nullptr;
     uint32_t* d_emap_ = nullptr;  // staged TupleRows::emap (null: no row has an early twin)
+    uint32_t* d_mmap_ = nullptr;  // staged TupleRows::mmap (null: no row takes an early sighash)
     // stage_der: the rows come from K_der over these (n_der_ = 0: rows staged by stage_parts)
     size_t n_der_ = 0;
     const uint8_t *d_pub_ = nullptr, *d_sig_ = nullptr;
@@ -571,7 +588,9 @@ public:
     // pre-extracted (key, signature) rows, launched on a stream of their own while the host still
     // interprets the call; a later round whose rows carry TupleRows::emap copies them instead of
     // running its own K_keyq on those rows.  early_reset forgets the set (a new call).
-    int early_launch(const TupleRows* const* rows, size_t P);
+    // jobs (optional, one per part): legacy template jobs whose rows are the early rows of the same
+    // part (early sighashes, TPL_EARLY), hashed on a stream of their own
+    int early_launch(const TupleRows* const* rows, size_t P, const SighashJobs* const* jobs = nullptr);
     void early_reset();
     size_t early_rows() const { return early_n_; }
 
@@ -585,11 +604,17 @@ private:
     size_t early_cap_ = 0;
     void* early_host_ = nullptr;    // pinned image of early_arena_
     size_t early_host_cap_ = 0;
+    void* early_sig_stream_ = nullptr;  // hipStream_t: the early sighash jobs
+    void* ev_early_up_ = nullptr;       // hipEvent_t: the early image uploaded
+    void* ev_early_sig_ = nullptr;      // hipEvent_t: the early sighashes done
+    bool early_msgs_ = false;           // the current early set has sighashes (early_msg_)
+    uint8_t* early_msg_ = nullptr;      // 32 bytes per early row (only job rows written)
 };
 
 // The calling thread's device batch on `device` (the one gpu_verify_parts runs): early Q halves
 // for the call's pre-extracted rows (DeviceBatch::early_launch), and the reset of a new call.
-int gpu_early_launch(int device, const TupleRows* const* rows, size_t P);
+int gpu_early_launch(int device, const TupleRows* const* rows, size_t P,
+                     const SighashJobs* const* jobs = nullptr);
 void gpu_early_reset(int device);
 
 // Threads the calling thread's device batches use to fill their pinned staging image (0: one per

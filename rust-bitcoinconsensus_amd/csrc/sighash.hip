@@ -216,6 +216,7 @@ __device__ __forceinline__ void sha256d_tpl_lane(const uint8_t* __restrict__ tpl
                                                  const TplJob* __restrict__ jobs, uint32_t i,
                                                  uint8_t* __restrict__ out) {
     const TplJob j = jobs[i];
+    if (tpl_early(j)) return;  // the digest comes from the call's early set (TPL_EARLY)
     TplMsg m;
     m.T = tpl + j.tpl_off;
     m.C = code + j.code_off;
@@ -901,7 +902,13 @@ DeviceBatch::~DeviceBatch() {
         (void)hipStreamSynchronize((hipStream_t)early_stream_);
         (void)hipStreamDestroy((hipStream_t)early_stream_);
     }
+    if (early_sig_stream_) {
+        (void)hipStreamSynchronize((hipStream_t)early_sig_stream_);
+        (void)hipStreamDestroy((hipStream_t)early_sig_stream_);
+    }
     if (ev_early_) (void)hipEventDestroy((hipEvent_t)ev_early_);
+    if (ev_early_up_) (void)hipEventDestroy((hipEvent_t)ev_early_up_);
+    if (ev_early_sig_) (void)hipEventDestroy((hipEvent_t)ev_early_sig_);
     if (early_arena_) (void)hipFree(early_arena_);
     if (early_host_) (void)hipHostFree(early_host_);
 }
@@ -909,34 +916,49 @@ DeviceBatch::~DeviceBatch() {
 // Early Q halves: the rows go up on the batch's early stream, then K_inv and K_keyq over them into
 // early_scratch_ (their own scratch: the round's K_keyq copies from it).  The previous set's work
 // (a call whose rounds never needed it) is waited for before its image and scratch are reused.
-int DeviceBatch::early_launch(const TupleRows* const* Rw, size_t P) {
+int DeviceBatch::early_launch(const TupleRows* const* Rw, size_t P, const SighashJobs* const* Jp) {
     early_n_ = 0;
+    early_msgs_ = false;
     BCC_HIP_TRY(hipSetDevice(dev_));
     if (!early_stream_) {
-        hipStream_t s = nullptr;
-        hipEvent_t e = nullptr;
+        hipStream_t s = nullptr, s2 = nullptr;
+        hipEvent_t e = nullptr, e2 = nullptr, e3 = nullptr;
         BCC_HIP_TRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+        BCC_HIP_TRY(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
         BCC_HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        BCC_HIP_TRY(hipEventCreateWithFlags(&e2, hipEventDisableTiming));
+        BCC_HIP_TRY(hipEventCreateWithFlags(&e3, hipEventDisableTiming));
         early_stream_ = s;
+        early_sig_stream_ = s2;
         ev_early_ = e;
+        ev_early_up_ = e2;
+        ev_early_sig_ = e3;
     }
-    hipStream_t es = (hipStream_t)early_stream_;
+    hipStream_t es = (hipStream_t)early_stream_, ss = (hipStream_t)early_sig_stream_;
     if (early_pending_) {
         BCC_HIP_TRY(hipStreamSynchronize(es));
+        BCC_HIP_TRY(hipStreamSynchronize(ss));
         early_pending_ = false;
     }
-    std::vector<size_t> row0(P + 1, 0);
+    std::vector<size_t> row0(P + 1, 0), tpl0(P + 1, 0), code0(P + 1, 0), tj0(P + 1, 0);
     bool need_y = false;
     for (size_t p = 0; p < P; p++) {
         row0[p + 1] = row0[p] + Rw[p]->size();
         need_y |= !Rw[p]->y_unused && Rw[p]->size() != 0;
+        const SighashJobs* j = Jp ? Jp[p] : nullptr;
+        tpl0[p + 1] = tpl0[p] + (j ? j->tpl.size() : 0);
+        code0[p + 1] = code0[p] + (j ? j->code.size() : 0);
+        tj0[p + 1] = tj0[p] + (j ? j->tjobs.size() : 0);
     }
-    const size_t R = row0[P];
+    const size_t R = row0[P], NT = tj0[P];
     if (R == 0) return 0;
-    // tag | x | y | r | s, each 256-aligned
+    if (tpl0[P] >= ((size_t)1 << 32) || code0[P] >= ((size_t)1 << 32)) return (int)hipErrorInvalidValue;
+    // tag | x | y | r | s | TPL | CODE | TJOB (uploaded) | MSG (device-written), each 256-aligned
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
     const size_t o_tag = 0, o_x = al(R), o_y = o_x + al(32 * R), o_r = o_y + al(32 * R),
-                 o_s = o_r + al(32 * R), total = o_s + al(32 * R);
+                 o_s = o_r + al(32 * R), o_tpl = o_s + al(32 * R), o_code = o_tpl + al(tpl0[P] + 64),
+                 o_tj = o_code + al(code0[P] + 64), o_msg = o_tj + al(sizeof(TplJob) * NT),
+                 upload = NT ? o_msg : o_tpl, total = o_msg + al(NT ? 32 * R : 0);
     if (total > early_cap_) {
         if (early_arena_) BCC_HIP_TRY(hipFree(early_arena_));
         early_arena_ = nullptr;
@@ -944,12 +966,12 @@ int DeviceBatch::early_launch(const TupleRows* const* Rw, size_t P) {
         BCC_HIP_TRY(hipMalloc(&early_arena_, total));
         early_cap_ = total;
     }
-    if (total > early_host_cap_) {
+    if (upload > early_host_cap_) {
         if (early_host_) BCC_HIP_TRY(hipHostFree(early_host_));
         early_host_ = nullptr;
         early_host_cap_ = 0;
-        BCC_HIP_TRY(hipHostMalloc(&early_host_, total, hipHostMallocDefault));
-        early_host_cap_ = total;
+        BCC_HIP_TRY(hipHostMalloc(&early_host_, upload, hipHostMallocDefault));
+        early_host_cap_ = upload;
     }
     uint8_t* h = (uint8_t*)early_host_;
     auto fill = [&](size_t p) {
@@ -961,15 +983,43 @@ int DeviceBatch::early_launch(const TupleRows* const* Rw, size_t P) {
         if (need_y) rw.copy_y(h + o_y + 32 * r0, 0, nr);
         memcpy(h + o_r + 32 * r0, rw.r.data(), 32 * nr);
         memcpy(h + o_s + 32 * r0, rw.s.data(), 32 * nr);
+        if (!NT || !Jp || !Jp[p]) return;
+        const SighashJobs& j = *Jp[p];
+        if (!j.tpl.empty()) memcpy(h + o_tpl + tpl0[p], j.tpl.data(), j.tpl.size());
+        if (!j.code.empty()) memcpy(h + o_code + code0[p], j.code.data(), j.code.size());
+        TplJob* tj = (TplJob*)(h + o_tj) + tj0[p];
+        for (size_t k = 0; k < j.tjobs.size(); k++) {
+            TplJob t = j.tjobs[k];
+            t.tpl_off += (uint32_t)tpl0[p];
+            t.code_off += (uint32_t)code0[p];
+            t.row += (uint32_t)r0;
+            t.nblk &= ~TPL_EARLY;
+            tj[k] = t;
+        }
     };
+    if (NT) {  // the blobs' tails the lanes may read past (dword loads)
+        memset(h + o_tpl + tpl0[P], 0, 64);
+        memset(h + o_code + code0[P], 0, 64);
+    }
     if (P > 1 && R >= 4096) host::run_team((unsigned)std::min<size_t>(P, 16), [&](unsigned t) {
         for (size_t p = t; p < P; p += std::min<size_t>(P, 16)) fill(p);
     });
     else
         for (size_t p = 0; p < P; p++) fill(p);
     uint8_t* a = (uint8_t*)early_arena_;
-    BCC_HIP_TRY(hipMemcpyAsync(a, h, need_y ? total : o_y, hipMemcpyHostToDevice, es));
-    if (!need_y) BCC_HIP_TRY(hipMemcpyAsync(a + o_r, h + o_r, total - o_r, hipMemcpyHostToDevice, es));
+    BCC_HIP_TRY(hipMemcpyAsync(a, h, need_y ? upload : o_y, hipMemcpyHostToDevice, es));
+    if (!need_y) BCC_HIP_TRY(hipMemcpyAsync(a + o_r, h + o_r, upload - o_r, hipMemcpyHostToDevice, es));
+    if (NT) {  // the early sighashes on their own stream, beside K_inv / K_keyq
+        BCC_HIP_TRY(hipEventRecord((hipEvent_t)ev_early_up_, es));
+        BCC_HIP_TRY(hipStreamWaitEvent(ss, (hipEvent_t)ev_early_up_, 0));
+        hipLaunchKernelGGL(sighash_front_kernel, dim3((unsigned)((NT + XS_WG - 1) / XS_WG)), dim3(XS_WG), 0,
+                           ss, nullptr, nullptr, 0u, nullptr, nullptr, a + o_tpl, a + o_code,
+                           (const TplJob*)(a + o_tj), (uint32_t)NT, nullptr, nullptr, nullptr, 0u,
+                           nullptr, a + o_msg);
+        BCC_HIP_TRY(hipGetLastError());
+        BCC_HIP_TRY(hipEventRecord((hipEvent_t)ev_early_sig_, ss));
+        early_msg_ = a + o_msg;
+    }
     const uint8_t *dt = a + o_tag, *dx = a + o_x, *dy = a + o_y, *dr = a + o_r, *ds = a + o_s;
     if (int e = ecdsa_launch_pre(early_scratch_, dt, dx, dy, ds, R, es)) return e;
     if (int e = ecdsa_launch_key(early_scratch_, dt, dx, dy, R, es)) return e;
@@ -979,11 +1029,17 @@ int DeviceBatch::early_launch(const TupleRows* const* Rw, size_t P) {
     early_scratch_.q_ready = 0;
     BCC_HIP_TRY(hipEventRecord((hipEvent_t)ev_early_, es));
     early_pending_ = true;
-    if (launched) early_n_ = R;
+    if (launched) {
+        early_n_ = R;
+        early_msgs_ = NT != 0;
+    }
     return 0;
 }
 
-void DeviceBatch::early_reset() { early_n_ = 0; }
+void DeviceBatch::early_reset() {
+    early_n_ = 0;
+    early_msgs_ = false;
+}
 
 void* DeviceBatch::pick(void* stream) {
     if (!stream) {
@@ -1083,19 +1139,23 @@ int DeviceBatch::stage_parts(const SighashJobs* const* J, const TupleRows* const
     const size_t R = n_rows_;
     // regions filled from the host image first (one copy), device-written ones after them
     // Y and M go up only when some part needs them (TupleRows::y_unused / msg_one)
-    enum { TAG, X, RR, S, EMAP, AUX, PRE, AUX_OFF, AUX_NBLK, PRE_OFF, PRE_NBLK, PRE_ROW, PATCH,
+    enum { TAG, X, RR, S, EMAP, MMAP, AUX, PRE, AUX_OFF, AUX_NBLK, PRE_OFF, PRE_NBLK, PRE_ROW, PATCH,
            TPL, CODE, TJOB, TXRAW, WTX, WJOB, HROW, HPROG, ZEROS, UPLOADED, Y = UPLOADED, M, V, AUXD, INTAB, TXD,
            NB };
-    bool need_y = false, need_m = false, need_e = false;
+    bool need_y = false, need_m = false, need_e = false, need_mm = false;
     for (size_t p = 0; p < P; p++) {
         need_y |= !Rw[p]->y_unused && Rw[p]->size() != 0;
         need_m |= !Rw[p]->msg_one && Rw[p]->size() != 0;
         need_e |= !Rw[p]->emap.empty();
+        need_mm |= !Rw[p]->mmap.empty();
     }
     need_e = need_e && early_n_ != 0;  // early twins exist for this batch's call (early_launch)
+    // early sighashes (TPL_EARLY jobs) only with live early digests; else the jobs run as usual
+    need_mm = need_mm && early_n_ != 0 && early_msgs_;
     size_t sizes[NB] = {};
     sizes[TAG] = R; sizes[X] = sizes[Y] = sizes[RR] = sizes[S] = sizes[M] = 32 * R;
     sizes[EMAP] = need_e ? 4 * R : 0;
+    sizes[MMAP] = need_mm ? 4 * R : 0;
     sizes[AUX] = auxb0[P]; sizes[PRE] = preb0[P];
     sizes[AUX_OFF] = sizes[AUX_NBLK] = 4 * n_aux_;
     sizes[PRE_OFF] = sizes[PRE_NBLK] = sizes[PRE_ROW] = 4 * n_pre_;
@@ -1137,6 +1197,7 @@ int DeviceBatch::stage_parts(const SighashJobs* const* J, const TupleRows* const
     d_hrow_ = (uint32_t*)(a + off[HROW]); d_hprog_ = a + off[HPROG];
     d_zeros_ = a + off[ZEROS]; d_intab_ = (uint32_t*)(a + off[INTAB]); d_txd_ = a + off[TXD];
     d_emap_ = need_e ? (uint32_t*)(a + off[EMAP]) : nullptr;
+    d_mmap_ = need_mm ? (uint32_t*)(a + off[MMAP]) : nullptr;
     uint8_t* h = (uint8_t*)host_image_;
     memset(h + off[ZEROS], 0, 64);
     // the rows of part p in [lo, hi): the bulk of a tuple batch, copied in blocks by the team
@@ -1153,6 +1214,7 @@ int DeviceBatch::stage_parts(const SighashJobs* const* J, const TupleRows* const
         cp(S, 32 * r0, rw.s.data() + 32 * lo, 32 * nr);
         if (need_m && nr) rw.copy_msg(h + off[M] + 32 * r0, lo, hi);  // past the stored prefix: ONE
         if (need_e && nr) rw.copy_emap((uint32_t*)(h + off[EMAP]) + r0, lo, hi);
+        if (need_mm && nr) rw.copy_mmap((uint32_t*)(h + off[MMAP]) + r0, lo, hi);
     };
     // part p's jobs and key-hash records (offsets fixed up for the concatenation)
     auto fill = [&](size_t p) {
@@ -1186,6 +1248,7 @@ int DeviceBatch::stage_parts(const SighashJobs* const* J, const TupleRows* const
             t.tpl_off += (uint32_t)tpl0[p];
             t.code_off += (uint32_t)code0[p];
             t.row += (uint32_t)r0;
+            if (!need_mm) t.nblk &= ~TPL_EARLY;  // no early digests for this round: hash it here
             tj[k] = t;
         }
         cp(TXRAW, raw0[p], j.txraw.data(), j.txraw.size());
@@ -1483,6 +1546,18 @@ int DeviceBatch::queue_verdicts(hipStream_t st) {
     return 0;
 }
 
+// Early sighashes (TPL_EARLY): row t's message from early row mmap[t] (DeviceBatch::early_launch).
+__global__ void __launch_bounds__(256) early_msgs_kernel(const uint32_t* __restrict__ mmap, uint32_t n,
+                                                         uint32_t early_n, const uint4* __restrict__ emsg,
+                                                         uint4* __restrict__ m) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n) return;
+    const uint32_t e = mmap[t];
+    if (e >= early_n) return;
+    m[2 * (size_t)t] = emsg[2 * (size_t)e];
+    m[2 * (size_t)t + 1] = emsg[2 * (size_t)e + 1];
+}
+
 // K_late: the host-hashed messages (LateMsgFill) into their rows, one lane per row.
 __global__ void __launch_bounds__(256) late_msgs_kernel(const uint32_t* __restrict__ rows,
                                                         const uint4* __restrict__ digs, uint32_t n,
@@ -1584,6 +1659,14 @@ int DeviceBatch::run_stages(void* stream, const LateMsgFill* late) {
     }
     BCC_HIP_TRY(hipEventRecord((hipEvent_t)ev_join_, side));
     if (int e = launch_front(st)) return e;
+    if (d_mmap_ && early_n_ && early_msgs_) {  // the early sighashes into their rows
+        BCC_HIP_TRY(hipStreamWaitEvent(st, (hipEvent_t)ev_early_sig_, 0));
+        BCC_HIP_TRY(hipStreamWaitEvent(st, (hipEvent_t)ev_up_, 0));  // the MMAP rows uploaded
+        hipLaunchKernelGGL(early_msgs_kernel, dim3((unsigned)((n_rows_ + 255) / 256)), dim3(256), 0, st,
+                           d_mmap_, (uint32_t)n_rows_, (uint32_t)early_n_, (const uint4*)early_msg_,
+                           (uint4*)d_m);
+        BCC_HIP_TRY(hipGetLastError());
+    }
     if (n_hash_) {
         BCC_HIP_TRY(hipMemsetAsync(d_v, 1, n_rows_, st));
         BCC_HIP_TRY(hipStreamWaitEvent(st, (hipEvent_t)ev_up_, 0));  // K_h160 reads the key rows
@@ -1650,10 +1733,10 @@ static DeviceBatch* thread_batch(int device) {
     return cache[device].get();
 }
 
-int gpu_early_launch(int device, const TupleRows* const* rows, size_t P) {
+int gpu_early_launch(int device, const TupleRows* const* rows, size_t P, const SighashJobs* const* jobs) {
     DeviceBatch* b = thread_batch(device);
     if (!b) return (int)hipErrorInvalidDevice;
-    return b->early_launch(rows, P);
+    return b->early_launch(rows, P, jobs);
 }
 
 void gpu_early_reset(int device) {

@@ -32,12 +32,23 @@ void release_tuple_thread_state() {}
 // engine maps to an early twin (TupleRows::emap) is that twin byte for byte (tag, x, y, r, s) --
 // the property DeviceBatch's K_keyq copy relies on; the verdicts are computed in full regardless.
 thread_local TupleRows tl_early;
-thread_local size_t tl_early_checked = 0;
-int gpu_early_launch(int, const TupleRows* const* rows, size_t P) {
+thread_local size_t tl_early_checked = 0, tl_early_msg_checked = 0;
+static void stub_tpl_digest(const SighashJobs& j, const TplJob& t, uint8_t out[32]);
+// Early sighashes: the early jobs' digests (oracle SHA-256d of the assembled preimages) land in
+// tl_early.msg at their early rows; gpu_verify_parts compares every row that takes one (mmap) with
+// the digest of its own job.
+int gpu_early_launch(int, const TupleRows* const* rows, size_t P, const SighashJobs* const* jobs) {
     tl_early.clear();
     for (size_t p = 0; p < P; p++) {
+        const size_t r0 = tl_early.tag.size();
         TupleRows r = *rows[p];
         r.materialize();
+        tl_early.msg.resize(32 * (r0 + r.size()), 0);
+        if (jobs && jobs[p])
+            for (const TplJob& t : jobs[p]->tjobs) {
+                if (t.row >= r.size()) abort();
+                stub_tpl_digest(*jobs[p], t, &tl_early.msg[32 * (r0 + t.row)]);
+            }
         tl_early.tag.insert(tl_early.tag.end(), r.tag.begin(), r.tag.end());
         tl_early.x.insert(tl_early.x.end(), r.x.begin(), r.x.end());
         tl_early.y.insert(tl_early.y.end(), r.y.begin(), r.y.end());
@@ -65,6 +76,18 @@ static void check_early_twins(const TupleRows& rw) {  // rw materialized
     }
 }
 extern "C" size_t stub_early_checked(void) { return tl_early_checked; }
+extern "C" size_t stub_early_msg_checked(void) { return tl_early_msg_checked; }
+static void check_early_msgs(const TupleRows& rw, const uint8_t* msg) {  // msg: the round's digests
+    for (size_t k = 0; k < rw.mmap.size() && k < rw.size(); k++) {
+        const uint32_t e = rw.mmap[k];
+        if (e == TupleRows::NO_EARLY) continue;
+        if ((size_t)e >= tl_early.size() || memcmp(&tl_early.msg[32 * (size_t)e], msg + 32 * k, 32) != 0) {
+            fprintf(stderr, "engine_host_stub: row %zu's early sighash (early row %u) differs\n", k, e);
+            abort();
+        }
+        tl_early_msg_checked++;
+    }
+}
 // As DeviceBatch: the rows are copied (staged) first, the sighash jobs hash into the copy, then the
 // late rows (host-hashed while the device runs) land in it (put_late), then the ECDSA stage.
 int gpu_verify_parts(int, const SighashJobs* const* jobs, const TupleRows* const* rows, size_t parts,
@@ -91,6 +114,7 @@ int gpu_verify_parts(int, const SighashJobs* const* jobs, const TupleRows* const
     }
     size_t r0 = 0;
     for (size_t p = 0; p < parts; p++) {
+        check_early_msgs(staged[p], &msg[32 * r0]);
         stub_ecdsa(staged[p], &msg[32 * r0], verdict + r0);
         r0 += staged[p].size();
     }
@@ -174,12 +198,7 @@ static void stub_sighash(const SighashJobs& j, std::vector<uint8_t>& msg) {
         bcco_sha256d(m, unpadded_len(m, L), &msg[32 * j.pre_row[k]]);
     }
     for (const TplJob& t : j.tjobs) {  // template jobs: assemble the preimage, then hash
-        std::vector<uint8_t> m(j.tpl.begin() + t.tpl_off, j.tpl.begin() + t.tpl_off + t.pos);
-        m.insert(m.end(), j.code.begin() + t.code_off, j.code.begin() + t.code_off + t.code_len);
-        m.insert(m.end(), j.tpl.begin() + t.tpl_off + t.pos + 1,
-                 j.tpl.begin() + t.tpl_off + t.tpl_len);
-        for (int b = 0; b < 4; b++) m.push_back((uint8_t)(t.hashtype >> (8 * b)));
-        bcco_sha256d(m.data(), m.size(), &msg[32 * t.row]);
+        stub_tpl_digest(j, t, &msg[32 * t.row]);
         if (tpl_has_mid(t)) {  // the product's midstate path must give the same digest
             uint8_t d[32];
             host::tpl_job_sighash(j.tpl.data(), j.code.data(), t, d);
@@ -197,6 +216,16 @@ static void stub_sighash(const SighashJobs& j, std::vector<uint8_t>& msg) {
         bcco_sighash(&j.txraw[r.tx_off], r.tx_len, w.nin, c + hdr, w.code_len - hdr,
                      (int)w.hashtype, amount, 1, &msg[32 * w.row]);
     }
+}
+
+// A legacy template job's digest from its full preimage (template | code field | template rest |
+// hashtype), whatever its flags (TPL_MID / TPL_EARLY only change how the device gets there).
+static void stub_tpl_digest(const SighashJobs& j, const TplJob& t, uint8_t out[32]) {
+    std::vector<uint8_t> m(j.tpl.begin() + t.tpl_off, j.tpl.begin() + t.tpl_off + t.pos);
+    m.insert(m.end(), j.code.begin() + t.code_off, j.code.begin() + t.code_off + t.code_len);
+    m.insert(m.end(), j.tpl.begin() + t.tpl_off + t.pos + 1, j.tpl.begin() + t.tpl_off + t.tpl_len);
+    for (int b = 0; b < 4; b++) m.push_back((uint8_t)(t.hashtype >> (8 * b)));
+    bcco_sha256d(m.data(), m.size(), out);
 }
 
 int gpu_verify_batch(int dev, const SighashJobs& j, const TupleRows& rows, uint8_t* verdict, double*) {

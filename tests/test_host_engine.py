@@ -509,14 +509,15 @@ def _many_input_legacy_tx(R, O, n_in, seed):
 @pytest.mark.parametrize("chain_blocks,early,devs", [(0, 1, []), (1, 1, []), (12, 0, []), (160, 1, []),
                                                      (160, 0, []), (1, 1, [0, 1, 2]), (12, 1, [0, 0])])
 def test_many_input_legacy_tx_template_midstates(eng, chain_blocks, early, devs):
-    """Legacy txs of 12..90 P2PKH inputs (templates of 8..58 blocks: every job carries the
+    """Legacy txs of 12..250 P2PKH inputs (templates of 8..160 blocks: every job carries the
     template midstates, TPL_MID) through verify_batch: the stub evaluates each template job from
     the full preimage with the oracle and aborts if the product's midstate path disagrees; jobs
     whose remaining blocks exceed chain_blocks are hashed on the host from their midstate.  All
     inputs valid, and a byte flipped in the 40-input tx's first inputs or the 90-input tx's first
     outpoint gives the reference's (ret, err) for every input.  early: the P2PKH (key, signature)
     pairs are pre-extracted (bcc_set_early_q) and every deferred row is mapped to its early twin,
-    which the stub checks byte for byte (engine_host_stub.cpp check_early_twins).  devs: a
+    which the stub checks byte for byte (engine_host_stub.cpp check_early_twins), and with it the
+    early sighash of every long-template job (check_early_msgs).  devs: a
     multi-device list (no early rows there), whose device workers all wait for the one host pass
     over the offloaded chains (LateHost) before their G ladders."""
     from oracle_ctypes import Oracle, Reference, reference_available
@@ -524,13 +525,15 @@ def test_many_input_legacy_tx_template_midstates(eng, chain_blocks, early, devs)
         pytest.skip("oracle/_ref not built")
     R, O = Reference(), Oracle()
     eng.bcc_set_host_chain_blocks.argtypes = [ctypes.c_uint]
-    txs = [_many_input_legacy_tx(R, O, n, 11 + n) for n in (12, 40, 90)]
+    # 250 inputs: a 160-block template, whose first inputs' chains (>= 96 blocks from their
+    # midstate) get early sighashes
+    txs = [_many_input_legacy_tx(R, O, n, 11 + n) for n in (12, 40, 90, 250)]
     # mutations: byte 200 of the 40-input tx (its first inputs), an outpoint byte of input 0
     tx40 = bytearray(txs[1][0])
     tx40[200] ^= 0x01
     tx90 = bytearray(txs[2][0])
     tx90[5 + 3] ^= 0x10
-    txs += [(bytes(tx40), txs[1][1]), (bytes(tx90), txs[2][1])]
+    txs = txs[:3] + [(bytes(tx40), txs[1][1]), (bytes(tx90), txs[2][1])] + txs[3:]
     items, keep, exp = [], [], []
     for tx, spks in txs:
         bt = ctypes.create_string_buffer(tx, len(tx))
@@ -545,7 +548,9 @@ def test_many_input_legacy_tx_template_midstates(eng, chain_blocks, early, devs)
     err = (ctypes.c_int * len(arr))()
     eng.bcc_set_early_q.argtypes = [ctypes.c_int]
     eng.stub_early_checked.restype = ctypes.c_size_t
+    eng.stub_early_msg_checked.restype = ctypes.c_size_t
     checked0 = eng.stub_early_checked()
+    msg0 = eng.stub_early_msg_checked()
     try:
         eng.bcc_set_host_chain_blocks(chain_blocks)
         eng.bcc_set_early_q(early)
@@ -564,10 +569,17 @@ def test_many_input_legacy_tx_template_midstates(eng, chain_blocks, early, devs)
         assert st.devices == len(devs) and st.early_rows == 0
     elif early:
         # every input is a P2PKH spend with one check: one early row each, and the first round's
-        # rows (the only round) all mapped to their twins
+        # rows (the only round) all mapped to their twins; every device template job (all of them
+        # unless chain_blocks sends long ones to the host) takes its twin's early sighash, which the
+        # stub compares with the job's own digest
         assert st.early_rows == len(items) and st.early_mapped == len(items)
         assert eng.stub_early_checked() - checked0 == len(items)
+        assert eng.stub_early_msg_checked() - msg0 == st.early_msgs
+        if chain_blocks in (0, 160):
+            assert st.early_msgs > 0  # the 250-input tx's long chains
+        else:
+            assert st.early_msgs < len(items)  # the long remainders went to the host
     else:
         assert st.early_rows == 0 and st.early_mapped == 0
     # the originals all valid; both flips sit in bytes every legacy preimage of their tx contains
-    assert sum(r for r, _ in exp) == 12 + 40 + 90
+    assert sum(r for r, _ in exp) == 12 + 40 + 90 + 250

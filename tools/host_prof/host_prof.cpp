@@ -48,7 +48,7 @@ int gpu_staged_run(StagedRound* s, uint8_t* verdict, const LateMsgFill* late) {
     return gpu_verify_parts(0, nullptr, s->rows.data(), s->rows.size(), verdict, nullptr, late);
 }
 int gpu_staged_launch(StagedRound*, const LateMsgFill*) { return 0; }
-int gpu_early_launch(int, const TupleRows* const*, size_t) { return 0; }  // early Q halves: no-op
+int gpu_early_launch(int, const TupleRows* const*, size_t, const SighashJobs* const*) { return 0; }  // early Q: no-op
 void gpu_early_reset(int) {}
 int gpu_verify_der(int, const DerTuples& t, uint8_t* verdict) {
     memset(verdict, 1, t.n);
