@@ -1,6 +1,6 @@
 # Round-5 final evidence on the current tree: pytest -m gpu, smoke(), one bench line per config.
 set -o pipefail
-O=gpurun_out/r05_final; mkdir -p $O
+O=gpurun_out/${1:-r05_final}; mkdir -p $O
 timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { tail -40 $O/pytest_gpu.log; exit 1; }
 tail -2 $O/pytest_gpu.log
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 1; }

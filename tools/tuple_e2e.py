@@ -7,6 +7,11 @@ import time
 
 import numpy as np
 
+if os.environ.get("WITH_TORCH"):  # bench.py's process: torch imported and its HIP context up
+    import torch
+    torch.cuda.init()
+    torch.zeros(1, device="cuda")
+
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "rust-bitcoinconsensus_amd"))
 import bitcoinconsensus_amd as B  # noqa: E402
 
