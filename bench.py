@@ -757,6 +757,12 @@ def main():
     else:
         job = TupleJob(B, n, seed, dev, args.config, first=first, total=total)
     log(f"[rank {rank}] staged {args.config} x{n} in {time.time() - t0:.1f}s")
+    probe = os.environ.get("BCC_BENCH_E2E_PROBE") and args.config == "c4"
+
+    def e2e_probe(where):  # (diagnostics: the C4 drop-in leg at points of the run)
+        if probe:
+            log(f"[e2e probe] {where}: {job.end_to_end(job.ts.host())['calls_ms']}")
+    e2e_probe("after staging")
     # a dedicated (non-null) stream: every launch of a step and the HIP events that time the
     # kernels sit on it (torch's default stream is the null handle, which the engine maps to its
     # own internal stream)
@@ -764,10 +770,12 @@ def main():
     torch.cuda.set_stream(stream)
     sp = stream.cuda_stream
 
+    e2e_probe("after set_stream")
     for _ in range(args.warmup):
         job.step(sp)
     torch.cuda.synchronize()
     n_valid = job.valid()
+    e2e_probe("after warmup + valid")
 
     def barrier():
         if world > 1:
@@ -823,8 +831,10 @@ def main():
     bitmap = dict(units=int(len(gathered)), valid=int(gathered.sum()),
                   collective="all_gather_into_tensor (RCCL)" if world > 1 else "none (1 rank)")
 
+    e2e_probe("after timed + sustained")
     # per-kernel timing with HIP events on the launch stream (outside the timed region)
     sighash_ms, sig_ms = job.kernel_times(stream, max(3, args.steps))
+    e2e_probe("after kernel_times")
     sig_units = job.shape["tuples"] if args.config in ("c2", "c3", "c5t") else job.units
 
     total = job.units * world * args.steps
@@ -837,6 +847,7 @@ def main():
         cus = torch.cuda.get_device_properties(dev).multi_processor_count
         peak = 2.4e9 * cus * 4 * 16
         m_rate, m_clk, m_ms = B.microbench_sustained(25, 8, 20.0, 1.0, 3)
+        e2e_probe("after microbench_sustained")
         achieved = sig_units * job.mads / (sig_ms * 1e-3)
         traffic, tsrc = args.traffic, "--traffic" if args.traffic else None
         tf = os.path.join(ROOT, "profiles", "traffic.json")
@@ -889,6 +900,7 @@ def main():
             "roofline": roof,
             "cpu_baseline": cpu,
         }
+        e2e_probe("before extra")
         if not args.no_extra:
             out.update(job.extra(sighash_ms))
         if sustained:

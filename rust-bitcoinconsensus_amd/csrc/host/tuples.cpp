@@ -8,6 +8,7 @@
 #include "tuples.h"
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -232,6 +233,10 @@ int tuple_rounds(int dev, const uint8_t* pub_blob, const uint64_t* pub_off, cons
                      bcc::gpu_staged_launch(s.staged.get(), nullptr) == 0;
         }
         if (!staged) {
+            static std::atomic<int> warned{0};
+            if (warned.fetch_add(1) < 3)
+                fprintf(stderr, "[bcc] pubkey_verify_batch: round of %zu tuples not staged on device %d; "
+                                "running it through the host parse and the general path\n", m, dev);
             bcc::TupleRows& rows = host_rows(s);
             s.n = 0;
             if (int e = tuple_round(dev, rows, verdict + lo)) err = e;
