@@ -763,7 +763,9 @@ def main():
         if probe:
             log(f"[e2e probe] {where}: {job.end_to_end(job.ts.host())['calls_ms']}")
     e2e_probe("after staging")
-    if args.config == "c4" and not args.no_extra:
+    # (the same for the C2 drop-in leg measured neutral within the boxes' noise: not done)
+    early_alloc = not os.environ.get("BCC_BENCH_NO_EARLY_ALLOC")  # (A/B of the note below)
+    if args.config == "c4" and not args.no_extra and early_alloc:
         # one untimed drop-in call now, so that its pinned round images, device batches and
         # scratch are allocated beside the staged set rather than after the whole run: allocated
         # last, the same calls ran ~40 % slower on the device (profiles/r05/c4_der/
