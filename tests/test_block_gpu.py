@@ -86,3 +86,27 @@ def _mutations(B, wl):
         got = [(r, int(e)) for r, e in B.verify_batch(items, flags)]
         exp = [R.verify_script_with_amount(s, a, t, k, flags) for s, a, t, k in items]
         assert got == exp
+
+
+def test_block_workload_device_fault_with_early_work(wl):
+    """Round 5: the block call runs early Q halves and early sighashes (flagged TPL_EARLY jobs whose
+    digests the round copies from the early set).  One injected device fault: the round is retried
+    on a fresh device batch, which has no early state, so staging must clear the flags and hash
+    those jobs itself; every input stays valid, as the reference says.  (The host fallback, which
+    hashes flagged jobs like any other, is covered on the CPU: test_host_engine.py's failure tests
+    run with early work on; here the autouse fixture forbids host rounds.)"""
+    faults = 1
+    import bitcoinconsensus_amd as B
+    B.set_host_chain_blocks(B.HOST_CHAIN_BLOCKS_DEFAULT)
+    n_valid, _ = wl.verify_batch()
+    st = B.last_batch_stats()
+    assert n_valid == wl.n
+    assert st["early_rows"] > 0 and st["early_msgs"] > 0  # the paths under test are in use
+    B.debug_fail_device_rounds(faults)
+    try:
+        n_valid, ret = wl.verify_batch()
+        st = B.last_batch_stats()
+    finally:
+        B.debug_fail_device_rounds(0)
+    assert n_valid == wl.n and all(r == 1 for r in ret)
+    assert st["device_retries"] >= 1 and st["host_rounds"] == 0
