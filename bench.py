@@ -106,6 +106,97 @@ def host_cpu_info():
     return info
 
 
+def newest_cost_model():
+    """The ladder's instruction-class decomposition of the newest round that committed one
+    (profiles/rNN/ladder_cost_model.json, tools/isa/cost_model.py)."""
+    import glob
+    import re
+    found = [(int(re.search(r"/r(\d+)/", c).group(1)), c)
+             for c in glob.glob(os.path.join(ROOT, "profiles", "r*", "ladder_cost_model.json"))
+             if re.search(r"/r(\d+)/", c)]
+    return max(found)[1] if found else ""
+
+
+def _proc_stat_busy():
+    """(busy, total) jiffies over all CPUs of the machine (/proc/stat 'cpu' line)."""
+    try:
+        f = [int(x) for x in open("/proc/stat").readline().split()[1:]]
+    except (OSError, ValueError):
+        return None
+    idle = f[3] + (f[4] if len(f) > 4 else 0)
+    return sum(f) - idle, sum(f)
+
+
+def _cpu_topology():
+    """cpu -> (numa node, physical core key) from sysfs (empty when unavailable)."""
+    import glob
+    topo = {}
+    for nd in glob.glob("/sys/devices/system/node/node[0-9]*"):
+        node = int(nd.rsplit("node", 1)[1])
+        try:
+            spec = open(os.path.join(nd, "cpulist")).read().strip()
+        except OSError:
+            continue
+        for part in spec.split(","):
+            if not part:
+                continue
+            a, _, b = part.partition("-")
+            for c in range(int(a), int(b or a) + 1):
+                topo[c] = [node, None]
+    for c in list(topo):
+        try:
+            sib = open(f"/sys/devices/system/cpu/cpu{c}/topology/thread_siblings_list").read().strip()
+            topo[c][1] = sib
+        except OSError:
+            pass
+    return topo
+
+
+def _thread_cpus():
+    """{tid: (last cpu, utime+stime jiffies)} of this process's threads (/proc/self/task)."""
+    out = {}
+    try:
+        tids = os.listdir("/proc/self/task")
+    except OSError:
+        return out
+    for t in tids:
+        try:
+            f = open(f"/proc/self/task/{t}/stat").read().rsplit(")", 1)[1].split()
+            out[int(t)] = (int(f[36]), int(f[11]) + int(f[12]))
+        except (OSError, ValueError, IndexError):
+            pass
+    return out
+
+
+def gpu_numa_node(dev):
+    """NUMA node of GPU `dev` (sysfs of its PCI function; None when unknown)."""
+    try:
+        import torch
+        bus = torch.cuda.get_device_properties(dev).pci_bus_id
+        dom = getattr(torch.cuda.get_device_properties(dev), "pci_domain_id", 0)
+        for cand in (f"/sys/bus/pci/devices/{dom:04x}:{bus:02x}:00.0/numa_node",):
+            if os.path.exists(cand):
+                return int(open(cand).read())
+    except Exception:  # noqa: BLE001 (diagnostic only)
+        pass
+    return None
+
+
+def host_placement(before, after, topo):
+    """Where the call's busy threads ran: the CPUs (and NUMA nodes / distinct physical cores) of
+    the threads that used CPU time between two _thread_cpus() snapshots."""
+    busy = {t: (c, j - before.get(t, (c, 0))[1]) for t, (c, j) in after.items()}
+    busy = {t: v for t, v in busy.items() if v[1] > 0}
+    cpus = sorted({c for c, _ in busy.values()})
+    nodes = {}
+    for c in cpus:
+        n = topo.get(c, [None])[0]
+        nodes[str(n)] = nodes.get(str(n), 0) + 1
+    cores = {topo[c][1] for c in cpus if c in topo and topo[c][1]}
+    return dict(busy_threads=len(busy), cpus=cpus, cpus_per_numa_node=nodes,
+                distinct_physical_cores=len(cores) or None)
+
+
 def median_rate(run, n, passes=CPU_PASSES):
     """1 warm-up + `passes` timed runs of run() (returns seconds); median items/s and all passes."""
     run()
@@ -241,6 +332,7 @@ class C2:
 
     def __init__(self, B, n, seed, dev, first=0, total=None):
         self.B = B
+        self.dev = dev
         self.wl = B.Workload(n, seed=seed, device=dev, first=first)
         self.shape = self.wl.shape()
         self.units = self.shape["tuples"]
@@ -286,10 +378,14 @@ class C2:
             out["single_call"] = single_call_latency(self.B)
         return out
 
-    def end_to_end(self, reps=3):
+    def end_to_end(self, reps=3, calls=20):
         """The same inputs through bitcoinconsensus_verify_batch from host buffers (deserialize,
         interpreter, sighash jobs, H2D, kernels, verdicts back): what a drop-in caller sees.
-        Reported beside value, never as value (inputs are not HBM-resident)."""
+        Reported beside value, never as value (inputs are not HBM-resident).  Also the host phase
+        split (bcc_batch_stats, median per field over the sustained calls), the process CPU time
+        per call, where the host threads ran (CPUs, NUMA nodes, physical cores vs the GPU's node)
+        and how busy the whole machine was meanwhile (other tenants share its cores)."""
+        import statistics
         best, st = None, None
         for _ in range(reps):
             t0 = time.perf_counter()
@@ -299,18 +395,46 @@ class C2:
                 best, st = dt, self.B.last_batch_stats()
         # sustained: calls back to back (a CFS CPU quota lets one call burst above it, a run of
         # calls pays for that in throttling), whole-run wall time
-        calls = 10
+        runs = []
+        topo = _cpu_topology()
+        th0, ps0 = _thread_cpus(), _proc_stat_busy()
         t0, c0 = time.perf_counter(), time.process_time()
         for _ in range(calls):
             self.wl.verify_batch()
+            runs.append(self.B.last_batch_stats())
         sus, cpu_s = time.perf_counter() - t0, time.process_time() - c0
+        th1, ps1 = _thread_cpus(), _proc_stat_busy()
+        med = lambda k: statistics.median(r[k] for r in runs)  # noqa: E731
+        ms = lambda k: round(med(k) * 1e3, 3)  # noqa: E731
+        phases = dict(prepare_ms=ms("prepare_seconds"), prepare_parse_ms=ms("prepare_parse_seconds"),
+                      prepare_hash_ms=ms("prepare_hash_seconds"),
+                      interpret_ms=ms("interpret_seconds"), stage_ms=ms("stage_seconds"),
+                      stitch_ms=ms("stitch_seconds"), finish_ms=ms("finish_seconds"),
+                      host_ms=ms("host_seconds"), gpu_wait_ms=ms("gpu_seconds"),
+                      total_ms=ms("total_seconds"),
+                      process_cpu_s_per_call=round(med("process_cpu_seconds"), 4),
+                      process_cpu_in_gpu_wait_s=round(med("process_cpu_in_gpu_wait_seconds"), 4),
+                      rounds=med("rounds"),
+                      note=f"median per field over the {calls} sustained calls (bcc_batch_stats); "
+                           "the host phases of pipelined chunks overlap their device rounds")
+        machine = None
+        if ps0 and ps1 and ps1[1] > ps0[1]:
+            machine = dict(busy_fraction_all_cpus=round((ps1[0] - ps0[0]) / (ps1[1] - ps0[1]), 3),
+                           logical_cpus=os.cpu_count(),
+                           loadavg=open("/proc/loadavg").read().split()[:3]
+                           if os.path.exists("/proc/loadavg") else None,
+                           note="whole machine over the sustained calls, this process included")
+        place = host_placement(th0, th1, topo)
+        place["gpu_numa_node"] = gpu_numa_node(getattr(self, "dev", 0))
         return dict(inputs_per_s=self.n / best, ms=best * 1e3, valid=nv,
                     host_ms=st["host_seconds"] * 1e3, gpu_ms=st["gpu_seconds"] * 1e3,
                     h2d_ms=st["stage_seconds"] * 1e3, host_threads=self.B.host_threads(),
                     cpu_share=self.B.cpu_share(), sustained_inputs_per_s=calls * self.n / sus,
                     sustained_calls=calls,
                     # process CPU (every thread) per 1M inputs over the sustained calls
-                    sustained_cpu_s_per_M=cpu_s / (calls * self.n) * 1e6)
+                    sustained_cpu_s_per_M=cpu_s / (calls * self.n) * 1e6,
+                    sustained_cpus_busy=cpu_s / sus,
+                    phases=phases, host_placement=place, machine=machine)
 
     def cpu(self, sample):
         sample = min(sample, self.n)
@@ -709,6 +833,71 @@ class C5T:
                 "parallelism": f"shard x{world} (independent checks, no collective)"}
 
 
+class SideLegs:
+    """The default C2 line's end-to-end legs of two other configs, on the driver's clock
+    (VERDICT r05 #4): C3 block replay through bitcoinconsensus_verify_batch (4,000 txs, every
+    item against the reference, its own 16-thread reference baseline) and C4 through
+    bcc_pubkey_verify_batch from host buffers (8M tuples, every verdict against the staged
+    kernels' and the construction labels, a reference sample).  Built and called once right after
+    staging (their pinned images, device batches and scratch allocated early, as a library caller
+    sets up once: DESIGN.md §3.10, allocation order), measured after C2's timed region."""
+
+    def __init__(self, B, dev, c4_n):
+        self.B, self.dev = B, dev
+        t0 = time.time()
+        self.c3 = C3(B, DEFAULT_N["c3"], SEEDS["c3"], dev)
+        self.c3.wl.verify_batch()
+        self.c4 = TupleJob(B, c4_n, SEEDS["c4"], dev, "c4") if c4_n else None
+        if self.c4:
+            self.c4.ts.run()  # the staged kernels' verdicts (the leg's parity reference)
+            self.c4.end_to_end(self.c4.ts.host(), reps=1)
+        self.setup_s = time.time() - t0
+
+    def c3_leg(self, calls=21, cpu=True):
+        import statistics
+        job = self.c3
+        nv, ret = job.wl.verify_batch()
+        ts, runs = [], []
+        for _ in range(calls):
+            t0 = time.perf_counter()
+            job.wl.verify_batch()
+            ts.append(time.perf_counter() - t0)
+            runs.append(self.B.last_batch_stats())
+        med = statistics.median(ts)
+        out = dict(workload=job.config(1)["workload"], inputs=job.n, calls=calls,
+                   inputs_per_s=job.n / med, ms_median=med * 1e3, ms_best=min(ts) * 1e3,
+                   valid=nv,
+                   batch_stats_median={k: statistics.median(r[k] for r in runs)
+                                       for k in ("host_seconds", "gpu_seconds", "prepare_seconds",
+                                                 "interpret_seconds", "stage_seconds", "rounds",
+                                                 "tuples", "early_rows", "host_hashed")})
+        if cpu:
+            cb = cpu_baseline_script([job.wl.item(i) for i in range(job.n)],
+                                     f"C3 inputs (all {job.n})", gpu_verdicts=ret)
+            if cb:
+                cb.pop("host", None)
+                out["cpu_baseline"] = cb
+                out["gpu_vs_cpu"] = out["inputs_per_s"] / cb["value"]
+                out["gpu_verdict_mismatches_all_items"] = cb["gpu_verdict_mismatches"]
+        return out
+
+    def c4_leg(self, cpu=True):
+        import numpy as np
+        job = self.c4
+        h = job.ts.host()
+        e = job.end_to_end(h, reps=3)
+        v = np.frombuffer(job.ts.verdicts(), np.uint8)
+        e.update(workload=job.config(1)["workload"], tuples=job.n,
+                 mismatches_vs_construction=int((v != h["expect"]).sum()))
+        if cpu:
+            cb = job.cpu(100_000)
+            if cb:
+                cb.pop("host", None)
+                e["cpu_baseline"] = cb
+                e["gpu_vs_cpu"] = e["verifies_per_s"] / cb["value"]
+        return e
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -726,6 +915,10 @@ def main():
     ap.add_argument("--sustain-s", type=float, default=3.0,
                     help="after the timed steps, keep stepping for this long (HIP-event timed, "
                          "reported as `sustained`; gives a GPU-busy sampler a multi-second window)")
+    ap.add_argument("--side-c4", type=int, default=8_000_000,
+                    help="C2 line only: tuples of the C4 bcc_pubkey_verify_batch leg (0: no C4 leg)")
+    ap.add_argument("--no-side", action="store_true",
+                    help="C2 line only: skip the C3 / C4 end-to-end legs")
     ap.add_argument("--traffic", type=float, default=None,
                     help="HBM bytes per ECDSA launch from a rocprofv3 --pmc run (profiles/)")
     args = ap.parse_args()
@@ -763,6 +956,10 @@ def main():
         if probe:
             log(f"[e2e probe] {where}: {job.end_to_end(job.ts.host())['calls_ms']}")
     e2e_probe("after staging")
+    side = None
+    if args.config == "c2" and world == 1 and not args.no_extra and not args.no_side:
+        side = SideLegs(B, dev, args.side_c4)
+        log(f"[rank {rank}] side legs (C3, C4 x{args.side_c4}) set up in {side.setup_s:.1f}s")
     # (the same for the C2 drop-in leg measured neutral within the boxes' noise: not done)
     early_alloc = not os.environ.get("BCC_BENCH_NO_EARLY_ALLOC")  # (A/B of the note below)
     if args.config == "c4" and not args.no_extra and early_alloc:
@@ -876,8 +1073,7 @@ def main():
                                               "own SGPR carries per asm block, 8 waves/SIMD)"),
                     per_launch=dict(verifies=sig_units, mads=sig_units * job.mads, avg_ms=sig_ms,
                                     verifies_per_s=sig_units / (sig_ms * 1e-3)))
-        cm = next((c for c in (os.path.join(ROOT, "profiles", r, "ladder_cost_model.json")
-                               for r in ("r04", "r03")) if os.path.exists(c)), "")
+        cm = newest_cost_model()
         if args.config == "c2" and os.path.exists(cm):
             # why frac stops where it does (committed PMC passes + microbenchmark): the ladder is
             # VALU-issue-bound; its cycles split by instruction class at the measured issue costs
@@ -889,6 +1085,7 @@ def main():
             if k:
                 roof["cost_model"] = dict(
                     kernel=kname, cycle_share=k["cycle_share"],
+                    salu_per_verify=k.get("salu"),
                     valu_per_verify=k["valu_per_wave"],
                     issue_cost_cycles=d["issue_cost_cycles_per_wave_instr"],
                     predicted_over_measured_cycles=k["predicted_over_measured"],
@@ -915,6 +1112,10 @@ def main():
             out["sustained"] = sustained
         if per_rank:
             out["drop_in_per_rank"] = per_rank
+        if side:
+            out["c3_block_replay"] = side.c3_leg(cpu=not args.no_cpu)
+            if side.c4:
+                out["c4_pubkey_verify_batch"] = side.c4_leg(cpu=not args.no_cpu)
         out["source_hash"] = B.source_hash()
         out["verdicts_valid"] = n_valid_all
         out["validity_bitmap"] = bitmap

@@ -96,8 +96,9 @@ int bcc_taproot_verify_batch(const bcc_taproot_check* items, size_t n, int* ret_
  * length filter and lax DER run there (K_der, csrc/der.hip), in pipelined rounds of 256k doubling
  * to 2M tuples; small rounds run on the host lane code.  Synchronous on `device`, or, for
  * device = -1, sharded in contiguous equal ranges over the bcc_set_devices() GPUs.  0, or -1 for
- * null arrays or offsets that run backwards (pub_off[n] < pub_off[0] or sig_off[n] < sig_off[0]),
- * or a device error.  A tuple whose own offsets run backwards or past the blob is invalid (0). */
+ * null arrays, offsets that are not non-decreasing (pub_off[i + 1] < pub_off[i] or
+ * sig_off[i + 1] < sig_off[i] for any i: nothing is verified, so no verdict depends on how the call
+ * is cut into rounds), or a device error. */
 int bcc_pubkey_verify_batch(const uint8_t* pub_blob, const uint64_t* pub_off,
                             const uint8_t* msg32, const uint8_t* sig_blob,
                             const uint64_t* sig_off, uint8_t* verdict, size_t n, int device);

@@ -80,8 +80,12 @@ int bcc_workload_run_ecdsa(bcc_workload* w, void* stream);
  * staged path on mutated inputs). */
 bcc_workload* bcc_workload_from_items(const bcc_batch_item* items, size_t n, unsigned flags,
                                       int device);
-/* copy back the verdicts of the staged tuple rows (one byte per tuple, bcc_workload_shape) */
-int bcc_workload_verdicts(bcc_workload* w, uint8_t* out);
+/* Copy back the verdicts of the staged tuple rows: one byte per tuple row (bcc_workload_shape's
+ * `tuples`; a block workload's multisig inputs stage several rows per item).  `cap` is the size of
+ * `out` in bytes.  Returns 0, -1 for a NULL workload / buffer, BCC_BENCH_ERR_CAPACITY when cap is
+ * smaller than the row count (nothing written), or a HIP error. */
+#define BCC_BENCH_ERR_CAPACITY (-2)
+int bcc_workload_verdicts(bcc_workload* w, uint8_t* out, size_t cap);
 /* Mutated copies of a workload's items for agreement runs (see workload.cpp): kinds[i] = 0 for an
  * untouched item, else 1 + the mutation (bit flip anywhere in the tx / in its back half, amount
  * +-1, spent-script bit flip, truncated tx, nIn out of range).  Valid while the set lives. */
@@ -90,10 +94,12 @@ bcc_itemset* bcc_workload_mutate(const bcc_workload* w, double rate, uint64_t se
                                  uint8_t* kinds);
 const bcc_batch_item* bcc_itemset_items(const bcc_itemset* m, size_t* n);
 void bcc_itemset_free(bcc_itemset* m);
-/* item index of every staged tuple row (uint32 per tuple) */
-int bcc_workload_tuple_items(const bcc_workload* w, uint32_t* out);
-/* the sighash (msg32) rows of the last run, 32 bytes per tuple (synchronous) */
-int bcc_workload_msgs(bcc_workload* w, uint8_t* out);
+/* item index of every staged tuple row (uint32 per tuple); `cap` in entries.  Returns 0, -1 for a
+ * NULL workload / buffer, BCC_BENCH_ERR_CAPACITY when cap < tuples (nothing written). */
+int bcc_workload_tuple_items(const bcc_workload* w, uint32_t* out, size_t cap);
+/* the sighash (msg32) rows of the last run, 32 bytes per tuple (synchronous); `cap` in bytes.
+ * Returns 0, -1, BCC_BENCH_ERR_CAPACITY when cap < 32 x tuples (nothing written), or a HIP error. */
+int bcc_workload_msgs(bcc_workload* w, uint8_t* out, size_t cap);
 /* algorithmic work of one run: bytes hashed + written by the sighash stage, tuples verified */
 /* algorithmic bytes of one sighash-stage run over the staged batch (DeviceBatch::sighash_bytes) */
 size_t bcc_workload_sighash_bytes(const bcc_workload* w);

@@ -46,6 +46,24 @@ class Error(enum.IntEnum):
 ERR_DEVICE_FAILURE = 6
 
 
+class DeviceFailure(enum.IntEnum):
+    """The one code a batch item can carry beyond the crate's Error: 'no verdict' (the device
+    round that item needed failed under DEVICE_FAILURE_ERROR).  Never a consensus result."""
+    ERR_DEVICE_FAILURE = ERR_DEVICE_FAILURE
+
+
+def error_from_code(code):
+    """An err_out code of the batch ABI -> Error (0-5, lib.rs:172-185) or
+    DeviceFailure.ERR_DEVICE_FAILURE (6).  Anything else is a ValueError: the crate's repr(C)
+    enum has no other discriminant, so an unknown code must never be cast to it."""
+    code = int(code)
+    if 0 <= code <= 5:
+        return Error(code)
+    if code == ERR_DEVICE_FAILURE:
+        return DeviceFailure.ERR_DEVICE_FAILURE
+    raise ValueError(f"unknown bitcoinconsensus error code {code}")
+
+
 class ConsensusError(Exception):
     def __init__(self, err):
         super().__init__(err.name)
@@ -128,11 +146,11 @@ def blib():
         L.bcc_workload_size.restype = sz
         for f in (L.bcc_workload_run, L.bcc_workload_run_sighash, L.bcc_workload_run_ecdsa):
             f.argtypes = [vp, vp]
-        L.bcc_workload_verdicts.argtypes = [vp, u8p]
+        L.bcc_workload_verdicts.argtypes = [vp, u8p, sz]
         L.bcc_workload_from_items.argtypes = [ctypes.POINTER(BatchItem), sz, ui, ctypes.c_int]
         L.bcc_workload_from_items.restype = vp
-        L.bcc_workload_tuple_items.argtypes = [vp, ctypes.POINTER(ctypes.c_uint32)]
-        L.bcc_workload_msgs.argtypes = [vp, u8p]
+        L.bcc_workload_tuple_items.argtypes = [vp, ctypes.POINTER(ctypes.c_uint32), sz]
+        L.bcc_workload_msgs.argtypes = [vp, u8p, sz]
         szp = ctypes.POINTER(sz)
         L.bcc_workload_shape.argtypes = [vp, szp, szp, szp, szp, szp]
         L.bcc_workload_sighash_bytes.argtypes = [vp]
@@ -298,7 +316,7 @@ class Workload:
         the buffer is sized by rows, not items)."""
         t = self.shape()["tuples"]
         out = ctypes.create_string_buffer(max(1, t))
-        rc = blib().bcc_workload_verdicts(self.h, out)
+        rc = blib().bcc_workload_verdicts(self.h, out, len(out))
         if rc:
             raise RuntimeError(f"bcc_workload_verdicts: {rc}")
         return out.raw[:t]
@@ -307,7 +325,7 @@ class Workload:
         """Item index of every staged tuple row."""
         t = self.shape()["tuples"]
         out = (ctypes.c_uint32 * max(1, t))()
-        if blib().bcc_workload_tuple_items(self.h, out):
+        if blib().bcc_workload_tuple_items(self.h, out, len(out)):
             raise RuntimeError("bcc_workload_tuple_items failed")
         return list(out)[:t]
 
@@ -315,7 +333,7 @@ class Workload:
         """The sighash rows (32 bytes per staged tuple) of the last run."""
         t = self.shape()["tuples"]
         out = ctypes.create_string_buffer(max(1, 32 * t))
-        if blib().bcc_workload_msgs(self.h, out):
+        if blib().bcc_workload_msgs(self.h, out, len(out)):
             raise RuntimeError("bcc_workload_msgs failed")
         return out.raw[: 32 * t]
 
@@ -406,15 +424,17 @@ def verify_batch_raw(items, flags=VERIFY_ALL):
     return rc, [(ret[i], err[i]) for i in range(n)]
 
 
-def verify_batch(items, flags=VERIFY_ALL):
+def verify_batch(items, flags=VERIFY_ALL, device_failure="raise"):
     """items: iterable of (spent_output_script, amount, spending_transaction, input_index).
     Returns a list of (ret, Error) equal to calling the C ABI once per item; all signature work
-    of the batch runs on the GPU in as few device rounds as the scripts allow.  Raises
-    RuntimeError when the device failed (no verdict is ever reported for a device error)."""
+    of the batch runs on the GPU in as few device rounds as the scripts allow.  When the device
+    failed (only under DEVICE_FAILURE_ERROR) it raises RuntimeError, or with
+    device_failure="mark" returns the results with DeviceFailure.ERR_DEVICE_FAILURE for the items
+    left without a verdict (no verdict is ever reported for a device error)."""
     rc, res = verify_batch_raw(items, flags)
-    if rc < 0:
+    if rc < 0 and device_failure != "mark":
         raise RuntimeError("bitcoinconsensus_verify_batch: device pipeline failed")
-    return [(r, Error(e)) for r, e in res]
+    return [(r, error_from_code(e)) for r, e in res]
 
 
 def last_batch_stats():

@@ -333,7 +333,11 @@ int bcc_workload_run(bcc_workload* w, void* stream) { return w->batch->run(strea
 int bcc_workload_run_sighash(bcc_workload* w, void* stream) { return w->batch->run_sighash(stream); }
 int bcc_workload_run_ecdsa(bcc_workload* w, void* stream) { return w->batch->run_ecdsa(stream); }
 
-int bcc_workload_verdicts(bcc_workload* w, uint8_t* out) { return w->batch->fetch_verdicts(out); }
+int bcc_workload_verdicts(bcc_workload* w, uint8_t* out, size_t cap) {
+    if (!w || !w->batch || !out) return -1;
+    if (cap < w->batch->n_tuples()) return BCC_BENCH_ERR_CAPACITY;  // one byte per row, not per item
+    return w->batch->fetch_verdicts(out);
+}
 
 void bcc_workload_shape(const bcc_workload* w, size_t* tuples, size_t* sighash_blocks,
                         size_t* aux_blocks, size_t* preimages, size_t* aux_messages) {
@@ -421,13 +425,18 @@ const bcc_batch_item* bcc_itemset_items(const bcc_itemset* m, size_t* n) {
 
 void bcc_itemset_free(bcc_itemset* m) { delete m; }
 
-int bcc_workload_tuple_items(const bcc_workload* w, uint32_t* out) {
-    if (!w) return -1;
+int bcc_workload_tuple_items(const bcc_workload* w, uint32_t* out, size_t cap) {
+    if (!w || !out) return -1;
+    if (cap < w->tuple_item.size()) return BCC_BENCH_ERR_CAPACITY;
     if (!w->tuple_item.empty()) memcpy(out, w->tuple_item.data(), 4 * w->tuple_item.size());
     return 0;
 }
 
-int bcc_workload_msgs(bcc_workload* w, uint8_t* out) { return w->batch->fetch_msgs(out); }
+int bcc_workload_msgs(bcc_workload* w, uint8_t* out, size_t cap) {
+    if (!w || !w->batch || !out) return -1;
+    if (cap / 32 < w->batch->n_tuples()) return BCC_BENCH_ERR_CAPACITY;
+    return w->batch->fetch_msgs(out);
+}
 
 // Any caller items (copied): the engine's first interpreter round over them under `flags`,
 // staged like the synthetic workloads, so tests can run the exact benchmarked path on mutated

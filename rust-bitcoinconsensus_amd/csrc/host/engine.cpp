@@ -15,6 +15,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <future>
+#include <condition_variable>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -765,11 +766,11 @@ bool mark_host_rows(std::vector<Round>& rds, unsigned T) {
     return any;
 }
 
-// The offloaded legacy jobs of every shard, hashed in parallel on the calling thread's team (their
-// rows' msg receive the sighash).
-void hash_host_jobs(std::vector<Round>& rds, unsigned T, unsigned maxW = 0) {
+// The offloaded legacy jobs of the shards `shards`, hashed in parallel on the calling thread's team
+// (their rows' msg receive the sighash).
+void hash_host_jobs(std::vector<Round>& rds, const std::vector<unsigned>& shards, unsigned maxW = 0) {
     std::vector<std::pair<uint32_t, uint32_t>> work;  // (shard, job): tjobs first, then pre
-    for (unsigned t = 0; t < T; t++)
+    for (unsigned t : shards)
         for (uint32_t k = 0; k < rds[t].host.pending(); k++) work.emplace_back(t, k);
     if (work.empty()) return;
     size_t blocks = 0;
@@ -777,6 +778,7 @@ void hash_host_jobs(std::vector<Round>& rds, unsigned T, unsigned maxW = 0) {
         const HostJobs& h = rds[w.first].host;
         blocks += w.second < h.tjobs.size() ? tpl_job_blocks(h.tjobs[w.second]) : 8;
     }
+    const unsigned T = (unsigned)shards.size();
     const unsigned W = (unsigned)std::max<size_t>(1, std::min<size_t>(std::min<size_t>(maxW ? maxW : T, host_threads()),
                                                                          blocks / 256 + 1));
     // jobs are dealt round-robin: the long ones of one tx are spread over every worker
@@ -798,27 +800,61 @@ void hash_host_jobs(std::vector<Round>& rds, unsigned T, unsigned maxW = 0) {
     });
 }
 
-// A round's offloaded jobs hashed while the device runs (single-GPU rounds): the device round
-// calls ensure() through its LateMsgFill once the message-independent kernels are queued; every
-// host path that needs the messages calls it first.  Hashes once per interpreter pass.
-// Round 5: the device workers of a multi-GPU round call ensure() concurrently (the first hashes on
-// its team, the others wait for it), and the hashing time is kept here for the caller's statistics
-// (chunk_finish), not added to the calling thread's t_stats: on a pipeline or device worker that
-// would have been the worker's.
+void hash_host_jobs(std::vector<Round>& rds, unsigned T, unsigned maxW = 0) {
+    std::vector<unsigned> all(T);
+    for (unsigned t = 0; t < T; t++) all[t] = t;
+    hash_host_jobs(rds, all, maxW);
+}
+
+// A round's offloaded jobs hashed while the device runs: the device round calls ensure() through
+// its LateMsgFill once the message-independent kernels are queued; every host path that needs the
+// messages calls it first.  Hashes each shard once per interpreter pass.
+// Multi-GPU rounds (round 6, after the round-5 advisory): each device group's fill hashes only its
+// own shards [g0, g1) -- concurrently with the other groups, on its worker's team -- so no worker
+// ever writes the msg rows of a shard another worker is staging (copy_msg).  A shard another
+// caller has claimed is waited for, never hashed twice.  The hashing time is kept here for the
+// caller's statistics (chunk_finish), not added to the calling thread's t_stats: on a pipeline or
+// device worker that would have been the worker's.
 struct LateHost {
     std::vector<Round>* rds = nullptr;
     unsigned T = 0;
-    bool done = false;
-    unsigned W = 0;       // worker threads (0: at most T)
-    double seconds = 0;   // hashing time, collected by chunk_finish
-    std::shared_ptr<std::mutex> mu = std::make_shared<std::mutex>();
-    void ensure() {
-        std::lock_guard<std::mutex> lk(*mu);
-        if (done) return;
-        auto h0 = std::chrono::steady_clock::now();
-        hash_host_jobs(*rds, T, W);
-        seconds += std::chrono::duration<double>(std::chrono::steady_clock::now() - h0).count();
-        done = true;
+    unsigned W = 0;       // worker threads (0: at most the shards hashed)
+    double seconds = 0;   // hashing time, collected by chunk_finish (read with no round running)
+    struct Sync {
+        std::mutex mu;
+        std::condition_variable cv;
+        std::vector<uint8_t> state;  // per shard: 0 to hash, 1 being hashed, 2 done
+    };
+    std::shared_ptr<Sync> sy = std::make_shared<Sync>();
+    LateHost() = default;
+    LateHost(std::vector<Round>* r, unsigned t, unsigned w) : rds(r), T(t), W(w) {}
+    void ensure() { ensure(0, T); }
+    void ensure(unsigned lo, unsigned hi) {
+        std::vector<unsigned> mine;
+        {
+            std::lock_guard<std::mutex> lk(sy->mu);
+            if (sy->state.size() != T) sy->state.assign(T, 0);
+            for (unsigned t = lo; t < hi; t++)
+                if (sy->state[t] == 0) {
+                    sy->state[t] = 1;
+                    mine.push_back(t);
+                }
+        }
+        if (!mine.empty()) {
+            auto h0 = std::chrono::steady_clock::now();
+            hash_host_jobs(*rds, mine, W);
+            const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - h0).count();
+            std::lock_guard<std::mutex> lk(sy->mu);
+            for (unsigned t : mine) sy->state[t] = 2;
+            seconds += dt;
+            sy->cv.notify_all();
+        }
+        std::unique_lock<std::mutex> lk(sy->mu);
+        sy->cv.wait(lk, [&] {
+            for (unsigned t = lo; t < hi; t++)
+                if (sy->state[t] != 2) return false;
+            return true;
+        });
     }
 };
 
@@ -1204,13 +1240,13 @@ int run_device_group(int dev, const std::vector<Round>& rds, unsigned t0, unsign
         }
         // the late rows of shards [g0, g1), batch-local
         const LateMsgFill fill = [&, g0, g1](std::vector<uint32_t>& rows, std::vector<uint8_t>& digs) {
-            late->ensure();
+            late->ensure(g0, g1);  // this group's shards only (the other workers stage theirs)
             late_rows(rds, row0, g0, g1, rows, digs);
         };
         double st = 0;
         int e = 1;
         if (too_big) {
-            if (late) late->ensure();
+            if (late) late->ensure(g0, g1);
             if (host_fallback_enabled()) {
                 host_verify_parts(pj.data(), pr.data(), pj.size(), verdict + row0[g0], host_threads());
                 note_host_fallback();
@@ -1337,7 +1373,7 @@ void chunk_interpret(ChunkRun& c) {
     // the offloaded jobs' rows are marked now; the host hashes the jobs while the device(s) run the
     // message-independent kernels (LateHost; every device worker's round waits for them)
     t_stats.host_jobs_seconds += c.late.seconds;  // a previous pass's hashing (pipelined chunks)
-    c.late = LateHost{&c.rds, c.T, false, c.W};
+    c.late = LateHost(&c.rds, c.T, c.W);
     c.late_pending = mark_host_rows(c.rds, c.T);
     size_t npend = 0;
     bool any = false;
@@ -1386,8 +1422,12 @@ void chunk_early(ChunkRun& c, bool allow) {
         c.rds[t].early_mapped = 0;
         c.rds[t].early_msgs = 0;
     }
-    if (!early_wanted(c.n, allow)) return;
     const std::vector<int> devs = device_list();
+    // the calling thread's device batches forget any early set of an earlier call or chunk first:
+    // only a launch below may make one live again (Round::early gates its use today; the reset
+    // keeps a future path that stages rows without that gate from reading a stale set)
+    for (int d : devs) gpu_early_reset(d);
+    if (!early_wanted(c.n, allow)) return;
     auto e0 = clk::now();
     std::vector<const TupleRows*> parts(c.T);
     size_t E = 0;

@@ -273,6 +273,20 @@ extern "C" int bcc_pubkey_verify_batch(const uint8_t* pub_blob, const uint64_t* 
     if (n == 0) return 0;
     if (!pub_off || !sig_off || !msg32 || !verdict) return -1;
     if (pub_off[n] < pub_off[0] || sig_off[n] < sig_off[0]) return -1;  // offsets run backwards
+    // Offsets must be non-decreasing over the whole call: every round checks a tuple against its
+    // own round's [off[lo], off[lo + m]] span (the bytes it uploads), so with offsets out of order
+    // a tuple's verdict would depend on how the call is cut into rounds and devices.  One O(n) pass
+    // on the team (~1 ms for 8M tuples) rejects such a call instead.
+    {
+        std::atomic<bool> bad{false};
+        bcc::host::pfor(n, 1 << 16, [&](size_t lo, size_t hi) {
+            bool b = false;
+            for (size_t i = lo; i < hi; i++)
+                b |= (pub_off[i + 1] < pub_off[i]) | (sig_off[i + 1] < sig_off[i]);
+            if (b) bad.store(true, std::memory_order_relaxed);
+        });
+        if (bad.load()) return -1;
+    }
     bcc::host::ActiveCaller active;
     std::vector<int> devs = device < 0 ? bcc::host::device_list() : std::vector<int>{device};
     const size_t D = std::min<size_t>(devs.size(), (n + 4095) / 4096);

@@ -99,3 +99,88 @@ def test_python_structs_match_c_layout(tmp_path):
     assert got == [ctypes.sizeof(B.BatchStats), ctypes.sizeof(B.BatchItem),
                    ctypes.sizeof(B.TuplesetHost), ctypes.sizeof(B.TaprootCheck),
                    B.TaprootCheck.codeseparator_pos.offset]
+
+
+def test_device_failure_code_through_verify_batch_raw():
+    """BCC_DEVICE_FAILURE_ERROR through the product library's verify_batch (no GPU needed: every
+    device round is made to fail): rc == -1, items that needed a signature verdict carry err 6
+    (BCC_ERR_DEVICE_FAILURE), and the Python mapping turns 6 into DeviceFailure, never into the
+    crate's Error (lib.rs:172-185 has discriminants 0-5 only; INTEGRATION.md binds err_out as
+    c_int for that reason)."""
+    import sys
+    code = f"""
+import sys
+sys.path[:0] = [{os.path.dirname(LIB)!r}, {os.path.join(ROOT, 'tests')!r}]
+import bitcoinconsensus_amd as B
+from fixtures import load_json
+vs = [v for v in load_json("crate_vectors.json") if v["flags"] == 0xE15]
+items = [(bytes.fromhex(v["spk"]), v["amount"], bytes.fromhex(v["tx"]), v["nin"]) for v in vs]
+B.set_device_failure_policy(B.DEVICE_FAILURE_ERROR)
+B.set_host_small_round(0)
+B.debug_fail_device_rounds(1 << 20)
+rc, res = B.verify_batch_raw(items)
+assert rc == -1, rc
+for v, (r, e) in zip(vs, res):
+    assert r == 0
+    assert e == 6 if v["ret"] == 1 else e in (6, v["err"]), (v["name"], e)
+marked = B.verify_batch(items, device_failure="mark")
+assert [int(e) for _, e in marked] == [e for _, e in res]
+assert all(isinstance(e, B.DeviceFailure) for (_, e), (_, c) in zip(marked, res) if c == 6)
+try:
+    B.verify_batch(items)
+    raise SystemExit("no RuntimeError")
+except RuntimeError:
+    pass
+for c in range(6):
+    assert B.error_from_code(c) is B.Error(c)
+try:
+    B.error_from_code(7)
+    raise SystemExit("no ValueError")
+except ValueError:
+    pass
+print("ok")
+"""
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0 and "ok" in p.stdout, (p.returncode, p.stdout, p.stderr[-2000:])
+
+
+def test_workload_accessors_pass_row_capacity(monkeypatch):
+    """Host logic of the bench library's row accessors (no GPU: the library is a stub object):
+    Workload.verdicts / msgs / tuple_items size their buffers by staged tuple ROWS (a block
+    workload's multisig inputs have several) and pass that capacity to the C entry points, which
+    refuse a short buffer (include/bcc_bench.h BCC_BENCH_ERR_CAPACITY) instead of writing past it;
+    a refusal surfaces as RuntimeError."""
+    import ctypes
+    import sys
+    sys.path.insert(0, os.path.dirname(LIB))
+    import bitcoinconsensus_amd as B
+    rows, seen = 7, {}
+
+    class Stub:
+        def _check(self, name, need, out, cap):
+            seen[name] = (cap, ctypes.sizeof(out))
+            assert cap <= ctypes.sizeof(out)
+            return -2 if cap < need else 0
+
+        def bcc_workload_verdicts(self, h, out, cap):
+            return self._check("verdicts", rows, out, cap)
+
+        def bcc_workload_msgs(self, h, out, cap):
+            return self._check("msgs", 32 * rows, out, cap)
+
+        def bcc_workload_tuple_items(self, h, out, cap):
+            seen["tuple_items"] = (cap, len(out))
+            return -2 if cap < rows else 0
+
+    w = B.Workload.__new__(B.Workload)
+    w.h = None
+    monkeypatch.setattr(B, "blib", lambda: Stub())
+    monkeypatch.setattr(B.Workload, "shape", lambda self: {"tuples": rows})
+    monkeypatch.setattr(B.Workload, "__del__", lambda self: None, raising=False)
+    assert len(w.verdicts()) == rows and seen["verdicts"] == (rows, rows)
+    assert len(w.msgs()) == 32 * rows and seen["msgs"] == (32 * rows, 32 * rows)
+    assert len(w.tuple_items()) == rows and seen["tuple_items"] == (rows, rows)
+    monkeypatch.setattr(B.Workload, "shape", lambda self: {"tuples": rows - 1})
+    for f in (w.verdicts, w.msgs, w.tuple_items):
+        with pytest.raises(RuntimeError):
+            f()

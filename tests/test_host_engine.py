@@ -211,9 +211,9 @@ def test_pubkey_verify_batch_front_end(eng, host_lane):
     """bcc_pubkey_verify_batch on the reference-labelled adversarial tuple fixtures.  host_lane:
     every round on the host lane code, i.e. the product's host front end (parse_rows: CPubKey
     length filter, lax DER, r/s == 0; the host_verify_rows curve code); else the device round
-    (stubbed by the oracle's CPubKey::Verify over the same blob slices).  Offsets out of order or
-    past the round's blob make just those tuples invalid, and offsets running backwards over the
-    whole call are an argument error."""
+    (stubbed by the oracle's CPubKey::Verify over the same blob slices).  Offsets that are not
+    non-decreasing anywhere (one tuple past the blob, one running backwards, or the whole call
+    backwards) are an argument error: -1, so that no verdict depends on the round split."""
     from fixtures import ecdsa_tuples
     ts = ecdsa_tuples()
 
@@ -233,14 +233,16 @@ def test_pubkey_verify_batch_front_end(eng, host_lane):
         assert eng.bcc_pubkey_verify_batch(pb, po, msg, sb, so, out, len(ts), 0) == 0
         bad = [(t["cls"], i) for i, t in enumerate(ts) if out.raw[i] != t["verdict"]]
         assert not bad, bad[:20]
-        po[10] = 1 << 40
-        so[20] = so[19] - 1
+        keep = po[10]
+        po[10] = 1 << 40  # tuple 9 past the blob, tuple 10 backwards
+        assert eng.bcc_pubkey_verify_batch(pb, po, msg, sb, so, out, len(ts), 0) == -1
+        po[10] = keep
+        keep = so[20]
+        so[20] = so[19] - 1  # tuple 19 backwards
+        assert eng.bcc_pubkey_verify_batch(pb, po, msg, sb, so, out, len(ts), 0) == -1
+        so[20] = keep
         assert eng.bcc_pubkey_verify_batch(pb, po, msg, sb, so, out, len(ts), 0) == 0
-        want = [t["verdict"] for t in ts]
-        want[9] = want[10] = want[19] = 0
-        got = list(out.raw)
-        del got[20], want[20]
-        assert got == want
+        assert list(out.raw) == [t["verdict"] for t in ts]
         po[0], po[len(ts)] = 1, 0
         assert eng.bcc_pubkey_verify_batch(pb, po, msg, sb, so, out, len(ts), 0) == -1
     finally:

@@ -268,16 +268,10 @@ def _der_variants(r, s, rng):
     return out
 
 
-@pytest.mark.skipif(not reference_available(), reason="oracle/_ref not built")
-def test_der_on_device_matches_reference():
-    """K_der (der.hip, round 5): bcc_pubkey_verify_batch parses the caller's blobs on the device.
-    Lax-DER variants of valid signatures (zero padding, long-form lengths, sequence-length garbage,
-    trailing bytes, >32-byte integers, r or s >= n, zero, truncation, wrong tags, random bytes),
-    pubkeys of every header and wrong lengths, all against the reference's CPubKey::Verify tuple by
-    tuple, through one round and through the pipelined rounds (tuple_rounds), and equal to the host
-    parse (a host-lane round)."""
+def _der_variant_set():
+    """Lax-DER variants of valid fixture signatures and pubkeys of every header, shuffled, as
+    (tuples, pub_blob, pub_off, msg, sig_blob, sig_off)."""
     import random
-    import bitcoinconsensus_amd as B
     rng = random.Random(0xDE5)
     base = [t for t in ecdsa_tuples() if t["verdict"] == 1 and t["sig"][:1] == b"\x30"]
     tuples = []
@@ -305,6 +299,19 @@ def test_der_on_device_matches_reference():
     so = np.zeros(len(tuples) + 1, np.uint64)
     so[1:] = np.cumsum([len(t[2]) for t in tuples])
     msg = np.frombuffer(b"".join(t[1] for t in tuples), np.uint8)
+    return tuples, pb, po, msg, sb, so
+
+
+@pytest.mark.skipif(not reference_available(), reason="oracle/_ref not built")
+def test_der_on_device_matches_reference():
+    """K_der (der.hip, round 5): bcc_pubkey_verify_batch parses the caller's blobs on the device.
+    Lax-DER variants of valid signatures (zero padding, long-form lengths, sequence-length garbage,
+    trailing bytes, >32-byte integers, r or s >= n, zero, truncation, wrong tags, random bytes),
+    pubkeys of every header and wrong lengths, all against the reference's CPubKey::Verify tuple by
+    tuple, through one round and through the pipelined rounds of a 2.1M-tuple call (the variants
+    tiled), and equal to the host parse (a host-lane round)."""
+    import bitcoinconsensus_amd as B
+    tuples, pb, po, msg, sb, so = _der_variant_set()
     ref, _ = Reference().pubkey_verify_blob(pb, po, msg, sb, so, threads=THREADS)
     got = np.frombuffer(B.pubkey_verify_batch(tuples), np.uint8)
     assert np.array_equal(got, ref), np.nonzero(got != ref)[0][:20]
@@ -316,32 +323,95 @@ def test_der_on_device_matches_reference():
     finally:
         B.set_host_small_round(_small_round_env())
     assert np.array_equal(host, ref[:3000])
-    # offsets out of order or past the round's blob: those tuples are invalid (never read), on the
-    # device and on the host lane code alike; the other tuples keep their verdicts
+    # offsets out of order anywhere (a tuple past the blob, a tuple running backwards) are an
+    # argument error, on the device and on the host lane code alike: no verdict may depend on how
+    # the call is cut into rounds (each round checks against its own uploaded span)
     import ctypes
     L = ctypes.CDLL(B.lib()._name)
     u64p, vp = ctypes.POINTER(ctypes.c_uint64), ctypes.c_void_p
     f = L.bcc_pubkey_verify_batch
     f.argtypes = [vp, u64p, vp, vp, u64p, vp, ctypes.c_size_t, ctypes.c_int]
     m = 4000
-    po2, so2 = po[:m + 1].copy(), so[:m + 1].copy()
-    po2[100] = 1 << 40            # tuples 99, 100: past the blob
-    so2[200] = so2[199] - 1       # tuple 199 backwards; 200 starts before 199 ends (in order: valid)
-    want = ref[:m].copy()
-    want[[99, 100, 199]] = 0
     for small in (_small_round_env(), 1 << 30):
         B.set_host_small_round(small)
         try:
-            out = np.zeros(m, np.uint8)
-            assert f(pb.ctypes.data, po2.ctypes.data_as(u64p), msg.ctypes.data, sb.ctypes.data,
-                     so2.ctypes.data_as(u64p), out.ctypes.data, m, 0) == 0
+            for which in ("past", "backwards"):
+                po2, so2 = po[:m + 1].copy(), so[:m + 1].copy()
+                if which == "past":
+                    po2[100] = 1 << 40
+                else:
+                    so2[200] = so2[199] - 1
+                out = np.zeros(m, np.uint8)
+                assert f(pb.ctypes.data, po2.ctypes.data_as(u64p), msg.ctypes.data, sb.ctypes.data,
+                         so2.ctypes.data_as(u64p), out.ctypes.data, m, 0) == -1, (small, which)
         finally:
             B.set_host_small_round(_small_round_env())
-        mask = np.ones(m, bool)
-        mask[200] = False  # its bytes are shifted by one: the verdict is whatever they parse to
-        assert np.array_equal(out[mask], want[mask]), (small, np.nonzero(out[mask] != want[mask])[0][:10])
     # the pipelined rounds (>= 512k tuples: rounds staged while the previous one runs)
     reps = (2_100_000 + len(tuples) - 1) // len(tuples)
     big = tuples * reps
     got_big = np.frombuffer(B.pubkey_verify_batch(big), np.uint8)
     assert np.array_equal(got_big, np.tile(ref, reps))
+
+
+_SMALL_ROUNDS_CHILD = """
+import ctypes, sys
+import numpy as np
+sys.path.insert(0, sys.argv[2])
+import bitcoinconsensus_amd as B
+d = np.load(sys.argv[1])
+pb, po, msg, sb, so = (np.ascontiguousarray(d[k]) for k in ("pb", "po", "msg", "sb", "so"))
+n = len(po) - 1
+L = ctypes.CDLL(B.lib()._name)
+u64p, vp = ctypes.POINTER(ctypes.c_uint64), ctypes.c_void_p
+f = L.bcc_pubkey_verify_batch
+f.argtypes = [vp, u64p, vp, vp, u64p, vp, ctypes.c_size_t, ctypes.c_int]
+
+def call(po, so):
+    out = np.zeros(n, np.uint8)
+    rc = f(pb.ctypes.data, po.ctypes.data_as(u64p), msg.ctypes.data, sb.ctypes.data,
+           so.ctypes.data_as(u64p), out.ctypes.data, n, 0)
+    return rc, out
+
+res = {}
+rc, res["plain"] = call(po, so)
+assert rc == 0, rc
+for k in (1, 2):  # a staged round fails: the round's rows re-parsed on the host, re-run
+    B.debug_fail_device_rounds(k)
+    try:
+        rc, res["fault%d" % k] = call(po, so)
+    finally:
+        B.debug_fail_device_rounds(0)
+    assert rc == 0, rc
+po2 = po.copy()
+po2[n // 2] = po2[n // 2 + 1] + 1  # out of order in a middle round: an argument error
+assert call(po2, so)[0] == -1
+assert B.host_fallback_rounds() == 0
+np.savez(sys.argv[3], **res)
+print("ok")
+"""
+
+
+@pytest.mark.skipif(not reference_available(), reason="oracle/_ref not built")
+def test_der_variants_through_small_pipelined_rounds(tmp_path):
+    """The lax-DER / pubkey variants through bcc_pubkey_verify_batch's pipelined rounds
+    (tuple_rounds) with the round sizes shrunk (BCC_TUPLE_FIRST=512, BCC_TUPLE_ROUND=1024, read
+    once at load: a child process), so a ~6k-tuple call runs ~7 rounds on the three-slot
+    K_der staging, each round checking its own offset span: every verdict equals the reference's,
+    also when a staged round fails (one and two injected faults: the round's host re-parse and the
+    single-round path), and offsets out of order in a middle round are an argument error."""
+    import os
+    import subprocess
+    import sys
+    tuples, pb, po, msg, sb, so = _der_variant_set()
+    ref, _ = Reference().pubkey_verify_blob(pb, po, msg, sb, so, threads=THREADS)
+    inp, outp = tmp_path / "in.npz", tmp_path / "out.npz"
+    np.savez(inp, pb=pb, po=po, msg=msg, sb=sb, so=so)
+    pkg = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                       "rust-bitcoinconsensus_amd")
+    env = dict(os.environ, BCC_TUPLE_FIRST="512", BCC_TUPLE_ROUND="1024")
+    p = subprocess.run([sys.executable, "-c", _SMALL_ROUNDS_CHILD, str(inp), pkg, str(outp)],
+                       capture_output=True, text=True, timeout=100, env=env)
+    assert p.returncode == 0 and "ok" in p.stdout, (p.returncode, p.stdout, p.stderr[-3000:])
+    got = np.load(outp)
+    for k in ("plain", "fault1", "fault2"):
+        assert np.array_equal(got[k], ref), (k, np.nonzero(got[k] != ref)[0][:20])
