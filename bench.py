@@ -168,6 +168,46 @@ def _thread_cpus():
     return out
 
 
+def _smaps_mib():
+    """This process's resident and transparent-huge-page memory (MiB, /proc/self/smaps_rollup)."""
+    out = {}
+    try:
+        for ln in open("/proc/self/smaps_rollup"):
+            k = ln.split(":")[0]
+            if k in ("Rss", "AnonHugePages"):
+                out[k] = int(ln.split()[1]) // 1024
+    except (OSError, ValueError, IndexError):
+        pass
+    try:
+        out["thp"] = open("/sys/kernel/mm/transparent_hugepage/enabled").read().strip()
+    except OSError:
+        pass
+    return out
+
+
+def host_memory_probe(threads=16, mib=64, reps=4):
+    """Aggregate host copy bandwidth (GB/s, read + write) of `threads` threads each copying its own
+    `mib` MiB buffer `reps` times (numpy copies release the GIL): the memory-side state of the
+    shared host at the moment the drop-in leg runs (its host pass is memory-heavy)."""
+    import threading
+    import numpy as np
+    bufs = [(np.ones(mib << 20, np.uint8), np.empty(mib << 20, np.uint8)) for _ in range(threads)]
+    for a, b in bufs:
+        np.copyto(b, a)  # fault in
+
+    def work(a, b):
+        for _ in range(reps):
+            np.copyto(b, a)
+    ts = [threading.Thread(target=work, args=ab) for ab in bufs]
+    t0 = time.perf_counter()
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    dt = time.perf_counter() - t0
+    return round(2 * threads * reps * (mib << 20) / dt / 1e9, 1)
+
+
 def gpu_numa_node(dev):
     """NUMA node of GPU `dev` (sysfs of its PCI function; None when unknown)."""
     try:
@@ -396,6 +436,7 @@ class C2:
         # sustained: calls back to back (a CFS CPU quota lets one call burst above it, a run of
         # calls pays for that in throttling), whole-run wall time
         runs = []
+        mem_probe = host_memory_probe(threads=self.B.host_threads())
         topo = _cpu_topology()
         th0, ps0 = _thread_cpus(), _proc_stat_busy()
         t0, c0 = time.perf_counter(), time.process_time()
@@ -424,7 +465,11 @@ class C2:
                            loadavg=open("/proc/loadavg").read().split()[:3]
                            if os.path.exists("/proc/loadavg") else None,
                            note="whole machine over the sustained calls, this process included")
+        machine = dict(machine or {}, host_copy_GBps=mem_probe,
+                       host_copy_note="host_memory_probe: host_threads threads x 64 MiB numpy "
+                                      "copies, read + write bytes, just before the sustained calls")
         place = host_placement(th0, th1, topo)
+        place["process_memory_MiB"] = _smaps_mib()
         place["gpu_numa_node"] = gpu_numa_node(getattr(self, "dev", 0))
         return dict(inputs_per_s=self.n / best, ms=best * 1e3, valid=nv,
                     host_ms=st["host_seconds"] * 1e3, gpu_ms=st["gpu_seconds"] * 1e3,
@@ -957,6 +1002,8 @@ def main():
             log(f"[e2e probe] {where}: {job.end_to_end(job.ts.host())['calls_ms']}")
     e2e_probe("after staging")
     side = None
+    if args.config == "c2" and os.environ.get("BCC_BENCH_DROPIN_EARLY") and not args.no_extra:
+        job.wl.verify_batch()  # (diagnostics: the drop-in's host state allocated first)
     if args.config == "c2" and world == 1 and not args.no_extra and not args.no_side:
         side = SideLegs(B, dev, args.side_c4)
         log(f"[rank {rank}] side legs (C3, C4 x{args.side_c4}) set up in {side.setup_s:.1f}s")

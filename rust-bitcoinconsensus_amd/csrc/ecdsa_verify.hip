@@ -426,8 +426,8 @@ __global__ __launch_bounds__(TLADDER_WG) __attribute__((amdgpu_waves_per_eu(BCC_
     const uint8_t* __restrict__ tag, const uint8_t* __restrict__ px, const uint8_t* __restrict__ py,
     const uint8_t* __restrict__ pr, const uint8_t* __restrict__ ps, const u32* __restrict__ psinv,
     size_t cnt, u32* __restrict__ qtab, u32* __restrict__ state, const u32* __restrict__ emap,
-    size_t ecount) {
-    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    size_t ecount, size_t base) {
+    const size_t t = base + (size_t)blockIdx.x * blockDim.x + threadIdx.x;  // lanes [base, cnt)
     if (t >= cnt) return;
     if (emap && emap[t] < ecount) return;  // an early twin's result is copied (keyq_copy_kernel)
     u32* w = lane_words(state, t, TSTATE_WORDS);
@@ -587,8 +587,8 @@ __global__ __launch_bounds__(256) void keyq_copy_kernel(const u32* __restrict__ 
 #endif
 __global__ __launch_bounds__(TLADDER_WG) __attribute__((amdgpu_waves_per_eu(BCC_LADDERG_WAVES, BCC_LADDERG_WAVES))) void twist_ladder_g_kernel(
     u32* __restrict__ state, u32* __restrict__ qtab, const u32* __restrict__ gcomb,
-    const uint8_t* __restrict__ pm, const u32* __restrict__ psinv, size_t cnt) {
-    const size_t t = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint8_t* __restrict__ pm, const u32* __restrict__ psinv, size_t cnt, size_t base) {
+    const size_t t = base + (size_t)blockIdx.x * blockDim.x + threadIdx.x;  // lanes [base, cnt)
     if (t >= cnt) return;
     u32* w = lane_words(state, t, TSTATE_WORDS);
     u32 flags = w[T_FLAGS * LANE_STRIDE];
@@ -755,13 +755,17 @@ static int device_tables(int* dev, const u32** gcomb, int* cus) {
 }
 
 SigScratch::~SigScratch() {
-    if (dev >= 0 && (sinv || chunk || qtab2)) {
+    if (dev >= 0 && (sinv || chunk || qtab2 || ev_qa || ev_ga || aux)) {
         int cur = 0;
         (void)hipGetDevice(&cur);
         (void)hipSetDevice(dev);
+        if (aux) (void)hipStreamSynchronize((hipStream_t)aux);
         if (sinv) (void)hipFree(sinv);
         if (chunk) (void)hipFree(chunk);
         if (qtab2) (void)hipFree(qtab2);
+        if (ev_qa) (void)hipEventDestroy((hipEvent_t)ev_qa);
+        if (ev_ga) (void)hipEventDestroy((hipEvent_t)ev_ga);
+        if (aux) (void)hipStreamDestroy((hipStream_t)aux);
         (void)hipSetDevice(cur);
     }
 }
@@ -894,9 +898,26 @@ static const bool g_keyq2 = [] {
     const char* e = getenv("BCC_KEYQ2");
     return !(e && atoi(e) == 0);
 }();
+// The residency tail (round 6).  K_keyq holds BCC_LADDERQ_WAVES waves per SIMD, so one residency
+// round is cus x 4 SIMDs x waves x 64 lanes (262,144 on MI355X); C2's 1M lanes are 3.81 rounds, and
+// the last 0.81-full round left ~19 % of the chip idle for a whole round (~5 % of the stage;
+// DESIGN §3.3).  Split at the last whole round, the tail round's idle slots take the G ladder of
+// the lanes before it.  Returns the split (a multiple of the group size) or 0 for none
+// (BCC_KEYQ_SPLIT=0, fewer than two rounds, or a whole number of rounds).
+static const bool g_keyq_split = [] {
+    const char* e = getenv("BCC_KEYQ_SPLIT");
+    return !(e && atoi(e) == 0);
+}();
+static size_t keyq_split_at(size_t n, int cus) {
+    const size_t R = (size_t)cus * 4 * BCC_LADDERQ_WAVES * 64;
+    if (!g_keyq_split || R == 0 || n <= R || n % R == 0) return 0;
+    return n / R * R;
+}
+
 static int launch_keyq(SigScratch& sc, int cus, const uint8_t* d_tag, const uint8_t* d_x,
                        const uint8_t* d_y, const uint8_t* d_r, const uint8_t* d_s, size_t n,
                        u32* qtab, u32* state, const u32* emap, size_t ecount, hipStream_t st) {
+    sc.q_split = 0;
     if (g_keyq2 && 2 * n <= (size_t)cus * 4 * 64) {
         if (2 * n > sc.qtab2_cap) {
             if (sc.qtab2) BCC_HIP_TRY(hipFree(sc.qtab2));
@@ -913,9 +934,30 @@ static int launch_keyq(SigScratch& sc, int cus, const uint8_t* d_tag, const uint
         return (int)hipGetLastError();
     }
     const size_t groups = (n + TLADDER_WG - 1) / TLADDER_WG;
+    // a launch of several residency rounds plus a partial one: the whole rounds first, then the
+    // partial round as a launch of its own, with an event between them (keyq_split_at)
+    const size_t A = keyq_split_at(n, cus);
+    if (A) {
+        if (!sc.ev_qa) {
+            hipEvent_t e = nullptr;
+            BCC_HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            sc.ev_qa = e;
+        }
+        hipLaunchKernelGGL(twist_keyq_kernel, dim3((unsigned)(A / TLADDER_WG)), dim3(TLADDER_WG), 0, st,
+                           d_tag, d_x, d_y, d_r, d_s, (const u32*)sc.sinv, A, qtab, state, emap,
+                           ecount, (size_t)0);
+        BCC_HIP_TRY(hipGetLastError());
+        BCC_HIP_TRY(hipEventRecord((hipEvent_t)sc.ev_qa, st));
+        hipLaunchKernelGGL(twist_keyq_kernel, dim3((unsigned)((n - A + TLADDER_WG - 1) / TLADDER_WG)),
+                           dim3(TLADDER_WG), 0, st, d_tag, d_x, d_y, d_r, d_s, (const u32*)sc.sinv,
+                           n, qtab, state, emap, ecount, A);
+        BCC_HIP_TRY(hipGetLastError());
+        sc.q_split = A;
+        return 0;
+    }
     hipLaunchKernelGGL(twist_keyq_kernel, dim3((unsigned)groups), dim3(TLADDER_WG),
                        (unsigned)keyq_lds(groups, cus), st, d_tag, d_x, d_y, d_r, d_s,
-                       (const u32*)sc.sinv, n, qtab, state, emap, ecount);
+                       (const u32*)sc.sinv, n, qtab, state, emap, ecount, (size_t)0);
     return (int)hipGetLastError();
 }
 
@@ -983,9 +1025,12 @@ int ecdsa_launch(SigScratch& sc, const uint8_t* d_tag, const uint8_t* d_x, const
 int ecdsa_launch_after_pre(SigScratch& sc, const uint8_t* d_tag, const uint8_t* d_x,
                            const uint8_t* d_y, const uint8_t* d_r, const uint8_t* d_s,
                            const uint8_t* d_m, uint8_t* d_verdict, size_t n, void* stream,
-                           void* ev_rows_read, bool verdict_and) {
+                           void* ev_rows_read, bool verdict_and, void* ev_q_done) {
     const int and_mode = verdict_and ? 1 : 0;
-    if (n == 0) return 0;
+    if (n == 0) {  // nothing to launch; the stream still joins the other one
+        if (ev_q_done) BCC_HIP_TRY(hipStreamWaitEvent((hipStream_t)stream, (hipEvent_t)ev_q_done, 0));
+        return 0;
+    }
     int dev = 0, cus = 0;
     const u32* gcomb = nullptr;
     size_t C = 0;
@@ -996,12 +1041,46 @@ int ecdsa_launch_after_pre(SigScratch& sc, const uint8_t* d_tag, const uint8_t* 
     u32* qtab = (u32*)sc.chunk;
     u32* state = qtab + C * QTABLE_WORDS;
     const bool q_ahead = sc.q_ready == n && n <= C;
+    const size_t A = q_ahead ? sc.q_split : 0;
     sc.key_ready = 0;
     sc.q_ready = 0;
-    if (q_ahead) {  // the key half, u2 and the Q ladder ran ahead (ecdsa_launch_q)
-        hipLaunchKernelGGL(twist_ladder_g_kernel, dim3((unsigned)((n + TLADDER_WG - 1) / TLADDER_WG)),
-                           dim3(TLADDER_WG), 0, sm, state, qtab, gcomb, d_m, sinv, n);
+    sc.q_split = 0;
+    if (q_ahead && A && A < n) {
+        // split K_keyq: the G ladder of lanes [0, A) as soon as their K_keyq is done, beside the
+        // tail launch [A, n); the tail's G ladder after it
+        if (ev_q_done) {  // K_keyq ran on another stream (DeviceBatch::run_stages)
+            BCC_HIP_TRY(hipStreamWaitEvent(sm, (hipEvent_t)sc.ev_qa, 0));
+            hipLaunchKernelGGL(twist_ladder_g_kernel, dim3((unsigned)(A / TLADDER_WG)), dim3(TLADDER_WG),
+                               0, sm, state, qtab, gcomb, d_m, sinv, A, (size_t)0);
+            BCC_HIP_TRY(hipGetLastError());
+            BCC_HIP_TRY(hipStreamWaitEvent(sm, (hipEvent_t)ev_q_done, 0));
+        } else {  // K_keyq queued on this stream: the first G ladder goes to the second stream
+            if (!sc.aux) {
+                hipStream_t a = nullptr;
+                hipEvent_t g = nullptr;
+                BCC_HIP_TRY(hipStreamCreateWithFlags(&a, hipStreamNonBlocking));
+                BCC_HIP_TRY(hipEventCreateWithFlags(&g, hipEventDisableTiming));
+                sc.aux = a;
+                sc.ev_ga = g;
+            }
+            hipStream_t ax = (hipStream_t)sc.aux;
+            BCC_HIP_TRY(hipStreamWaitEvent(ax, (hipEvent_t)sc.ev_qa, 0));
+            hipLaunchKernelGGL(twist_ladder_g_kernel, dim3((unsigned)(A / TLADDER_WG)), dim3(TLADDER_WG),
+                               0, ax, state, qtab, gcomb, d_m, sinv, A, (size_t)0);
+            BCC_HIP_TRY(hipGetLastError());
+            BCC_HIP_TRY(hipEventRecord((hipEvent_t)sc.ev_ga, ax));
+            BCC_HIP_TRY(hipStreamWaitEvent(sm, (hipEvent_t)sc.ev_ga, 0));
+        }
+        hipLaunchKernelGGL(twist_ladder_g_kernel, dim3((unsigned)((n - A + TLADDER_WG - 1) / TLADDER_WG)),
+                           dim3(TLADDER_WG), 0, sm, state, qtab, gcomb, d_m, sinv, n, A);
         BCC_HIP_TRY(hipGetLastError());
+    } else if (q_ahead) {  // the key half, u2 and the Q ladder ran ahead (ecdsa_launch_q)
+        if (ev_q_done) BCC_HIP_TRY(hipStreamWaitEvent(sm, (hipEvent_t)ev_q_done, 0));
+        hipLaunchKernelGGL(twist_ladder_g_kernel, dim3((unsigned)((n + TLADDER_WG - 1) / TLADDER_WG)),
+                           dim3(TLADDER_WG), 0, sm, state, qtab, gcomb, d_m, sinv, n, (size_t)0);
+        BCC_HIP_TRY(hipGetLastError());
+    }
+    if (q_ahead) {
         if (ev_rows_read) BCC_HIP_TRY(hipEventRecord((hipEvent_t)ev_rows_read, sm));
         const size_t T = std::max<size_t>((n + FIN_PER_THREAD - 1) / FIN_PER_THREAD, std::min<size_t>(n, (size_t)cus * 256));
         hipLaunchKernelGGL(twist_fin_kernel<false>, dim3((unsigned)((T + 255) / 256)), dim3(256), 0,
@@ -1010,6 +1089,7 @@ int ecdsa_launch_after_pre(SigScratch& sc, const uint8_t* d_tag, const uint8_t* 
         return 0;
     }
     // chunked (n above the scratch chunk): the whole prep, the fused ladder and K_tfin per chunk
+    if (ev_q_done) BCC_HIP_TRY(hipStreamWaitEvent(sm, (hipEvent_t)ev_q_done, 0));  // K_inv's s^-1
     for (size_t base = 0; base < n; base += C) {
         const size_t cnt = std::min(C, n - base);
         hipLaunchKernelGGL(ecdsa_tprep_kernel, dim3((unsigned)((cnt + 255) / 256)),

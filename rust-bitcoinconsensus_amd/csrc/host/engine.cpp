@@ -1710,6 +1710,15 @@ std::atomic<size_t> g_pipeline_chunk{[] {
 }()};
 size_t pipeline_chunk() { return g_pipeline_chunk.load(std::memory_order_relaxed); }
 
+// Items of a pipelined batch's last chunk (BCC_PIPELINE_TAIL; 0: the remainder, the round-5 cut).
+// Round 6: the last chunk's device round (upload + kernels) is the only one that no host pass
+// overlaps; 1M C2 inputs are cut 500k / 250k / 250k instead of 500k / 500k.
+std::atomic<size_t> g_pipeline_tail{[] {
+    const char* e = getenv("BCC_PIPELINE_TAIL");
+    return e ? (size_t)atoll(e) : (size_t)0;
+}()};
+size_t pipeline_tail() { return g_pipeline_tail.load(std::memory_order_relaxed); }
+
 // Staging threads of a pipelined device round: it fills its pinned image beside the next chunk's
 // host pass, which has the CPU share.
 constexpr unsigned PIPELINE_STAGE_THREADS = 4;
@@ -1765,10 +1774,15 @@ long run_batch(const bcc_batch_item* items, size_t n, unsigned flags, int* ret_o
         account(chunk_finish(c, ret_out, err_out, false, &gpu_s));
         chunk_release_if_large(c);
     } else {
-        // chunk boundaries between transactions (adjacent items of one tx stay together)
+        // chunk boundaries between transactions (adjacent items of one tx stay together); the last
+        // chunk is cut down to pipeline_tail() items: its device round is the one no host pass
+        // hides, so a smaller one returns the call sooner
         std::vector<size_t> cut{0};
+        const size_t tail = std::min(pipeline_tail(), chunk);
         while (cut.back() < n) {
-            size_t e = std::min(n, cut.back() + chunk);
+            const size_t rem = n - cut.back();
+            const size_t step = tail == 0 || rem > chunk + tail ? chunk : rem > tail ? rem - tail : rem;
+            size_t e = std::min(n, cut.back() + step);
             while (e < n && items[e].tx_to == items[e - 1].tx_to) e++;
             cut.push_back(e);
         }

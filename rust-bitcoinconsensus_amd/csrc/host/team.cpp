@@ -3,8 +3,16 @@
 
 #include "devices.h"
 
+#include <pthread.h>
+#include <sched.h>
+
+#include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <cstdio>
+#include <fstream>
+#include <set>
+#include <string>
 #include <cstdlib>
 #include <condition_variable>
 #include <exception>
@@ -24,6 +32,72 @@ namespace {
 // of the same call starts without a futex wake-up per worker (~70 us for a 48-thread team on the
 // GPU box's 16-CPU quota: C3 runs about six passes per call).  The caller likewise polls for the
 // pass's end before it sleeps.  Idle workers (between calls) sleep.
+// Worker placement (BCC_TEAM_AFFINITY; round 6 diagnosis of the drop-in's run-to-run spread on the
+// shared GPU box): "none" leaves the workers to the scheduler; "node" confines them to the NUMA
+// node the team's creator runs on; "core" additionally gives worker i its own physical core of that
+// node (the first logical CPU of each core, in the process's affinity mask).  The calling thread
+// itself is never re-pinned.
+enum class Affinity { NONE, NODE, CORE };
+
+Affinity affinity_mode() {
+    static const Affinity m = [] {
+        const char* e = getenv("BCC_TEAM_AFFINITY");
+        const std::string v = e ? e : "none";
+        return v == "node" ? Affinity::NODE : v == "core" ? Affinity::CORE : Affinity::NONE;
+    }();
+    return m;
+}
+
+std::vector<int> parse_cpulist(const std::string& spec) {
+    std::vector<int> out;
+    size_t i = 0;
+    while (i < spec.size()) {
+        size_t j = spec.find(',', i);
+        if (j == std::string::npos) j = spec.size();
+        const std::string part = spec.substr(i, j - i);
+        const size_t d = part.find('-');
+        if (!part.empty()) {
+            const int a = atoi(part.c_str());
+            const int b = d == std::string::npos ? a : atoi(part.c_str() + d + 1);
+            for (int c = a; c <= b; c++) out.push_back(c);
+        }
+        i = j + 1;
+    }
+    return out;
+}
+
+std::string read_line(const std::string& path) {
+    std::ifstream f(path);
+    std::string s;
+    std::getline(f, s);
+    return s;
+}
+
+// CPUs of the NUMA node of `cpu` that this process may run on; with one_per_core, only the first
+// logical CPU of each physical core.  Empty when sysfs says nothing.
+std::vector<int> node_cpus(int cpu, bool one_per_core) {
+    cpu_set_t aff;
+    CPU_ZERO(&aff);
+    if (sched_getaffinity(0, sizeof aff, &aff) != 0) return {};
+    for (int node = 0; node < 64; node++) {
+        const std::vector<int> cpus =
+            parse_cpulist(read_line("/sys/devices/system/node/node" + std::to_string(node) + "/cpulist"));
+        if (std::find(cpus.begin(), cpus.end(), cpu) == cpus.end()) continue;
+        std::vector<int> out;
+        for (int c : cpus) {
+            if (c >= CPU_SETSIZE || !CPU_ISSET(c, &aff)) continue;
+            if (one_per_core) {
+                const std::vector<int> sib = parse_cpulist(read_line(
+                    "/sys/devices/system/cpu/cpu" + std::to_string(c) + "/topology/thread_siblings_list"));
+                if (!sib.empty() && sib[0] != c) continue;
+            }
+            out.push_back(c);
+        }
+        return out;
+    }
+    return {};
+}
+
 class Team {
 public:
     ~Team() { stop(); }
@@ -90,6 +164,19 @@ private:
     }
 
     void grow(unsigned workers) {
+        if (th_.size() < workers && !placed_) {
+            placed_ = true;
+            const Affinity m = affinity_mode();
+            if (m != Affinity::NONE) {
+                const int cpu = sched_getcpu();
+                if (cpu >= 0) cpus_ = node_cpus(cpu, m == Affinity::CORE);
+                // the creator's own core goes last: the caller runs share 0 there
+                if (m == Affinity::CORE && !cpus_.empty()) {
+                    auto it = std::find(cpus_.begin(), cpus_.end(), cpu);
+                    if (it != cpus_.end()) std::rotate(cpus_.begin(), it + 1, cpus_.end());
+                }
+            }
+        }
         while (th_.size() < workers) {
             const unsigned id = (unsigned)th_.size() + 1;
             uint64_t seen;
@@ -98,6 +185,16 @@ private:
                 seen = gen_.load(std::memory_order_relaxed);  // a new worker waits for the next pass
             }
             th_.emplace_back([this, id, seen] { loop(id, seen); });
+            if (!cpus_.empty()) {
+                cpu_set_t set;
+                CPU_ZERO(&set);
+                if (affinity_mode() == Affinity::CORE) {
+                    CPU_SET(cpus_[(id - 1) % cpus_.size()], &set);
+                } else {
+                    for (int c : cpus_) CPU_SET(c, &set);
+                }
+                (void)pthread_setaffinity_np(th_.back().native_handle(), sizeof set, &set);
+            }
         }
     }
 
@@ -139,6 +236,8 @@ private:
     std::atomic<uint64_t> gen_{0};
     std::atomic<bool> spin_{false};  // the last pass's team fit the CPU share
     bool stop_ = false, caller_waits_ = false;
+    bool placed_ = false;   // the workers' CPUs are chosen (BCC_TEAM_AFFINITY)
+    std::vector<int> cpus_;  // ... and these are they (empty: no affinity)
 };
 
 thread_local std::unique_ptr<Team> tl_team;

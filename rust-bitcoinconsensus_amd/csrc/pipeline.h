@@ -415,6 +415,14 @@ struct SigScratch {
     size_t q_ready = 0;    // tuples whose Q ladder ran ahead (ecdsa_launch_q)
     void* qtab2 = nullptr;  // the Q tables of K_keyq's latency mode (two lanes per tuple)
     size_t qtab2_cap = 0;   // lanes
+    // Round 6, the residency tail: K_keyq of a launch that is not a whole number of residency
+    // rounds runs as two launches, [0, q_split) and [q_split, q_ready); ev_qa is recorded after
+    // the first, so the G ladder of those lanes can fill the idle slots of the second's last
+    // round (ecdsa_launch_after_pre).  aux / ev_ga: the second stream of the single-stream form.
+    size_t q_split = 0;
+    void* ev_qa = nullptr;
+    void* ev_ga = nullptr;
+    void* aux = nullptr;
     SigScratch() = default;
     SigScratch(const SigScratch&) = delete;
     SigScratch& operator=(const SigScratch&) = delete;
@@ -454,10 +462,14 @@ int ecdsa_launch_q_mapped(SigScratch& sc, const SigScratch& early, size_t early_
 // rows (the next run's front kernels) need only wait for it, not for the ladder.
 // verdict_and: the caller has set d_verdict[0, n) to 1 (and may already have cleared rows, e.g.
 // the key-hash conditions); K_tfin then only clears the rows that fail.
+// ev_q_done (optional hipEvent_t): recorded after the Q launches on another stream; `stream`
+// waits for it before the lanes that need it (with a split K_keyq, only the G ladder of the tail
+// lanes waits: the full rounds' G ladder goes first, beside the tail's K_keyq).
 int ecdsa_launch_after_pre(SigScratch& sc, const uint8_t* d_tag, const uint8_t* d_x,
                            const uint8_t* d_y, const uint8_t* d_r, const uint8_t* d_s,
                            const uint8_t* d_m, uint8_t* d_verdict, size_t n, void* stream,
-                           void* ev_rows_read = nullptr, bool verdict_and = false);
+                           void* ev_rows_read = nullptr, bool verdict_and = false,
+                           void* ev_q_done = nullptr);
 int schnorr_launch(SigScratch& sc, const uint8_t* d_sig64, const uint8_t* d_msg32,
                    const uint8_t* d_xonly32, uint8_t* d_verdict, size_t n, void* stream);
 

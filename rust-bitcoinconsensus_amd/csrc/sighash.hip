@@ -1677,9 +1677,10 @@ int DeviceBatch::run_stages(void* stream, const LateMsgFill* late) {
         if (!n_hash_) BCC_HIP_TRY(hipStreamWaitEvent(st, (hipEvent_t)ev_up_, 0));  // rows uploaded
         if (int e = put_late(st, late)) return e;
     }
-    BCC_HIP_TRY(hipStreamWaitEvent(st, (hipEvent_t)ev_join_, 0));
+    // (the wait for the Q launches, ev_join_, is placed by ecdsa_launch_after_pre: with a split
+    // K_keyq the G ladder of the whole rounds starts before the tail round's K_keyq is done)
     return ecdsa_launch_after_pre(scratch_, d_tag, d_x, d_y, d_r, d_s, d_m, d_v, n_rows_, st,
-                                  nullptr, kh_done_);
+                                  nullptr, kh_done_, ev_join_);
 }
 
 // Verdicts come back through a pinned buffer of the batch (an asynchronous copy on the run's stream,

@@ -167,7 +167,8 @@ def test_block_workload_rows_exceed_items_bench_abi(wl):
         assert t > w.n
         w.run()
         v = w.verdicts()
-        assert len(v) == t and all(x == 1 for x in v)
+        # (2-of-3 candidate pairs: some rows pair a signature with the wrong key -> 0)
+        assert len(v) == t and set(v) <= {0, 1} and sum(v) >= w.n
         ti = w.tuple_items()
         assert len(ti) == t and max(ti) < w.n and sorted(set(ti)) == list(range(w.n))
         m = w.msgs()
