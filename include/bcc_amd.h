@@ -132,6 +132,13 @@ int bcc_set_chunk_lanes(size_t lanes);
  * while the host deserializes and interprets the next chunk.  Default 500000 (or the
  * BCC_PIPELINE_CHUNK environment variable); 0 disables it.  Results never depend on it. */
 int bcc_set_pipeline_chunk(size_t items);
+/* Items of a pipelined batch's last chunk (its device round is the one no host pass hides):
+ * 0 (default, or BCC_PIPELINE_TAIL) keeps the remainder; results never depend on it. */
+int bcc_set_pipeline_tail(size_t items);
+/* Host shards per worker thread of a long bitcoinconsensus_verify_batch pass (default 1, or
+ * BCC_LONG_SHARDS_PER_WORKER): with k > 1 the k x workers shards are dealt dynamically.  Results
+ * never depend on it.  Returns 0, or -1 for k outside 1..64. */
+int bcc_set_long_shards_per_worker(unsigned k);
 
 /* Legacy signature checks whose serial SHA-256 chain is longer than `blocks` 64-byte blocks (the
  * preimages of many-input transactions) are hashed on the host CPU instead of in one GPU lane each,

@@ -1407,6 +1407,14 @@ unsigned SHARDS_PER_WORKER = [] {
     return e ? std::max(1, atoi(e)) : 1;
 }();
 
+// Shards per worker of a long pass (BCC_LONG_SHARDS_PER_WORKER, bcc_set_long_shards_per_worker;
+// default 1: one contiguous shard per worker).  With more, a worker that finishes early takes the
+// next shard, so a worker on a slower (shared) core sets less of the pass's length.
+std::atomic<unsigned> g_long_shards{[] {
+    const char* e = getenv("BCC_LONG_SHARDS_PER_WORKER");
+    return e ? (unsigned)std::max(1, atoi(e)) : 1u;
+}()};
+
 // Early Q halves for a single-GPU, single-chunk call (EarlyShard): per shard the candidates of its
 // active items, then one early launch over all shards' rows (concatenated in shard order).
 // Whether a chunk of n items takes early Q halves (its candidates are extracted by prepare).
@@ -1456,8 +1464,10 @@ void chunk_start(ChunkRun& c, const bcc_batch_item* items, size_t n, unsigned fl
     // passes only.
     const unsigned cap = n < SHORT_PASS_ITEMS ? std::min(host_threads(), cpu_share()) : host_threads();
     c.W = n >= 256 ? std::min<unsigned>(cap, (unsigned)(n / 64)) : 1u;
-    // a short pass: four shards per worker, dealt dynamically (run_shards)
-    c.T = n < SHORT_PASS_ITEMS && c.W > 1 ? std::min<unsigned>(SHARDS_PER_WORKER * c.W, (unsigned)(n / 64)) : c.W;
+    // shards per worker, dealt dynamically (run_shards): SHARDS_PER_WORKER for a short pass,
+    // g_long_shards for a long one (bcc_set_long_shards_per_worker)
+    const unsigned spw = n < SHORT_PASS_ITEMS ? SHARDS_PER_WORKER : g_long_shards.load(std::memory_order_relaxed);
+    c.T = c.W > 1 ? std::min<unsigned>(std::max(1u, spw) * c.W, (unsigned)(n / 64)) : c.W;
     const unsigned T = c.T;
     const bool early = early_wanted(n, allow_early);
     if (early && c.early.size() < T) c.early.resize(T);
@@ -2024,6 +2034,17 @@ int bcc_set_early_q(int on) {
 
 int bcc_set_pipeline_chunk(size_t items) {
     g_pipeline_chunk.store(items, std::memory_order_relaxed);
+    return 0;
+}
+
+int bcc_set_long_shards_per_worker(unsigned k) {
+    if (k == 0 || k > 64) return -1;
+    g_long_shards.store(k, std::memory_order_relaxed);
+    return 0;
+}
+
+int bcc_set_pipeline_tail(size_t items) {
+    g_pipeline_tail.store(items, std::memory_order_relaxed);
     return 0;
 }
 

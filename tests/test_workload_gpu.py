@@ -21,7 +21,9 @@ from oracle_ctypes import Reference, reference_available
 pytestmark = [pytest.mark.gpu,
               pytest.mark.skipif(not reference_available(), reason="oracle/_ref not built")]
 
-N = 200_000
+# above one K_keyq residency round (256 CUs x 4 SIMDs x 4 waves x 64 = 262,144 lanes): the staged
+# round runs the split K_keyq with the full round's G ladder beside the tail (round 6)
+N = 300_000
 SEED = 0x5EED0001  # bench.py SEEDS["c2"]
 
 
