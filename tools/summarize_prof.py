@@ -74,17 +74,18 @@ def main(d):
     for st, ks in stages.items():
         if not any("fetch_size_launches" in K.get(k, {}) for k in ks):
             continue
-        # one launch of each stage kernel per execution (one lane chunk): the launch count is
-        # the execution count, whatever else the run did (a bench.py sustained window)
+        # at least one launch of each stage kernel per execution (one lane chunk; round 6: K_keyq
+        # and K_tladder_g twice when K_keyq is split at the last whole residency round): the
+        # smallest launch count (K_inv / K_tfin) is the execution count
         nl = {K[k]["fetch_size_launches"] for k in ks if "fetch_size_launches" in K.get(k, {})}
-        n_stage = nl.pop() if len(nl) == 1 else n_default
+        n_stage = min(nl) if nl else n_default
         fb = sum(K[k].get("fetch_size_bytes_total", 0) for k in ks if k in K) / n_stage
         wb = sum(K[k].get("write_size_bytes_total", 0) for k in ks if k in K) / n_stage
         out.setdefault("stages", {})[st] = dict(executions=n_stage, fetch_bytes=fb, fetch_bytes_x2=2 * fb,
                                                write_bytes=wb, traffic_bytes=2 * fb + wb)
-        # the same from per-launch averages (every launch full-size: bench.py --no-extra runs)
-        fl = sum(K[k].get("fetch_size_bytes_per_launch", 0) for k in ks if k in K)
-        wl = sum(K[k].get("write_size_bytes_per_launch", 0) for k in ks if k in K)
+        # per stage execution from the PMC launches (bench.py --no-extra runs: every stage full-size)
+        fl = sum(K[k].get("fetch_size_bytes_total", 0) for k in ks if k in K) / n_stage
+        wl = sum(K[k].get("write_size_bytes_total", 0) for k in ks if k in K) / n_stage
         out["stages"][st].update(per_launch_fetch_bytes_x2=2 * fl, per_launch_write_bytes=wl,
                                  per_launch_traffic_bytes=2 * fl + wl,
                                  kernels=[k for k in ks if k in K])
