@@ -624,6 +624,18 @@ class TupleJob:
                "class_counts": np.bincount(h["cls"]).tolist()}
         if self.kind == "c4":
             out["drop_in_end_to_end"] = self.end_to_end(h)
+            # the late-allocation case: the caller's pinned round images, device
+            # batches and scratch released and allocated again by the next call, after the whole
+            # run -- its first call pays the allocation, the next ones show whether the late
+            # placement itself is slower
+            import bitcoinconsensus_amd as BB
+            BB.release_thread_state()
+            late = self.end_to_end(h, reps=4)
+            out["drop_in_late_alloc"] = dict(calls_ms=late["calls_ms"],
+                                             verifies_per_s_after_first=self.n / (min(late["calls_ms"][1:]) * 1e-3),
+                                             mismatches_vs_staged=late["mismatches_vs_staged"],
+                                             note="bcc_release_thread_state() after the timed run, then 4 "
+                                                  "calls; the first allocates the thread's state again")
         return out
 
     def end_to_end(self, h, reps=3):
