@@ -139,6 +139,11 @@ int bcc_set_pipeline_tail(size_t items);
  * BCC_LONG_SHARDS_PER_WORKER): with k > 1 the k x workers shards are dealt dynamically.  Results
  * never depend on it.  Returns 0, or -1 for k outside 1..64. */
 int bcc_set_long_shards_per_worker(unsigned k);
+/* bitcoinconsensus_verify_batch's first interpreter pass runs inside the parse pass, block by
+ * block per host shard, while each item's transaction is still in cache (default 1, or
+ * BCC_FUSED_PASS; 0: two passes).  Calls with early Q halves keep two passes.  Results never
+ * depend on it.  Returns 0. */
+int bcc_set_fused_pass(int on);
 
 /* Legacy signature checks whose serial SHA-256 chain is longer than `blocks` 64-byte blocks (the
  * preimages of many-input transactions) are hashed on the host CPU instead of in one GPU lane each,

@@ -933,10 +933,16 @@ std::vector<size_t> shard_bounds(const BatchState& b, unsigned T) {
 // deserialized once per adjacent run of items, in parallel over T threads.
 // With `shards` / `runs`, the workers' shares are the shard_bounds() shards, and each worker also
 // fills its shard's item list and run list (the items that passed the pre-checks).
+// fused (optional, with `runs`): the first interpreter pass runs inside the parse pass, shard t's
+// newly active items handed over every FUSE_BLOCK items while their tx bytes and entries are still
+// in cache (chunk_start; not with `early`, which needs every shard parsed first).
+using FusedPass = std::function<void(unsigned, const uint32_t*, size_t)>;
+constexpr size_t FUSE_BLOCK = 256;
 void prepare(BatchState& b, const bcc_batch_item* items, size_t n, unsigned flags, unsigned T,
              std::vector<std::vector<uint32_t>>* shards = nullptr,
              std::vector<std::vector<uint32_t>>* runs = nullptr,
-             std::vector<EarlyShard>* early = nullptr, unsigned W = 0) {
+             std::vector<EarlyShard>* early = nullptr, unsigned W = 0,
+             const FusedPass* fused = nullptr) {
     if (W == 0 || W > T) W = T;  // worker threads over the T shards (run_shards)
     if (b.st.size() < n) b.st.resize(n);  // reused across calls: every field is (re)set below
     b.n = n;
@@ -1021,6 +1027,7 @@ void prepare(BatchState& b, const bcc_batch_item* items, size_t n, unsigned flag
             sh->clear();
             rl->clear();
         }
+        size_t fused_done = 0;  // run-list items already handed to the fused pass
         for (size_t k = klo; k < khi; k++) {
             const bcc_batch_item* in = &items[b.tx_first[k]];
             TxEntry& e = b.txs[k];
@@ -1056,6 +1063,10 @@ void prepare(BatchState& b, const bcc_batch_item* items, size_t n, unsigned flag
                     sh->push_back((uint32_t)i);
                     if (it.active) rl->push_back((uint32_t)i);
                 }
+            }
+            if (fused && rl && (rl->size() - fused_done >= FUSE_BLOCK || k + 1 == khi)) {
+                (*fused)(t, rl->data() + fused_done, rl->size() - fused_done);
+                fused_done = rl->size();
             }
         }
         if (sh) {
@@ -1111,9 +1122,10 @@ void prepare(BatchState& b, const bcc_batch_item* items, size_t n, unsigned flag
 
 // Interpreter pass over the active items of one shard (idx: the shard's items that need a run);
 // deferred checks land in rd.  Returns whether any item ran.
-bool interpret_shard(BatchState& b, const std::vector<uint32_t>& idx, Round& rd) {
+bool interpret_items(BatchState& b, const uint32_t* idx, size_t m, Round& rd) {
     bool any = false;
-    for (uint32_t i : idx) {
+    for (size_t k = 0; k < m; k++) {
+        const uint32_t i = idx[k];
         Item& it = b.st[i];
         if (!it.active) continue;
         any = true;
@@ -1133,6 +1145,10 @@ bool interpret_shard(BatchState& b, const std::vector<uint32_t>& idx, Round& rd)
         it.active = false;
     }
     return any;
+}
+
+bool interpret_shard(BatchState& b, const std::vector<uint32_t>& idx, Round& rd) {
+    return interpret_items(b, idx.data(), idx.size(), rd);
 }
 
 // One device round over the parts [p0, p1): fault injection first, then the device pipeline.
@@ -1350,6 +1366,8 @@ inline double process_cpu() {
 }
 
 // One interpreter pass over the chunk's run lists; sets up the device round it needs (if any).
+void chunk_interpret_finish(ChunkRun& c, const std::vector<char>& ran, const std::vector<double>& ts);
+
 void chunk_interpret(ChunkRun& c) {
     std::vector<char> ran(c.T, 0);
     auto i0 = clk::now();
@@ -1363,6 +1381,11 @@ void chunk_interpret(ChunkRun& c) {
         ts[t] = since(s0);
     });
     t_stats.interpret_seconds += since(i0);
+    chunk_interpret_finish(c, ran, ts);
+}
+
+// What follows an interpreter pass: its statistics, the late host jobs, the round's row offsets.
+void chunk_interpret_finish(ChunkRun& c, const std::vector<char>& ran, const std::vector<double>& ts) {
     double tmax = 0, tsum = 0;
     for (double x : ts) {
         tmax = std::max(tmax, x);
@@ -1406,6 +1429,12 @@ unsigned SHARDS_PER_WORKER = [] {
     const char* e = getenv("BCC_SHARDS_PER_WORKER");
     return e ? std::max(1, atoi(e)) : 1;
 }();
+
+// The first interpreter pass fused into the parse pass (BCC_FUSED_PASS, bcc_set_fused_pass; round 6).
+std::atomic<bool> g_fused_pass{[] {
+    const char* e = getenv("BCC_FUSED_PASS");
+    return !(e && atoi(e) == 0);
+}()};
 
 // Shards per worker of a long pass (BCC_LONG_SHARDS_PER_WORKER, bcc_set_long_shards_per_worker;
 // default 1: one contiguous shard per worker).  With more, a worker that finishes early takes the
@@ -1471,21 +1500,54 @@ void chunk_start(ChunkRun& c, const bcc_batch_item* items, size_t n, unsigned fl
     const unsigned T = c.T;
     const bool early = early_wanted(n, allow_early);
     if (early && c.early.size() < T) c.early.resize(T);
+    auto round_state = [&] {  // per-shard state of the call (before its first interpreter pass)
+        c.next_list.resize(T);
+        for (auto& v : c.next_list) v.clear();
+        if (c.rds.size() < T) c.rds.resize(T);
+        for (unsigned t = 0; t < T; t++) {
+            c.rds[t].keys.clear();
+            c.rds[t].touched.clear();  // pointers into a previous call's tx entries: never followed
+            c.rds[t].host_rejected = 0;
+            c.rds[t].key_hashes = 0;
+        }
+        c.row0.assign(T + 1, 0);
+        c.stage_s = 0;
+        c.devices_used = 0;
+        c.retries = 0;
+    };
+    // Round 6: without early Q halves (every pipelined chunk) the first interpreter pass runs
+    // inside the parse pass, block by block per shard (prepare's FusedPass): each item is
+    // interpreted while its tx bytes and parsed entry are still in cache, instead of in a second
+    // pass over the whole chunk.  (The prepared HASH160s the pass reads exist only with
+    // BCC_DEVICE_KEY_HASH=0, which keeps the two passes.)
+    if (!early && g_fused_pass.load(std::memory_order_relaxed) &&
+        g_device_key_hash.load(std::memory_order_relaxed)) {
+        round_state();
+        chunk_early(c, false);  // (resets the early pointers and the device's early sets)
+        c.host_planned->store(0, std::memory_order_relaxed);
+        for (unsigned t = 0; t < T; t++) {
+            c.rds[t].reset(true);
+            c.rds[t].host.planned = c.host_planned.get();
+        }
+        std::vector<char> ran(T, 0);
+        std::vector<double> ts(T, 0);
+        const FusedPass pass = [&](unsigned t, const uint32_t* idx, size_t m) {
+            auto s0 = clk::now();
+            ran[t] |= interpret_items(c.b, idx, m, c.rds[t]) ? 1 : 0;
+            ts[t] += since(s0);
+        };
+        prepare(c.b, items, n, flags, T, &c.shards, &c.run_list, nullptr, c.W, &pass);
+        double tmax = 0;
+        for (double x : ts) tmax = std::max(tmax, x);
+        const double both = since(t0);  // parse + interpret, split by the slowest shard's share
+        t_stats.interpret_seconds += std::min(tmax, both);
+        t_stats.prepare_seconds += both - std::min(tmax, both);
+        chunk_interpret_finish(c, ran, ts);
+        return;
+    }
     prepare(c.b, items, n, flags, T, &c.shards, &c.run_list, early ? &c.early : nullptr, c.W);  // + the shard / run lists
     t_stats.prepare_seconds += since(t0);
-    c.next_list.resize(T);
-    for (auto& v : c.next_list) v.clear();
-    if (c.rds.size() < T) c.rds.resize(T);
-    for (unsigned t = 0; t < T; t++) {
-        c.rds[t].keys.clear();
-        c.rds[t].touched.clear();  // pointers into a previous call's tx entries: never followed
-        c.rds[t].host_rejected = 0;
-        c.rds[t].key_hashes = 0;
-    }
-    c.row0.assign(T + 1, 0);
-    c.stage_s = 0;
-    c.devices_used = 0;
-    c.retries = 0;
+    round_state();
     chunk_early(c, allow_early);
     chunk_interpret(c);
 }
@@ -2034,6 +2096,11 @@ int bcc_set_early_q(int on) {
 
 int bcc_set_pipeline_chunk(size_t items) {
     g_pipeline_chunk.store(items, std::memory_order_relaxed);
+    return 0;
+}
+
+int bcc_set_fused_pass(int on) {
+    g_fused_pass.store(on != 0, std::memory_order_relaxed);
     return 0;
 }
 
