@@ -1644,21 +1644,24 @@ int chunk_device_round(ChunkRun& c) {
 }
 
 // Stitches a device round's verdicts into the items; the items whose speculation failed get
-// another interpreter pass (their run lists).
+// another interpreter pass (their run lists).  Only those items' check caches receive the
+// round's verdicts (round 6): an item whose consulted checks all came back true is final, and
+// its cache is never read again in this call, so the common case touches each item once.
 void chunk_stitch(ChunkRun& c) {
     auto& st = c.b.st;
     run_shards(c.T, c.W, [&](unsigned t) {
-        const Round& rd = c.rds[t];
         const uint8_t* v = c.verdict.data() + c.row0[t];
-        for (size_t k = 0; k < rd.pending.size(); k++)
-            st[rd.pending[k].item].cache[rd.pending[k].slot].v = v[k] ? 1 : 0;
         c.next_list[t].clear();
         for (uint32_t i : c.run_list[t]) {
             Item& it = st[i];
             if (it.pending.empty()) continue;
             bool all_true = true;
             for (uint32_t k : it.pending) all_true &= v[k] != 0;
-            if (!all_true) {  // speculation was wrong somewhere: re-run
+            if (!all_true) {  // speculation was wrong somewhere: re-run with what the round learned
+                // every check this item deferred in this round (consulted or a multisig
+                // candidate hint) is still encoded as -2 - row; earlier rounds' are resolved
+                for (Item::Check& ch : it.cache)
+                    if (ch.v <= -2) ch.v = v[(uint32_t)(-2 - ch.v)] ? 1 : 0;
                 it.active = true;
                 c.next_list[t].push_back(i);
             }
