@@ -190,6 +190,9 @@ BCC_HD void fe_reduce512(fe& r, const u32 (&t)[16]) {
 #ifndef BCC_RED_V4
 #define BCC_RED_V4 1
 #endif
+// (Round 6 also replaced v4's e_k / c9 masks by a precheck of the high limbs -- all <= 2^32 - 979
+// rule them out -- and measured it slower: the max over eight limbs sits on the reduction's
+// critical path, C2 117.1 -> 114.5 M/s, profiles/r06/ab/reduction_precheck.txt.  Not kept.)
 #if BCC_RED_V4
 #define BCC_FE_REDUCE fe_reduce512_v4
 #else
@@ -200,6 +203,18 @@ BCC_HD void fe_reduce512(fe& r, const u32 (&t)[16]) {
 // with the exact columns.  BCC_MUL_FLAG=0 keeps the exact columns only.
 #ifndef BCC_MUL_FLAG
 #define BCC_MUL_FLAG 1
+#endif
+// Round 6: no flags at all.  The columns' first carries are provably zero when a[0] and b[7] (a[0]
+// and a[7] for a square) are at most 2^32 - 9 (tools/gen_fe_asm.py, mul_256x256_col_u); one
+// compare per operand and a wave-wide ballot pick the unguarded columns or, when any lane has such
+// a limb, the exact ones.  BCC_MUL_PRECHECK=0 keeps round 5's flags.
+#ifndef BCC_MUL_PRECHECK
+#define BCC_MUL_PRECHECK 1
+#endif
+#if defined(__HIP_DEVICE_COMPILE__)
+__device__ __forceinline__ bool any_lane_top_limbs(u32 lo_limb, u32 hi_limb) {
+    return __builtin_amdgcn_ballot_w64((lo_limb > 0xFFFFFFF7u) | (hi_limb > 0xFFFFFFF7u)) != 0;
+}
 #endif
 
 #if !defined(__HIP_DEVICE_COMPILE__) && defined(__SIZEOF_INT128__)
@@ -266,7 +281,10 @@ BCC_HD void fe_mul(fe& r, const fe& a, const fe& b) {
 #else
     u32 t[16];
 #if defined(__HIP_DEVICE_COMPILE__)
-#if BCC_MUL_FLAG
+#if BCC_MUL_PRECHECK
+    if (__builtin_expect(any_lane_top_limbs(a.v[0], b.v[7]), 0)) mul_256x256_col(t, a.v, b.v);
+    else mul_256x256_col_u(t, a.v, b.v);
+#elif BCC_MUL_FLAG
     uint64_t ovf;
     mul_256x256_col_f(t, a.v, b.v, ovf);
     if (__builtin_expect(ovf != 0, 0)) mul_256x256_col(t, a.v, b.v);
@@ -287,7 +305,15 @@ BCC_HD void fe_sqr(fe& r, const fe& a) {
 #else
     u32 t[16];
 #if defined(__HIP_DEVICE_COMPILE__)
-#if BCC_MUL_FLAG
+#if BCC_MUL_PRECHECK
+    if (__builtin_expect(any_lane_top_limbs(a.v[0], a.v[7]), 0)) {
+        sqr_256_col(t, a.v);
+    } else {
+        u32 x[16];
+        sqr_cross_col_u(x, a.v);
+        sqr_tail_col(t, x, a.v);
+    }
+#elif BCC_MUL_FLAG
     uint64_t ovf;
     u32 x[16];
     sqr_cross_col_f(x, a.v, ovf);
