@@ -928,15 +928,22 @@ class SideLegs:
                                        for k in ("host_seconds", "gpu_seconds", "prepare_seconds",
                                                  "interpret_seconds", "stage_seconds", "rounds",
                                                  "tuples", "early_rows", "host_hashed")})
+        self._c3_ret = ret
         if cpu:
-            cb = cpu_baseline_script([job.wl.item(i) for i in range(job.n)],
-                                     f"C3 inputs (all {job.n})", gpu_verdicts=ret)
-            if cb:
-                cb.pop("host", None)
-                out["cpu_baseline"] = cb
-                out["gpu_vs_cpu"] = out["inputs_per_s"] / cb["value"]
-                out["gpu_verdict_mismatches_all_items"] = cb["gpu_verdict_mismatches"]
+            self.c3_cpu(out)
         return out
+
+    def c3_cpu(self, out):
+        """The C3 leg's 16-thread reference baseline over all its items, with per-item verdict
+        mismatches against the GPU's (measured separately from the leg's calls)."""
+        job = self.c3
+        cb = cpu_baseline_script([job.wl.item(i) for i in range(job.n)],
+                                 f"C3 inputs (all {job.n})", gpu_verdicts=self._c3_ret)
+        if cb:
+            cb.pop("host", None)
+            out["cpu_baseline"] = cb
+            out["gpu_vs_cpu"] = out["inputs_per_s"] / cb["value"]
+            out["gpu_verdict_mismatches_all_items"] = cb["gpu_verdict_mismatches"]
 
     def c4_leg(self, cpu=True):
         import numpy as np
@@ -1072,6 +1079,10 @@ def main():
         sustained = dict(steps=k, seconds=sus, value=job.units * world * k / sus,
                          ms_per_step=sus / k * 1e3)
 
+    # the C3 block-replay leg right after the timed region (before the 1M-input drop-in calls
+    # below reshape the calling thread's host state and the pinned images)
+    c3_leg = side.c3_leg(cpu=False) if side else None
+
     # the drop-in per rank (north star: the per-input verify_batch API at 1..8 GPUs): every rank
     # calls bitcoinconsensus_verify_batch on its own slice from host buffers at the same time,
     # barrier-bracketed, max over ranks; reported beside value (host pass + H2D included)
@@ -1172,7 +1183,9 @@ def main():
         if per_rank:
             out["drop_in_per_rank"] = per_rank
         if side:
-            out["c3_block_replay"] = side.c3_leg(cpu=not args.no_cpu)
+            if not args.no_cpu:
+                side.c3_cpu(c3_leg)
+            out["c3_block_replay"] = c3_leg
             if side.c4:
                 out["c4_pubkey_verify_batch"] = side.c4_leg(cpu=not args.no_cpu)
         out["source_hash"] = B.source_hash()
