@@ -1155,7 +1155,7 @@ def main():
             if k:
                 roof["cost_model"] = dict(
                     kernel=kname, cycle_share=k["cycle_share"],
-                    salu_per_verify=k.get("salu"),
+                    salu_per_verify=k.get("salu_per_wave"),
                     valu_per_verify=k["valu_per_wave"],
                     issue_cost_cycles=d["issue_cost_cycles_per_wave_instr"],
                     predicted_over_measured_cycles=k["predicted_over_measured"],

@@ -59,6 +59,7 @@ def main():
                                other=oth / waves if waves else None),
             valu_total=c["SQ_INSTS_VALU"], int64=i64, int32=i32, other=oth,
             salu=c.get("SQ_INSTS_SALU"), vmem_rd=c.get("SQ_INSTS_VMEM_RD"),
+            salu_per_wave=c.get("SQ_INSTS_SALU", 0) / waves if waves else None,
             predicted_simd_cycles=pred, measured_simd_cycles=meas, predicted_over_measured=pred / meas,
             cycle_share=dict(int64_mad=i64 * c_mad / simds / pred, int32=i32 * c_i32 / simds / pred,
                              other=oth * c_oth / simds / pred),
