@@ -144,6 +144,11 @@ int bcc_set_long_shards_per_worker(unsigned k);
  * BCC_FUSED_PASS; 0: two passes).  Calls with early Q halves keep two passes.  Results never
  * depend on it.  Returns 0. */
 int bcc_set_fused_pass(int on);
+/* A device round's tuple rows, raw transactions and sighash blobs are written by the host pass into
+ * page-locked memory and go to HBM from there, one copy per host shard and array; staging copies
+ * only the records whose offsets it rebases (default 1, or BCC_DIRECT_UPLOAD; 0: every array is
+ * copied into one pinned image first).  Results never depend on it.  Returns 0. */
+int bcc_set_direct_upload(int on);
 
 /* Legacy signature checks whose serial SHA-256 chain is longer than `blocks` 64-byte blocks (the
  * preimages of many-input transactions) are hashed on the host CPU instead of in one GPU lane each,

@@ -1954,7 +1954,7 @@ void append_round(SighashJobs& dst, TupleRows& drows, const SighashJobs& src,
     const uint32_t row0 = (uint32_t)drows.size();
     const uint32_t aux_blk0 = (uint32_t)(dst.aux.size() / 64), pre_blk0 = (uint32_t)(dst.pre.size() / 64);
     const uint32_t aux_idx0 = (uint32_t)dst.aux_off.size();
-    auto cat = [](std::vector<uint8_t>& a, const std::vector<uint8_t>& b) { a.insert(a.end(), b.begin(), b.end()); };
+    auto cat = [](auto& a, const auto& b) { a.insert(a.end(), b.begin(), b.end()); };
     cat(drows.tag, srows.tag);
     cat(drows.x, srows.x);
     cat(drows.y, srows.y);
@@ -2102,6 +2102,11 @@ int bcc_set_pipeline_chunk(size_t items) {
     return 0;
 }
 
+int bcc_set_direct_upload(int on) {
+    bcc::set_direct_upload(on != 0);
+    return 0;
+}
+
 int bcc_set_fused_pass(int on) {
     g_fused_pass.store(on != 0, std::memory_order_relaxed);
     return 0;
@@ -2136,6 +2141,7 @@ void bcc_release_thread_state(void) {
             bcc::host::release_team();
         });
     }
+    bcc::pinned_trim();  // the page-locked blocks no array holds any more
 }
 
 int bcc_set_device(int device) {

@@ -114,7 +114,7 @@ void host_sighash(const SighashJobs& j, uint8_t* msg) {
         sha256d(m, unpadded_len(m, (size_t)j.aux_nblk[a] * 64), &auxd[32 * a]);
     }
     if (!j.pre_off.empty()) {
-        std::vector<uint8_t> pre = j.pre;
+        std::vector<uint8_t> pre(j.pre.begin(), j.pre.end());
         for (const auto& p : j.patches) memcpy(&pre[p.pre_byte], &auxd[32 * p.aux], 32);
         for (size_t k = 0; k < j.pre_off.size(); k++) {
             const uint8_t* m = &pre[(size_t)j.pre_off[k] * 64];

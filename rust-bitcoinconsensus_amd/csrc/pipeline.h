@@ -15,6 +15,33 @@
 
 namespace bcc {
 
+// Page-locked host memory for the arrays a device round uploads as they are (round 6): the
+// interpreter writes the tuple rows, the raw txs and the sighash blobs straight into buffers the
+// DMA engine reads, so staging copies only the records whose offsets it rebases
+// (DeviceBatch::stage_parts).  Blocks come from a process-wide pool in power-of-two classes and go
+// back to it, never to the runtime while the process runs (a hipHostFree would wait for the GPU in
+// the middle of a host pass), except through pinned_trim().  Without a device the pool hands out
+// ordinary memory (sighash.hip; the CPU test build's stub uses malloc).
+void* pinned_alloc(size_t bytes);
+void pinned_free(void* p, size_t bytes) noexcept;
+void pinned_trim();
+template <class T>
+struct PinnedAlloc {
+    using value_type = T;
+    PinnedAlloc() = default;
+    template <class U>
+    PinnedAlloc(const PinnedAlloc<U>&) {}
+    T* allocate(size_t n) { return static_cast<T*>(pinned_alloc(n * sizeof(T))); }
+    void deallocate(T* p, size_t n) noexcept { pinned_free(p, n * sizeof(T)); }
+    template <class U>
+    bool operator==(const PinnedAlloc<U>&) const { return true; }
+    template <class U>
+    bool operator!=(const PinnedAlloc<U>&) const { return false; }
+};
+template <class T>
+using pinned_vector = std::vector<T, PinnedAlloc<T>>;
+using pinned_bytes = pinned_vector<uint8_t>;
+
 struct PatchRec {
     uint32_t pre_byte;  // absolute byte offset in the padded preimage buffer
     uint32_t aux;       // index of the aux message whose digest goes there
@@ -24,8 +51,8 @@ struct PatchRec {
 // `prefix` = bytes already absorbed into the starting midstate (a tagged hash's 64-byte tag
 // block): they count in the length field but are not part of m.
 inline size_t sha_padded_len(size_t n) { return ((n + 8) / 64 + 1) * 64; }
-inline void sha_append_padded(std::vector<uint8_t>& buf, const uint8_t* m, size_t n,
-                              size_t prefix = 0) {
+template <class Buf>
+inline void sha_append_padded(Buf& buf, const uint8_t* m, size_t n, size_t prefix = 0) {
     size_t L = sha_padded_len(n), base = buf.size();
     buf.resize(base + L, 0);
     if (n) memcpy(&buf[base], m, n);
@@ -84,7 +111,8 @@ BCC_PL_HD inline uint32_t tpl_job_blocks(const TplJob& j) {
 }
 // Appends T (4-aligned, + 8 zero bytes) and, when mid != nullptr, its tpl_mid_count(n) midstates
 // (8 words each) to a template blob; returns T's offset.
-inline uint32_t append_tpl(std::vector<uint8_t>& blob, const uint8_t* m, size_t n,
+template <class Buf>
+inline uint32_t append_tpl(Buf& blob, const uint8_t* m, size_t n,
                            const uint32_t* mid) {
     const uint32_t off = (uint32_t)blob.size();
     blob.insert(blob.end(), m, m + n);
@@ -123,14 +151,14 @@ struct WinJob {
 };
 
 struct SighashJobs {
-    std::vector<uint8_t> aux, pre;                  // padded messages, back to back
+    pinned_bytes aux, pre;                          // padded messages, back to back
     std::vector<uint32_t> aux_off, aux_nblk;        // offsets / lengths in 64-byte blocks
     std::vector<uint32_t> pre_off, pre_nblk, pre_row;
     std::vector<PatchRec> patches;
-    std::vector<uint8_t> tpl, code;                 // templates / code segments (4-aligned,
+    pinned_bytes tpl, code;                         // templates / code segments (4-aligned,
                                                     // templates followed by 8 zero bytes)
     std::vector<TplJob> tjobs;
-    std::vector<uint8_t> txraw;                     // raw txs of the WinJobs (4-aligned)
+    pinned_bytes txraw;                             // raw txs of the WinJobs (4-aligned)
     std::vector<WtxRec> wtx;
     std::vector<WinJob> wjobs;
     uint32_t win_entries = 0;                       // sum of WtxRec::n_in
@@ -215,7 +243,8 @@ struct SighashJobs {
 // ECDSA tuple rows (big-endian 32-byte values).  msg rows whose sighash comes from a preimage
 // are overwritten on the device by K3; constant ones (SIGHASH_SINGLE bug) are set by the host.
 struct TupleRows {
-    std::vector<uint8_t> tag, x, y, r, s, msg;
+    pinned_bytes tag, x, r, s;  // uploaded as they are (page-locked)
+    std::vector<uint8_t> y, msg;
     // Producers that know may set these so that staging skips uploading rows (default: upload):
     // msg_one = every msg row is uint256 ONE (the rows the GPU sighash kernels do not overwrite
     // keep it; the device initialises the msg rows itself), y_unused = no 65-byte key (the y
@@ -225,7 +254,7 @@ struct TupleRows {
     // device, engine.cpp DeferringChecker::defer_key_hash): row hrow[k] is valid only if
     // HASH160(its key) == hprog[20k, 20k + 20); the device ANDs that into the row's verdict.
     std::vector<uint32_t> hrow;
-    std::vector<uint8_t> hprog;
+    pinned_bytes hprog;
     // Early Q halves (round 5, DeviceBatch::early_launch): emap[row] = the lane of the call's early
     // set whose (key, signature) bytes equal this row's, whose key half and Q ladder already ran
     // (K_keyq copies it instead of recomputing); rows past emap.size() or holding NO_EARLY have none.
@@ -507,7 +536,10 @@ public:
     ~DeviceBatch();
     int stage(const SighashJobs& jobs, const TupleRows& rows);
     // the concatenation of P parts (row / message / job indices fixed up per part)
-    int stage_parts(const SighashJobs* const* jobs, const TupleRows* const* rows, size_t P);
+    // direct: the parts' page-locked arrays go up as they are (set_direct_upload), so they must
+    // stay unchanged until the round has run; false copies everything into the pinned image
+    int stage_parts(const SighashJobs* const* jobs, const TupleRows* const* rows, size_t P,
+                    bool direct = false);
     // raw tuples (DerTuples): blobs, offsets and messages staged; run() starts with K_der
     int stage_der(const DerTuples& t);
     int run(void* stream, const LateMsgFill* late = nullptr);  // K1..K4
@@ -537,7 +569,14 @@ private:
     int launch_front(struct ihipStream_t* st);        // K_wtx + K3' + K1 fused, then the rest
     int upload_on(struct ihipStream_t* rows_stream, struct ihipStream_t* rest_stream);
     bool up_pending_ = false;      // the staged image is not on the device yet (issued by run)
-    size_t up_rows_ = 0, up_total_ = 0;
+    struct UpCopy {  // one host -> HBM copy of the pending upload
+        size_t dst;      // arena offset
+        const void* src; // the pinned image or a part's own page-locked array
+        size_t len;
+        bool rows;       // a tuple-row region (the ECDSA stream's) or a sighash input
+    };
+    std::vector<UpCopy> up_copies_;
+    bool up_msg_one_ = false;      // the msg rows are set to ONE with the upload
     int launch_after_front(struct ihipStream_t* st);  // K_win, K2, K3
     int launch_key_hash(struct ihipStream_t* st);     // K_h160: key-hash conditions into the verdicts
     int run_stages(void* stream, const LateMsgFill* late);
@@ -635,6 +674,13 @@ void gpu_early_reset(int device);
 // throttled for the rest of the quota period.
 void set_stage_threads(unsigned n);
 
+// Direct upload (round 6, default on; bcc_set_direct_upload, BCC_DIRECT_UPLOAD=0 turns it off):
+// DeviceBatch::stage_parts sends the parts' page-locked arrays (tuple rows, raw txs, sighash
+// blobs, key-hash programs) to HBM as they are, one copy per part and array, and fills the pinned
+// image only with the records it rebases.  Off: every array is copied into the image first.
+void set_direct_upload(bool on);
+bool direct_upload();
+
 // Free the calling thread's cached device state: the verify_batch / Taproot device batches and
 // contexts (sighash.hip) and the tuple-path contexts (ecdsa_verify.hip).
 void release_device_thread_state();
@@ -651,7 +697,8 @@ int gpu_verify_batch(int device, const SighashJobs& jobs, const TupleRows& rows,
 struct StagedRound;
 StagedRound* gpu_staged_new(int device);
 void gpu_staged_free(StagedRound* s);
-// Fills s's pinned image from the parts (which must stay unchanged until gpu_staged_run returns).
+// Fills s's pinned image from the parts, which must stay unchanged until gpu_staged_run /
+// gpu_staged_finish returns: with direct upload the launch's copies read their arrays.
 int gpu_staged_stage(StagedRound* s, const SighashJobs* const* jobs, const TupleRows* const* rows,
                      size_t parts, double* stage_seconds);
 // Fills s's pinned image with raw tuples (DeviceBatch::stage_der; the caller's buffers are copied).

@@ -4,8 +4,12 @@
 //   K3 sha256d_msgs   preimages -> sighash, written straight into the ECDSA tuple msg rows
 // Integer-ALU bound (~2k VALU ops per 64-byte block); HBM traffic per launch is reported by
 // bench.py as the algorithmic bytes (message bytes in + 32 B out per message).
+#include <atomic>
 #include <chrono>
+#include <cstdlib>
 #include <memory>
+#include <mutex>
+#include <new>
 #include <thread>
 #include <vector>
 #include <cstring>
@@ -1076,6 +1080,80 @@ int DeviceBatch::sync() {
 thread_local unsigned tl_stage_threads = 0;
 void set_stage_threads(unsigned n) { tl_stage_threads = n; }
 
+static std::atomic<bool> g_direct_upload{[] {
+    const char* e = getenv("BCC_DIRECT_UPLOAD");
+    return !(e && atoi(e) == 0);
+}()};
+void set_direct_upload(bool on) { g_direct_upload.store(on, std::memory_order_relaxed); }
+bool direct_upload() { return g_direct_upload.load(std::memory_order_relaxed); }
+
+// The page-locked pool (pipeline.h, pinned_alloc): free lists per power-of-two class from 4 KiB,
+// under one mutex; the pool object is never destroyed (thread-exit destructors of cached
+// TupleRows may return blocks after static destruction began).  A block the runtime refused to
+// pin (no device) is ordinary memory, remembered so that it is freed as such.
+namespace {
+struct PinPool {
+    std::mutex mu;
+    std::vector<void*> free_[64];
+    std::vector<void*> pageable;
+};
+PinPool& pin_pool() {
+    static PinPool* p = new PinPool;
+    return *p;
+}
+int pin_class(size_t bytes) {
+    int k = 12;
+    while (((size_t)1 << k) < bytes) k++;
+    return k;
+}
+}  // namespace
+void* pinned_alloc(size_t bytes) {
+    const int k = pin_class(bytes ? bytes : 1);
+    PinPool& pp = pin_pool();
+    {
+        std::lock_guard<std::mutex> g(pp.mu);
+        if (!pp.free_[k].empty()) {
+            void* q = pp.free_[k].back();
+            pp.free_[k].pop_back();
+            return q;
+        }
+    }
+    void* q = nullptr;
+    if (hipHostMalloc(&q, (size_t)1 << k, hipHostMallocDefault) == hipSuccess && q) return q;
+    (void)hipGetLastError();
+    q = aligned_alloc(4096, (size_t)1 << k);
+    if (!q) throw std::bad_alloc();
+    std::lock_guard<std::mutex> g(pp.mu);
+    pp.pageable.push_back(q);
+    return q;
+}
+void pinned_free(void* q, size_t bytes) noexcept {
+    if (!q) return;
+    PinPool& pp = pin_pool();
+    std::lock_guard<std::mutex> g(pp.mu);
+    try {
+        pp.free_[pin_class(bytes ? bytes : 1)].push_back(q);
+    } catch (...) {  // out of memory for the list itself: keep the block
+    }
+}
+void pinned_trim() {
+    PinPool& pp = pin_pool();
+    std::lock_guard<std::mutex> g(pp.mu);
+    for (auto& l : pp.free_) {
+        for (void* q : l) {
+            auto it = std::find(pp.pageable.begin(), pp.pageable.end(), q);
+            if (it != pp.pageable.end()) {
+                pp.pageable.erase(it);
+                free(q);
+            } else {
+                (void)hipHostFree(q);
+            }
+        }
+        l.clear();
+        l.shrink_to_fit();
+    }
+}
+
 static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 int DeviceBatch::stage(const SighashJobs& j, const TupleRows& rows) {
@@ -1088,7 +1166,8 @@ int DeviceBatch::stage(const SighashJobs& j, const TupleRows& rows) {
 // host image of the device arena, each part by its own thread with its index fix-ups (the
 // append_round rules), then the image goes to HBM in one DMA copy: no merged host copy of the
 // jobs and no pageable-memory staging.
-int DeviceBatch::stage_parts(const SighashJobs* const* J, const TupleRows* const* Rw, size_t P) {
+int DeviceBatch::stage_parts(const SighashJobs* const* J, const TupleRows* const* Rw, size_t P,
+                             bool direct_arg) {
     if (int e = sync()) return e;  // the previous run may still read the arena / the image
     n_der_ = 0;
     std::vector<size_t> row0(P + 1, 0), auxb0(P + 1, 0), preb0(P + 1, 0), auxi0(P + 1, 0),
@@ -1200,6 +1279,7 @@ int DeviceBatch::stage_parts(const SighashJobs* const* J, const TupleRows* const
     d_mmap_ = need_mm ? (uint32_t*)(a + off[MMAP]) : nullptr;
     uint8_t* h = (uint8_t*)host_image_;
     memset(h + off[ZEROS], 0, 64);
+    const bool direct = direct_arg && direct_upload();
     // the rows of part p in [lo, hi): the bulk of a tuple batch, copied in blocks by the team
     auto fill_rows = [&](size_t p, size_t lo, size_t hi) {
         const TupleRows& rw = *Rw[p];
@@ -1207,11 +1287,13 @@ int DeviceBatch::stage_parts(const SighashJobs* const* J, const TupleRows* const
         auto cp = [&](int b, size_t at, const void* src, size_t len) {
             if (len) memcpy(h + off[b] + at, src, len);
         };
-        cp(TAG, r0, rw.tag.data() + lo, nr);
-        cp(X, 32 * r0, rw.x.data() + 32 * lo, 32 * nr);
+        if (!direct) {
+            cp(TAG, r0, rw.tag.data() + lo, nr);
+            cp(X, 32 * r0, rw.x.data() + 32 * lo, 32 * nr);
+            cp(RR, 32 * r0, rw.r.data() + 32 * lo, 32 * nr);
+            cp(S, 32 * r0, rw.s.data() + 32 * lo, 32 * nr);
+        }
         if (need_y && nr) rw.copy_y(h + off[Y] + 32 * r0, lo, hi);  // past the stored prefix: zero
-        cp(RR, 32 * r0, rw.r.data() + 32 * lo, 32 * nr);
-        cp(S, 32 * r0, rw.s.data() + 32 * lo, 32 * nr);
         if (need_m && nr) rw.copy_msg(h + off[M] + 32 * r0, lo, hi);  // past the stored prefix: ONE
         if (need_e && nr) rw.copy_emap((uint32_t*)(h + off[EMAP]) + r0, lo, hi);
         if (need_mm && nr) rw.copy_mmap((uint32_t*)(h + off[MMAP]) + r0, lo, hi);
@@ -1224,8 +1306,14 @@ int DeviceBatch::stage_parts(const SighashJobs* const* J, const TupleRows* const
         auto cp = [&](int b, size_t at, const void* src, size_t len) {
             if (len) memcpy(h + off[b] + at, src, len);
         };
-        cp(AUX, auxb0[p], j.aux.data(), j.aux.size());
-        cp(PRE, preb0[p], j.pre.data(), j.pre.size());
+        if (!direct) {
+            cp(AUX, auxb0[p], j.aux.data(), j.aux.size());
+            cp(PRE, preb0[p], j.pre.data(), j.pre.size());
+            cp(TPL, tpl0[p], j.tpl.data(), j.tpl.size());
+            cp(CODE, code0[p], j.code.data(), j.code.size());
+            cp(TXRAW, raw0[p], j.txraw.data(), j.txraw.size());
+            cp(HPROG, 20 * h0[p], rw.hprog.data(), rw.hprog.size());
+        }
         const uint32_t ablk = (uint32_t)(auxb0[p] / 64), pblk = (uint32_t)(preb0[p] / 64);
         uint32_t* ao = (uint32_t*)(h + off[AUX_OFF]) + auxi0[p];
         for (size_t k = 0; k < j.aux_off.size(); k++) ao[k] = j.aux_off[k] + ablk;
@@ -1240,8 +1328,6 @@ int DeviceBatch::stage_parts(const SighashJobs* const* J, const TupleRows* const
         PatchRec* pt = (PatchRec*)(h + off[PATCH]) + pat0[p];
         for (size_t k = 0; k < j.patches.size(); k++)
             pt[k] = PatchRec{j.patches[k].pre_byte + pblk * 64, j.patches[k].aux + (uint32_t)auxi0[p]};
-        cp(TPL, tpl0[p], j.tpl.data(), j.tpl.size());
-        cp(CODE, code0[p], j.code.data(), j.code.size());
         TplJob* tj = (TplJob*)(h + off[TJOB]) + tj0[p];
         for (size_t k = 0; k < j.tjobs.size(); k++) {
             TplJob t = j.tjobs[k];
@@ -1251,7 +1337,6 @@ int DeviceBatch::stage_parts(const SighashJobs* const* J, const TupleRows* const
             if (!need_mm) t.nblk &= ~TPL_EARLY;  // no early digests for this round: hash it here
             tj[k] = t;
         }
-        cp(TXRAW, raw0[p], j.txraw.data(), j.txraw.size());
         WtxRec* wr = (WtxRec*)(h + off[WTX]) + wtx0[p];
         for (size_t k = 0; k < j.wtx.size(); k++) {
             WtxRec t = j.wtx[k];
@@ -1269,7 +1354,6 @@ int DeviceBatch::stage_parts(const SighashJobs* const* J, const TupleRows* const
         }
         uint32_t* hr = (uint32_t*)(h + off[HROW]) + h0[p];
         for (size_t k = 0; k < rw.hrow.size(); k++) hr[k] = rw.hrow[k] + (uint32_t)r0;
-        cp(HPROG, 20 * h0[p], rw.hprog.data(), rw.hprog.size());
     };
     // work items: blocks of <= 64k rows of every part, then every part's jobs
     struct Work {
@@ -1277,9 +1361,10 @@ int DeviceBatch::stage_parts(const SighashJobs* const* J, const TupleRows* const
     };
     std::vector<Work> work;
     constexpr size_t RB = (size_t)1 << 16;
-    for (size_t p = 0; p < P; p++)
-        for (size_t lo = 0, nr = Rw[p]->size(); lo < nr; lo += RB)
-            work.push_back(Work{p, lo, std::min(nr, lo + RB)});
+    if (!direct || need_y || need_m || need_e || need_mm)
+        for (size_t p = 0; p < P; p++)
+            for (size_t lo = 0, nr = Rw[p]->size(); lo < nr; lo += RB)
+                work.push_back(Work{p, lo, std::min(nr, lo + RB)});
     for (size_t p = 0; p < P; p++) work.push_back(Work{p, 0, 0});
     auto run_work = [&](const Work& w) {
         if (w.hi) fill_rows(w.p, w.lo, w.hi);
@@ -1299,18 +1384,45 @@ int DeviceBatch::stage_parts(const SighashJobs* const* J, const TupleRows* const
     // (upload_on): the tuple rows on the side stream ahead of K_inv / K_tkey / the Q ladder, the
     // sighash inputs on the main stream ahead of the front kernel
     up_pending_ = true;
-    up_rows_ = off[AUX];
-    up_total_ = upload;
-    if (need_y) BCC_HIP_TRY(hipMemcpy(a + off[Y], h + off[Y], 32 * R, hipMemcpyHostToDevice));
-    if (need_m) {
-        BCC_HIP_TRY(hipMemcpy(a + off[M], h + off[M], 32 * R, hipMemcpyHostToDevice));
-    } else if (R) {  // every row's msg is uint256 ONE (byte 0 = 1); the sighash kernels overwrite theirs
-        BCC_HIP_TRY(hipMemset(a + off[M], 0, 32 * R));
-        BCC_HIP_TRY(hipMemset2D(a + off[M], 32, 1, 1, R));
-        // device memsets are asynchronous on the null stream, which the batch's non-blocking run
-        // streams do not wait for: finish them before any run can write the rows
-        BCC_HIP_TRY(hipStreamSynchronize(nullptr));
+    up_copies_.clear();
+    if (!direct) {
+        up_copies_.push_back(UpCopy{0, h, off[AUX], true});
+        up_copies_.push_back(UpCopy{off[AUX], h + off[AUX], upload - off[AUX], false});
+    } else {
+        // the image's spans of rebased records, then each part's own arrays where they belong
+        auto span = [&](int b0, int b1, bool rows) {
+            if (off[b1] > off[b0]) up_copies_.push_back(UpCopy{off[b0], h + off[b0], off[b1] - off[b0], rows});
+        };
+        span(EMAP, AUX, true);
+        span(AUX_OFF, TPL, false);
+        span(TJOB, TXRAW, false);
+        span(WTX, HPROG, false);
+        span(ZEROS, UPLOADED, false);
+        auto part = [&](int b, size_t at, const void* src, size_t len, bool rows) {
+            if (len) up_copies_.push_back(UpCopy{off[b] + at, src, len, rows});
+        };
+        for (size_t p = 0; p < P; p++) {
+            const TupleRows& rw = *Rw[p];
+            const SighashJobs& j = *J[p];
+            const size_t nr = rw.size();
+            part(TAG, row0[p], rw.tag.data(), nr, true);
+            part(X, 32 * row0[p], rw.x.data(), 32 * nr, true);
+            part(RR, 32 * row0[p], rw.r.data(), 32 * nr, true);
+            part(S, 32 * row0[p], rw.s.data(), 32 * nr, true);
+            part(AUX, auxb0[p], j.aux.data(), j.aux.size(), false);
+            part(PRE, preb0[p], j.pre.data(), j.pre.size(), false);
+            part(TPL, tpl0[p], j.tpl.data(), j.tpl.size(), false);
+            part(CODE, code0[p], j.code.data(), j.code.size(), false);
+            part(TXRAW, raw0[p], j.txraw.data(), j.txraw.size(), false);
+            part(HPROG, 20 * h0[p], rw.hprog.data(), rw.hprog.size(), false);
+        }
     }
+    if (need_y) BCC_HIP_TRY(hipMemcpy(a + off[Y], h + off[Y], 32 * R, hipMemcpyHostToDevice));
+    // every row's msg is uint256 ONE (byte 0 = 1) unless a part stores its own; the sighash kernels
+    // overwrite theirs.  Set with the upload, on the stream of the kernels that write the rows
+    // (upload_on), so that staging never waits for the GPU.
+    up_msg_one_ = !need_m && R;
+    if (need_m) BCC_HIP_TRY(hipMemcpy(a + off[M], h + off[M], 32 * R, hipMemcpyHostToDevice));
     return ensure_vbuf();
 }
 
@@ -1385,7 +1497,8 @@ int DeviceBatch::stage_der(const DerTuples& t) {
     }
     BCC_HIP_TRY(hipSetDevice(dev_));
     up_pending_ = true;
-    up_rows_ = up_total_ = upload;
+    up_msg_one_ = false;
+    up_copies_.assign(1, UpCopy{0, host_image_, upload, true});
     n_der_ = R;
     pub_base_ = t.pub_off[0];
     pub_bytes_ = pb;
@@ -1401,15 +1514,15 @@ int DeviceBatch::upload_on(hipStream_t rows_stream, hipStream_t rest_stream) {
     if (!up_pending_) return 0;
     up_pending_ = false;
     uint8_t* a = (uint8_t*)arena_;
-    const uint8_t* h = (const uint8_t*)host_image_;
-    if (!rest_stream) {
-        BCC_HIP_TRY(hipMemcpyAsync(a, h, up_total_, hipMemcpyHostToDevice, rows_stream));
-        return 0;
+    for (const UpCopy& c : up_copies_)
+        BCC_HIP_TRY(hipMemcpyAsync(a + c.dst, c.src, c.len, hipMemcpyHostToDevice,
+                                   c.rows || !rest_stream ? rows_stream : rest_stream));
+    if (up_msg_one_) {
+        up_msg_one_ = false;
+        hipStream_t ms = rest_stream ? rest_stream : rows_stream;
+        BCC_HIP_TRY(hipMemsetAsync(d_m, 0, 32 * n_rows_, ms));
+        BCC_HIP_TRY(hipMemset2DAsync(d_m, 32, 1, 1, n_rows_, ms));
     }
-    BCC_HIP_TRY(hipMemcpyAsync(a, h, up_rows_, hipMemcpyHostToDevice, rows_stream));
-    if (up_total_ > up_rows_)
-        BCC_HIP_TRY(hipMemcpyAsync(a + up_rows_, h + up_rows_, up_total_ - up_rows_,
-                                   hipMemcpyHostToDevice, rest_stream));
     return 0;
 }
 
@@ -1755,7 +1868,7 @@ int gpu_verify_parts(int device, const SighashJobs* const* jobs, const TupleRows
     if (!cache[device]) cache[device] = std::make_unique<DeviceBatch>(device);
     DeviceBatch& b = *cache[device];
     auto t0 = std::chrono::steady_clock::now();
-    int e = b.stage_parts(jobs, rows, parts);
+    int e = b.stage_parts(jobs, rows, parts, true);  // the parts outlive this synchronous round
     if (!e && stage_seconds)
         *stage_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     if (!e) e = b.run(nullptr, late);
@@ -1790,7 +1903,7 @@ int gpu_staged_stage(StagedRound* s, const SighashJobs* const* jobs, const Tuple
     BCC_HIP_TRY(hipSetDevice(s->dev));
     if (!s->b) s->b = std::make_unique<DeviceBatch>(s->dev);
     auto t0 = std::chrono::steady_clock::now();
-    int e = s->b->stage_parts(jobs, rows, parts);
+    int e = s->b->stage_parts(jobs, rows, parts, true);  // held until gpu_staged_finish (pipeline.h)
     if (!e && stage_seconds)
         *stage_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     if (e) s->b.reset();

@@ -8,6 +8,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <new>
 #include <vector>
 
 #include "../../oracle/bcc_oracle.h"
@@ -26,6 +27,16 @@ static size_t unpadded_len(const uint8_t* m, size_t padded) {
 static void stub_sighash(const SighashJobs& j, std::vector<uint8_t>& msg);
 static void stub_ecdsa(const TupleRows& rows, const uint8_t* msg, uint8_t* verdict);
 void set_stage_threads(unsigned) {}  // the device batch is stubbed out
+static bool stub_direct = true;
+void set_direct_upload(bool on) { stub_direct = on; }
+bool direct_upload() { return stub_direct; }
+void* pinned_alloc(size_t bytes) {  // ordinary memory: nothing is uploaded here
+    void* p = malloc(bytes ? bytes : 1);
+    if (!p) throw std::bad_alloc();
+    return p;
+}
+void pinned_free(void* p, size_t) noexcept { free(p); }
+void pinned_trim() {}
 void release_device_thread_state() {}
 void release_tuple_thread_state() {}
 // Early Q halves: the stub keeps the calling thread's early rows and checks that every row the
@@ -190,7 +201,7 @@ static void stub_sighash(const SighashJobs& j, std::vector<uint8_t>& msg) {
         size_t L = (size_t)j.aux_nblk[a] * 64;
         bcco_sha256d(m, unpadded_len(m, L), &auxd[32 * a]);
     }
-    std::vector<uint8_t> pre = j.pre;
+    std::vector<uint8_t> pre(j.pre.begin(), j.pre.end());
     for (const auto& p : j.patches) memcpy(&pre[p.pre_byte], &auxd[32 * p.aux], 32);
     for (size_t k = 0; k < j.pre_off.size(); k++) {
         const uint8_t* m = &pre[(size_t)j.pre_off[k] * 64];
