@@ -1173,7 +1173,6 @@ int DeviceBatch::stage_parts(const SighashJobs* const* J, const TupleRows* const
     std::vector<size_t> row0(P + 1, 0), auxb0(P + 1, 0), preb0(P + 1, 0), auxi0(P + 1, 0),
         prei0(P + 1, 0), pat0(P + 1, 0), tpl0(P + 1, 0), code0(P + 1, 0), tj0(P + 1, 0),
         raw0(P + 1, 0), wtx0(P + 1, 0), wj0(P + 1, 0), win0(P + 1, 0), h0(P + 1, 0);
-    size_t tjblk = 0;
     for (size_t p = 0; p < P; p++) {
         row0[p + 1] = row0[p] + Rw[p]->size();
         auxb0[p + 1] = auxb0[p] + J[p]->aux.size();
@@ -1189,8 +1188,10 @@ int DeviceBatch::stage_parts(const SighashJobs* const* J, const TupleRows* const
         wj0[p + 1] = wj0[p] + J[p]->wjobs.size();
         win0[p + 1] = win0[p] + J[p]->win_entries;
         h0[p + 1] = h0[p] + Rw[p]->hrow.size();
-        for (const auto& t : J[p]->tjobs) tjblk += tpl_job_blocks(t);
     }
+    // per part, summed by the fill below (one pass over the records, in parallel): the template
+    // jobs' blocks and the BIP143 inputs' algorithmic bytes (bcc_workload_sighash_bytes)
+    std::vector<size_t> part_tjblk(P, 0), part_wbytes(P, 0);
     const size_t LIM = (size_t)1 << 32;
     if (auxb0[P] >= LIM || preb0[P] >= LIM || tpl0[P] >= LIM || code0[P] >= LIM ||
         raw0[P] >= LIM || row0[P] >= LIM || win0[P] >= LIM / 2) {
@@ -1205,16 +1206,11 @@ int DeviceBatch::stage_parts(const SighashJobs* const* J, const TupleRows* const
     pre_blocks_ = preb0[P] / 64;
     aux_blocks_ = auxb0[P] / 64;
     n_tjob_ = tj0[P];
-    tjob_blocks_ = tjblk;
+
     n_wtx_ = wtx0[P];
     n_wjob_ = wj0[P];
     n_win_ = win0[P];
     n_hash_ = h0[P];
-    sighash_bytes_ = 64 * (pre_blocks_ + aux_blocks_ + tjob_blocks_) + 32 * (n_pre_ + n_aux_ + n_tjob_);
-    for (size_t p = 0; p < P; p++) {
-        for (const WtxRec& r : J[p]->wtx) sighash_bytes_ += r.tx_len + 96;
-        for (const WinJob& w : J[p]->wjobs) sighash_bytes_ += w.code_len + sizeof(WinJob) + 32;
-    }
     const size_t R = n_rows_;
     // regions filled from the host image first (one copy), device-written ones after them
     // Y and M go up only when some part needs them (TupleRows::y_unused / msg_one)
@@ -1329,8 +1325,10 @@ int DeviceBatch::stage_parts(const SighashJobs* const* J, const TupleRows* const
         for (size_t k = 0; k < j.patches.size(); k++)
             pt[k] = PatchRec{j.patches[k].pre_byte + pblk * 64, j.patches[k].aux + (uint32_t)auxi0[p]};
         TplJob* tj = (TplJob*)(h + off[TJOB]) + tj0[p];
+        size_t wb = 0, tb = 0;
         for (size_t k = 0; k < j.tjobs.size(); k++) {
             TplJob t = j.tjobs[k];
+            tb += tpl_job_blocks(t);
             t.tpl_off += (uint32_t)tpl0[p];
             t.code_off += (uint32_t)code0[p];
             t.row += (uint32_t)r0;
@@ -1340,6 +1338,7 @@ int DeviceBatch::stage_parts(const SighashJobs* const* J, const TupleRows* const
         WtxRec* wr = (WtxRec*)(h + off[WTX]) + wtx0[p];
         for (size_t k = 0; k < j.wtx.size(); k++) {
             WtxRec t = j.wtx[k];
+            wb += t.tx_len + 96;
             t.tx_off += (uint32_t)raw0[p];
             t.in_base += (uint32_t)win0[p];
             wr[k] = t;
@@ -1347,6 +1346,7 @@ int DeviceBatch::stage_parts(const SighashJobs* const* J, const TupleRows* const
         WinJob* wj = (WinJob*)(h + off[WJOB]) + wj0[p];
         for (size_t k = 0; k < j.wjobs.size(); k++) {
             WinJob t = j.wjobs[k];
+            wb += t.code_len + sizeof(WinJob) + 32;
             t.tx += (uint32_t)wtx0[p];
             t.code_off += (uint32_t)code0[p];
             t.row += (uint32_t)r0;
@@ -1354,6 +1354,8 @@ int DeviceBatch::stage_parts(const SighashJobs* const* J, const TupleRows* const
         }
         uint32_t* hr = (uint32_t*)(h + off[HROW]) + h0[p];
         for (size_t k = 0; k < rw.hrow.size(); k++) hr[k] = rw.hrow[k] + (uint32_t)r0;
+        part_tjblk[p] = tb;
+        part_wbytes[p] = wb;
     };
     // work items: blocks of <= 64k rows of every part, then every part's jobs
     struct Work {
@@ -1379,6 +1381,13 @@ int DeviceBatch::stage_parts(const SighashJobs* const* J, const TupleRows* const
             for (size_t k = t; k < work.size(); k += nth) run_work(work[k]);
         });
     }
+    tjob_blocks_ = 0;
+    sighash_bytes_ = 0;
+    for (size_t p = 0; p < P; p++) {
+        tjob_blocks_ += part_tjblk[p];
+        sighash_bytes_ += part_wbytes[p];
+    }
+    sighash_bytes_ += 64 * (pre_blocks_ + aux_blocks_ + tjob_blocks_) + 32 * (n_pre_ + n_aux_ + n_tjob_);
     BCC_HIP_TRY(hipSetDevice(dev_));
     // the copy is issued by the next run, in two parts on the two streams that need them first
     // (upload_on): the tuple rows on the side stream ahead of K_inv / K_tkey / the Q ladder, the
