@@ -524,6 +524,15 @@ def set_device_key_hash(on):
     L.bcc_set_device_key_hash(1 if on else 0)
 
 
+def set_direct_upload(on):
+    """bcc_set_direct_upload: a device round's tuple rows, raw txs and sighash blobs go to HBM
+    from the page-locked arrays the host pass wrote (default on); off: through one pinned image.
+    Results never depend on it."""
+    L = lib()
+    L.bcc_set_direct_upload.argtypes = [ctypes.c_int]
+    L.bcc_set_direct_upload(1 if on else 0)
+
+
 def set_pipeline_chunk(items):
     """bcc_set_pipeline_chunk: verify_batch overlaps chunk k's device round with chunk k+1's host
     pass (0 disables)."""

@@ -299,7 +299,7 @@ int gpu_taproot_verify(int, const TaprootJobs& j, uint8_t* verdict, uint8_t* msg
         const uint8_t* m = &j.aux[(size_t)j.aux_off[a] * 64];
         bcco_sha256(m, unpadded_len(m, (size_t)j.aux_nblk[a] * 64), &auxd[32 * a]);
     }
-    std::vector<uint8_t> msgs = j.msg;
+    std::vector<uint8_t> msgs(j.msg.begin(), j.msg.end());
     for (const auto& p : j.patches) memcpy(&msgs[p.pre_byte], &auxd[32 * p.aux], 32);
     uint8_t tag[32];
     bcco_sha256(reinterpret_cast<const uint8_t*>("TapSighash"), 10, tag);

@@ -151,3 +151,31 @@ def test_c2_staged_mutated_matches_reference(wl):
     bad = [i for i in range(N) if got[i] != exp[i]]
     assert not bad, [(i, kinds.get(i), got[i], exp[i]) for i in bad[:10]]
     assert sum(r for r, _ in exp) < N - len(kinds) // 2
+
+
+def test_c2_mutated_drop_in_upload_modes_and_pipelined_chunks(wl):
+    """The drop-in's host -> HBM paths give the reference's (ret, err) on every item: the direct
+    upload from the host pass's page-locked arrays (default) and the pinned-image upload, each
+    in one round and in pipelined chunks (chunk 64k: the caller stages every chunk's round while
+    the worker runs the previous one, so the direct copies read arrays the next chunk must not
+    touch)."""
+    import bitcoinconsensus_amd as B
+    R = Reference()
+    rng = random.Random(0xD1)
+    n = 200_000
+    items = []
+    for i in range(n):
+        it = wl.item(i)
+        items.append(mutate(rng, it)[:4] if rng.random() < 0.10 else it)
+    exp, _ = R.bulk_verify_script(items, B.VERIFY_ALL)
+    try:
+        for chunk in (0, 64_000):
+            B.set_pipeline_chunk(chunk)
+            for direct in (True, False, True):
+                B.set_direct_upload(direct)
+                got = [(r, int(e)) for r, e in B.verify_batch(items)]
+                bad = [i for i in range(n) if got[i] != exp[i]]
+                assert not bad, (chunk, direct, [(i, got[i], exp[i]) for i in bad[:10]])
+    finally:
+        B.set_direct_upload(True)
+        B.set_pipeline_chunk(500_000)
