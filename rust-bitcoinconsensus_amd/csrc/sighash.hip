@@ -1275,7 +1275,18 @@ int DeviceBatch::stage_parts(const SighashJobs* const* J, const TupleRows* const
     d_mmap_ = need_mm ? (uint32_t*)(a + off[MMAP]) : nullptr;
     uint8_t* h = (uint8_t*)host_image_;
     memset(h + off[ZEROS], 0, 64);
-    const bool direct = direct_arg && direct_upload();
+    // Per array, direct upload from the parts' page-locked arrays only in rounds of at least 64k
+    // rows and when the array's pieces are large:
+    // each piece is its own copy, and a copy costs a few microseconds on the issuing thread, while
+    // the team fills the image at several GB/s per thread (a 13k-input C3 round and the 65,536-check
+    // Taproot rounds measured slower direct, 1M C2 inputs faster: profiles/r06/ab/dropin_direct_*,
+    // c3_direct_upload.txt).  Small arrays go through the image, uploaded as one span.
+    constexpr size_t DIRECT_MIN_PIECE = (size_t)256 << 10, DIRECT_MIN_ROWS = 65536;
+    bool dm[NB] = {};
+    if (direct_arg && direct_upload() && P && R >= DIRECT_MIN_ROWS) {
+        for (int b : {TAG, X, RR, S, AUX, PRE, TPL, CODE, TXRAW, HPROG})
+            dm[b] = sizes[b] / P >= DIRECT_MIN_PIECE;
+    }
     // the rows of part p in [lo, hi): the bulk of a tuple batch, copied in blocks by the team
     auto fill_rows = [&](size_t p, size_t lo, size_t hi) {
         const TupleRows& rw = *Rw[p];
@@ -1283,12 +1294,10 @@ int DeviceBatch::stage_parts(const SighashJobs* const* J, const TupleRows* const
         auto cp = [&](int b, size_t at, const void* src, size_t len) {
             if (len) memcpy(h + off[b] + at, src, len);
         };
-        if (!direct) {
-            cp(TAG, r0, rw.tag.data() + lo, nr);
-            cp(X, 32 * r0, rw.x.data() + 32 * lo, 32 * nr);
-            cp(RR, 32 * r0, rw.r.data() + 32 * lo, 32 * nr);
-            cp(S, 32 * r0, rw.s.data() + 32 * lo, 32 * nr);
-        }
+        if (!dm[TAG]) cp(TAG, r0, rw.tag.data() + lo, nr);
+        if (!dm[X]) cp(X, 32 * r0, rw.x.data() + 32 * lo, 32 * nr);
+        if (!dm[RR]) cp(RR, 32 * r0, rw.r.data() + 32 * lo, 32 * nr);
+        if (!dm[S]) cp(S, 32 * r0, rw.s.data() + 32 * lo, 32 * nr);
         if (need_y && nr) rw.copy_y(h + off[Y] + 32 * r0, lo, hi);  // past the stored prefix: zero
         if (need_m && nr) rw.copy_msg(h + off[M] + 32 * r0, lo, hi);  // past the stored prefix: ONE
         if (need_e && nr) rw.copy_emap((uint32_t*)(h + off[EMAP]) + r0, lo, hi);
@@ -1302,14 +1311,12 @@ int DeviceBatch::stage_parts(const SighashJobs* const* J, const TupleRows* const
         auto cp = [&](int b, size_t at, const void* src, size_t len) {
             if (len) memcpy(h + off[b] + at, src, len);
         };
-        if (!direct) {
-            cp(AUX, auxb0[p], j.aux.data(), j.aux.size());
-            cp(PRE, preb0[p], j.pre.data(), j.pre.size());
-            cp(TPL, tpl0[p], j.tpl.data(), j.tpl.size());
-            cp(CODE, code0[p], j.code.data(), j.code.size());
-            cp(TXRAW, raw0[p], j.txraw.data(), j.txraw.size());
-            cp(HPROG, 20 * h0[p], rw.hprog.data(), rw.hprog.size());
-        }
+        if (!dm[AUX]) cp(AUX, auxb0[p], j.aux.data(), j.aux.size());
+        if (!dm[PRE]) cp(PRE, preb0[p], j.pre.data(), j.pre.size());
+        if (!dm[TPL]) cp(TPL, tpl0[p], j.tpl.data(), j.tpl.size());
+        if (!dm[CODE]) cp(CODE, code0[p], j.code.data(), j.code.size());
+        if (!dm[TXRAW]) cp(TXRAW, raw0[p], j.txraw.data(), j.txraw.size());
+        if (!dm[HPROG]) cp(HPROG, 20 * h0[p], rw.hprog.data(), rw.hprog.size());
         const uint32_t ablk = (uint32_t)(auxb0[p] / 64), pblk = (uint32_t)(preb0[p] / 64);
         uint32_t* ao = (uint32_t*)(h + off[AUX_OFF]) + auxi0[p];
         for (size_t k = 0; k < j.aux_off.size(); k++) ao[k] = j.aux_off[k] + ablk;
@@ -1363,7 +1370,7 @@ int DeviceBatch::stage_parts(const SighashJobs* const* J, const TupleRows* const
     };
     std::vector<Work> work;
     constexpr size_t RB = (size_t)1 << 16;
-    if (!direct || need_y || need_m || need_e || need_mm)
+    if (!dm[TAG] || !dm[X] || !dm[RR] || !dm[S] || need_y || need_m || need_e || need_mm)
         for (size_t p = 0; p < P; p++)
             for (size_t lo = 0, nr = Rw[p]->size(); lo < nr; lo += RB)
                 work.push_back(Work{p, lo, std::min(nr, lo + RB)});
@@ -1394,37 +1401,35 @@ int DeviceBatch::stage_parts(const SighashJobs* const* J, const TupleRows* const
     // sighash inputs on the main stream ahead of the front kernel
     up_pending_ = true;
     up_copies_.clear();
-    if (!direct) {
-        up_copies_.push_back(UpCopy{0, h, off[AUX], true});
-        up_copies_.push_back(UpCopy{off[AUX], h + off[AUX], upload - off[AUX], false});
-    } else {
-        // the image's spans of rebased records, then each part's own arrays where they belong
-        auto span = [&](int b0, int b1, bool rows) {
-            if (off[b1] > off[b0]) up_copies_.push_back(UpCopy{off[b0], h + off[b0], off[b1] - off[b0], rows});
-        };
-        span(EMAP, AUX, true);
-        span(AUX_OFF, TPL, false);
-        span(TJOB, TXRAW, false);
-        span(WTX, HPROG, false);
-        span(ZEROS, UPLOADED, false);
-        auto part = [&](int b, size_t at, const void* src, size_t len, bool rows) {
-            if (len) up_copies_.push_back(UpCopy{off[b] + at, src, len, rows});
-        };
-        for (size_t p = 0; p < P; p++) {
-            const TupleRows& rw = *Rw[p];
-            const SighashJobs& j = *J[p];
-            const size_t nr = rw.size();
-            part(TAG, row0[p], rw.tag.data(), nr, true);
-            part(X, 32 * row0[p], rw.x.data(), 32 * nr, true);
-            part(RR, 32 * row0[p], rw.r.data(), 32 * nr, true);
-            part(S, 32 * row0[p], rw.s.data(), 32 * nr, true);
-            part(AUX, auxb0[p], j.aux.data(), j.aux.size(), false);
-            part(PRE, preb0[p], j.pre.data(), j.pre.size(), false);
-            part(TPL, tpl0[p], j.tpl.data(), j.tpl.size(), false);
-            part(CODE, code0[p], j.code.data(), j.code.size(), false);
-            part(TXRAW, raw0[p], j.txraw.data(), j.txraw.size(), false);
-            part(HPROG, 20 * h0[p], rw.hprog.data(), rw.hprog.size(), false);
+    // the image's spans (runs of arrays not uploaded directly; the tuple rows, before AUX, on the
+    // rows stream), then each part's own piece of every direct array where it belongs
+    for (int b = 0; b < UPLOADED;) {
+        if (dm[b]) {
+            b++;
+            continue;
         }
+        int e = b + 1;
+        while (e < UPLOADED && !dm[e] && (e != AUX)) e++;
+        if (off[e] > off[b]) up_copies_.push_back(UpCopy{off[b], h + off[b], off[e] - off[b], b < AUX});
+        b = e;
+    }
+    auto piece = [&](int b, size_t at, const void* src, size_t len) {
+        if (dm[b] && len) up_copies_.push_back(UpCopy{off[b] + at, src, len, b < AUX});
+    };
+    for (size_t p = 0; p < P; p++) {
+        const TupleRows& rw = *Rw[p];
+        const SighashJobs& j = *J[p];
+        const size_t nr = rw.size();
+        piece(TAG, row0[p], rw.tag.data(), nr);
+        piece(X, 32 * row0[p], rw.x.data(), 32 * nr);
+        piece(RR, 32 * row0[p], rw.r.data(), 32 * nr);
+        piece(S, 32 * row0[p], rw.s.data(), 32 * nr);
+        piece(AUX, auxb0[p], j.aux.data(), j.aux.size());
+        piece(PRE, preb0[p], j.pre.data(), j.pre.size());
+        piece(TPL, tpl0[p], j.tpl.data(), j.tpl.size());
+        piece(CODE, code0[p], j.code.data(), j.code.size());
+        piece(TXRAW, raw0[p], j.txraw.data(), j.txraw.size());
+        piece(HPROG, 20 * h0[p], rw.hprog.data(), rw.hprog.size());
     }
     if (need_y) BCC_HIP_TRY(hipMemcpy(a + off[Y], h + off[Y], 32 * R, hipMemcpyHostToDevice));
     // every row's msg is uint256 ONE (byte 0 = 1) unless a part stores its own; the sighash kernels
