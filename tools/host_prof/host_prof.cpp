@@ -7,6 +7,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <new>
 #include <vector>
 
 #include "../../include/bitcoinconsensus.h"
@@ -20,6 +21,15 @@ int gpu_verify_batch(int, const SighashJobs&, const TupleRows& rows, uint8_t* ve
     return 0;
 }
 void set_stage_threads(unsigned) {}  // the device batch is stubbed out
+void set_direct_upload(bool) {}
+bool direct_upload() { return true; }
+void* pinned_alloc(size_t bytes) {  // ordinary memory: nothing is uploaded here
+    void* p = malloc(bytes ? bytes : 1);
+    if (!p) throw std::bad_alloc();
+    return p;
+}
+void pinned_free(void* p, size_t) noexcept { free(p); }
+void pinned_trim() {}
 void release_device_thread_state() {}
 void release_tuple_thread_state() {}
 int gpu_verify_parts(int, const SighashJobs* const*, const TupleRows* const* rows, size_t parts,
