@@ -184,3 +184,33 @@ def test_workload_accessors_pass_row_capacity(monkeypatch):
     for f in (w.verdicts, w.msgs, w.tuple_items):
         with pytest.raises(RuntimeError):
             f()
+
+
+def test_host_rounds_without_gpu_through_the_page_locked_pool():
+    """The product library's verify_batch with every round on the host lane code, on a machine
+    without a GPU: the interpreter's rows and blobs come from the page-locked pool
+    (pipeline.h pinned_alloc), which falls back to ordinary memory when the runtime cannot pin;
+    results equal the crate vectors' before and after bcc_release_thread_state hands the pool's
+    blocks back (pinned_trim) and across repeated calls that reuse them."""
+    import sys
+    code = f"""
+import sys
+sys.path[:0] = [{os.path.dirname(LIB)!r}, {os.path.join(ROOT, 'tests')!r}]
+import bitcoinconsensus_amd as B
+from fixtures import load_json
+vs = [v for v in load_json("crate_vectors.json")] * 300
+items = [(bytes.fromhex(v["spk"]), v["amount"], bytes.fromhex(v["tx"]), v["nin"]) for v in vs]
+B.set_host_small_round(1 << 30)
+for rep in range(3):
+    for flags in sorted(set(v["flags"] for v in vs)):
+        idx = [i for i, v in enumerate(vs) if v["flags"] == flags]
+        got = B.verify_batch([items[i] for i in idx], flags)
+        for i, (r, e) in zip(idx, got):
+            assert r == vs[i]["ret"], (vs[i]["name"], r)
+            assert r == 1 or int(e) == vs[i]["err"], (vs[i]["name"], int(e))
+    if rep == 1:
+        B.release_thread_state()
+print("ok")
+"""
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0 and "ok" in p.stdout, (p.returncode, p.stdout, p.stderr[-2000:])
