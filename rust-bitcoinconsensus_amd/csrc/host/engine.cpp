@@ -954,11 +954,20 @@ void prepare(BatchState& b, const bcc_batch_item* items, size_t n, unsigned flag
         return i == 0 || items[i].tx_to != items[i - 1].tx_to || items[i].tx_to_len != items[i - 1].tx_to_len;
     };
     b.tx_first.clear();
+    // A run longer than a quarter of a shard (a many-input tx) is cut into pieces of at most that
+    // many items, each its own TxEntry (the tx parsed once per piece, with its own per-round
+    // template / aux slots), so that shard_bounds can balance the interpreter passes: C3's
+    // 442-input txs made one shard 2.4x the mean (bcc_batch_stats interpret_shard_*).
+    const size_t M = std::max<size_t>(32, n / (4 * (size_t)std::max(1u, T)));
+    bool longrun = false;
     if (T <= 1 || n < 1024) {
         for (size_t i = 0; i < n; i++)
             if (starts_tx(i)) b.tx_first.push_back((uint32_t)i);
+        for (size_t k = 0; T > 1 && k < b.tx_first.size() && !longrun; k++)
+            longrun = (k + 1 < b.tx_first.size() ? b.tx_first[k + 1] : n) - b.tx_first[k] > M;
     } else {
         b.tx_slices.resize(T);
+        std::vector<size_t> gap(T, 0);  // per slice: the longest run between its own starts
         run_shards(T, W, [&](unsigned t) {
             // appended through a local header (swapped in and out): the shards' vector headers
             // share cache lines, and a push_back per item on them cost every writer its line
@@ -966,8 +975,13 @@ void prepare(BatchState& b, const bcc_batch_item* items, size_t n, unsigned flag
             std::vector<uint32_t> v;
             v.swap(b.tx_slices[t]);
             v.clear();
+            size_t g = 0;
             for (size_t i = share_lo(n, t, T); i < share_lo(n, t + 1, T); i++)
-                if (starts_tx(i)) v.push_back((uint32_t)i);
+                if (starts_tx(i)) {
+                    if (!v.empty()) g = std::max<size_t>(g, i - v.back());
+                    v.push_back((uint32_t)i);
+                }
+            gap[t] = g;
             v.swap(b.tx_slices[t]);
         });
         size_t total = 0;
@@ -978,16 +992,17 @@ void prepare(BatchState& b, const bcc_batch_item* items, size_t n, unsigned flag
             std::copy(b.tx_slices[t].begin(), b.tx_slices[t].end(), b.tx_first.begin() + at);
             at += b.tx_slices[t].size();
         }
+        // the runs inside each slice, then the ones across slice boundaries (a slice's last start
+        // to the next start of any later slice, or n)
+        size_t next = n;
+        for (unsigned t = T; t-- > 0 && !longrun;) {
+            const auto& v = b.tx_slices[t];
+            if (v.empty()) continue;
+            longrun = gap[t] > M || next - v.back() > M;
+            next = v.front();
+        }
     }
-    // A run longer than a quarter of a shard (a many-input tx) is cut into pieces of at most that
-    // many items, each its own TxEntry (the tx parsed once per piece, with its own per-round
-    // template / aux slots), so that shard_bounds can balance the interpreter passes: C3's
-    // 442-input txs made one shard 2.4x the mean (bcc_batch_stats interpret_shard_*).
     if (T > 1) {
-        const size_t M = std::max<size_t>(32, n / (4 * (size_t)T));
-        bool longrun = false;
-        for (size_t k = 0; k < b.tx_first.size() && !longrun; k++)
-            longrun = (k + 1 < b.tx_first.size() ? b.tx_first[k + 1] : n) - b.tx_first[k] > M;
         if (longrun) {
             std::vector<uint32_t> cut;
             cut.reserve(b.tx_first.size() + n / M + 1);
@@ -1652,6 +1667,13 @@ void chunk_stitch(ChunkRun& c) {
     run_shards(c.T, c.W, [&](unsigned t) {
         const uint8_t* v = c.verdict.data() + c.row0[t];
         c.next_list[t].clear();
+        // every row of this shard's round true (the common case): every speculation held and no
+        // item of the shard re-runs -- one scan of the verdict bytes instead of a pass over items
+        const size_t nr = c.row0[t + 1] - c.row0[t];
+        if (nr == 0 || memchr(v, 0, nr) == nullptr) {
+            c.run_list[t].clear();
+            return;
+        }
         for (uint32_t i : c.run_list[t]) {
             Item& it = st[i];
             if (it.pending.empty()) continue;
