@@ -594,6 +594,7 @@ private:
     void* ev_fork_ = nullptr;      // hipEvent_t: run() start on the main stream
     void* ev_join_ = nullptr;      // hipEvent_t: the Q ladder done on the side stream
     void* ev_up_ = nullptr;        // hipEvent_t: the tuple rows uploaded (side stream)
+    void* ev_rows_up_ = nullptr;   // hipEvent_t: upload_on's row copies done (the rest waits)
     void* ev_block_ = nullptr;     // hipEvent_t (blocking sync): host waits sleep, not spin
     int wait(void* stream);
     SigScratch scratch_;

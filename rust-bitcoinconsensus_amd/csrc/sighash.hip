@@ -896,6 +896,7 @@ DeviceBatch::~DeviceBatch() {
     if (ev_fork_) (void)hipEventDestroy((hipEvent_t)ev_fork_);
     if (ev_join_) (void)hipEventDestroy((hipEvent_t)ev_join_);
     if (ev_up_) (void)hipEventDestroy((hipEvent_t)ev_up_);
+    if (ev_rows_up_) (void)hipEventDestroy((hipEvent_t)ev_rows_up_);
     if (ev_block_) (void)hipEventDestroy((hipEvent_t)ev_block_);
     if (arena_) (void)hipFree(arena_);
     if (host_image_) (void)hipHostFree(host_image_);
@@ -1401,29 +1402,39 @@ int DeviceBatch::stage_parts(const SighashJobs* const* J, const TupleRows* const
     // sighash inputs on the main stream ahead of the front kernel
     up_pending_ = true;
     up_copies_.clear();
-    // the image's spans (runs of arrays not uploaded directly; the tuple rows, before AUX, on the
-    // rows stream), then each part's own piece of every direct array where it belongs
-    for (int b = 0; b < UPLOADED;) {
-        if (dm[b]) {
-            b++;
-            continue;
+    // The tuple rows first, then the sighash inputs: the copies of all streams leave in issue order
+    // (one copy queue), and K_inv / K_keyq -- the round's long pole -- wait only for the rows
+    // (round 6: issued part by part, rows and sighash inputs interleaved, the rows of a 500k-input
+    // round landed 2.4 instead of ~1 ms after the upload began).  Each class: the image's spans (runs
+    // of arrays not uploaded directly), then each part's own piece of every direct array.
+    auto spans = [&](int lo, int hi) {
+        for (int b = lo; b < hi;) {
+            if (dm[b]) {
+                b++;
+                continue;
+            }
+            int e = b + 1;
+            while (e < hi && !dm[e]) e++;
+            if (off[e] > off[b]) up_copies_.push_back(UpCopy{off[b], h + off[b], off[e] - off[b], lo < AUX});
+            b = e;
         }
-        int e = b + 1;
-        while (e < UPLOADED && !dm[e] && (e != AUX)) e++;
-        if (off[e] > off[b]) up_copies_.push_back(UpCopy{off[b], h + off[b], off[e] - off[b], b < AUX});
-        b = e;
-    }
+    };
     auto piece = [&](int b, size_t at, const void* src, size_t len) {
         if (dm[b] && len) up_copies_.push_back(UpCopy{off[b] + at, src, len, b < AUX});
     };
+    spans(0, AUX);
     for (size_t p = 0; p < P; p++) {
         const TupleRows& rw = *Rw[p];
-        const SighashJobs& j = *J[p];
         const size_t nr = rw.size();
         piece(TAG, row0[p], rw.tag.data(), nr);
         piece(X, 32 * row0[p], rw.x.data(), 32 * nr);
         piece(RR, 32 * row0[p], rw.r.data(), 32 * nr);
         piece(S, 32 * row0[p], rw.s.data(), 32 * nr);
+    }
+    spans(AUX, UPLOADED);
+    for (size_t p = 0; p < P; p++) {
+        const TupleRows& rw = *Rw[p];
+        const SighashJobs& j = *J[p];
         piece(AUX, auxb0[p], j.aux.data(), j.aux.size());
         piece(PRE, preb0[p], j.pre.data(), j.pre.size());
         piece(TPL, tpl0[p], j.tpl.data(), j.tpl.size());
@@ -1524,18 +1535,43 @@ int DeviceBatch::stage_der(const DerTuples& t) {
 // The staged image's pending upload: all of it on `rows_stream` when `rest_stream` is null, else
 // the tuple rows on `rows_stream` and the rest on `rest_stream`.  Stream order puts every kernel
 // launched after it on the same stream behind its bytes.
+// Every msg row uint256 ONE (byte 0 = 1), one lane per row, two 16-byte stores: the runtime's
+// memset + strided memset for the same rows took ~0.34 ms per 500k rows beside K_keyq.
+__global__ void __launch_bounds__(256) msg_one_kernel(uint4* __restrict__ m, size_t n) {
+    const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    m[2 * k] = make_uint4(1u, 0u, 0u, 0u);
+    m[2 * k + 1] = make_uint4(0u, 0u, 0u, 0u);
+}
+
 int DeviceBatch::upload_on(hipStream_t rows_stream, hipStream_t rest_stream) {
     if (!up_pending_) return 0;
     up_pending_ = false;
     uint8_t* a = (uint8_t*)arena_;
-    for (const UpCopy& c : up_copies_)
-        BCC_HIP_TRY(hipMemcpyAsync(a + c.dst, c.src, c.len, hipMemcpyHostToDevice,
-                                   c.rows || !rest_stream ? rows_stream : rest_stream));
+    // the rows first (up_copies_ lists them first), and the rest only after them: copies queued on
+    // two streams share the copy engines, so K_inv / K_keyq would otherwise wait for most of the
+    // upload (a 500k-input round's rows landed after 2.3 of its 3.6 ms of copies)
+    bool rest_waits = false;
+    for (const UpCopy& c : up_copies_) {
+        hipStream_t cs = c.rows || !rest_stream ? rows_stream : rest_stream;
+        if (cs == rest_stream && rest_stream && !rest_waits) {
+            if (!ev_rows_up_) {
+                hipEvent_t e = nullptr;
+                BCC_HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+                ev_rows_up_ = e;
+            }
+            BCC_HIP_TRY(hipEventRecord((hipEvent_t)ev_rows_up_, rows_stream));
+            BCC_HIP_TRY(hipStreamWaitEvent(rest_stream, (hipEvent_t)ev_rows_up_, 0));
+            rest_waits = true;
+        }
+        BCC_HIP_TRY(hipMemcpyAsync(a + c.dst, c.src, c.len, hipMemcpyHostToDevice, cs));
+    }
     if (up_msg_one_) {
         up_msg_one_ = false;
         hipStream_t ms = rest_stream ? rest_stream : rows_stream;
-        BCC_HIP_TRY(hipMemsetAsync(d_m, 0, 32 * n_rows_, ms));
-        BCC_HIP_TRY(hipMemset2DAsync(d_m, 32, 1, 1, n_rows_, ms));
+        hipLaunchKernelGGL(msg_one_kernel, dim3((unsigned)((n_rows_ + 255) / 256)), dim3(256), 0, ms,
+                           (uint4*)d_m, n_rows_);
+        BCC_HIP_TRY(hipGetLastError());
     }
     return 0;
 }
