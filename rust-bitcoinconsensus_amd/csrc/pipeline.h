@@ -147,8 +147,8 @@ struct WinJob {
     uint32_t hashtype;  // not SIGHASH_SINGLE (those keep the host preimage path)
     uint32_t row;       // tuple row whose msg receives the sighash
     uint32_t amount_lo, amount_hi;
-    uint32_t pad[2];
 };
+static_assert(sizeof(WinJob) == 32, "WinJob: two 16-byte loads");
 
 struct SighashJobs {
     pinned_bytes aux, pre;                          // padded messages, back to back
