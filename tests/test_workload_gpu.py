@@ -179,3 +179,42 @@ def test_c2_mutated_drop_in_upload_modes_and_pipelined_chunks(wl):
     finally:
         B.set_direct_upload(True)
         B.set_pipeline_chunk(500_000)
+
+
+def test_c2_drop_in_concurrent_callers_direct_upload(wl):
+    """Two threads calling the drop-in at once (ctypes drops the GIL), each on its own half of the
+    300k C2 items with ~10 % mutated: first in one round each (150k rows: every large array goes
+    up directly from the page-locked pool, so both threads' arrays are in flight together), then
+    in pipelined 70k chunks (the raw txs direct, the rows through the image).  Every item's
+    (ret, err) equals the reference's."""
+    import threading
+    import bitcoinconsensus_amd as B
+    R = Reference()
+    rng = random.Random(0xD2)
+    items = []
+    for i in range(N):
+        it = wl.item(i)
+        items.append(mutate(rng, it)[:4] if rng.random() < 0.10 else it)
+    exp, _ = R.bulk_verify_script(items, B.VERIFY_ALL)
+    errors = []
+
+    def caller(k):
+        mine = items[k::2]
+        want = exp[k::2]
+        for _ in range(2):
+            got = [(r, int(e)) for r, e in B.verify_batch(mine)]
+            bad = [i for i in range(len(mine)) if got[i] != want[i]]
+            if bad:
+                errors.append((k, bad[:5]))
+
+    try:
+        for chunk in (500_000, 70_000):
+            B.set_pipeline_chunk(chunk)
+            th = [threading.Thread(target=caller, args=(k,)) for k in range(2)]
+            for t in th:
+                t.start()
+            for t in th:
+                t.join()
+            assert not errors, (chunk, errors)
+    finally:
+        B.set_pipeline_chunk(500_000)
