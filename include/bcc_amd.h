@@ -149,6 +149,11 @@ int bcc_set_fused_pass(int on);
  * only the records whose offsets it rebases (default 1, or BCC_DIRECT_UPLOAD; 0: every array is
  * copied into one pinned image first).  Results never depend on it.  Returns 0. */
 int bcc_set_direct_upload(int on);
+/* With the direct upload, each host shard of a pipelined bitcoinconsensus_verify_batch chunk sends
+ * its tuple rows to the GPU as soon as the pass has finished it, and the chunk's device round
+ * gathers them in HBM instead of uploading them (default 1, or BCC_PRE_UPLOAD).  Results never
+ * depend on it.  Returns 0. */
+int bcc_set_pre_upload(int on);
 
 /* Legacy signature checks whose serial SHA-256 chain is longer than `blocks` 64-byte blocks (the
  * preimages of many-input transactions) are hashed on the host CPU instead of in one GPU lane each,

@@ -223,6 +223,11 @@ std::atomic<int> g_early_q{[] {
     return e ? atoi(e) : 1;
 }()};
 constexpr size_t EARLY_MAX_ITEMS = (size_t)1 << 18;
+// Per-shard row pre-upload for pipelined chunks (round 6, bcc_set_pre_upload / BCC_PRE_UPLOAD).
+std::atomic<bool> g_pre_upload{[] {
+    const char* e = getenv("BCC_PRE_UPLOAD");
+    return !(e && atoi(e) == 0);
+}()};
 // early sighashes (BCC_EARLY_SIGHASH, default 1): legacy template jobs with the early rows.  Only
 // the chains between BCC_EARLY_SIGHASH_MIN blocks (from the midstate) and the host's share
 // (host_chain_blocks) go early: C3 5.4-5.7 -> 5.7-6.6 M inputs/s at 96 (64: 5.2-6.4; every long
@@ -942,7 +947,8 @@ void prepare(BatchState& b, const bcc_batch_item* items, size_t n, unsigned flag
              std::vector<std::vector<uint32_t>>* shards = nullptr,
              std::vector<std::vector<uint32_t>>* runs = nullptr,
              std::vector<EarlyShard>* early = nullptr, unsigned W = 0,
-             const FusedPass* fused = nullptr) {
+             const FusedPass* fused = nullptr,
+             const std::function<void(unsigned)>* shard_done = nullptr) {
     if (W == 0 || W > T) W = T;  // worker threads over the T shards (run_shards)
     if (b.st.size() < n) b.st.resize(n);  // reused across calls: every field is (re)set below
     b.n = n;
@@ -1088,6 +1094,7 @@ void prepare(BatchState& b, const bcc_batch_item* items, size_t n, unsigned flag
             lsh.swap((*shards)[t]);
             lrl.swap((*runs)[t]);
         }
+        if (shard_done) (*shard_done)(t);  // (with the fused pass: shard t's rows are final)
         if (early) {  // early Q halves: this shard's candidates while its txs are in cache
             EarlyShard& es = (*early)[t];
             es.clear();
@@ -1365,6 +1372,7 @@ struct ChunkRun {
     // their blocks (HostJobs::take); held by pointer so that ChunkRun stays movable
     std::unique_ptr<std::atomic<uint64_t>> host_planned = std::make_unique<std::atomic<uint64_t>>(0);
     bool late_pending = false;
+    bool pipelined = false;  // a chunk of a pipelined call (its round goes to `staged`)
 };
 
 // Host state of bitcoinconsensus_verify_batch, per calling thread, reused across its calls: two
@@ -1551,7 +1559,22 @@ void chunk_start(ChunkRun& c, const bcc_batch_item* items, size_t n, unsigned fl
             ran[t] |= interpret_items(c.b, idx, m, c.rds[t]) ? 1 : 0;
             ts[t] += since(s0);
         };
-        prepare(c.b, items, n, flags, T, &c.shards, &c.run_list, nullptr, c.W, &pass);
+        // a pipelined chunk's rows go to its staged batch shard by shard as the pass finishes them
+        // (DeviceBatch::pre_upload), so its round's K_keyq need not wait for their upload
+        std::function<void(unsigned)> sent;
+        const std::function<void(unsigned)>* done = nullptr;
+        if (c.pipelined && g_pre_upload.load(std::memory_order_relaxed) && direct_upload()) {
+            const std::vector<int> devs = device_list();
+            if (devs.size() == 1 && n > host_small_round()) {
+                if (!c.staged) c.staged.reset(gpu_staged_new(devs[0]));
+                const size_t cap = 2 * ((n + T - 1) / T) + 4096;  // rows per shard (more: the round sends them)
+                if (gpu_staged_pre_arm(c.staged.get(), T, cap) == 0) {
+                    sent = [&](unsigned t) { gpu_staged_pre_upload(c.staged.get(), t, c.rds[t].rows); };
+                    done = &sent;
+                }
+            }
+        }
+        prepare(c.b, items, n, flags, T, &c.shards, &c.run_list, nullptr, c.W, &pass, done);
         double tmax = 0;
         for (double x : ts) tmax = std::max(tmax, x);
         const double both = since(t0);  // parse + interpret, split by the slowest shard's share
@@ -1867,6 +1890,7 @@ long run_batch(const bcc_batch_item* items, size_t n, unsigned flags, int* ret_o
     } drain;
     if (chunk == 0 || n < 2 * chunk) {
         ChunkRun& c = tl_chunk[0];
+        c.pipelined = false;
         chunk_start(c, items, n, flags, true);
         account(chunk_finish(c, ret_out, err_out, false, &gpu_s));
         chunk_release_if_large(c);
@@ -1887,6 +1911,7 @@ long run_batch(const bcc_batch_item* items, size_t n, unsigned flags, int* ret_o
         size_t prev_lo = 0;
         for (size_t k = 0; k + 1 < cut.size(); k++) {
             ChunkRun& c = tl_chunk[k & 1];
+            c.pipelined = true;
             chunk_start(c, items + cut[k], cut[k + 1] - cut[k], flags);
             if (c.pending_round && g_chunk_launch_early) {
                 // staged and queued before the previous chunk is waited for: its upload runs
@@ -2121,6 +2146,11 @@ int bcc_set_early_q(int on) {
 
 int bcc_set_pipeline_chunk(size_t items) {
     g_pipeline_chunk.store(items, std::memory_order_relaxed);
+    return 0;
+}
+
+int bcc_set_pre_upload(int on) {
+    bcc::host::g_pre_upload.store(on != 0, std::memory_order_relaxed);
     return 0;
 }
 

@@ -540,6 +540,14 @@ public:
     // stay unchanged until the round has run; false copies everything into the pinned image
     int stage_parts(const SighashJobs* const* jobs, const TupleRows* const* rows, size_t P,
                     bool direct = false);
+    // Rows uploaded per host shard while the host pass still runs (round 6): pre_arm on the
+    // calling thread before the pass (P shards of at most cap_rows rows), pre_upload by the worker
+    // that finished shard t (its tag / x / r / s to the shard's own HBM buffer, on the batch's
+    // pre stream); stage_parts then gathers them into the arena with K_rowgather instead of
+    // uploading them (falling back to the upload for a shard that did not fit or was not sent).
+    // The rows must stay unchanged until the round has run, as with the direct upload.
+    int pre_arm(unsigned P, size_t cap_rows);
+    void pre_upload(unsigned t, const TupleRows& rows);
     // raw tuples (DerTuples): blobs, offsets and messages staged; run() starts with K_der
     int stage_der(const DerTuples& t);
     int run(void* stream, const LateMsgFill* late = nullptr);  // K1..K4
@@ -567,7 +575,8 @@ private:
     int sync();
     void* pick(void* stream);
     int launch_front(struct ihipStream_t* st);        // K_wtx + K3' + K1 fused, then the rest
-    int upload_on(struct ihipStream_t* rows_stream, struct ihipStream_t* rest_stream);
+    // part 1: the tuple rows (and the pre-uploaded rows' gather), part 2: the rest; 3: both
+    int upload_on(struct ihipStream_t* rows_stream, struct ihipStream_t* rest_stream, int part = 3);
     bool up_pending_ = false;      // the staged image is not on the device yet (issued by run)
     struct UpCopy {  // one host -> HBM copy of the pending upload
         size_t dst;      // arena offset
@@ -577,6 +586,17 @@ private:
     };
     std::vector<UpCopy> up_copies_;
     bool up_msg_one_ = false;      // the msg rows are set to ONE with the upload
+    // per-shard row pre-upload (pre_arm / pre_upload): shard t's tag | x | r | s at pre_buf_[t]
+    static constexpr unsigned PRE_MAX_SHARDS = 64;
+    std::vector<uint8_t*> pre_buf_;
+    size_t pre_cap_ = 0;               // rows per shard buffer
+    std::vector<size_t> pre_rows_;     // rows sent per shard (SIZE_MAX: none)
+    unsigned pre_P_ = 0;
+    bool pre_armed_ = false;
+    void* pre_stream_ = nullptr;       // hipStream_t of the pre-uploads
+    void* ev_pre_ = nullptr;           // hipEvent_t: every pre-upload issued so far is done
+    bool gather_pending_ = false;      // the next run gathers the pre-uploaded rows (upload_on)
+    std::vector<size_t> gather_row0_;  // the shards' first rows in the arena (P + 1)
     int launch_after_front(struct ihipStream_t* st);  // K_win, K2, K3
     int launch_key_hash(struct ihipStream_t* st);     // K_h160: key-hash conditions into the verdicts
     int run_stages(void* stream, const LateMsgFill* late);
@@ -702,6 +722,10 @@ void gpu_staged_free(StagedRound* s);
 // gpu_staged_finish returns: with direct upload the launch's copies read their arrays.
 int gpu_staged_stage(StagedRound* s, const SighashJobs* const* jobs, const TupleRows* const* rows,
                      size_t parts, double* stage_seconds);
+// Per-shard row pre-upload on s's batch (DeviceBatch::pre_arm / pre_upload): armed by the caller
+// before a host pass of P shards, sent by each shard's worker when its rows are final.
+int gpu_staged_pre_arm(StagedRound* s, unsigned P, size_t cap_rows);
+void gpu_staged_pre_upload(StagedRound* s, unsigned t, const TupleRows& rows);
 // Fills s's pinned image with raw tuples (DeviceBatch::stage_der; the caller's buffers are copied).
 int gpu_staged_stage_der(StagedRound* s, const DerTuples& t, double* stage_seconds);
 // One synchronous round of raw tuples on the calling thread's batch of `device`.

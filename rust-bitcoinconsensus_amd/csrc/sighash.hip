@@ -897,6 +897,13 @@ DeviceBatch::~DeviceBatch() {
     if (ev_join_) (void)hipEventDestroy((hipEvent_t)ev_join_);
     if (ev_up_) (void)hipEventDestroy((hipEvent_t)ev_up_);
     if (ev_rows_up_) (void)hipEventDestroy((hipEvent_t)ev_rows_up_);
+    if (pre_stream_) {
+        (void)hipStreamSynchronize((hipStream_t)pre_stream_);
+        (void)hipStreamDestroy((hipStream_t)pre_stream_);
+    }
+    if (ev_pre_) (void)hipEventDestroy((hipEvent_t)ev_pre_);
+    for (uint8_t* b : pre_buf_)
+        if (b) (void)hipFree(b);
     if (ev_block_) (void)hipEventDestroy((hipEvent_t)ev_block_);
     if (arena_) (void)hipFree(arena_);
     if (host_image_) (void)hipHostFree(host_image_);
@@ -1288,6 +1295,15 @@ int DeviceBatch::stage_parts(const SighashJobs* const* J, const TupleRows* const
         for (int b : {TAG, X, RR, S, AUX, PRE, TPL, CODE, TXRAW, HPROG})
             dm[b] = sizes[b] / P >= DIRECT_MIN_PIECE;
     }
+    // the rows the host pass pre-uploaded per shard (pre_upload): gathered in the run, not sent
+    bool gathered = direct_arg && pre_armed_ && pre_P_ == P && R < ((size_t)1 << 32);
+    for (size_t p = 0; gathered && p < P; p++) gathered = pre_rows_[p] == Rw[p]->size();
+    pre_armed_ = false;
+    gather_pending_ = gathered;
+    if (gathered) {
+        gather_row0_.assign(row0.begin(), row0.end());
+        for (int b : {TAG, X, RR, S}) dm[b] = true;  // neither filled into the image nor uploaded
+    }
     // the rows of part p in [lo, hi): the bulk of a tuple batch, copied in blocks by the team
     auto fill_rows = [&](size_t p, size_t lo, size_t hi) {
         const TupleRows& rw = *Rw[p];
@@ -1423,7 +1439,7 @@ int DeviceBatch::stage_parts(const SighashJobs* const* J, const TupleRows* const
         if (dm[b] && len) up_copies_.push_back(UpCopy{off[b] + at, src, len, b < AUX});
     };
     spans(0, AUX);
-    for (size_t p = 0; p < P; p++) {
+    for (size_t p = 0; p < P && !gathered; p++) {
         const TupleRows& rw = *Rw[p];
         const size_t nr = rw.size();
         piece(TAG, row0[p], rw.tag.data(), nr);
@@ -1535,6 +1551,100 @@ int DeviceBatch::stage_der(const DerTuples& t) {
 // The staged image's pending upload: all of it on `rows_stream` when `rest_stream` is null, else
 // the tuple rows on `rows_stream` and the rest on `rest_stream`.  Stream order puts every kernel
 // launched after it on the same stream behind its bytes.
+// Per-shard row pre-upload (DeviceBatch::pre_arm / pre_upload).  Shard buffer layout for cap rows:
+// tag at 0, then x, r, s (32 bytes a row each) from align256(cap).
+static size_t pre_x_off(size_t cap) { return (cap + 255) & ~(size_t)255; }
+int DeviceBatch::pre_arm(unsigned P, size_t cap_rows) {
+    pre_armed_ = false;
+    gather_pending_ = false;
+    if (P == 0 || P > PRE_MAX_SHARDS || cap_rows == 0) return 0;
+    BCC_HIP_TRY(hipSetDevice(dev_));
+    if (!pre_stream_) {
+        hipStream_t st = nullptr;
+        hipEvent_t e = nullptr;
+        BCC_HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+        BCC_HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        pre_stream_ = st;
+        ev_pre_ = e;
+    }
+    // the buffers' previous round (its gather) and pre-uploads are done before they are rewritten
+    if (int e = sync()) return e;
+    BCC_HIP_TRY(hipStreamSynchronize((hipStream_t)pre_stream_));
+    if (cap_rows > pre_cap_ || pre_buf_.size() < P) {
+        const size_t cap = std::max(cap_rows, pre_cap_);
+        for (uint8_t*& b : pre_buf_) {
+            if (b) BCC_HIP_TRY(hipFree(b));
+            b = nullptr;
+        }
+        pre_buf_.assign(std::max<size_t>(P, pre_buf_.size()), nullptr);
+        pre_cap_ = 0;
+        for (uint8_t*& b : pre_buf_) BCC_HIP_TRY(hipMalloc(&b, pre_x_off(cap) + 96 * cap));
+        pre_cap_ = cap;
+    }
+    pre_rows_.assign(P, SIZE_MAX);
+    pre_P_ = P;
+    pre_armed_ = true;
+    return 0;
+}
+
+void DeviceBatch::pre_upload(unsigned t, const TupleRows& rw) {
+    if (!pre_armed_ || t >= pre_P_) return;
+    const size_t n = rw.size();
+    if (n > pre_cap_) return;  // stays SIZE_MAX: this shard's rows go up with the round
+    if (hipSetDevice(dev_) != hipSuccess) {
+        (void)hipGetLastError();
+        return;
+    }
+    hipStream_t st = (hipStream_t)pre_stream_;
+    uint8_t* b = pre_buf_[t];
+    const size_t xo = pre_x_off(pre_cap_);
+    bool ok = true;
+    if (n) {
+        ok = hipMemcpyAsync(b, rw.tag.data(), n, hipMemcpyHostToDevice, st) == hipSuccess &&
+             hipMemcpyAsync(b + xo, rw.x.data(), 32 * n, hipMemcpyHostToDevice, st) == hipSuccess &&
+             hipMemcpyAsync(b + xo + 32 * pre_cap_, rw.r.data(), 32 * n, hipMemcpyHostToDevice, st) == hipSuccess &&
+             hipMemcpyAsync(b + xo + 64 * pre_cap_, rw.s.data(), 32 * n, hipMemcpyHostToDevice, st) == hipSuccess;
+    }
+    if (!ok) {
+        (void)hipGetLastError();
+        return;
+    }
+    pre_rows_[t] = n;  // (each worker writes its own shard's entry; read after the pass joins)
+}
+
+// K_rowgather: the pre-uploaded shards' rows into the arena's tag / x / r / s, one lane per row.
+struct RowGather {
+    const uint8_t* base[64];
+    uint32_t row0[64 + 1];
+    uint32_t P;
+    uint32_t xoff;  // x's offset in a shard buffer; r, s follow at + 32 cap, + 64 cap
+    uint32_t cap;
+};
+__global__ void __launch_bounds__(256) row_gather_kernel(RowGather g, uint8_t* __restrict__ tag,
+                                                        uint4* __restrict__ x, uint4* __restrict__ r,
+                                                        uint4* __restrict__ s, uint32_t R) {
+    const uint32_t row = blockIdx.x * blockDim.x + threadIdx.x;
+    if (row >= R) return;
+    uint32_t lo = 0, hi = g.P;  // the shard: the last p with row0[p] <= row
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) / 2;
+        if (g.row0[mid] <= row) lo = mid;
+        else hi = mid;
+    }
+    const size_t k = row - g.row0[lo];
+    const uint8_t* b = g.base[lo];
+    tag[row] = b[k];
+    const uint4* xs = reinterpret_cast<const uint4*>(b + g.xoff) + 2 * k;
+    const uint4* rs = reinterpret_cast<const uint4*>(b + g.xoff + 32 * (size_t)g.cap) + 2 * k;
+    const uint4* ss = reinterpret_cast<const uint4*>(b + g.xoff + 64 * (size_t)g.cap) + 2 * k;
+    x[2 * row] = xs[0];
+    x[2 * row + 1] = xs[1];
+    r[2 * row] = rs[0];
+    r[2 * row + 1] = rs[1];
+    s[2 * row] = ss[0];
+    s[2 * row + 1] = ss[1];
+}
+
 // Every msg row uint256 ONE (byte 0 = 1), one lane per row, two 16-byte stores: the runtime's
 // memset + strided memset for the same rows took ~0.34 ms per 500k rows beside K_keyq.
 __global__ void __launch_bounds__(256) msg_one_kernel(uint4* __restrict__ m, size_t n) {
@@ -1544,34 +1654,62 @@ __global__ void __launch_bounds__(256) msg_one_kernel(uint4* __restrict__ m, siz
     m[2 * k + 1] = make_uint4(0u, 0u, 0u, 0u);
 }
 
-int DeviceBatch::upload_on(hipStream_t rows_stream, hipStream_t rest_stream) {
+int DeviceBatch::upload_on(hipStream_t rows_stream, hipStream_t rest_stream, int part) {
     if (!up_pending_) return 0;
-    up_pending_ = false;
     uint8_t* a = (uint8_t*)arena_;
-    // the rows first (up_copies_ lists them first), and the rest only after them: copies queued on
-    // two streams share the copy engines, so K_inv / K_keyq would otherwise wait for most of the
-    // upload (a 500k-input round's rows landed after 2.3 of its 3.6 ms of copies)
-    bool rest_waits = false;
-    for (const UpCopy& c : up_copies_) {
-        hipStream_t cs = c.rows || !rest_stream ? rows_stream : rest_stream;
-        if (cs == rest_stream && rest_stream && !rest_waits) {
+    // The rows first, and the rest only after them: copies queued on two streams share the copy
+    // engines, so K_inv / K_keyq would otherwise wait for most of the upload (a 500k-input round's
+    // rows landed after 2.3 of its 3.6 ms of copies).  run_stages issues the rows (part 1), queues
+    // the Q kernels behind them, then issues the rest (part 2): the ~50 copy calls of the rest no
+    // longer hold up the Q kernels' launch.
+    if (part & 1) {
+        if (gather_pending_) {  // the rows the host pass already sent, into place first
+            gather_pending_ = false;
+            BCC_HIP_TRY(hipEventRecord((hipEvent_t)ev_pre_, (hipStream_t)pre_stream_));
+            BCC_HIP_TRY(hipStreamWaitEvent(rows_stream, (hipEvent_t)ev_pre_, 0));
+            RowGather g{};
+            g.P = pre_P_;
+            g.xoff = (uint32_t)pre_x_off(pre_cap_);
+            g.cap = (uint32_t)pre_cap_;
+            for (unsigned p = 0; p < pre_P_; p++) {
+                g.base[p] = pre_buf_[p];
+                g.row0[p] = (uint32_t)gather_row0_[p];
+            }
+            g.row0[pre_P_] = (uint32_t)gather_row0_[pre_P_];
+            if (n_rows_) {
+                hipLaunchKernelGGL(row_gather_kernel, dim3((unsigned)((n_rows_ + 255) / 256)), dim3(256), 0,
+                                   rows_stream, g, (uint8_t*)d_tag, (uint4*)d_x, (uint4*)d_r, (uint4*)d_s,
+                                   (uint32_t)n_rows_);
+                BCC_HIP_TRY(hipGetLastError());
+            }
+        }
+        for (const UpCopy& c : up_copies_)
+            if (c.rows || !rest_stream)
+                BCC_HIP_TRY(hipMemcpyAsync(a + c.dst, c.src, c.len, hipMemcpyHostToDevice, rows_stream));
+        if (rest_stream) {
             if (!ev_rows_up_) {
                 hipEvent_t e = nullptr;
                 BCC_HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
                 ev_rows_up_ = e;
             }
             BCC_HIP_TRY(hipEventRecord((hipEvent_t)ev_rows_up_, rows_stream));
-            BCC_HIP_TRY(hipStreamWaitEvent(rest_stream, (hipEvent_t)ev_rows_up_, 0));
-            rest_waits = true;
         }
-        BCC_HIP_TRY(hipMemcpyAsync(a + c.dst, c.src, c.len, hipMemcpyHostToDevice, cs));
     }
-    if (up_msg_one_) {
-        up_msg_one_ = false;
-        hipStream_t ms = rest_stream ? rest_stream : rows_stream;
-        hipLaunchKernelGGL(msg_one_kernel, dim3((unsigned)((n_rows_ + 255) / 256)), dim3(256), 0, ms,
-                           (uint4*)d_m, n_rows_);
-        BCC_HIP_TRY(hipGetLastError());
+    if (part & 2) {
+        up_pending_ = false;
+        if (rest_stream) {
+            BCC_HIP_TRY(hipStreamWaitEvent(rest_stream, (hipEvent_t)ev_rows_up_, 0));
+            for (const UpCopy& c : up_copies_)
+                if (!c.rows)
+                    BCC_HIP_TRY(hipMemcpyAsync(a + c.dst, c.src, c.len, hipMemcpyHostToDevice, rest_stream));
+        }
+        if (up_msg_one_) {
+            up_msg_one_ = false;
+            hipStream_t ms = rest_stream ? rest_stream : rows_stream;
+            hipLaunchKernelGGL(msg_one_kernel, dim3((unsigned)((n_rows_ + 255) / 256)), dim3(256), 0, ms,
+                               (uint4*)d_m, n_rows_);
+            BCC_HIP_TRY(hipGetLastError());
+        }
     }
     return 0;
 }
@@ -1808,7 +1946,7 @@ int DeviceBatch::run_stages(void* stream, const LateMsgFill* late) {
     hipStream_t side = (hipStream_t)side_stream_;
     BCC_HIP_TRY(hipEventRecord((hipEvent_t)ev_fork_, st));
     BCC_HIP_TRY(hipStreamWaitEvent(side, (hipEvent_t)ev_fork_, 0));
-    if (int e = upload_on(side, st)) return e;
+    if (int e = upload_on(side, st, 1)) return e;
     BCC_HIP_TRY(hipEventRecord((hipEvent_t)ev_up_, side));  // the tuple rows are on the device
     if (int e = ecdsa_launch_pre(scratch_, d_tag, d_x, d_y, d_s, n_rows_, side)) return e;
     if (int e = ecdsa_launch_key(scratch_, d_tag, d_x, d_y, n_rows_, side)) return e;
@@ -1821,6 +1959,7 @@ int DeviceBatch::run_stages(void* stream, const LateMsgFill* late) {
         return e;
     }
     BCC_HIP_TRY(hipEventRecord((hipEvent_t)ev_join_, side));
+    if (int e = upload_on(side, st, 2)) return e;  // the sighash inputs, behind the rows
     if (int e = launch_front(st)) return e;
     if (d_mmap_ && early_n_ && early_msgs_) {  // the early sighashes into their rows
         BCC_HIP_TRY(hipStreamWaitEvent(st, (hipEvent_t)ev_early_sig_, 0));
@@ -1970,6 +2109,19 @@ int gpu_staged_stage_der(StagedRound* s, const DerTuples& t, double* stage_secon
         *stage_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     if (e) s->b.reset();
     return e;
+}
+
+int gpu_staged_pre_arm(StagedRound* s, unsigned P, size_t cap_rows) {
+    if (s->dev < 0) return (int)hipErrorInvalidDevice;
+    BCC_HIP_TRY(hipSetDevice(s->dev));
+    if (!s->b) s->b = std::make_unique<DeviceBatch>(s->dev);
+    const int e = s->b->pre_arm(P, cap_rows);
+    if (e) s->b.reset();
+    return e;
+}
+
+void gpu_staged_pre_upload(StagedRound* s, unsigned t, const TupleRows& rows) {
+    if (s->b) s->b->pre_upload(t, rows);
 }
 
 int gpu_staged_launch(StagedRound* s, const LateMsgFill* late) {

@@ -162,6 +162,9 @@ int gpu_staged_launch(StagedRound* s, const LateMsgFill* late) {
     v.assign(n, 0);
     return gpu_staged_run(s, v.data(), late);
 }
+// per-shard row pre-upload: nothing to send here (the staged round evaluates its parts itself)
+int gpu_staged_pre_arm(StagedRound*, unsigned, size_t) { return 0; }
+void gpu_staged_pre_upload(StagedRound*, unsigned, const TupleRows&) {}
 int gpu_staged_finish(StagedRound* s, uint8_t* verdict) {
     if (!s->verdicts.empty()) memcpy(verdict, s->verdicts.data(), s->verdicts.size());
     return 0;

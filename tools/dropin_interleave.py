@@ -1,6 +1,6 @@
 """Drop-in A/B inside ONE process: settings alternate call by call (the box's state drifts
 between processes far more than between neighbouring calls), medians per setting.
-    python tools/dropin_interleave.py N CALLS_PER_SETTING "chunk:tail[:shards_per_worker[:fused[:direct[:host_threads]]]]" ...
+    python tools/dropin_interleave.py N CALLS_PER_SETTING "chunk:tail[:shards_per_worker[:fused[:direct[:host_threads[:pre_upload]]]]]" ...
 """
 import ctypes
 import os
@@ -19,6 +19,7 @@ L.bcc_set_pipeline_tail.argtypes = [ctypes.c_size_t]
 L.bcc_set_long_shards_per_worker.argtypes = [ctypes.c_uint]
 L.bcc_set_fused_pass.argtypes = [ctypes.c_int]
 L.bcc_set_direct_upload.argtypes = [ctypes.c_int]
+L.bcc_set_pre_upload.argtypes = [ctypes.c_int]
 wl = B.Workload(n, seed=0x5EED0001)
 wl.run()
 for _ in range(2):
@@ -35,6 +36,7 @@ for k in range(calls):
         L.bcc_set_fused_pass(s[3] if len(s) > 3 else 1)
         L.bcc_set_direct_upload(s[4] if len(s) > 4 else 1)
         B.set_host_threads(s[5] if len(s) > 5 else 0)
+        L.bcc_set_pre_upload(s[6] if len(s) > 6 else 1)
         c0, t0 = time.process_time(), time.perf_counter()
         nv, _ = wl.verify_batch()
         res[s].append(time.perf_counter() - t0)
@@ -46,7 +48,7 @@ for k in range(calls):
 for s in settings:
     m = statistics.median(res[s])
     print(f"chunk {s[0]:>7} tail {s[1]:>7} spw {s[2] if len(s) > 2 else 1} fused {s[3] if len(s) > 3 else 1} "
-          f"direct {s[4] if len(s) > 4 else 1} threads {s[5] if len(s) > 5 else 0}: median {m * 1e3:6.2f} ms = {n / m / 1e6:5.1f} M/s, "
+          f"direct {s[4] if len(s) > 4 else 1} threads {s[5] if len(s) > 5 else 0} pre {s[6] if len(s) > 6 else 1}: median {m * 1e3:6.2f} ms = {n / m / 1e6:5.1f} M/s, "
           f"mean {n / statistics.mean(res[s]) / 1e6:5.1f} M/s, cpu {statistics.median(cpu[s]) / n * 1e6:.3f} "
           f"CPU-s/1M, stage {statistics.median(stage[s]) * 1e3:.2f} ms, host {statistics.median(host[s]) * 1e3:.2f} ms",
           flush=True)

@@ -68,6 +68,9 @@ int gpu_staged_stage_der(StagedRound* s, const DerTuples&, double*) {
     s->rows.clear();
     return 0;
 }
+// per-shard row pre-upload: nothing to send here (the staged round evaluates its parts itself)
+int gpu_staged_pre_arm(StagedRound*, unsigned, size_t) { return 0; }
+void gpu_staged_pre_upload(StagedRound*, unsigned, const TupleRows&) {}
 int gpu_staged_finish(StagedRound* s, uint8_t* verdict) {
     return gpu_staged_run(s, verdict, nullptr);
 }
